@@ -1,0 +1,919 @@
+/*
+ * disq_oracle.c -- CPU restatement of Disq's BAM read path (TEST INFRASTRUCTURE ONLY).
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load this code, and only
+ * as the checker; the product path (libdisq_gpu.so) never links it.
+ *
+ * Each function cites the reference file:line it restates.  Abbreviations:
+ *   D/  = /root/reference/src/main/java/org/disq_bio/disq/
+ *   H/  = /root/reference/src/main/java/htsjdk/samtools/   (vendored htsjdk shims)
+ * htsjdk 2.16.0 classes that are NOT vendored (BlockCompressedInputStream, BlockGunzipper,
+ * BAMRecordCodec, QueryInterval, BAMQueryMultipleIntervalsIteratorFilter) are restated from their
+ * published 2.16.0 behaviour; their call sites in the reference are cited instead.
+ *
+ * Stream model.  htsjdk's BlockCompressedInputStream reads BGZF blocks one after another by the
+ * BSIZE field at header offset 16 (BLOCK_HEADER_LENGTH = 18) and raw-inflates exactly ISIZE
+ * bytes from each (BlockGunzipper.unzipBlock).  A file pointer is (block address << 16 | offset);
+ * a pointer at the end of a non-empty block reads as (next block address, 0) -- confirmed by the
+ * final offset (597454, 0) of the reference fixture 1-with-splitting-index.bam.sbi.  Empty BGZF
+ * blocks in the middle of a stream are treated as transparent (documented limitation).
+ */
+#include "disq_oracle.h"
+
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <zlib.h>
+
+#define MAX_USIZE 65536
+#define NCACHE 4
+#define R_EOF 11      /* java.io.EOFException */
+#define R_IOERR 12    /* other java.io.IOException */
+#define R_FORMAT 13   /* htsjdk SAMFormatException / RuntimeIOException (not caught by Disq) */
+
+struct dqo_file {
+  const uint8_t* data;
+  int64_t len;
+  int verify_crc;
+  /* header */
+  int have_header;
+  int32_t n_ref;
+  int32_t* ref_len;
+  char** ref_name;
+  uint64_t first_record;
+  char err[256];
+};
+
+static void set_err(dqo_file* f, const char* msg) {
+  if (f) snprintf(f->err, sizeof f->err, "%s", msg);
+}
+
+static inline uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+static inline int32_t rd32(const uint8_t* p) {
+  return (int32_t)((uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) |
+                   ((uint32_t)p[3] << 24));
+}
+static inline uint64_t rd64(const uint8_t* p) {
+  uint64_t v = 0;
+  for (int i = 7; i >= 0; i--) v = (v << 8) | p[i];
+  return v;
+}
+/* Java int32 wrap-around arithmetic. */
+static inline int32_t jadd(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
+static inline int32_t jmul(int32_t a, int32_t b) { return (int32_t)((uint32_t)a * (uint32_t)b); }
+static inline int32_t jdiv2(int32_t a) { return a / 2; } /* Java truncates toward zero, as C99 */
+
+/* ------------------------------------------------------------------ hashes */
+static inline uint64_t mix64(uint64_t z) {
+  z ^= z >> 30;
+  z *= 0xBF58476D1CE4E5B9ULL;
+  z ^= z >> 27;
+  z *= 0x94D049BB133111EBULL;
+  z ^= z >> 31;
+  return z;
+}
+
+uint64_t dqo_record_hash(const uint8_t* b, int64_t n) {
+  uint64_t h = (uint64_t)n * 0x9E3779B97F4A7C15ULL;
+  int64_t nw = (n + 7) / 8;
+  for (int64_t i = 0; i < nw; i++) {
+    uint64_t w = 0;
+    for (int k = 7; k >= 0; k--) {
+      int64_t j = i * 8 + k;
+      w = (w << 8) | (j < n ? b[j] : 0);
+    }
+    h += mix64(w ^ ((uint64_t)(i + 1) * 0xD6E8FEB86659FD93ULL));
+  }
+  return mix64(h);
+}
+
+uint64_t dqo_stream_digest(const uint64_t* hs, int64_t n, uint64_t start_index) {
+  uint64_t d = 0;
+  for (int64_t k = 0; k < n; k++)
+    d += mix64(hs[k] + (start_index + (uint64_t)k + 1) * 0x9E3779B97F4A7C15ULL);
+  return d;
+}
+
+/* ------------------------------------------------------------------ file */
+dqo_file* dqo_open_mem(const uint8_t* data, int64_t len, int verify_crc) {
+  dqo_file* f = (dqo_file*)calloc(1, sizeof(dqo_file));
+  if (!f) return NULL;
+  f->data = data;
+  f->len = len;
+  f->verify_crc = verify_crc;
+  return f;
+}
+
+void dqo_close(dqo_file* f) {
+  if (!f) return;
+  if (f->ref_name)
+    for (int i = 0; i < f->n_ref; i++) free(f->ref_name[i]);
+  free(f->ref_name);
+  free(f->ref_len);
+  free(f);
+}
+
+const char* dqo_last_error(dqo_file* f) { return f ? f->err : "null file"; }
+
+/* ------------------------------------------------------------------ a1 splits */
+/* PathSplitSource.getPathSplits: D/impl/file/PathSplitSource.java:26-64.
+ * NIO branch :32-42; Hadoop branch :44-62 -> Hadoop 2.7 FileInputFormat.getSplits
+ * (computeSplitSize = max(minSize=1, min(maxSize, blockSize)); SPLIT_SLOP = 1.1). */
+int64_t dqo_path_splits(int64_t len, int32_t split_size, int nio, int64_t local_block_size,
+                        int64_t* starts, int64_t* ends, int64_t cap) {
+  int64_t n = 0;
+  if (nio) {
+    if (split_size <= 0) return DQO_EINVAL; /* ceil(len/0) is undefined in the reference */
+    int64_t ns = (len + split_size - 1) / split_size;
+    for (int64_t i = 0; i < ns; i++) {
+      int64_t s = i * (int64_t)split_size;
+      int64_t e = s + split_size > len ? len : s + split_size;
+      if (n < cap) { starts[n] = s; ends[n] = e; }
+      n++;
+    }
+    return n;
+  }
+  int64_t max_size = split_size > 0 ? split_size : INT64_MAX;
+  int64_t ss = local_block_size < max_size ? local_block_size : max_size;
+  if (ss < 1) ss = 1;
+  if (len == 0) {
+    if (n < cap) { starts[n] = 0; ends[n] = 0; }
+    return 1;
+  }
+  int64_t rem = len;
+  while (((double)rem) / ss > 1.1) {
+    if (n < cap) { starts[n] = len - rem; ends[n] = len - rem + ss; }
+    n++;
+    rem -= ss;
+  }
+  if (rem != 0) {
+    if (n < cap) { starts[n] = len - rem; ends[n] = len; }
+    n++;
+  }
+  return n;
+}
+
+/* ------------------------------------------------------------------ a2/a3 block guesser */
+/* BgzfBlockGuesser.guessNextBGZFPos: D/impl/formats/bgzf/BgzfBlockGuesser.java:76-149.
+ * Any read past EOF is an IOException caught at :146-148 -> null. */
+int dqo_guess_next_bgzf(dqo_file* f, int64_t p, int64_t end, int64_t* opos, int32_t* ocsize,
+                        int32_t* ousize) {
+  const uint8_t* d = f->data;
+  const int64_t L = f->len;
+#define NEED(q, n) \
+  do {             \
+    if ((q) < 0 || (q) + (n) > L) return 0; \
+  } while (0)
+  for (;;) {
+    for (;;) { /* :79-92 */
+      NEED(p, 4);
+      uint32_t n = (uint32_t)rd32(d + p);
+      if (n == 0x04088b1fu) break;
+      if ((n >> 8) == 0x00088b1fu) p += 1;
+      else if ((n >> 16) == 0x8b1fu) p += 2;
+      else p += 3;
+      if (p >= end) return 0;
+    }
+    const int64_t p0 = p; /* :95 */
+    p += 10;
+    NEED(p, 2);
+    int32_t xlen = rd16(d + p);
+    p += 2;
+    const int64_t sub_end = p + xlen;
+    int64_t q = p; /* stream position */
+    int cancelled = 0;
+    while (p < sub_end) { /* :103 */
+      NEED(q, 4);
+      uint32_t id = (uint32_t)rd32(d + q);
+      if (id != 0x00024342u) {
+        p += 4 + rd16(d + q + 2);
+        q = p;
+        continue;
+      }
+      NEED(q + 4, 2);
+      int32_t bsize = rd16(d + q + 4); /* :117-118 */
+      p += 6;                          /* :121 */
+      while (p < sub_end) {            /* :122-126 */
+        NEED(p, 4);
+        p += 4 + rd16(d + p + 2);
+      }
+      if (p != sub_end) { /* :127-131 */
+        cancelled = 1;
+        break;
+      }
+      p += (int64_t)bsize - xlen - 19 + 4; /* :134 */
+      NEED(p, 4);
+      *opos = p0;
+      *ocsize = (int32_t)(p + 4 - p0);
+      *ousize = rd32(d + p);
+      return 1;
+    }
+    (void)cancelled;
+    p = p0 + 4; /* :144 -- note: the inner loop tests this position before any end check */
+  }
+#undef NEED
+}
+
+/* BgzfBlockSource iterator: D/impl/formats/bgzf/BgzfBlockSource.java:63-84. */
+int64_t dqo_split_blocks(dqo_file* f, int64_t s, int64_t e, int64_t* pos, int32_t* cs, int32_t* us,
+                         int64_t cap) {
+  int64_t n = 0;
+  int64_t start = s;
+  for (;;) {
+    if (start > e) break; /* :70 */
+    int64_t bp;
+    int32_t bc, bu;
+    if (!dqo_guess_next_bgzf(f, start, e, &bp, &bc, &bu)) break;
+    if (n < cap) { pos[n] = bp; cs[n] = bc; us[n] = bu; }
+    n++;
+    start = bp + bc; /* :79 */
+  }
+  return n;
+}
+
+/* ------------------------------------------------------------------ block reader */
+typedef struct {
+  int64_t addr;
+  int32_t csize; /* 0 for the EOF pseudo-block */
+  int32_t len;
+  int valid;
+  uint64_t stamp;
+  uint8_t data[MAX_USIZE];
+} blkbuf;
+
+typedef struct {
+  dqo_file* f;
+  blkbuf* c[NCACHE];
+  uint64_t clock;
+  blkbuf* cur;
+  int32_t off;
+  z_stream zs;
+  int zinit;
+} rdr;
+
+static int rdr_init(rdr* r, dqo_file* f) {
+  memset(r, 0, sizeof *r);
+  r->f = f;
+  for (int i = 0; i < NCACHE; i++) {
+    r->c[i] = (blkbuf*)calloc(1, sizeof(blkbuf));
+    if (!r->c[i]) return DQO_ENOMEM;
+  }
+  if (inflateInit2(&r->zs, -15) != Z_OK) return DQO_ENOMEM;
+  r->zinit = 1;
+  return 0;
+}
+
+static void rdr_free(rdr* r) {
+  for (int i = 0; i < NCACHE; i++) free(r->c[i]);
+  if (r->zinit) inflateEnd(&r->zs);
+}
+
+/* htsjdk BlockCompressedInputStream.processNextBlock + BlockGunzipper.unzipBlock (htsjdk 2.16.0,
+ * not vendored; used through BamSource.java:158,174). Returns 0 or R_IOERR / R_FORMAT. */
+static int inflate_block(rdr* r, int64_t addr, blkbuf* b) {
+  const uint8_t* d = r->f->data;
+  const int64_t L = r->f->len;
+  b->addr = addr;
+  b->valid = 1;
+  if (addr >= L) { /* headerByteCount == 0: "no empty gzip block at end" -> empty block */
+    b->csize = 0;
+    b->len = 0;
+    return 0;
+  }
+  if (L - addr < 18) { set_err(r->f, "incorrect header size"); b->valid = 0; return R_IOERR; }
+  const uint8_t* h = d + addr;
+  int32_t blen = rd16(h + 16) + 1;
+  if (blen < 18 || blen > 65536) { set_err(r->f, "unexpected block length"); b->valid = 0; return R_IOERR; }
+  if (L - addr < blen) { set_err(r->f, "premature end of file"); b->valid = 0; return R_IOERR; }
+  if (h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || h[3] != 4 || rd16(h + 10) != 6) {
+    set_err(r->f, "Invalid GZIP header");
+    b->valid = 0;
+    return R_FORMAT;
+  }
+  int32_t defl = blen - 18 - 8;
+  uint32_t crc_exp = (uint32_t)rd32(h + 18 + defl);
+  int32_t isize = rd32(h + 18 + defl + 4);
+  if (isize < 0 || isize > MAX_USIZE) { set_err(r->f, "ISIZE out of range"); b->valid = 0; return R_FORMAT; }
+  inflateReset(&r->zs);
+  r->zs.next_in = (Bytef*)(h + 18);
+  r->zs.avail_in = (uInt)defl;
+  r->zs.next_out = b->data;
+  r->zs.avail_out = (uInt)isize;
+  int zr = Z_OK;
+  while (r->zs.avail_out > 0) {
+    zr = inflate(&r->zs, Z_SYNC_FLUSH);
+    if (zr != Z_OK) break;
+  }
+  if (zr == Z_DATA_ERROR || zr == Z_MEM_ERROR || zr == Z_NEED_DICT) {
+    set_err(r->f, "inflate data error");
+    b->valid = 0;
+    return R_FORMAT;
+  }
+  if ((int32_t)((uint8_t*)r->zs.next_out - b->data) != isize) {
+    set_err(r->f, "Did not inflate expected amount");
+    b->valid = 0;
+    return R_FORMAT;
+  }
+  if (r->f->verify_crc) {
+    uint32_t c = (uint32_t)crc32(0L, b->data, (uInt)isize);
+    if (c != crc_exp) { set_err(r->f, "CRC mismatch"); b->valid = 0; return R_FORMAT; }
+  }
+  b->csize = blen;
+  b->len = isize;
+  return 0;
+}
+
+static int rdr_load(rdr* r, int64_t addr, blkbuf** out) {
+  blkbuf* victim = NULL;
+  for (int i = 0; i < NCACHE; i++) {
+    if (r->c[i]->valid && r->c[i]->addr == addr) {
+      r->c[i]->stamp = ++r->clock;
+      *out = r->c[i];
+      return 0;
+    }
+  }
+  for (int i = 0; i < NCACHE; i++) {
+    if (r->c[i] == r->cur) continue;
+    if (!victim || !r->c[i]->valid || r->c[i]->stamp < victim->stamp) victim = r->c[i];
+  }
+  int e = inflate_block(r, addr, victim);
+  if (e) return e;
+  victim->stamp = ++r->clock;
+  *out = victim;
+  return 0;
+}
+
+/* Move to the following block, skipping empty mid-stream blocks (documented limitation). */
+static int rdr_next_block(rdr* r) {
+  for (;;) {
+    if (r->cur->csize == 0) return R_EOF; /* EOF pseudo-block */
+    blkbuf* nb;
+    int e = rdr_load(r, r->cur->addr + r->cur->csize, &nb);
+    if (e) return e;
+    r->cur = nb;
+    r->off = 0;
+    if (nb->len > 0 || nb->csize == 0) return nb->len > 0 ? 0 : R_EOF;
+  }
+}
+
+/* BlockCompressedInputStream.seek.  An offset beyond the block is "Invalid file pointer",
+ * which BamRecordGuesser.seek turns into EOFException (BamRecordGuesser.java:206-216). */
+static int rdr_seek(rdr* r, uint64_t v) {
+  blkbuf* b;
+  int e = rdr_load(r, (int64_t)(v >> 16), &b);
+  if (e) return e;
+  r->cur = b;
+  r->off = (int32_t)(v & 0xffff);
+  if (b->len == 0 && b->csize != 0) { /* empty mid-stream block: available() reads the next */
+    if (r->off != 0) return R_EOF;
+    e = rdr_next_block(r);
+    if (e && e != R_EOF) return e;
+    return 0;
+  }
+  if (r->off > b->len) return R_EOF;
+  return 0;
+}
+
+static int rdr_read(rdr* r, uint8_t* dst, int64_t n) {
+  while (n > 0) {
+    if (r->off >= r->cur->len) {
+      int e = rdr_next_block(r);
+      if (e) return e;
+    }
+    int64_t a = r->cur->len - r->off;
+    if (a > n) a = n;
+    if (dst) {
+      memcpy(dst, r->cur->data + r->off, (size_t)a);
+      dst += a;
+    }
+    r->off += (int32_t)a;
+    n -= a;
+  }
+  return 0;
+}
+
+/* BlockCompressedInputStream.getFilePointer (end-of-block normalisation). */
+static uint64_t rdr_ptr(const rdr* r) {
+  if (r->off > 0 && r->off == r->cur->len)
+    return (uint64_t)(r->cur->addr + r->cur->csize) << 16;
+  return ((uint64_t)r->cur->addr << 16) | (uint32_t)r->off;
+}
+
+/* ------------------------------------------------------------------ a10 header */
+/* BAMFileReader2.readHeader / readSequenceRecord: H/BAMFileReader2.java:747-821. */
+int dqo_read_header(dqo_file* f, int32_t* n_ref, uint64_t* first, int32_t* lens, int32_t cap) {
+  rdr r;
+  int e = rdr_init(&r, f);
+  if (e) { rdr_free(&r); return e; }
+  int rc = DQO_OK;
+  uint8_t b4[4];
+  char* text = NULL;
+  if (rdr_seek(&r, 0) || rdr_read(&r, b4, 4) || memcmp(b4, "BAM\1", 4) != 0) {
+    set_err(f, "Invalid BAM file header");
+    rc = DQO_EFORMAT;
+    goto out;
+  }
+  if (rdr_read(&r, b4, 4)) { rc = DQO_EFORMAT; goto out; }
+  int32_t l_text = rd32(b4);
+  if (l_text < 0) { rc = DQO_EFORMAT; goto out; }
+  if (rdr_read(&r, NULL, l_text)) { rc = DQO_EFORMAT; goto out; }
+  if (rdr_read(&r, b4, 4)) { rc = DQO_EFORMAT; goto out; }
+  int32_t nr = rd32(b4);
+  if (nr < 0) { rc = DQO_EFORMAT; goto out; }
+  if (f->ref_name) {
+    for (int i = 0; i < f->n_ref; i++) free(f->ref_name[i]);
+    free(f->ref_name);
+    free(f->ref_len);
+  }
+  f->n_ref = nr;
+  f->ref_len = (int32_t*)calloc((size_t)nr + 1, sizeof(int32_t));
+  f->ref_name = (char**)calloc((size_t)nr + 1, sizeof(char*));
+  for (int32_t i = 0; i < nr; i++) {
+    if (rdr_read(&r, b4, 4)) { rc = DQO_EFORMAT; goto out; }
+    int32_t ln = rd32(b4);
+    if (ln <= 1) { set_err(f, "missing sequence name"); rc = DQO_EFORMAT; goto out; }
+    f->ref_name[i] = (char*)calloc((size_t)ln, 1);
+    if (rdr_read(&r, (uint8_t*)f->ref_name[i], ln)) { rc = DQO_EFORMAT; goto out; }
+    f->ref_name[i][ln - 1] = 0;
+    if (rdr_read(&r, b4, 4)) { rc = DQO_EFORMAT; goto out; }
+    f->ref_len[i] = rd32(b4);
+  }
+  f->first_record = rdr_ptr(&r);
+  f->have_header = 1;
+  *n_ref = nr;
+  *first = f->first_record;
+  for (int32_t i = 0; i < nr && i < cap; i++) lens[i] = f->ref_len[i];
+out:
+  free(text);
+  rdr_free(&r);
+  return rc;
+}
+
+int32_t dqo_ref_index(dqo_file* f, const char* name) {
+  for (int32_t i = 0; i < f->n_ref; i++)
+    if (strcmp(f->ref_name[i], name) == 0) return i;
+  return -1;
+}
+
+/* ------------------------------------------------------------------ a5 record guesser */
+static int valid_name_char(uint8_t c) {
+  int8_t b = (int8_t)c; /* Java byte comparison: BamRecordGuesser.java:196-198 */
+  return ((int8_t)'!' <= b && b <= (int8_t)'?') || ((int8_t)'A' <= b && b <= (int8_t)'~');
+}
+
+/* checkRecordStartInternal: D/impl/formats/bam/BamRecordGuesser.java:79-194.
+ * Returns 1 (start, *next set), 0 (no start), or R_EOF / R_IOERR / R_FORMAT. */
+static int check_internal(rdr* r, uint64_t v, uint64_t* next) {
+  dqo_file* f = r->f;
+  uint8_t b[36];
+  uint8_t name[256];
+  int e = rdr_seek(r, v);
+  if (e) return e;
+  if ((e = rdr_read(r, b, 36))) return e; /* :98-99 */
+  int32_t remaining = rd32(b);
+  int32_t id = rd32(b + 4), pos = rd32(b + 8);
+  if (id < -1 || id >= f->n_ref || pos < -1) return 0;  /* :110 */
+  if (id >= 0 && pos > f->ref_len[id]) return 0;        /* :114 */
+  int32_t nid = rd32(b + 24), npos = rd32(b + 28);
+  if (nid < -1 || nid >= f->n_ref || npos < -1) return 0; /* :125 */
+  if (nid >= 0 && npos > f->ref_len[nid]) return 0;       /* :129 */
+  int32_t name_len = rd32(b + 12) & 0xff;
+  if (name_len < 2) return 0; /* :138 */
+  uint32_t flag_nc = (uint32_t)rd32(b + 16);
+  int32_t flags = (int32_t)(flag_nc >> 16);
+  int32_t n_cig = (int32_t)(flag_nc & 0xffff);
+  int32_t cig_len = jmul(n_cig, 4);
+  int32_t l_seq = rd32(b + 20);
+  int32_t seq_len = jadd(l_seq, jdiv2(jadd(l_seq, 1))); /* :146 */
+  if ((flags & 4) == 0 && (seq_len == 0 || n_cig == 0)) return 0;
+  if ((e = rdr_read(r, name, name_len))) return e; /* :153-155 */
+  if (name[name_len - 1] != 0) return 0;
+  for (int i = 0; i < name_len - 1; i++)
+    if (!valid_name_char(name[i])) return 0;
+  for (int i = 0; i < n_cig; i++) { /* :167-176 */
+    uint8_t c[4];
+    if ((e = rdr_read(r, c, 4))) return e;
+    int32_t op = rd32(c);
+    if (op == -1) return R_EOF;
+    if ((op & 0xf) > 8) return 0;
+  }
+  int32_t zero_min = jadd(jadd(jadd(32, name_len), cig_len), seq_len); /* :186 */
+  if (remaining >= zero_min) {
+    if ((e = rdr_seek(r, v))) return e; /* :189 */
+    int32_t skip = jadd(4, remaining); /* int arithmetic, widened to long by skipFully */
+    if (skip > 0 && (e = rdr_read(r, NULL, skip))) return e;
+    *next = rdr_ptr(r);
+    return 1;
+  }
+  return 0;
+}
+
+/* checkRecordStart: BamRecordGuesser.java:34-52 (READS_TO_CHECK = 10 at :16). */
+static int check_record_start(rdr* r, uint64_t v) {
+  for (int k = 0; k < 10; k++) {
+    uint64_t nv = 0;
+    int res = check_internal(r, v, &nv);
+    if (res == 1) { v = nv; continue; }
+    if (res == 0) return 0;
+    if (res == R_EOF) return k > 0;
+    if (res == R_IOERR) return 0;
+    return DQO_EFORMAT; /* runtime exception escapes Disq */
+  }
+  return 1;
+}
+
+int dqo_check_record_start(dqo_file* f, uint64_t v) {
+  if (!f->have_header) return DQO_EINVAL;
+  rdr r;
+  if (rdr_init(&r, f)) { rdr_free(&r); return DQO_ENOMEM; }
+  int res = check_record_start(&r, v);
+  rdr_free(&r);
+  return res;
+}
+
+/* ------------------------------------------------------------------ a4 first read */
+/* BamSource.getFirstReadInPartition: D/impl/formats/bam/BamSource.java:110-153,
+ * MAX_READ_SIZE = 10_000_000 at :44. */
+static int first_read(rdr* r, int64_t s, int64_t e, uint64_t* vs, uint64_t* ve) {
+  dqo_file* f = r->f;
+  int64_t index = 0;
+  int64_t start = s;
+  for (;;) { /* lazy BgzfBlockSource iterator, BgzfBlockSource.java:63-84 */
+    if (start > e) break;
+    int64_t bp;
+    int32_t bc, bu;
+    if (!dqo_guess_next_bgzf(f, start, e, &bp, &bc, &bu)) break;
+    start = bp + bc;
+    for (int32_t up = 0; up < bu; up++) {
+      index++;
+      if (index > 10000000) return 0;
+      if (up > 0xffff) return DQO_EFORMAT; /* makeFilePointer rejects offsets > 0xffff */
+      uint64_t v = ((uint64_t)bp << 16) | (uint32_t)up;
+      int res = check_record_start(r, v);
+      if (res < 0) return res;
+      if (res) {
+        *vs = v;
+        *ve = ((uint64_t)e << 16) | 0xffff;
+        return 1;
+      }
+    }
+  }
+  return 0;
+}
+
+int dqo_first_read_in_split(dqo_file* f, int64_t s, int64_t e, uint64_t* vs, uint64_t* ve) {
+  if (!f->have_header) return DQO_EINVAL;
+  rdr r;
+  if (rdr_init(&r, f)) { rdr_free(&r); return DQO_ENOMEM; }
+  int res = first_read(&r, s, e, vs, ve);
+  rdr_free(&r);
+  return res;
+}
+
+
+/* BamRecordGuesserChecker.check with granularity 1 (D/impl/formats/bam/BamRecordGuesserChecker.java:
+ * 96-124): run the guesser at every uncompressed position of every block of one split and
+ * return the positions where it fires. */
+int64_t dqo_scan_record_starts(dqo_file* f, int64_t s, int64_t e, uint64_t* out, int64_t cap) {
+  if (!f->have_header) return DQO_EINVAL;
+  rdr r;
+  if (rdr_init(&r, f)) { rdr_free(&r); return DQO_ENOMEM; }
+  int64_t n = 0;
+  int64_t start = s;
+  for (;;) {
+    if (start > e) break;
+    int64_t bp;
+    int32_t bc, bu;
+    if (!dqo_guess_next_bgzf(f, start, e, &bp, &bc, &bu)) break;
+    start = bp + bc;
+    for (int32_t up = 0; up < bu; up++) {
+      uint64_t v = ((uint64_t)bp << 16) | (uint32_t)up;
+      int res = check_record_start(&r, v);
+      if (res < 0) { n = res; goto out; }
+      if (res) {
+        if (out && n < cap) out[n] = v;
+        n++;
+      }
+    }
+  }
+out:
+  rdr_free(&r);
+  return n;
+}
+
+/* ------------------------------------------------------------------ a6-a8 decode */
+static int32_t cigar_ref_len(const uint8_t* cig, int n) {
+  int32_t len = 0;
+  for (int i = 0; i < n; i++) {
+    uint32_t op = (uint32_t)rd32(cig + 4 * i);
+    uint32_t o = op & 0xf;
+    if (o == 0 || o == 2 || o == 3 || o == 7 || o == 8) len += (int32_t)(op >> 4);
+  }
+  return len;
+}
+
+/* htsjdk BAMRecordCodec.decode field layout (SAMv1 §4.2); BAMRecord.getAlignmentEnd. */
+static void fill_rec(dqo_rec* o, uint64_t v, const uint8_t* rec, int32_t block_size) {
+  const uint8_t* p = rec + 4;
+  o->voffset = v;
+  o->lin = -1;
+  o->block_size = block_size;
+  o->ref_id = rd32(p + 0);
+  o->pos = rd32(p + 4);
+  uint32_t bmn = (uint32_t)rd32(p + 8);
+  o->l_read_name = (uint8_t)(bmn & 0xff);
+  o->mapq = (uint8_t)((bmn >> 8) & 0xff);
+  o->bin = (uint16_t)(bmn >> 16);
+  uint32_t fnc = (uint32_t)rd32(p + 12);
+  o->n_cigar = (uint16_t)(fnc & 0xffff);
+  o->flag = (uint16_t)(fnc >> 16);
+  o->l_seq = rd32(p + 16);
+  o->next_ref_id = rd32(p + 20);
+  o->next_pos = rd32(p + 24);
+  o->tlen = rd32(p + 28);
+  if (o->flag & 4) {
+    o->align_end = 0;
+  } else {
+    int64_t cig_off = 32 + (int64_t)o->l_read_name;
+    int32_t rl = 0;
+    if (cig_off + 4 * (int64_t)o->n_cigar <= block_size)
+      rl = cigar_ref_len(p + cig_off, o->n_cigar);
+    o->align_end = o->pos + 1 + rl - 1;
+  }
+  o->hash = dqo_record_hash(rec, 4 + (int64_t)block_size);
+}
+
+/* Read one record at the current position.  Returns 1 record, 0 end, <0 error. */
+static int read_record(rdr* r, uint8_t** buf, int64_t* bufcap, int32_t* bs_out) {
+  uint8_t b4[4];
+  int e = rdr_read(r, b4, 4);
+  if (e == R_EOF) return 0; /* BinaryCodec.readInt -> RuntimeEOFException -> decode() null */
+  if (e) return DQO_EFORMAT;
+  int32_t bs = rd32(b4);
+  if (bs < 32) { set_err(r->f, "Invalid record length"); return DQO_EFORMAT; }
+  if (*bufcap < 4 + (int64_t)bs) {
+    int64_t nc = 4 + (int64_t)bs + 1024;
+    uint8_t* nb = (uint8_t*)realloc(*buf, (size_t)nc);
+    if (!nb) return DQO_ENOMEM;
+    *buf = nb;
+    *bufcap = nc;
+  }
+  memcpy(*buf, b4, 4);
+  e = rdr_read(r, *buf + 4, bs);
+  if (e) { set_err(r->f, "truncated record"); return DQO_EFORMAT; }
+  *bs_out = bs;
+  return 1;
+}
+
+/* BAMFileIndexIterator.getNextRecord: H/BAMFileReader2.java:1082-1095 with one chunk. */
+int64_t dqo_read_chunk(dqo_file* f, uint64_t vs, uint64_t ve, dqo_rec* out, int64_t cap) {
+  rdr r;
+  if (rdr_init(&r, f)) { rdr_free(&r); return DQO_ENOMEM; }
+  uint8_t* buf = NULL;
+  int64_t bufcap = 0, n = 0;
+  int e = rdr_seek(&r, vs);
+  if (e == R_EOF) goto done;
+  if (e) { n = DQO_EFORMAT; goto done; }
+  for (;;) {
+    uint64_t v = rdr_ptr(&r);
+    if (v >= ve) break;
+    int32_t bs;
+    int res = read_record(&r, &buf, &bufcap, &bs);
+    if (res < 0) { n = res; break; }
+    if (res == 0) break;
+    if (out && n < cap) fill_rec(&out[n], v, buf, bs);
+    n++;
+  }
+done:
+  free(buf);
+  rdr_free(&r);
+  return n;
+}
+
+/* BAMFileIndexUnmappedIterator: H/BAMFileReader2.java:1199-1206 (skip until refID == -1, then
+ * everything to EOF), after queryUnmapped's seek (:715-738). */
+int64_t dqo_read_unmapped(dqo_file* f, uint64_t start, dqo_rec* out, int64_t cap) {
+  rdr r;
+  if (rdr_init(&r, f)) { rdr_free(&r); return DQO_ENOMEM; }
+  uint8_t* buf = NULL;
+  int64_t bufcap = 0, n = 0;
+  int skipping = 1;
+  int e = rdr_seek(&r, start);
+  if (e == R_EOF) goto done;
+  if (e) { n = DQO_EFORMAT; goto done; }
+  for (;;) {
+    uint64_t v = rdr_ptr(&r);
+    int32_t bs;
+    int res = read_record(&r, &buf, &bufcap, &bs);
+    if (res < 0) { n = res; break; }
+    if (res == 0) break;
+    if (skipping && rd32(buf + 4) != -1) continue;
+    skipping = 0;
+    if (out && n < cap) fill_rec(&out[n], v, buf, bs);
+    n++;
+  }
+done:
+  free(buf);
+  rdr_free(&r);
+  return n;
+}
+
+/* BAMSBIIndexer.createIndex walk (H/BAMSBIIndexer.java:45-66): every record from the first. */
+int64_t dqo_read_all(dqo_file* f, dqo_rec* out, int64_t cap) {
+  if (!f->have_header) return DQO_EINVAL;
+  return dqo_read_chunk(f, f->first_record, UINT64_MAX, out, cap);
+}
+
+/* ------------------------------------------------------------------ a9 intervals */
+/* AbstractBAMFileIndex.getStartOfLastLinearBin / getNoCoordinateCount (htsjdk 2.16.0), used at
+ * D/impl/formats/sam/AbstractBinarySamSource.java:92-94. */
+int dqo_bai_info(const uint8_t* b, int64_t len, int32_t* n_ref, int64_t* solb, int64_t* ncc) {
+  int64_t p = 0;
+#define NEED(n) do { if (p + (n) > len) return DQO_EFORMAT; } while (0)
+  NEED(8);
+  if (memcmp(b, "BAI\1", 4) != 0) return DQO_EFORMAT;
+  int32_t nr = rd32(b + 4);
+  p = 8;
+  int64_t last = -1;
+  for (int32_t i = 0; i < nr; i++) {
+    NEED(4);
+    int32_t nbin = rd32(b + p);
+    p += 4;
+    for (int32_t j = 0; j < nbin; j++) {
+      NEED(8);
+      int32_t nch = rd32(b + p + 4);
+      p += 8 + 16 * (int64_t)nch;
+    }
+    NEED(4);
+    int32_t nint = rd32(b + p);
+    p += 4;
+    if (nint > 0) {
+      NEED(8 * (int64_t)nint);
+      last = (int64_t)rd64(b + p + 8 * ((int64_t)nint - 1));
+      p += 8 * (int64_t)nint;
+    }
+  }
+  *n_ref = nr;
+  *solb = last;
+  *ncc = (p + 8 <= len) ? (int64_t)rd64(b + p) : -1; /* null for old indexes */
+#undef NEED
+  return 0;
+}
+
+/* QueryInterval compareTo / overlaps / abuts and optimizeIntervals (htsjdk 2.16.0), called from
+ * D/impl/formats/BoundedTraversalUtil.java:26.  end <= 0 means "to the end of the contig". */
+typedef struct { int32_t ref, start, end; } qiv;
+static int32_t qend(int32_t e) { return e <= 0 ? INT32_MAX : e; }
+static int qcmp(const void* a, const void* b) {
+  const qiv* x = (const qiv*)a;
+  const qiv* y = (const qiv*)b;
+  if (x->ref != y->ref) return x->ref < y->ref ? -1 : 1;
+  if (x->start != y->start) return x->start < y->start ? -1 : 1;
+  int32_t ex = qend(x->end), ey = qend(y->end);
+  if (ex != ey) return ex < ey ? -1 : 1;
+  return 0;
+}
+
+int64_t dqo_optimize_intervals(int32_t* ref, int32_t* start, int32_t* end, int64_t n) {
+  if (n <= 0) return 0;
+  qiv* v = (qiv*)malloc(sizeof(qiv) * (size_t)n);
+  for (int64_t i = 0; i < n; i++) { v[i].ref = ref[i]; v[i].start = start[i]; v[i].end = end[i]; }
+  qsort(v, (size_t)n, sizeof(qiv), qcmp);
+  int64_t m = 0;
+  qiv prev = v[0];
+  for (int64_t i = 1; i < n; i++) {
+    qiv nx = v[i];
+    int same = prev.ref == nx.ref;
+    int64_t pe = qend(prev.end), ne = qend(nx.end);
+    int ovl = same && prev.start <= ne && nx.start <= pe;
+    int abut = same && (pe + 1 == nx.start || ne + 1 == prev.start);
+    if (ovl || abut) {
+      if (ne > pe) prev.end = nx.end;
+    } else {
+      ref[m] = prev.ref; start[m] = prev.start; end[m] = prev.end; m++;
+      prev = nx;
+    }
+  }
+  ref[m] = prev.ref; start[m] = prev.start; end[m] = prev.end; m++;
+  free(v);
+  return m;
+}
+
+/* BAMQueryMultipleIntervalsIteratorFilter.compareIntervalToRecord with contained=false: a record
+ * matches iff some interval is neither BEFORE nor AFTER it.  The filter's running interval index
+ * only skips intervals that are BEFORE every later record of a coordinate-sorted file, so the
+ * stateless test below selects the same records. */
+int dqo_record_overlaps(const dqo_rec* r, const int32_t* ref, const int32_t* start,
+                        const int32_t* end, int64_t n) {
+  int32_t astart = r->pos + 1;
+  int32_t aend = ((r->flag & 4) && astart != 0) ? astart : r->align_end;
+  for (int64_t i = 0; i < n; i++) {
+    if (ref[i] != r->ref_id) continue;
+    int32_t ie = qend(end[i]);
+    if (ie < astart) continue;      /* BEFORE */
+    if (aend < start[i]) continue;  /* AFTER */
+    return 1;
+  }
+  return 0;
+}
+
+/* ------------------------------------------------------------------ whole-file inflate */
+int64_t dqo_inflate_file(dqo_file* f, uint8_t* out, int64_t cap) {
+  rdr r;
+  if (rdr_init(&r, f)) { rdr_free(&r); return DQO_ENOMEM; }
+  int64_t addr = 0, n = 0;
+  while (addr < f->len) {
+    blkbuf* b;
+    int e = rdr_load(&r, addr, &b);
+    if (e) { n = e == R_FORMAT ? DQO_EFORMAT : DQO_EIO; break; }
+    if (out) {
+      if (n + b->len > cap) { n = DQO_EINVAL; break; }
+      memcpy(out + n, b->data, (size_t)b->len);
+    }
+    n += b->len;
+    addr += b->csize;
+  }
+  rdr_free(&r);
+  return n;
+}
+
+/* ------------------------------------------------------------------ CPU baseline */
+typedef struct {
+  const uint8_t* data;
+  int64_t len;
+  const int64_t* starts;
+  const int64_t* ends;
+  int64_t n;
+  int64_t* counts;
+  uint64_t* digests;
+  int64_t* ubytes;
+  int64_t next;
+  pthread_mutex_t mu;
+  int err;
+} job_t;
+
+static void* worker(void* arg) {
+  job_t* j = (job_t*)arg;
+  dqo_file* f = dqo_open_mem(j->data, j->len, 0);
+  int32_t nr;
+  uint64_t first;
+  int32_t dummy;
+  if (dqo_read_header(f, &nr, &first, &dummy, 0) != 0) {
+    j->err = 1;
+    dqo_close(f);
+    return NULL;
+  }
+  rdr r;
+  rdr_init(&r, f);
+  uint8_t* buf = NULL;
+  int64_t bufcap = 0;
+  for (;;) {
+    pthread_mutex_lock(&j->mu);
+    int64_t i = j->next++;
+    pthread_mutex_unlock(&j->mu);
+    if (i >= j->n) break;
+    uint64_t vs, ve;
+    int64_t cnt = 0, ub = 0;
+    uint64_t dig = 0;
+    int res = first_read(&r, j->starts[i], j->ends[i], &vs, &ve);
+    if (res < 0) { j->err = 1; break; }
+    if (res == 1 && rdr_seek(&r, vs) == 0) {
+      for (;;) {
+        uint64_t v = rdr_ptr(&r);
+        if (v >= ve) break;
+        int32_t bs;
+        int rr = read_record(&r, &buf, &bufcap, &bs);
+        if (rr <= 0) { if (rr < 0) j->err = 1; break; }
+        uint64_t h = dqo_record_hash(buf, 4 + (int64_t)bs);
+        dig += mix64(h + ((uint64_t)cnt + 1) * 0x9E3779B97F4A7C15ULL);
+        cnt++;
+        ub += 4 + (int64_t)bs;
+      }
+    }
+    j->counts[i] = cnt;
+    j->digests[i] = dig;
+    if (j->ubytes) j->ubytes[i] = ub;
+  }
+  free(buf);
+  rdr_free(&r);
+  dqo_close(f);
+  return NULL;
+}
+
+int dqo_run_partitions(const uint8_t* data, int64_t len, const int64_t* starts,
+                       const int64_t* ends, int64_t n, int nthreads, int64_t* counts,
+                       uint64_t* digests, int64_t* ubytes) {
+  if (nthreads < 1) nthreads = 1;
+  job_t j;
+  memset(&j, 0, sizeof j);
+  j.data = data; j.len = len; j.starts = starts; j.ends = ends; j.n = n;
+  j.counts = counts; j.digests = digests; j.ubytes = ubytes;
+  pthread_mutex_init(&j.mu, NULL);
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
+  for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, worker, &j);
+  for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+  free(th);
+  pthread_mutex_destroy(&j.mu);
+  return j.err ? DQO_EFORMAT : 0;
+}

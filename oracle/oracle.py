@@ -1,0 +1,343 @@
+"""ctypes wrapper for the CPU restatement of Disq's BAM read path.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg as the checker.  The product (disq_amd/, libdisq_gpu.so) never imports it.
+
+Every function mirrors a reference method; see oracle/disq_oracle.c for file:line citations.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libdisq_oracle.so")
+
+REC_DTYPE = np.dtype(
+    [
+        ("voffset", "<u8"),
+        ("lin", "<i8"),
+        ("block_size", "<i4"),
+        ("ref_id", "<i4"),
+        ("pos", "<i4"),
+        ("l_seq", "<i4"),
+        ("next_ref_id", "<i4"),
+        ("next_pos", "<i4"),
+        ("tlen", "<i4"),
+        ("align_end", "<i4"),
+        ("flag", "<u2"),
+        ("bin", "<u2"),
+        ("n_cigar", "<u2"),
+        ("mapq", "u1"),
+        ("l_read_name", "u1"),
+        ("hash", "<u8"),
+    ],
+    align=True,
+)
+
+HADOOP_LOCAL_BLOCK_SIZE = 32 * 1024 * 1024  # fs.local.block.size default (Hadoop 2.7)
+
+
+def build() -> str:
+    if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(
+        os.path.join(_HERE, "disq_oracle.c")
+    ):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = C.CDLL(build())
+        L = _lib
+        P = C.POINTER
+        L.dqo_open_mem.restype = C.c_void_p
+        L.dqo_open_mem.argtypes = [C.c_void_p, C.c_int64, C.c_int]
+        L.dqo_close.argtypes = [C.c_void_p]
+        L.dqo_last_error.restype = C.c_char_p
+        L.dqo_last_error.argtypes = [C.c_void_p]
+        L.dqo_path_splits.restype = C.c_int64
+        L.dqo_path_splits.argtypes = [C.c_int64, C.c_int32, C.c_int, C.c_int64,
+                                      P(C.c_int64), P(C.c_int64), C.c_int64]
+        L.dqo_guess_next_bgzf.argtypes = [C.c_void_p, C.c_int64, C.c_int64, P(C.c_int64),
+                                          P(C.c_int32), P(C.c_int32)]
+        L.dqo_split_blocks.restype = C.c_int64
+        L.dqo_split_blocks.argtypes = [C.c_void_p, C.c_int64, C.c_int64, P(C.c_int64),
+                                       P(C.c_int32), P(C.c_int32), C.c_int64]
+        L.dqo_read_header.argtypes = [C.c_void_p, P(C.c_int32), P(C.c_uint64), P(C.c_int32),
+                                      C.c_int32]
+        L.dqo_ref_index.restype = C.c_int32
+        L.dqo_ref_index.argtypes = [C.c_void_p, C.c_char_p]
+        L.dqo_check_record_start.argtypes = [C.c_void_p, C.c_uint64]
+        L.dqo_scan_record_starts.restype = C.c_int64
+        L.dqo_scan_record_starts.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p,
+                                             C.c_int64]
+        L.dqo_first_read_in_split.argtypes = [C.c_void_p, C.c_int64, C.c_int64, P(C.c_uint64),
+                                              P(C.c_uint64)]
+        for fn in (L.dqo_read_chunk,):
+            fn.restype = C.c_int64
+            fn.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int64]
+        L.dqo_read_unmapped.restype = C.c_int64
+        L.dqo_read_unmapped.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_int64]
+        L.dqo_read_all.restype = C.c_int64
+        L.dqo_read_all.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        L.dqo_bai_info.argtypes = [C.c_void_p, C.c_int64, P(C.c_int32), P(C.c_int64),
+                                   P(C.c_int64)]
+        L.dqo_optimize_intervals.restype = C.c_int64
+        L.dqo_optimize_intervals.argtypes = [P(C.c_int32)] * 3 + [C.c_int64]
+        L.dqo_record_overlaps.argtypes = [C.c_void_p] + [P(C.c_int32)] * 3 + [C.c_int64]
+        L.dqo_record_hash.restype = C.c_uint64
+        L.dqo_record_hash.argtypes = [C.c_void_p, C.c_int64]
+        L.dqo_stream_digest.restype = C.c_uint64
+        L.dqo_stream_digest.argtypes = [C.c_void_p, C.c_int64, C.c_uint64]
+        L.dqo_inflate_file.restype = C.c_int64
+        L.dqo_inflate_file.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        L.dqo_run_partitions.argtypes = [C.c_void_p, C.c_int64, P(C.c_int64), P(C.c_int64),
+                                         C.c_int64, C.c_int, P(C.c_int64), P(C.c_uint64),
+                                         P(C.c_int64)]
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+class OracleError(RuntimeError):
+    pass
+
+
+def path_splits(file_len, split_size, nio=False, local_block_size=HADOOP_LOCAL_BLOCK_SIZE):
+    """PathSplitSource.getPathSplits for one file -> list of (start, end)."""
+    L = lib()
+    n = L.dqo_path_splits(file_len, split_size, int(nio), local_block_size, None, None, 0)
+    if n < 0:
+        raise OracleError("invalid split size")
+    s = np.zeros(max(n, 1), np.int64)
+    e = np.zeros(max(n, 1), np.int64)
+    L.dqo_path_splits(file_len, split_size, int(nio), local_block_size, _p(s, C.c_int64),
+                      _p(e, C.c_int64), n)
+    return list(zip(s[:n].tolist(), e[:n].tolist()))
+
+
+class OracleBam:
+    """A BAM held in memory, read with Disq + htsjdk semantics."""
+
+    def __init__(self, data: bytes, verify_crc: bool = False):
+        self._buf = np.frombuffer(data, np.uint8).copy()
+        self.len = len(self._buf)
+        self._h = lib().dqo_open_mem(self._buf.ctypes.data, self.len, int(verify_crc))
+        self._header = None
+
+    @classmethod
+    def from_path(cls, path, verify_crc=False):
+        with open(path, "rb") as fh:
+            return cls(fh.read(), verify_crc)
+
+    def close(self):
+        if self._h:
+            lib().dqo_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _err(self, rc):
+        return OracleError(f"oracle error {rc}: {lib().dqo_last_error(self._h).decode()}")
+
+    # a2/a3
+    def guess_next_bgzf(self, p, end):
+        pos, cs, us = C.c_int64(), C.c_int32(), C.c_int32()
+        if lib().dqo_guess_next_bgzf(self._h, p, end, C.byref(pos), C.byref(cs), C.byref(us)):
+            return (pos.value, cs.value, us.value)
+        return None
+
+    def split_blocks(self, start, end):
+        cap = max(16, (end - start) // 16 + 16)
+        pos = np.zeros(cap, np.int64)
+        cs = np.zeros(cap, np.int32)
+        us = np.zeros(cap, np.int32)
+        n = lib().dqo_split_blocks(self._h, start, end, _p(pos, C.c_int64), _p(cs, C.c_int32),
+                                   _p(us, C.c_int32), cap)
+        assert n <= cap
+        return list(zip(pos[:n].tolist(), cs[:n].tolist(), us[:n].tolist()))
+
+    # a10
+    def header(self):
+        if self._header is None:
+            nr, first = C.c_int32(), C.c_uint64()
+            lens = np.zeros(1 << 16, np.int32)
+            rc = lib().dqo_read_header(self._h, C.byref(nr), C.byref(first), _p(lens, C.c_int32),
+                                       len(lens))
+            if rc != 0:
+                raise self._err(rc)
+            self._header = {"n_ref": nr.value, "first_record": first.value,
+                            "ref_lengths": lens[: nr.value].copy()}
+        return self._header
+
+    def ref_index(self, name):
+        self.header()
+        return lib().dqo_ref_index(self._h, name.encode())
+
+    # a5
+    def check_record_start(self, vpos):
+        self.header()
+        rc = lib().dqo_check_record_start(self._h, vpos)
+        if rc < 0:
+            raise self._err(rc)
+        return bool(rc)
+
+    def scan_record_starts(self, start, end):
+        """BamRecordGuesserChecker, granularity 1: guesser hits over one split's blocks."""
+        self.header()
+        cap = 1 << 20
+        out = np.zeros(cap, np.uint64)
+        n = lib().dqo_scan_record_starts(self._h, start, end, out.ctypes.data, cap)
+        if n < 0:
+            raise self._err(n)
+        return out[:n].copy()
+
+    # a4
+    def first_read_in_split(self, start, end):
+        self.header()
+        vs, ve = C.c_uint64(), C.c_uint64()
+        rc = lib().dqo_first_read_in_split(self._h, start, end, C.byref(vs), C.byref(ve))
+        if rc < 0:
+            raise self._err(rc)
+        return (vs.value, ve.value) if rc == 1 else None
+
+    def _recs(self, fn, *args):
+        self.header()
+        n = fn(self._h, *args, None, 0)
+        if n < 0:
+            raise self._err(n)
+        out = np.zeros(n, REC_DTYPE)
+        m = fn(self._h, *args, out.ctypes.data, n)
+        assert m == n
+        return out
+
+    # a6-a8
+    def read_chunk(self, vstart, vend):
+        return self._recs(lib().dqo_read_chunk, vstart, vend)
+
+    def read_unmapped(self, start):
+        return self._recs(lib().dqo_read_unmapped, start)
+
+    def read_all(self):
+        return self._recs(lib().dqo_read_all)
+
+    def inflate_all(self):
+        n = lib().dqo_inflate_file(self._h, None, 0)
+        if n < 0:
+            raise self._err(n)
+        out = np.zeros(n, np.uint8)
+        lib().dqo_inflate_file(self._h, out.ctypes.data, n)
+        return out
+
+    # L2/L3: AbstractBinarySamSource.getReads over BamSource.getPathChunks
+    def plan(self, split_size=0, nio=False, local_block_size=HADOOP_LOCAL_BLOCK_SIZE):
+        """getPathChunks: one (split_start, split_end, vstart, vend) or None per split."""
+        out = []
+        for s, e in path_splits(self.len, split_size, nio, local_block_size):
+            out.append((s, e, self.first_read_in_split(s, e)))
+        return out
+
+    def read_partitions(self, split_size=0, nio=False, local_block_size=HADOOP_LOCAL_BLOCK_SIZE,
+                        traversal=None, bai=None):
+        """Records per partition, as Disq's RDD would hold them.
+
+        traversal: None, or (intervals, traverse_unplaced_unmapped) where intervals is None or
+        a list of (ref_index, start, end) (1-based closed, already converted from contig names).
+        """
+        if traversal is not None:
+            ivs, unplaced = traversal
+            if ivs is None and not unplaced:
+                raise ValueError("Traversing mapped reads only is not supported.")
+        parts = []
+        plan = self.plan(split_size, nio, local_block_size)
+        if traversal is not None:
+            if bai is None:
+                raise ValueError("Intervals set but no index file found")
+            solb, ncc = bai_info(bai)
+            q = optimize_intervals(ivs) if ivs else []
+        for s, e, ch in plan:
+            if ch is None:
+                continue  # empty partition (no chunk)
+            recs = self.read_chunk(*ch)
+            if traversal is None:
+                parts.append(recs)
+                continue
+            if ivs:
+                keep = np.array([overlaps(r, q) for r in recs], bool)
+                sel = recs[keep] if len(recs) else recs
+            else:
+                sel = recs[:0]
+            if unplaced and solb != -1 and ncc >= 1 and ch[0] <= solb < ch[1]:
+                sel = np.concatenate([sel, self.read_unmapped(solb)])
+            parts.append(sel)
+        return parts
+
+
+def bai_info(bai_bytes):
+    b = np.frombuffer(bai_bytes, np.uint8)
+    nr, solb, ncc = C.c_int32(), C.c_int64(), C.c_int64()
+    rc = lib().dqo_bai_info(b.ctypes.data, len(b), C.byref(nr), C.byref(solb), C.byref(ncc))
+    if rc != 0:
+        raise OracleError("bad .bai")
+    return solb.value, ncc.value
+
+
+def optimize_intervals(ivs):
+    n = len(ivs)
+    if n == 0:
+        return []
+    r = np.array([i[0] for i in ivs], np.int32)
+    s = np.array([i[1] for i in ivs], np.int32)
+    e = np.array([i[2] for i in ivs], np.int32)
+    m = lib().dqo_optimize_intervals(_p(r, C.c_int32), _p(s, C.c_int32), _p(e, C.c_int32), n)
+    return list(zip(r[:m].tolist(), s[:m].tolist(), e[:m].tolist()))
+
+
+def overlaps(rec, q):
+    r = np.array([i[0] for i in q], np.int32)
+    s = np.array([i[1] for i in q], np.int32)
+    e = np.array([i[2] for i in q], np.int32)
+    one = np.array([rec], REC_DTYPE)
+    return bool(lib().dqo_record_overlaps(one.ctypes.data, _p(r, C.c_int32), _p(s, C.c_int32),
+                                          _p(e, C.c_int32), len(q)))
+
+
+def record_hash(b: bytes) -> int:
+    a = np.frombuffer(b, np.uint8)
+    return int(lib().dqo_record_hash(a.ctypes.data, len(a)))
+
+
+def stream_digest(hashes, start_index=0) -> int:
+    h = np.ascontiguousarray(hashes, np.uint64)
+    return int(lib().dqo_stream_digest(h.ctypes.data, len(h), start_index))
+
+
+def run_partitions(data: bytes, splits, nthreads):
+    """CPU baseline: per-partition (count, digest, bytes) on nthreads threads."""
+    buf = np.frombuffer(data, np.uint8)
+    n = len(splits)
+    s = np.array([a for a, _ in splits], np.int64)
+    e = np.array([b for _, b in splits], np.int64)
+    cnt = np.zeros(n, np.int64)
+    dig = np.zeros(n, np.uint64)
+    ub = np.zeros(n, np.int64)
+    rc = lib().dqo_run_partitions(buf.ctypes.data, len(buf), _p(s, C.c_int64), _p(e, C.c_int64),
+                                  n, nthreads, _p(cnt, C.c_int64), _p(dig, C.c_uint64),
+                                  _p(ub, C.c_int64))
+    if rc != 0:
+        raise OracleError("run_partitions failed")
+    return cnt, dig, ub
