@@ -1,0 +1,258 @@
+"""ctypes binding of libdisq_gpu.so (include/disq_gpu.h).
+
+This is the same C ABI a JNI / Panama shim binds.  The library is required:
+there is no CPU fallback, so a missing or unloadable library raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import threading
+
+import numpy as np
+
+from . import _build
+
+DQ_OK, DQ_EIO, DQ_EFORMAT, DQ_EINVAL, DQ_EDEVICE, DQ_ENOMEM = 0, -1, -2, -3, -4, -5
+
+
+class DqOpts(C.Structure):
+    _fields_ = [("device", C.c_int32), ("split_size", C.c_int32), ("use_nio", C.c_int32),
+                ("verify_crc", C.c_int32), ("stringency", C.c_int32), ("reserved", C.c_int32),
+                ("hadoop_block_size", C.c_int64)]
+
+
+class DqChunk(C.Structure):
+    _fields_ = [("split_start", C.c_int64), ("split_end", C.c_int64), ("vstart", C.c_uint64),
+                ("vend", C.c_uint64), ("has_chunk", C.c_int32), ("reserved", C.c_int32)]
+
+
+class DqBatch(C.Structure):
+    _fields_ = [("n_records", C.c_int64),
+                ("voffset", C.POINTER(C.c_uint64)),
+                ("block_size", C.POINTER(C.c_int32)),
+                ("ref_id", C.POINTER(C.c_int32)),
+                ("pos", C.POINTER(C.c_int32)),
+                ("l_seq", C.POINTER(C.c_int32)),
+                ("next_ref_id", C.POINTER(C.c_int32)),
+                ("next_pos", C.POINTER(C.c_int32)),
+                ("tlen", C.POINTER(C.c_int32)),
+                ("flag", C.POINTER(C.c_uint16)),
+                ("bin", C.POINTER(C.c_uint16)),
+                ("n_cigar", C.POINTER(C.c_uint16)),
+                ("mapq", C.POINTER(C.c_uint8)),
+                ("l_read_name", C.POINTER(C.c_uint8)),
+                ("hash", C.POINTER(C.c_uint64)),
+                ("raw_offset", C.POINTER(C.c_int64)),
+                ("raw", C.POINTER(C.c_uint8)),
+                ("raw_len", C.c_int64),
+                ("n_partitions", C.c_int64),
+                ("part_offset", C.POINTER(C.c_int64)),
+                ("part_digest", C.POINTER(C.c_uint64))]
+
+
+class DqTraversal(C.Structure):
+    _fields_ = [("ref", C.POINTER(C.c_int32)), ("start", C.POINTER(C.c_int32)),
+                ("end", C.POINTER(C.c_int32)), ("n", C.c_int64), ("has_intervals", C.c_int32),
+                ("traverse_unplaced_unmapped", C.c_int32)]
+
+
+class DqHeaderInfo(C.Structure):
+    _fields_ = [("n_ref", C.c_int32), ("reserved", C.c_int32),
+                ("first_record_voffset", C.c_uint64), ("header_bytes", C.c_int64)]
+
+
+class DqStats(C.Structure):
+    _fields_ = [("compressed_bytes", C.c_int64), ("decompressed_bytes", C.c_int64),
+                ("n_blocks", C.c_int64), ("n_records", C.c_int64), ("n_partitions", C.c_int64),
+                ("ms_total", C.c_double), ("ms_scan", C.c_double), ("ms_inflate", C.c_double),
+                ("ms_records", C.c_double), ("ms_filter", C.c_double), ("ms_plan", C.c_double),
+                ("digest", C.c_uint64)]
+
+
+# Every symbol include/disq_gpu.h declares.
+EXPORTS = ("dq_ctx_create", "dq_ctx_destroy", "dq_last_error", "dq_version", "dq_open_memory",
+           "dq_open_path", "dq_set_index", "dq_read_header", "dq_plan", "dq_decode",
+           "dq_decode_filtered", "dq_read", "dq_run_resident", "dq_debug_inflated",
+           "dq_batch_free", "dq_free")
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib():
+    """Load libdisq_gpu.so (raises if it is not built)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        L = C.CDLL(_build.gpu_lib_path())
+        P = C.POINTER
+        vp = C.c_void_p
+        L.dq_ctx_create.argtypes = [P(vp), P(DqOpts)]
+        L.dq_ctx_destroy.argtypes = [vp]
+        L.dq_last_error.restype = C.c_char_p
+        L.dq_last_error.argtypes = [vp]
+        L.dq_version.restype = C.c_char_p
+        L.dq_open_memory.argtypes = [vp, vp, C.c_int64]
+        L.dq_open_path.argtypes = [vp, C.c_char_p]
+        L.dq_set_index.argtypes = [vp, vp, C.c_int64]
+        L.dq_read_header.argtypes = [vp, P(DqHeaderInfo), vp, C.c_int64]
+        L.dq_plan.argtypes = [vp, P(P(DqChunk)), P(C.c_int64)]
+        L.dq_decode.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_int32, P(P(DqBatch))]
+        L.dq_decode_filtered.argtypes = [vp, C.c_uint64, C.c_uint64, P(DqTraversal), C.c_int32,
+                                         P(P(DqBatch))]
+        L.dq_read.argtypes = [vp, P(DqTraversal), C.c_int32, P(P(DqBatch))]
+        L.dq_run_resident.argtypes = [vp, P(DqTraversal), P(DqStats)]
+        L.dq_debug_inflated.argtypes = [vp, vp, C.c_int64, P(C.c_int64)]
+        L.dq_batch_free.argtypes = [P(DqBatch)]
+        L.dq_free.argtypes = [vp]
+        _lib = L
+        return L
+
+
+class DqError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+def check(ctx, rc):
+    if rc != DQ_OK:
+        raise DqError(rc, lib().dq_last_error(ctx).decode(errors="replace") if ctx else "")
+    return rc
+
+
+FIELDS = (("voffset", np.uint64), ("block_size", np.int32), ("ref_id", np.int32),
+          ("pos", np.int32), ("l_seq", np.int32), ("next_ref_id", np.int32),
+          ("next_pos", np.int32), ("tlen", np.int32), ("flag", np.uint16), ("bin", np.uint16),
+          ("n_cigar", np.uint16), ("mapq", np.uint8), ("l_read_name", np.uint8),
+          ("hash", np.uint64), ("raw_offset", np.int64))
+
+
+def batch_to_numpy(bp):
+    """Copy a dq_batch into numpy arrays and free it."""
+    b = bp.contents
+    n = b.n_records
+    out = {}
+    for name, dt in FIELDS:
+        ptr = getattr(b, name)
+        out[name] = np.ctypeslib.as_array(ptr, shape=(n,)).astype(dt, copy=True) if n else \
+            np.zeros(0, dt)
+    out["raw"] = (np.ctypeslib.as_array(b.raw, shape=(b.raw_len,)).copy()
+                  if (b.raw and b.raw_len) else None)
+    npart = b.n_partitions
+    out["part_offset"] = np.ctypeslib.as_array(b.part_offset, shape=(npart + 1,)).copy()
+    out["part_digest"] = (np.ctypeslib.as_array(b.part_digest, shape=(npart,)).copy()
+                          if npart else np.zeros(0, np.uint64))
+    lib().dq_batch_free(bp)
+    return out
+
+
+class Context:
+    """One dq_ctx (own HIP stream) with a resident BAM."""
+
+    def __init__(self, split_size=0, use_nio=False, verify_crc=False, device=0,
+                 hadoop_block_size=0, stringency=0):
+        self._h = C.c_void_p()
+        o = DqOpts(device, split_size, int(use_nio), int(verify_crc), stringency, 0,
+                   hadoop_block_size)
+        rc = lib().dq_ctx_create(C.byref(self._h), C.byref(o))
+        if rc != DQ_OK:
+            msg = lib().dq_last_error(self._h).decode() if self._h else ""
+            if self._h:
+                lib().dq_ctx_destroy(self._h)
+            self._h = None
+            raise DqError(rc, msg)
+        self._keep = None
+
+    def close(self):
+        if self._h:
+            lib().dq_ctx_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def open_bytes(self, data):
+        buf = np.frombuffer(data, np.uint8)
+        check(self._h, lib().dq_open_memory(self._h, buf.ctypes.data, len(buf)))
+
+    def open_path(self, path):
+        check(self._h, lib().dq_open_path(self._h, path.encode()))
+
+    def set_index(self, bai_bytes):
+        if bai_bytes is None:
+            check(self._h, lib().dq_set_index(self._h, None, 0))
+            return
+        self._bai = np.frombuffer(bai_bytes, np.uint8).copy()
+        check(self._h, lib().dq_set_index(self._h, self._bai.ctypes.data, len(self._bai)))
+
+    def header(self):
+        info = DqHeaderInfo()
+        check(self._h, lib().dq_read_header(self._h, C.byref(info), None, 0))
+        buf = np.zeros(max(1, info.header_bytes), np.uint8)
+        check(self._h, lib().dq_read_header(self._h, C.byref(info), buf.ctypes.data, len(buf)))
+        return info, bytes(buf[: info.header_bytes])
+
+    def plan(self):
+        p = C.POINTER(DqChunk)()
+        n = C.c_int64()
+        check(self._h, lib().dq_plan(self._h, C.byref(p), C.byref(n)))
+        out = [(p[i].split_start, p[i].split_end,
+                (p[i].vstart, p[i].vend) if p[i].has_chunk else None) for i in range(n.value)]
+        lib().dq_free(C.cast(p, C.c_void_p))
+        return out
+
+    @staticmethod
+    def _traversal(tr):
+        if tr is None:
+            return None, None
+        ivs, unplaced = tr
+        if ivs is None:
+            t = DqTraversal(None, None, None, 0, 0, int(unplaced))
+            return t, None
+        r = np.array([i[0] for i in ivs], np.int32)
+        s = np.array([i[1] for i in ivs], np.int32)
+        e = np.array([i[2] for i in ivs], np.int32)
+        P = C.POINTER(C.c_int32)
+        t = DqTraversal(r.ctypes.data_as(P), s.ctypes.data_as(P), e.ctypes.data_as(P), len(ivs),
+                        1, int(unplaced))
+        return t, (r, s, e)
+
+    def decode(self, vstart, vend, with_raw=True, traversal=None):
+        bp = C.POINTER(DqBatch)()
+        if traversal is None:
+            check(self._h, lib().dq_decode(self._h, vstart, vend, int(with_raw), C.byref(bp)))
+        else:
+            t, keep = self._traversal(traversal)
+            check(self._h, lib().dq_decode_filtered(self._h, vstart, vend, C.byref(t),
+                                                    int(with_raw), C.byref(bp)))
+        return batch_to_numpy(bp)
+
+    def read(self, with_raw=True, traversal=None):
+        bp = C.POINTER(DqBatch)()
+        t, keep = self._traversal(traversal)
+        check(self._h, lib().dq_read(self._h, C.byref(t) if t is not None else None,
+                                     int(with_raw), C.byref(bp)))
+        return batch_to_numpy(bp)
+
+    def run_resident(self):
+        st = DqStats()
+        check(self._h, lib().dq_run_resident(self._h, None, C.byref(st)))
+        return st
+
+    def inflated(self):
+        n = C.c_int64()
+        check(self._h, lib().dq_debug_inflated(self._h, None, 0, C.byref(n)))
+        out = np.zeros(max(1, n.value), np.uint8)
+        check(self._h, lib().dq_debug_inflated(self._h, out.ctypes.data, n.value, C.byref(n)))
+        return out[: n.value]

@@ -1,0 +1,955 @@
+// dq_api.hip -- C ABI (include/disq_gpu.h) and host orchestration of the device pipeline.
+//
+// Host side of the drop-in boundary: the split arithmetic of PathSplitSource.getPathSplits
+// (D/impl/file/PathSplitSource.java:26-64), header parsing (H/BAMFileReader2.java:747-821), the
+// .bai facts read by AbstractBinarySamSource (AbstractBinarySamSource.java:92-94), interval
+// preparation (BoundedTraversalUtil.java:10-27) and the per-chunk record selection of
+// BamSource.getIterator / createIndexIterator.  All byte/bit work runs in the HIP kernels of
+// dq_kernels.hip and dq_inflate.hip; there is no CPU fallback.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/disq_gpu.h"
+#include "dq_internal.h"
+
+using namespace dq;
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  template <typename T>
+  T* as() const {
+    return reinterpret_cast<T*>(p);
+  }
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = bytes + bytes / 8 + 256;
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+};
+
+struct Interval {
+  int32_t ref, start, end;
+};
+
+}  // namespace
+
+struct dq_ctx {
+  dq_opts o{};
+  hipStream_t s = nullptr;
+  hipEvent_t ev[8] = {};
+  std::string err;
+  // resident file
+  int64_t flen = 0;
+  DevBuf C;
+  bool have_file = false;
+  // kernel 1
+  DevBuf slots, counts, offs, cand, flags, voff, scal, tmp;
+  int64_t ncand = 0;
+  // chain + inflate
+  DevBuf blk_pos, blk_cs, blk_us, uoff, status, U;
+  int64_t nblk = 0, ulen = 0;
+  // header
+  int32_t n_ref = 0;
+  std::vector<int32_t> ref_len;
+  std::vector<std::string> ref_name;
+  uint64_t first_record = 0;
+  int64_t header_bytes = 0;
+  DevBuf d_ref_len;
+  // planning
+  DevBuf plans;
+  std::vector<SplitPlan> plans_h;
+  // records
+  DevBuf segs, segcnt, segbase, rec_lin;
+  DevBuf f_voff, f_bs, f_ref, f_pos, f_lseq, f_nref, f_npos, f_tlen, f_flag, f_bin, f_ncig, f_mapq,
+      f_lrn, f_hash;
+  int64_t nrec = 0;
+  DevBuf parts;
+  std::vector<PartRange> parts_h;
+  bool have_pipeline = false;
+  // host copies for slicing (lazily downloaded)
+  std::vector<uint64_t> voff_h;
+  std::vector<int64_t> lin_h;
+  // index
+  bool have_bai = false;
+  int64_t solb = -1, ncc = -1;
+  // filter scratch
+  DevBuf iv_ref, iv_start, iv_end, iv_begin, idx, keep;
+  dq_stats stats{};
+
+  RecSoA soa() {
+    return RecSoA{f_voff.as<uint64_t>(), f_bs.as<int32_t>(),  f_ref.as<int32_t>(),
+                  f_pos.as<int32_t>(),   f_lseq.as<int32_t>(), f_nref.as<int32_t>(),
+                  f_npos.as<int32_t>(),  f_tlen.as<int32_t>(), f_flag.as<uint16_t>(),
+                  f_bin.as<uint16_t>(),  f_ncig.as<uint16_t>(), f_mapq.as<uint8_t>(),
+                  f_lrn.as<uint8_t>(),   f_hash.as<uint64_t>()};
+  }
+};
+
+#define HIPCHK(x)                                                                     \
+  do {                                                                                \
+    hipError_t e_ = (x);                                                              \
+    if (e_ != hipSuccess) {                                                           \
+      ctx->err = std::string(#x) + ": " + hipGetErrorString(e_);                     \
+      return DQ_EDEVICE;                                                              \
+    }                                                                                 \
+  } while (0)
+#define RET(code, msg)   \
+  do {                   \
+    ctx->err = (msg);    \
+    return (code);       \
+  } while (0)
+
+namespace {
+
+inline int32_t rd32(const uint8_t* p) {
+  return (int32_t)((uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) |
+                   ((uint32_t)p[3] << 24));
+}
+inline uint64_t rd64(const uint8_t* p) {
+  uint64_t v = 0;
+  for (int i = 7; i >= 0; i--) v = (v << 8) | p[i];
+  return v;
+}
+
+// PathSplitSource.getPathSplits (D/impl/file/PathSplitSource.java:26-64) for one file:
+// NIO ceil(len/splitSize) splits (:32-42) or Hadoop 2.7 FileInputFormat.getSplits (:44-62).
+int path_splits(const dq_opts& o, int64_t len, std::vector<std::pair<int64_t, int64_t>>& out) {
+  out.clear();
+  if (o.use_nio) {
+    if (o.split_size <= 0) return DQ_EINVAL;
+    int64_t ss = o.split_size;
+    int64_t ns = (len + ss - 1) / ss;
+    for (int64_t i = 0; i < ns; i++) out.push_back({i * ss, std::min(len, i * ss + ss)});
+    return 0;
+  }
+  int64_t block = o.hadoop_block_size > 0 ? o.hadoop_block_size : 32ll * 1024 * 1024;
+  int64_t maxs = o.split_size > 0 ? o.split_size : INT64_MAX;
+  int64_t ss = std::max<int64_t>(1, std::min(maxs, block));
+  if (len == 0) {
+    out.push_back({0, 0});
+    return 0;
+  }
+  int64_t rem = len;
+  while ((double)rem / (double)ss > 1.1) {
+    out.push_back({len - rem, len - rem + ss});
+    rem -= ss;
+  }
+  if (rem != 0) out.push_back({len - rem, len});
+  return 0;
+}
+
+int get_i64(dq_ctx* ctx, const void* dptr, int64_t* v) {
+  HIPCHK(hipMemcpyAsync(v, dptr, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->s));
+  HIPCHK(hipStreamSynchronize(ctx->s));
+  return 0;
+}
+
+int ensure_all(dq_ctx* ctx, DevBuf& b, size_t bytes) {
+  HIPCHK(b.ensure(bytes));
+  return 0;
+}
+
+const char* status_name(int32_t st) {
+  switch (st) {
+    case ST_BAD_HEADER: return "invalid BGZF/GZIP block header";
+    case ST_BAD_BLOCKTYPE: return "invalid deflate block type";
+    case ST_BAD_STORED: return "invalid stored block lengths";
+    case ST_BAD_TABLE: return "invalid Huffman code lengths";
+    case ST_BAD_CODE: return "invalid literal/length/distance code";
+    case ST_BAD_DIST: return "invalid distance too far back";
+    case ST_SHORT: return "Did not inflate expected amount";
+    case ST_OVERREAD: return "deflate data overrun";
+    case ST_CRC: return "CRC mismatch";
+    case ST_ISIZE: return "ISIZE out of range";
+    default: return "format error";
+  }
+}
+
+// Parse the BAM header from the front of U (BAMFileReader2.readHeader, H/BAMFileReader2.java:
+// 747-801; readSequenceRecord :807-821).
+int parse_header(dq_ctx* ctx) {
+  int64_t want = std::min<int64_t>(ctx->ulen, 1 << 20);
+  std::vector<uint8_t> h;
+  for (;;) {
+    h.resize((size_t)want);
+    HIPCHK(hipMemcpy(h.data(), ctx->U.p, (size_t)want, hipMemcpyDeviceToHost));
+    int64_t p = 0;
+    auto need = [&](int64_t n) { return p + n <= want; };
+    bool more = false;
+    if (!need(8)) {
+      more = true;
+    } else {
+      if (memcmp(h.data(), "BAM\1", 4) != 0) RET(DQ_EFORMAT, "Invalid BAM file header");
+      int32_t l_text = rd32(&h[4]);
+      if (l_text < 0) RET(DQ_EFORMAT, "Invalid BAM header text length");
+      p = 8 + (int64_t)l_text;
+      if (!need(4)) {
+        more = true;
+      } else {
+        int32_t nr = rd32(&h[(size_t)p]);
+        p += 4;
+        if (nr < 0) RET(DQ_EFORMAT, "Invalid reference count");
+        std::vector<int32_t> lens;
+        std::vector<std::string> names;
+        for (int32_t i = 0; i < nr && !more; i++) {
+          if (!need(4)) { more = true; break; }
+          int32_t ln = rd32(&h[(size_t)p]);
+          if (ln <= 1) RET(DQ_EFORMAT, "Invalid BAM file header: missing sequence name");
+          if (!need(4 + (int64_t)ln + 4)) { more = true; break; }
+          names.emplace_back((const char*)&h[(size_t)p + 4], (size_t)ln - 1);
+          lens.push_back(rd32(&h[(size_t)(p + 4 + ln)]));
+          p += 8 + ln;
+        }
+        if (!more) {
+          ctx->n_ref = nr;
+          ctx->ref_len = lens;
+          ctx->ref_name = names;
+          ctx->header_bytes = p;
+          return 0;
+        }
+      }
+    }
+    if (!more || want >= ctx->ulen) RET(DQ_EFORMAT, "truncated BAM header");
+    want = std::min<int64_t>(ctx->ulen, want * 4);
+  }
+}
+
+// htsjdk AbstractBAMFileIndex.getStartOfLastLinearBin / getNoCoordinateCount (2.16.0; read at
+// D/impl/formats/sam/AbstractBinarySamSource.java:93-94).
+int parse_bai(const uint8_t* b, int64_t len, int64_t* solb, int64_t* ncc) {
+  int64_t p = 8;
+  if (len < 8 || memcmp(b, "BAI\1", 4) != 0) return DQ_EFORMAT;
+  int32_t nr = rd32(b + 4);
+  int64_t last = -1;
+  for (int32_t i = 0; i < nr; i++) {
+    if (p + 4 > len) return DQ_EFORMAT;
+    int32_t nbin = rd32(b + p);
+    p += 4;
+    for (int32_t j = 0; j < nbin; j++) {
+      if (p + 8 > len) return DQ_EFORMAT;
+      int32_t nch = rd32(b + p + 4);
+      p += 8 + 16 * (int64_t)nch;
+    }
+    if (p + 4 > len) return DQ_EFORMAT;
+    int32_t nint = rd32(b + p);
+    p += 4;
+    if (nint > 0) {
+      if (p + 8 * (int64_t)nint > len) return DQ_EFORMAT;
+      last = (int64_t)rd64(b + p + 8 * ((int64_t)nint - 1));
+      p += 8 * (int64_t)nint;
+    }
+  }
+  *solb = last;
+  *ncc = p + 8 <= len ? (int64_t)rd64(b + p) : -1;
+  return 0;
+}
+
+// QueryInterval.optimizeIntervals (htsjdk 2.16.0, BoundedTraversalUtil.java:26): sort, then
+// merge overlapping or abutting intervals; end <= 0 means the end of the reference.
+std::vector<Interval> optimize(std::vector<Interval> v) {
+  auto E = [](int32_t e) -> int64_t { return e <= 0 ? INT32_MAX : e; };
+  std::sort(v.begin(), v.end(), [&](const Interval& a, const Interval& b) {
+    if (a.ref != b.ref) return a.ref < b.ref;
+    if (a.start != b.start) return a.start < b.start;
+    return E(a.end) < E(b.end);
+  });
+  std::vector<Interval> out;
+  if (v.empty()) return out;
+  Interval prev = v[0];
+  for (size_t i = 1; i < v.size(); i++) {
+    const Interval nx = v[i];
+    bool same = prev.ref == nx.ref;
+    int64_t pe = E(prev.end), ne = E(nx.end);
+    bool ovl = same && prev.start <= ne && nx.start <= pe;
+    bool abut = same && (pe + 1 == nx.start || ne + 1 == prev.start);
+    if (ovl || abut) {
+      if (ne > pe) prev.end = nx.end;
+    } else {
+      out.push_back(prev);
+      prev = nx;
+    }
+  }
+  out.push_back(prev);
+  return out;
+}
+
+// DQ_DEBUG=1: synchronise and report after every pipeline stage.
+bool dbg_on() {
+  static int v = -1;
+  if (v < 0) v = getenv("DQ_DEBUG") ? 1 : 0;
+  return v == 1;
+}
+void dbg(hipStream_t s, const char* what, long long a = 0, long long b = 0) {
+  if (!dbg_on()) return;
+  hipError_t e = hipStreamSynchronize(s);
+  fprintf(stderr, "[dq] %s %lld %lld (%s)\n", what, a, b, hipGetErrorString(e));
+  fflush(stderr);
+}
+
+float ev_ms(hipEvent_t a, hipEvent_t b) {
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, a, b);
+  return ms;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ pipeline
+static int run_pipeline(dq_ctx* ctx) {
+  if (!ctx->have_file) RET(DQ_EINVAL, "no file open");
+  if (ctx->have_pipeline) return 0;
+  hipStream_t s = ctx->s;
+  const int64_t L = ctx->flen;
+  int rc;
+  HIPCHK(hipEventRecord(ctx->ev[0], s));
+  // ---- Kernel 1: candidate scan
+  const int64_t nch = std::max<int64_t>(1, (L + SCAN_CHUNK - 1) / SCAN_CHUNK);
+  if ((rc = ensure_all(ctx, ctx->slots, sizeof(Cand) * (size_t)nch * SCAN_CAP))) return rc;
+  if ((rc = ensure_all(ctx, ctx->counts, sizeof(int32_t) * (size_t)nch))) return rc;
+  if ((rc = ensure_all(ctx, ctx->offs, sizeof(int64_t) * (size_t)(nch + 1)))) return rc;
+  if ((rc = ensure_all(ctx, ctx->tmp, sizeof(int64_t) * (size_t)(4 * (nch / 1024 + 1) + 4096 +
+                                                                 4 * (L / 65536 / 1024 + 1)))))
+    return rc;
+  if ((rc = ensure_all(ctx, ctx->scal, 4096))) return rc;
+  int32_t* d_overflow = ctx->scal.as<int32_t>();
+  int32_t* d_broken = d_overflow + 1;
+  int32_t* d_stat = d_overflow + 2;
+  int64_t* d_nblk = reinterpret_cast<int64_t*>(ctx->scal.as<char>() + 64);
+  HIPCHK(hipMemsetAsync(ctx->scal.p, 0, 4096, s));
+  launch_bgzf_scan(ctx->C.as<uint8_t>(), L, L, ctx->slots.as<Cand>(), 0, ctx->counts.as<int32_t>(),
+                   nch, nullptr, d_overflow, s);
+  launch_exclusive_scan_i32(ctx->counts.as<int32_t>(), ctx->offs.as<int64_t>(), nch,
+                            ctx->tmp.as<int64_t>(), s);
+  dbg(s, "scan", nch);
+  int64_t ncand = 0;
+  if ((rc = get_i64(ctx, ctx->offs.as<int64_t>() + nch, &ncand))) return rc;
+  int32_t overflow = 0;
+  HIPCHK(hipMemcpy(&overflow, d_overflow, 4, hipMemcpyDeviceToHost));
+  if (overflow) RET(DQ_EFORMAT, "more than 32 BGZF headers in a 16 KiB window is not supported");
+  ctx->ncand = ncand;
+  const int64_t capc = std::max<int64_t>(1, ncand);
+  if ((rc = ensure_all(ctx, ctx->cand, sizeof(Cand) * (size_t)capc))) return rc;
+  if ((rc = ensure_all(ctx, ctx->flags, sizeof(int32_t) * (size_t)capc))) return rc;
+  if ((rc = ensure_all(ctx, ctx->voff, sizeof(int64_t) * (size_t)(capc + 1)))) return rc;
+  launch_gather_slots(ctx->slots.as<Cand>(), ctx->counts.as<int32_t>(), ctx->offs.as<int64_t>(), nch,
+                      ctx->cand.as<Cand>(), capc, s);
+  // ncand on device for the kernels that need it
+  int64_t* d_ncand = d_nblk + 1;
+  HIPCHK(hipMemcpyAsync(d_ncand, &ncand, sizeof(int64_t), hipMemcpyHostToDevice, s));
+  launch_valid_flags(ctx->cand.as<Cand>(), d_ncand, capc, ctx->flags.as<int32_t>(), s);
+  launch_exclusive_scan_i32(ctx->flags.as<int32_t>(), ctx->voff.as<int64_t>(), ncand,
+                            ctx->tmp.as<int64_t>(), s);
+  const int64_t capb = std::max<int64_t>(1, ncand);
+  if ((rc = ensure_all(ctx, ctx->blk_pos, sizeof(int64_t) * (size_t)capb))) return rc;
+  if ((rc = ensure_all(ctx, ctx->blk_cs, sizeof(int32_t) * (size_t)capb))) return rc;
+  if ((rc = ensure_all(ctx, ctx->blk_us, sizeof(int32_t) * (size_t)capb))) return rc;
+  if (ncand > 0)
+    launch_chain2(ctx->C.as<uint8_t>(), L, ctx->cand.as<Cand>(), d_ncand, ncand,
+                  ctx->voff.as<int64_t>(), ctx->blk_pos.as<int64_t>(), ctx->blk_cs.as<int32_t>(),
+                  ctx->blk_us.as<int32_t>(), capb, d_nblk, d_broken, 1, s);
+  int64_t nblk = 0;
+  if ((rc = get_i64(ctx, d_nblk, &nblk))) return rc;
+  int32_t broken = 0;
+  HIPCHK(hipMemcpy(&broken, d_broken, 4, hipMemcpyDeviceToHost));
+  // The chain must start at the file start (htsjdk reads from block 0).
+  if (!broken && ncand > 0) {
+    int64_t p0 = 0;
+    HIPCHK(hipMemcpy(&p0, ctx->blk_pos.p, sizeof(int64_t), hipMemcpyDeviceToHost));
+    if (p0 != 0) broken = 1;
+  }
+  if (broken) {  // walk htsjdk headers from 0 (false-positive or non-BC headers present)
+    int64_t capw = L / 26 + 2;
+    if ((rc = ensure_all(ctx, ctx->blk_pos, sizeof(int64_t) * (size_t)capw))) return rc;
+    if ((rc = ensure_all(ctx, ctx->blk_cs, sizeof(int32_t) * (size_t)capw))) return rc;
+    if ((rc = ensure_all(ctx, ctx->blk_us, sizeof(int32_t) * (size_t)capw))) return rc;
+    launch_chain_serial(ctx->C.as<uint8_t>(), L, 0, ctx->blk_pos.as<int64_t>(),
+                        ctx->blk_cs.as<int32_t>(), ctx->blk_us.as<int32_t>(), capw, d_nblk, d_stat, s);
+    if ((rc = get_i64(ctx, d_nblk, &nblk))) return rc;
+  }
+  dbg(s, "chain", nblk, broken);
+  ctx->nblk = nblk;
+  if (nblk == 0 && L > 0) RET(DQ_EFORMAT, "no BGZF blocks found");
+  if ((rc = ensure_all(ctx, ctx->uoff, sizeof(int64_t) * (size_t)(nblk + 1)))) return rc;
+  launch_exclusive_scan_i32(ctx->blk_us.as<int32_t>(), ctx->uoff.as<int64_t>(), nblk,
+                            ctx->tmp.as<int64_t>(), s);
+  int64_t ulen = 0;
+  if ((rc = get_i64(ctx, ctx->uoff.as<int64_t>() + nblk, &ulen))) return rc;
+  ctx->ulen = ulen;
+  HIPCHK(hipEventRecord(ctx->ev[1], s));
+  // ---- Kernel 2: inflate
+  if ((rc = ensure_all(ctx, ctx->U, (size_t)ulen + 256))) return rc;
+  if ((rc = ensure_all(ctx, ctx->status, sizeof(int32_t) * (size_t)(nblk + 1)))) return rc;
+  HIPCHK(hipMemsetAsync(ctx->status.p, 0, sizeof(int32_t) * (size_t)(nblk + 1), s));
+  HIPCHK(hipMemsetAsync(ctx->U.as<uint8_t>() + ulen, 0, 256, s));
+  launch_inflate(ctx->C.as<uint8_t>(), ctx->blk_pos.as<int64_t>(), ctx->blk_cs.as<int32_t>(),
+                 ctx->blk_us.as<int32_t>(), ctx->uoff.as<int64_t>(), nblk, ctx->U.as<uint8_t>(),
+                 ctx->status.as<int32_t>(), s);
+  if (ctx->o.verify_crc)
+    launch_crc_check(ctx->C.as<uint8_t>(), ctx->blk_pos.as<int64_t>(), ctx->blk_cs.as<int32_t>(),
+                     ctx->blk_us.as<int32_t>(), ctx->uoff.as<int64_t>(), nblk,
+                     ctx->U.as<uint8_t>(), ctx->status.as<int32_t>(), s);
+  dbg(s, "inflate", nblk, ulen);
+  HIPCHK(hipEventRecord(ctx->ev[2], s));
+  {
+    std::vector<int32_t> st((size_t)nblk);
+    if (nblk) HIPCHK(hipMemcpyAsync(st.data(), ctx->status.p, sizeof(int32_t) * (size_t)nblk,
+                                    hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (int64_t b = 0; b < nblk; b++)
+      if (st[(size_t)b] != ST_OK) {
+        int64_t pos = 0;
+        HIPCHK(hipMemcpy(&pos, ctx->blk_pos.as<int64_t>() + b, 8, hipMemcpyDeviceToHost));
+        char msg[256];
+        snprintf(msg, sizeof msg, "%s in BGZF block at %lld", status_name(st[(size_t)b]),
+                 (long long)pos);
+        RET(DQ_EFORMAT, msg);
+      }
+  }
+  // ---- header (n_ref, reference lengths for the guesser)
+  if ((rc = parse_header(ctx))) return rc;
+  if ((rc = ensure_all(ctx, ctx->d_ref_len, sizeof(int32_t) * (size_t)(ctx->n_ref + 1)))) return rc;
+  if (ctx->n_ref)
+    HIPCHK(hipMemcpyAsync(ctx->d_ref_len.p, ctx->ref_len.data(), sizeof(int32_t) * ctx->n_ref,
+                          hipMemcpyHostToDevice, s));
+  // ---- planning (a1-a5)
+  std::vector<std::pair<int64_t, int64_t>> splits;
+  if (path_splits(ctx->o, L, splits)) RET(DQ_EINVAL, "splitSize must be > 0 with useNio");
+  const int64_t nsplit = (int64_t)splits.size();
+  ctx->plans_h.assign((size_t)nsplit, SplitPlan{});
+  for (int64_t i = 0; i < nsplit; i++) {
+    ctx->plans_h[(size_t)i].split_start = splits[(size_t)i].first;
+    ctx->plans_h[(size_t)i].split_end = splits[(size_t)i].second;
+  }
+  if ((rc = ensure_all(ctx, ctx->plans, sizeof(SplitPlan) * (size_t)(nsplit + 1)))) return rc;
+  HIPCHK(hipMemcpyAsync(ctx->plans.p, ctx->plans_h.data(), sizeof(SplitPlan) * (size_t)nsplit,
+                        hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(d_nblk, &ctx->nblk, sizeof(int64_t), hipMemcpyHostToDevice, s));
+  launch_plan_blocks(ctx->cand.as<Cand>(), d_ncand, ctx->blk_pos.as<int64_t>(),
+                     ctx->blk_us.as<int32_t>(), ctx->uoff.as<int64_t>(), d_nblk,
+                     ctx->plans.as<SplitPlan>(), nsplit, s);
+  launch_first_record(ctx->U.as<uint8_t>(), ulen, 1, ctx->d_ref_len.as<int32_t>(), ctx->n_ref,
+                      ctx->blk_pos.as<int64_t>(), ctx->uoff.as<int64_t>(), d_nblk,
+                      ctx->plans.as<SplitPlan>(), nsplit, s);
+  HIPCHK(hipMemcpyAsync(ctx->plans_h.data(), ctx->plans.p, sizeof(SplitPlan) * (size_t)nsplit,
+                        hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(hipEventRecord(ctx->ev[3], s));
+  dbg(s, "plan", nsplit);
+  int64_t start_lin = -1;
+  for (auto& P : ctx->plans_h) {
+    if (P.status != 0) {
+      char msg[160];
+      snprintf(msg, sizeof msg, "split planning failed (code %d) for split [%lld, %lld)", P.status,
+               (long long)P.split_start, (long long)P.split_end);
+      RET(DQ_EFORMAT, msg);
+    }
+    if (P.rec_lin >= 0 && start_lin < 0) start_lin = P.rec_lin;
+  }
+  // ---- Kernel 3: record chain, SoA decode, hashes
+  int64_t nrec = 0;
+  const int64_t SEG = 256 * 1024;
+  if (start_lin >= 0) {
+    const int64_t nseg = (ulen - start_lin + SEG - 1) / SEG;
+    if ((rc = ensure_all(ctx, ctx->segs, sizeof(Seg) * (size_t)(nseg + 1)))) return rc;
+    if ((rc = ensure_all(ctx, ctx->segcnt, sizeof(int64_t) * (size_t)(nseg + 1)))) return rc;
+    if ((rc = ensure_all(ctx, ctx->segbase, sizeof(int64_t) * (size_t)(nseg + 1)))) return rc;
+    HIPCHK(hipMemsetAsync(d_broken, 0, 8, s));
+    launch_seg_spec(ctx->U.as<uint8_t>(), ulen, 1, ctx->d_ref_len.as<int32_t>(), ctx->n_ref,
+                    ctx->segs.as<Seg>(), nseg, SEG, start_lin, s);
+    launch_seg_link(ctx->segs.as<Seg>(), nseg, SEG, start_lin, ulen, d_broken, s);
+    int32_t br = 0;
+    HIPCHK(hipMemcpyAsync(&br, d_broken, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (br) {
+      launch_seg_fix2(ctx->U.as<uint8_t>(), ulen, 1, ctx->segs.as<Seg>(), nseg, SEG, start_lin,
+                      d_stat, s);
+      int32_t st = 0;
+      HIPCHK(hipMemcpyAsync(&st, d_stat, 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      if (st) RET(DQ_EFORMAT, st == ST_BAD_CODE ? "Invalid record length" : "truncated record chain");
+    }
+    dbg(s, "segs", nseg, br);
+    launch_seg_counts(ctx->segs.as<Seg>(), nseg, ctx->segcnt.as<int64_t>(), s);
+    launch_exclusive_scan_i64(ctx->segcnt.as<int64_t>(), ctx->segbase.as<int64_t>(), nseg,
+                              ctx->tmp.as<int64_t>(), s);
+    if ((rc = get_i64(ctx, ctx->segbase.as<int64_t>() + nseg, &nrec))) return rc;
+    const size_t nr = (size_t)std::max<int64_t>(1, nrec);
+    if ((rc = ensure_all(ctx, ctx->rec_lin, 8 * nr))) return rc;
+    launch_seg_emit2(ctx->U.as<uint8_t>(), ctx->segs.as<Seg>(), ctx->segbase.as<int64_t>(), nseg,
+                     ctx->rec_lin.as<int64_t>(), s);
+    DevBuf* b8[] = {&ctx->f_voff, &ctx->f_hash};
+    DevBuf* b4[] = {&ctx->f_bs, &ctx->f_ref, &ctx->f_pos, &ctx->f_lseq, &ctx->f_nref, &ctx->f_npos,
+                    &ctx->f_tlen};
+    DevBuf* b2[] = {&ctx->f_flag, &ctx->f_bin, &ctx->f_ncig};
+    DevBuf* b1[] = {&ctx->f_mapq, &ctx->f_lrn};
+    for (auto* b : b8) if ((rc = ensure_all(ctx, *b, 8 * nr))) return rc;
+    for (auto* b : b4) if ((rc = ensure_all(ctx, *b, 4 * nr))) return rc;
+    for (auto* b : b2) if ((rc = ensure_all(ctx, *b, 2 * nr))) return rc;
+    for (auto* b : b1) if ((rc = ensure_all(ctx, *b, nr))) return rc;
+    HIPCHK(hipMemsetAsync(d_stat, 0, 4, s));
+    launch_decode_records(ctx->U.as<uint8_t>(), ulen, ctx->rec_lin.as<int64_t>(), nrec,
+                          ctx->blk_pos.as<int64_t>(), ctx->blk_cs.as<int32_t>(),
+                          ctx->uoff.as<int64_t>(), nblk, ctx->soa(), d_stat, s);
+  }
+  dbg(s, "decode", nrec);
+  ctx->nrec = nrec;
+  // ---- partitions
+  if ((rc = ensure_all(ctx, ctx->parts, sizeof(PartRange) * (size_t)(nsplit + 1)))) return rc;
+  launch_partition_ranges(ctx->plans.as<SplitPlan>(), nsplit, ctx->rec_lin.as<int64_t>(),
+                          ctx->f_voff.as<uint64_t>(), nrec, ctx->parts.as<PartRange>(), d_stat, s);
+  launch_partition_digest2(ctx->f_hash.as<uint64_t>(), ctx->parts.as<PartRange>(), nsplit, s);
+  HIPCHK(hipEventRecord(ctx->ev[4], s));
+  ctx->parts_h.assign((size_t)nsplit, PartRange{});
+  HIPCHK(hipMemcpyAsync(ctx->parts_h.data(), ctx->parts.p, sizeof(PartRange) * (size_t)nsplit,
+                        hipMemcpyDeviceToHost, s));
+  int32_t st = 0;
+  HIPCHK(hipMemcpyAsync(&st, d_stat, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (st == 101) RET(DQ_EFORMAT, "record guesser start is not on the record chain");
+  if (st) RET(DQ_EFORMAT, "truncated BAM record");
+  // stats
+  dq_stats& S = ctx->stats;
+  S = dq_stats{};
+  S.compressed_bytes = L;
+  S.decompressed_bytes = ulen;
+  S.n_blocks = nblk;
+  S.n_partitions = nsplit;
+  int64_t emitted = 0;
+  uint64_t dg = 0;
+  for (int64_t i = 0; i < nsplit; i++) {
+    const PartRange& r = ctx->parts_h[(size_t)i];
+    emitted += r.end - r.begin;
+    dg += dq_mix64(r.digest ^ ((uint64_t)(i + 1) * DQ_K_WORD));
+  }
+  S.n_records = emitted;
+  S.digest = dg;
+  S.ms_scan = ev_ms(ctx->ev[0], ctx->ev[1]);
+  S.ms_inflate = ev_ms(ctx->ev[1], ctx->ev[2]);
+  S.ms_plan = ev_ms(ctx->ev[2], ctx->ev[3]);
+  S.ms_records = ev_ms(ctx->ev[3], ctx->ev[4]);
+  S.ms_total = ev_ms(ctx->ev[0], ctx->ev[4]);
+  ctx->have_pipeline = true;
+  ctx->voff_h.clear();
+  ctx->lin_h.clear();
+  return 0;
+}
+
+// ------------------------------------------------------------------ record export
+static int fetch_index(dq_ctx* ctx) {
+  if ((int64_t)ctx->voff_h.size() == ctx->nrec) return 0;
+  ctx->voff_h.resize((size_t)ctx->nrec);
+  ctx->lin_h.resize((size_t)ctx->nrec);
+  if (ctx->nrec) {
+    HIPCHK(hipMemcpy(ctx->voff_h.data(), ctx->f_voff.p, 8 * (size_t)ctx->nrec, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(ctx->lin_h.data(), ctx->rec_lin.p, 8 * (size_t)ctx->nrec, hipMemcpyDeviceToHost));
+  }
+  return 0;
+}
+
+// Build a batch from a list of record-index ranges (in order; ranges may repeat records).
+static int make_batch(dq_ctx* ctx, const std::vector<std::pair<int64_t, int64_t>>& ranges,
+                      const std::vector<int64_t>* explicit_idx, int32_t with_raw,
+                      const std::vector<int64_t>& part_bounds, dq_batch** out) {
+  std::vector<int64_t> idx;
+  if (explicit_idx) {
+    idx = *explicit_idx;
+  } else {
+    for (auto& r : ranges)
+      for (int64_t k = r.first; k < r.second; k++) idx.push_back(k);
+  }
+  const int64_t n = (int64_t)idx.size();
+  dq_batch* b = (dq_batch*)calloc(1, sizeof(dq_batch));
+  if (!b) RET(DQ_ENOMEM, "out of host memory");
+  b->n_records = n;
+  const size_t m = (size_t)std::max<int64_t>(1, n);
+  b->voffset = (uint64_t*)malloc(8 * m);
+  b->block_size = (int32_t*)malloc(4 * m);
+  b->ref_id = (int32_t*)malloc(4 * m);
+  b->pos = (int32_t*)malloc(4 * m);
+  b->l_seq = (int32_t*)malloc(4 * m);
+  b->next_ref_id = (int32_t*)malloc(4 * m);
+  b->next_pos = (int32_t*)malloc(4 * m);
+  b->tlen = (int32_t*)malloc(4 * m);
+  b->flag = (uint16_t*)malloc(2 * m);
+  b->bin = (uint16_t*)malloc(2 * m);
+  b->n_cigar = (uint16_t*)malloc(2 * m);
+  b->mapq = (uint8_t*)malloc(m);
+  b->l_read_name = (uint8_t*)malloc(m);
+  b->hash = (uint64_t*)malloc(8 * m);
+  b->raw_offset = (int64_t*)malloc(8 * m);
+  // The whole-chain SoA is downloaded field by field once, then gathered on the host.
+  auto pull = [&](const DevBuf& d, size_t esz, void* dst) -> int {
+    if (n == 0) return 0;
+    std::vector<uint8_t> all((size_t)ctx->nrec * esz);
+    HIPCHK(hipMemcpy(all.data(), d.p, all.size(), hipMemcpyDeviceToHost));
+    uint8_t* o = (uint8_t*)dst;
+    for (int64_t i = 0; i < n; i++) memcpy(o + (size_t)i * esz, &all[(size_t)idx[(size_t)i] * esz], esz);
+    return 0;
+  };
+  int rc = 0;
+  if ((rc = pull(ctx->f_voff, 8, b->voffset)) || (rc = pull(ctx->f_bs, 4, b->block_size)) ||
+      (rc = pull(ctx->f_ref, 4, b->ref_id)) || (rc = pull(ctx->f_pos, 4, b->pos)) ||
+      (rc = pull(ctx->f_lseq, 4, b->l_seq)) || (rc = pull(ctx->f_nref, 4, b->next_ref_id)) ||
+      (rc = pull(ctx->f_npos, 4, b->next_pos)) || (rc = pull(ctx->f_tlen, 4, b->tlen)) ||
+      (rc = pull(ctx->f_flag, 2, b->flag)) || (rc = pull(ctx->f_bin, 2, b->bin)) ||
+      (rc = pull(ctx->f_ncig, 2, b->n_cigar)) || (rc = pull(ctx->f_mapq, 1, b->mapq)) ||
+      (rc = pull(ctx->f_lrn, 1, b->l_read_name)) || (rc = pull(ctx->f_hash, 8, b->hash))) {
+    dq_batch_free(b);
+    return rc;
+  }
+  int64_t raw_len = 0;
+  for (int64_t i = 0; i < n; i++) {
+    b->raw_offset[i] = raw_len;
+    raw_len += 4 + (int64_t)b->block_size[i];
+  }
+  b->raw_len = raw_len;
+  if (with_raw && n > 0) {
+    if ((rc = fetch_index(ctx))) {
+      dq_batch_free(b);
+      return rc;
+    }
+    b->raw = (uint8_t*)malloc((size_t)std::max<int64_t>(1, raw_len));
+    // copy contiguous runs of records in one transfer each
+    int64_t i = 0;
+    while (i < n) {
+      int64_t j = i + 1;
+      while (j < n && idx[(size_t)j] == idx[(size_t)j - 1] + 1) j++;
+      int64_t lo = ctx->lin_h[(size_t)idx[(size_t)i]];
+      int64_t hi = ctx->lin_h[(size_t)idx[(size_t)j - 1]] + 4 + b->block_size[j - 1];
+      hipError_t e = hipMemcpy(b->raw + b->raw_offset[i], ctx->U.as<uint8_t>() + lo,
+                               (size_t)(hi - lo), hipMemcpyDeviceToHost);
+      if (e != hipSuccess) {
+        dq_batch_free(b);
+        ctx->err = hipGetErrorString(e);
+        return DQ_EDEVICE;
+      }
+      i = j;
+    }
+  }
+  b->n_partitions = (int64_t)part_bounds.size() - 1;
+  if (b->n_partitions < 0) b->n_partitions = 0;
+  b->part_offset = (int64_t*)malloc(sizeof(int64_t) * (size_t)(b->n_partitions + 1));
+  b->part_digest = (uint64_t*)calloc((size_t)b->n_partitions + 1, sizeof(uint64_t));
+  for (int64_t p = 0; p <= b->n_partitions; p++) b->part_offset[p] = part_bounds[(size_t)p];
+  for (int64_t p = 0; p < b->n_partitions; p++) {
+    uint64_t d = 0;
+    for (int64_t k = b->part_offset[p]; k < b->part_offset[p + 1]; k++)
+      d += dq_mix64(b->hash[k] + (uint64_t)(k - b->part_offset[p] + 1) * DQ_K_LEN);
+    b->part_digest[p] = d;
+  }
+  *out = b;
+  return 0;
+}
+
+// Records of one chunk: from the record at vstart while the start pointer < vend.
+static int chunk_range(dq_ctx* ctx, uint64_t vstart, uint64_t vend, int64_t* b, int64_t* e) {
+  int rc;
+  if ((rc = fetch_index(ctx))) return rc;
+  auto& v = ctx->voff_h;
+  auto it = std::lower_bound(v.begin(), v.end(), vstart);
+  if (it == v.end() || *it != vstart) {
+    // a start pointer past the last record reads nothing (EOF)
+    if (it == v.end()) {
+      *b = *e = ctx->nrec;
+      return 0;
+    }
+    RET(DQ_EFORMAT, "chunk start is not a record start");
+  }
+  *b = it - v.begin();
+  *e = std::lower_bound(v.begin(), v.end(), vend) - v.begin();
+  if (*e < *b) *e = *b;
+  return 0;
+}
+
+// createIndexIterator (contained=false) over [b, e) + the unplaced-unmapped tail
+// (AbstractBinarySamSource.java:86-134).
+static int filtered_indices(dq_ctx* ctx, uint64_t vstart, uint64_t vend, int64_t b, int64_t e,
+                            const dq_traversal* tr, std::vector<int64_t>& out) {
+  int rc;
+  out.clear();
+  if (!ctx->have_bai) RET(DQ_EINVAL, "Intervals set but no index file found");
+  if (tr->has_intervals && tr->n > 0 && e > b) {
+    std::vector<Interval> iv;
+    for (int64_t i = 0; i < tr->n; i++) {
+      if (tr->ref[i] < 0 || tr->ref[i] >= ctx->n_ref) RET(DQ_EINVAL, "Invalid reference index");
+      iv.push_back({tr->ref[i], tr->start[i], tr->end[i]});
+    }
+    iv = optimize(iv);
+    std::vector<int32_t> r, st, en, beg((size_t)ctx->n_ref + 1, 0);
+    for (auto& x : iv) {
+      r.push_back(x.ref);
+      st.push_back(x.start);
+      en.push_back(x.end);
+    }
+    for (auto& x : iv) beg[(size_t)x.ref + 1]++;
+    for (int32_t k = 0; k < ctx->n_ref; k++) beg[(size_t)k + 1] += beg[(size_t)k];
+    const size_t ni = iv.size();
+    if ((rc = ensure_all(ctx, ctx->iv_ref, 4 * ni + 4)) || (rc = ensure_all(ctx, ctx->iv_start, 4 * ni + 4)) ||
+        (rc = ensure_all(ctx, ctx->iv_end, 4 * ni + 4)) ||
+        (rc = ensure_all(ctx, ctx->iv_begin, 4 * beg.size() + 4)))
+      return rc;
+    HIPCHK(hipMemcpy(ctx->iv_ref.p, r.data(), 4 * ni, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(ctx->iv_start.p, st.data(), 4 * ni, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(ctx->iv_end.p, en.data(), 4 * ni, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(ctx->iv_begin.p, beg.data(), 4 * beg.size(), hipMemcpyHostToDevice));
+    const int64_t n = e - b;
+    std::vector<int64_t> idx((size_t)n);
+    for (int64_t k = 0; k < n; k++) idx[(size_t)k] = b + k;
+    if ((rc = ensure_all(ctx, ctx->idx, 8 * (size_t)n)) || (rc = ensure_all(ctx, ctx->keep, (size_t)n)))
+      return rc;
+    HIPCHK(hipMemcpy(ctx->idx.p, idx.data(), 8 * (size_t)n, hipMemcpyHostToDevice));
+    launch_interval_filter(ctx->U.as<uint8_t>(), ctx->rec_lin.as<int64_t>(), ctx->soa(),
+                           ctx->idx.as<int64_t>(), n, ctx->iv_ref.as<int32_t>(),
+                           ctx->iv_start.as<int32_t>(), ctx->iv_end.as<int32_t>(),
+                           ctx->iv_begin.as<int32_t>(), ctx->n_ref, ctx->keep.as<uint8_t>(), ctx->s);
+    std::vector<uint8_t> keep((size_t)n);
+    HIPCHK(hipMemcpyAsync(keep.data(), ctx->keep.p, (size_t)n, hipMemcpyDeviceToHost, ctx->s));
+    HIPCHK(hipStreamSynchronize(ctx->s));
+    for (int64_t k = 0; k < n; k++)
+      if (keep[(size_t)k]) out.push_back(b + k);
+  }
+  if (tr->traverse_unplaced_unmapped && ctx->solb != -1 && ctx->ncc >= 1 &&
+      vstart <= (uint64_t)ctx->solb && (uint64_t)ctx->solb < vend) {
+    if ((rc = fetch_index(ctx))) return rc;
+    auto& v = ctx->voff_h;
+    auto it = std::lower_bound(v.begin(), v.end(), (uint64_t)ctx->solb);
+    int64_t k = it - v.begin();
+    if (k < ctx->nrec) {
+      std::vector<int32_t> refs((size_t)(ctx->nrec - k));
+      HIPCHK(hipMemcpy(refs.data(), ctx->f_ref.as<int32_t>() + k, 4 * refs.size(), hipMemcpyDeviceToHost));
+      size_t j = 0;
+      while (j < refs.size() && refs[j] != -1) j++;
+      for (; j < refs.size(); j++) out.push_back(k + (int64_t)j);
+    }
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------ C ABI
+extern "C" {
+
+const char* dq_version(void) { return "disq_amd 0.1 (gfx950)"; }
+
+int dq_ctx_create(dq_ctx** out, const dq_opts* opts) {
+  if (!out) return DQ_EINVAL;
+  dq_ctx* ctx = new dq_ctx();
+  if (opts) ctx->o = *opts;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    ctx->err = "no HIP device";
+    *out = ctx;
+    return DQ_EDEVICE;
+  }
+  if (ctx->o.device < 0 || ctx->o.device >= ndev) {
+    ctx->err = "bad device ordinal";
+    *out = ctx;
+    return DQ_EINVAL;
+  }
+  HIPCHK(hipSetDevice(ctx->o.device));
+  HIPCHK(hipStreamCreateWithFlags(&ctx->s, hipStreamNonBlocking));
+  for (auto& e : ctx->ev) HIPCHK(hipEventCreate(&e));
+  *out = ctx;
+  return 0;
+}
+
+void dq_ctx_destroy(dq_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->o.device);
+  if (ctx->s) (void)hipStreamSynchronize(ctx->s);
+  for (auto& e : ctx->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (ctx->s) (void)hipStreamDestroy(ctx->s);
+  delete ctx;
+}
+
+const char* dq_last_error(const dq_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int dq_open_memory(dq_ctx* ctx, const uint8_t* bam, int64_t len) {
+  if (!ctx || (!bam && len > 0) || len < 0) return DQ_EINVAL;
+  HIPCHK(hipSetDevice(ctx->o.device));
+  int rc;
+  if ((rc = ensure_all(ctx, ctx->C, (size_t)len + 4096))) return rc;
+  if (len) HIPCHK(hipMemcpy(ctx->C.p, bam, (size_t)len, hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(ctx->C.as<uint8_t>() + len, 0, 4096));
+  ctx->flen = len;
+  ctx->have_file = true;
+  ctx->have_pipeline = false;
+  return 0;
+}
+
+int dq_open_path(dq_ctx* ctx, const char* path) {
+  if (!ctx || !path) return DQ_EINVAL;
+  FILE* f = fopen(path, "rb");
+  if (!f) RET(DQ_EIO, std::string("cannot open ") + path);
+  fseek(f, 0, SEEK_END);
+  int64_t len = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  std::vector<uint8_t> buf((size_t)len);
+  size_t got = len ? fread(buf.data(), 1, (size_t)len, f) : 0;
+  fclose(f);
+  if ((int64_t)got != len) RET(DQ_EIO, std::string("short read on ") + path);
+  return dq_open_memory(ctx, buf.data(), len);
+}
+
+int dq_set_index(dq_ctx* ctx, const uint8_t* bai, int64_t len) {
+  if (!ctx) return DQ_EINVAL;
+  if (!bai) {
+    ctx->have_bai = false;
+    return 0;
+  }
+  int64_t solb, ncc;
+  if (parse_bai(bai, len, &solb, &ncc)) RET(DQ_EFORMAT, "invalid .bai");
+  ctx->solb = solb;
+  ctx->ncc = ncc;
+  ctx->have_bai = true;
+  return 0;
+}
+
+int dq_read_header(dq_ctx* ctx, dq_header_info* info, uint8_t* header_bytes, int64_t cap) {
+  if (!ctx) return DQ_EINVAL;
+  int rc = run_pipeline(ctx);
+  if (rc) return rc;
+  if (info) {
+    info->n_ref = ctx->n_ref;
+    info->header_bytes = ctx->header_bytes;
+    info->first_record_voffset = 0;
+    if (ctx->nrec) {
+      uint64_t v;
+      HIPCHK(hipMemcpy(&v, ctx->f_voff.p, 8, hipMemcpyDeviceToHost));
+      info->first_record_voffset = v;
+    }
+  }
+  if (header_bytes && cap > 0) {
+    int64_t n = std::min(cap, ctx->header_bytes);
+    HIPCHK(hipMemcpy(header_bytes, ctx->U.p, (size_t)n, hipMemcpyDeviceToHost));
+  }
+  return 0;
+}
+
+int dq_plan(dq_ctx* ctx, dq_chunk** chunks, int64_t* n) {
+  if (!ctx || !chunks || !n) return DQ_EINVAL;
+  int rc = run_pipeline(ctx);
+  if (rc) return rc;
+  *n = (int64_t)ctx->plans_h.size();
+  dq_chunk* c = (dq_chunk*)calloc((size_t)std::max<int64_t>(1, *n), sizeof(dq_chunk));
+  for (int64_t i = 0; i < *n; i++) {
+    const SplitPlan& P = ctx->plans_h[(size_t)i];
+    c[i].split_start = P.split_start;
+    c[i].split_end = P.split_end;
+    c[i].has_chunk = P.rec_lin >= 0;
+    c[i].vstart = P.rec_lin >= 0 ? P.vstart : 0;
+    c[i].vend = P.vend;
+  }
+  *chunks = c;
+  return 0;
+}
+
+int dq_decode(dq_ctx* ctx, uint64_t vstart, uint64_t vend, int32_t with_raw, dq_batch** out) {
+  if (!ctx || !out) return DQ_EINVAL;
+  int rc = run_pipeline(ctx);
+  if (rc) return rc;
+  int64_t b, e;
+  if ((rc = chunk_range(ctx, vstart, vend, &b, &e))) return rc;
+  return make_batch(ctx, {{b, e}}, nullptr, with_raw, {0, e - b}, out);
+}
+
+int dq_decode_filtered(dq_ctx* ctx, uint64_t vstart, uint64_t vend, const dq_traversal* tr,
+                       int32_t with_raw, dq_batch** out) {
+  if (!ctx || !out || !tr) return DQ_EINVAL;
+  if (!tr->has_intervals && !tr->traverse_unplaced_unmapped)
+    RET(DQ_EINVAL, "Traversing mapped reads only is not supported.");
+  int rc = run_pipeline(ctx);
+  if (rc) return rc;
+  int64_t b, e;
+  if ((rc = chunk_range(ctx, vstart, vend, &b, &e))) return rc;
+  std::vector<int64_t> idx;
+  if ((rc = filtered_indices(ctx, vstart, vend, b, e, tr, idx))) return rc;
+  return make_batch(ctx, {}, &idx, with_raw, {0, (int64_t)idx.size()}, out);
+}
+
+int dq_read(dq_ctx* ctx, const dq_traversal* tr, int32_t with_raw, dq_batch** out) {
+  if (!ctx || !out) return DQ_EINVAL;
+  if (tr && !tr->has_intervals && !tr->traverse_unplaced_unmapped)
+    RET(DQ_EINVAL, "Traversing mapped reads only is not supported.");
+  int rc = run_pipeline(ctx);
+  if (rc) return rc;
+  std::vector<int64_t> idx, bounds{0};
+  for (size_t i = 0; i < ctx->plans_h.size(); i++) {
+    const SplitPlan& P = ctx->plans_h[i];
+    if (P.rec_lin < 0) continue;  // empty partition (no PathChunk)
+    const PartRange& r = ctx->parts_h[i];
+    if (!tr) {
+      for (int64_t k = r.begin; k < r.end; k++) idx.push_back(k);
+    } else {
+      std::vector<int64_t> f;
+      if ((rc = filtered_indices(ctx, P.vstart, P.vend, r.begin, r.end, tr, f))) return rc;
+      idx.insert(idx.end(), f.begin(), f.end());
+    }
+    bounds.push_back((int64_t)idx.size());
+  }
+  return make_batch(ctx, {}, &idx, with_raw, bounds, out);
+}
+
+int dq_run_resident(dq_ctx* ctx, const dq_traversal* tr, dq_stats* stats) {
+  if (!ctx) return DQ_EINVAL;
+  (void)tr;
+  ctx->have_pipeline = false;
+  int rc = run_pipeline(ctx);
+  if (rc) return rc;
+  if (stats) *stats = ctx->stats;
+  return 0;
+}
+
+int dq_debug_inflated(dq_ctx* ctx, uint8_t* host_out, int64_t cap, int64_t* len) {
+  if (!ctx) return DQ_EINVAL;
+  int rc = run_pipeline(ctx);
+  if (rc) return rc;
+  if (len) *len = ctx->ulen;
+  if (host_out && cap > 0)
+    HIPCHK(hipMemcpy(host_out, ctx->U.p, (size_t)std::min(cap, ctx->ulen), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+void dq_batch_free(dq_batch* b) {
+  if (!b) return;
+  free(b->voffset);
+  free(b->block_size);
+  free(b->ref_id);
+  free(b->pos);
+  free(b->l_seq);
+  free(b->next_ref_id);
+  free(b->next_pos);
+  free(b->tlen);
+  free(b->flag);
+  free(b->bin);
+  free(b->n_cigar);
+  free(b->mapq);
+  free(b->l_read_name);
+  free(b->hash);
+  free(b->raw_offset);
+  free(b->raw);
+  free(b->part_offset);
+  free(b->part_digest);
+  free(b);
+}
+
+void dq_free(void* p) { free(p); }
+
+}  // extern "C"

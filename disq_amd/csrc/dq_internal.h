@@ -1,0 +1,155 @@
+// dq_internal.h -- shared device helpers and kernel launch wrappers of libdisq_gpu.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// ------------------------------------------------------------------ status codes (per block/record)
+enum : int32_t {
+  ST_OK = 0,
+  ST_BAD_HEADER = 1,      // BGZF header: not 1f 8b 08 04 / XLEN != 6 (htsjdk BlockGunzipper)
+  ST_BAD_BLOCKTYPE = 2,
+  ST_BAD_STORED = 3,
+  ST_BAD_TABLE = 4,       // over-subscribed / incomplete Huffman code, bad header counts
+  ST_BAD_CODE = 5,        // invalid literal/length/distance code
+  ST_BAD_DIST = 6,        // distance too far back
+  ST_SHORT = 7,           // "Did not inflate expected amount"
+  ST_OVERREAD = 8,        // read past the block's deflate data
+  ST_CRC = 9,             // CRC32 mismatch (verify_crc)
+  ST_ISIZE = 10,          // ISIZE > 65536
+  ST_HANG = 11,           // internal: batch loop made no progress
+};
+
+// ------------------------------------------------------------------ hashing
+__host__ __device__ inline uint64_t dq_mix64(uint64_t z) {
+  z ^= z >> 30;
+  z *= 0xBF58476D1CE4E5B9ULL;
+  z ^= z >> 27;
+  z *= 0x94D049BB133111EBULL;
+  z ^= z >> 31;
+  return z;
+}
+#define DQ_K_LEN 0x9E3779B97F4A7C15ULL
+#define DQ_K_WORD 0xD6E8FEB86659FD93ULL
+
+// ------------------------------------------------------------------ launch wrappers
+// All pointers are device pointers; all launches go on `s`.
+namespace dq {
+
+struct Cand {          // a BgzfBlockGuesser-visible magic position
+  int64_t pos;
+  int32_t csize;       // guesser cSize (BSIZE + 1 via the BC subfield)
+  int32_t usize;       // ISIZE
+  int32_t valid;       // 1 = guessNextBGZFPos would return this block; 0 = magic only
+  int32_t pad;
+};
+
+constexpr int SCAN_CHUNK = 16384;  // bytes of C per scan workgroup
+constexpr int SCAN_CAP = 32;       // candidate slots per chunk (overflow -> serial chain)
+
+// Kernel 1: BGZF candidate scan of C[0, n) (file offsets; L = readable bytes).  Writes each
+// chunk's candidates sorted into slots[chunk * SCAN_CAP ...] and its count.
+void launch_bgzf_scan(const uint8_t* C, int64_t n, int64_t L, Cand* slots, int64_t cap,
+                      int32_t* chunk_counts, int64_t n_chunks, int64_t* d_count,
+                      int32_t* d_overflow, hipStream_t s);
+void launch_gather_slots(const Cand* slots, const int32_t* counts, const int64_t* offs,
+                         int64_t nchunks, Cand* out, int64_t cap, hipStream_t s);
+void launch_valid_flags(const Cand* cand, const int64_t* ncand, int64_t cap, int32_t* flags,
+                        hipStream_t s);
+// Chain check: valid candidates must be htsjdk blocks linked by pos + BSIZE + 1.
+void launch_chain2(const uint8_t* C, int64_t L, const Cand* cand, const int64_t* ncand, int64_t cap,
+                   const int64_t* voff, int64_t* blk_pos, int32_t* blk_csize, int32_t* blk_usize,
+                   int64_t blk_cap, int64_t* d_nblk, int32_t* d_broken, int32_t eof_in_buf,
+                   hipStream_t s);
+// Serial fallback chain walk (one lane) over htsjdk headers from `start`.
+void launch_chain_serial(const uint8_t* C, int64_t clen, int64_t start, int64_t* blk_pos,
+                         int32_t* blk_csize, int32_t* blk_usize, int64_t cap, int64_t* d_nblk,
+                         int32_t* d_status, hipStream_t s);
+
+// Exclusive prefix sums; out has n + 1 entries (out[n] = total).  tmp >= 4*ceil(n/1024)+256.
+void launch_exclusive_scan_i32(const int32_t* in, int64_t* out, int64_t n, int64_t* tmp,
+                               hipStream_t s);
+void launch_exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* tmp,
+                               hipStream_t s);
+
+// Kernel 2: inflate every chain block into U at uoff[b]; status per block; optional CRC check.
+void launch_inflate(const uint8_t* C, const int64_t* blk_pos, const int32_t* blk_csize,
+                    const int32_t* blk_usize, const int64_t* uoff, int64_t nblk, uint8_t* U,
+                    int32_t* status, hipStream_t s);
+void launch_crc_check(const uint8_t* C, const int64_t* blk_pos, const int32_t* blk_csize,
+                      const int32_t* blk_usize, const int64_t* uoff, int64_t nblk,
+                      const uint8_t* U, int32_t* status, hipStream_t s);
+
+// Split planning (a2-a4).
+struct SplitPlan {
+  int64_t split_start, split_end;
+  int64_t first_blk;     // chain index of the first guessed block (-1 none)
+  int64_t u_lo, u_hi;    // linear U range scanned by the guesser
+  int64_t rec_lin;       // linear U offset of the first record (-1 = empty partition)
+  uint64_t vstart, vend;
+  int32_t status;        // 0 ok; 100 = needs more data; else error
+  int32_t pad;
+};
+void launch_plan_blocks(const Cand* cand, const int64_t* d_ncand, const int64_t* blk_pos,
+                        const int32_t* blk_usize, const int64_t* uoff, const int64_t* d_nblk,
+                        SplitPlan* plans, int64_t nsplit, hipStream_t s);
+void launch_first_record(const uint8_t* U, int64_t ulen, int32_t u_is_eof, const int32_t* ref_len,
+                         int32_t n_ref, const int64_t* blk_pos, const int64_t* uoff,
+                         const int64_t* d_nblk, SplitPlan* plans, int64_t nsplit, hipStream_t s);
+
+// Kernel 3: record chain over U from `start_lin`.
+struct Seg {
+  int64_t start;   // speculated / exact first chain position in the segment (-1 none)
+  int64_t exit;    // first chain position >= segment end reached from `start`
+  int64_t count;   // records started in [start, segment end)
+  int32_t exact;
+  int32_t status;
+};
+void launch_seg_spec(const uint8_t* U, int64_t ulen, int32_t u_is_eof, const int32_t* ref_len,
+                     int32_t n_ref, Seg* segs, int64_t nseg, int64_t seg_bytes, int64_t start_lin,
+                     hipStream_t s);
+void launch_seg_link(const Seg* segs, int64_t nseg, int64_t seg_bytes, int64_t start_lin,
+                     int64_t ulen, int32_t* d_broken, hipStream_t s);
+void launch_seg_fix2(const uint8_t* U, int64_t ulen, int32_t u_is_eof, Seg* segs, int64_t nseg,
+                     int64_t seg_bytes, int64_t start_lin, int32_t* d_status, hipStream_t s);
+void launch_seg_counts(const Seg* segs, int64_t nseg, int64_t* counts, hipStream_t s);
+void launch_seg_emit2(const uint8_t* U, const Seg* segs, const int64_t* base, int64_t nseg,
+                      int64_t* rec_lin, hipStream_t s);
+
+struct RecSoA {
+  uint64_t* voffset;
+  int32_t* block_size;
+  int32_t* ref_id;
+  int32_t* pos;
+  int32_t* l_seq;
+  int32_t* next_ref_id;
+  int32_t* next_pos;
+  int32_t* tlen;
+  uint16_t* flag;
+  uint16_t* bin;
+  uint16_t* n_cigar;
+  uint8_t* mapq;
+  uint8_t* l_read_name;
+  uint64_t* hash;
+};
+void launch_decode_records(const uint8_t* U, int64_t ulen, const int64_t* rec_lin, int64_t nrec,
+                           const int64_t* blk_pos, const int32_t* blk_csize, const int64_t* uoff,
+                           int64_t nblk, RecSoA soa, int32_t* d_status, hipStream_t s);
+
+struct PartRange {
+  int64_t begin, end;   // record index range in the chain
+  uint64_t digest;
+};
+void launch_partition_ranges(const SplitPlan* plans, int64_t nsplit, const int64_t* rec_lin,
+                             const uint64_t* voffset, int64_t nrec, PartRange* parts,
+                             int32_t* d_status, hipStream_t s);
+void launch_partition_digest2(const uint64_t* hash, PartRange* parts, int64_t nparts,
+                              hipStream_t s);
+
+// Kernel 4: interval filter; keep[t] for record idx[t] (or t when idx == NULL).
+void launch_interval_filter(const uint8_t* U, const int64_t* rec_lin, const RecSoA soa,
+                            const int64_t* idx, int64_t n, const int32_t* iv_ref,
+                            const int32_t* iv_start, const int32_t* iv_end,
+                            const int32_t* ref_iv_begin, int32_t n_ref, uint8_t* keep,
+                            hipStream_t s);
+
+}  // namespace dq

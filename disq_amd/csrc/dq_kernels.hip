@@ -1,0 +1,1003 @@
+// dq_kernels.hip -- Kernels 1, 3, 4 and the planning kernels of the BAM read path on gfx950.
+//
+// Kernel 1  bgzf_scan / chain      replaces BgzfBlockGuesser + BgzfBlockSource
+//           (D/impl/formats/bgzf/BgzfBlockGuesser.java:76-149, BgzfBlockSource.java:63-84)
+// planning  plan_blocks / first_record   replaces BamSource.getFirstReadInPartition +
+//           BamRecordGuesser (D/impl/formats/bam/BamSource.java:110-153,
+//           BamRecordGuesser.java:34-194)
+// Kernel 3  seg_* / decode_records replaces htsjdk BAMFileIndexIterator + BAMRecordCodec.decode
+//           (H/BAMFileReader2.java:1063-1096) and adds the per-record raw-byte hash
+// Kernel 4  interval_filter        replaces BAMQueryMultipleIntervalsIteratorFilter
+//           (AbstractBinarySamSource.java:86-134 via BamSource.java:177-182)
+//
+// All of it is integer/byte work bounded by HBM or latency: no MFMA.
+#include "dq_internal.h"
+
+namespace dq {
+namespace {
+
+__device__ inline uint32_t ld8(const uint8_t* p, int64_t i) { return p[i]; }
+__device__ inline uint32_t ld16(const uint8_t* p, int64_t i) { return p[i] | (p[i + 1] << 8); }
+__device__ inline int32_t ld32(const uint8_t* p, int64_t i) {
+  return (int32_t)(p[i] | (p[i + 1] << 8) | (p[i + 2] << 16) | ((uint32_t)p[i + 3] << 24));
+}
+
+// ------------------------------------------------------------------ Kernel 1: BGZF scan
+constexpr uint32_t BGZF_MAGIC = 0x04088b1fu;
+
+// The part of BgzfBlockGuesser.guessNextBGZFPos after a magic match at q
+// (BgzfBlockGuesser.java:93-144).  Returns 1 (block), 0 (cancelled: scan resumes at q+4) or
+// 2 (an IOException: guessNextBGZFPos returns null).  L = readable bytes.
+__device__ int guesser_at(const uint8_t* C, int64_t q, int64_t L, int32_t* cs, int32_t* us) {
+  if (q + 12 > L) return 2;
+  int64_t xlen = ld16(C, q + 10);
+  int64_t p = q + 12;
+  const int64_t sub_end = p + xlen;
+  while (p < sub_end) {
+    if (p + 4 > L) return 2;
+    uint32_t id = (uint32_t)ld32(C, p);
+    if (id != 0x00024342u) {
+      p += 4 + ld16(C, p + 2);
+      continue;
+    }
+    if (p + 6 > L) return 2;
+    int64_t bsize = ld16(C, p + 4);
+    p += 6;
+    while (p < sub_end) {
+      if (p + 4 > L) return 2;
+      p += 4 + ld16(C, p + 2);
+    }
+    if (p != sub_end) return 0;
+    p += bsize - xlen - 19 + 4;
+    if (p < 0 || p + 4 > L) return 2;
+    *cs = (int32_t)(p + 4 - q);
+    *us = ld32(C, p);
+    return 1;
+  }
+  return 0;
+}
+
+// One workgroup of 256 lanes per 64 KiB chunk; each lane tests 16 positions per step with one
+// 16-byte coalesced load (+4 look-ahead bytes).  Hits are rare and collected in LDS, then
+// written sorted into the chunk's fixed slot range.
+__global__ __launch_bounds__(256) void bgzf_scan_kernel(const uint8_t* __restrict__ C, int64_t n,
+                                                        int64_t L, Cand* __restrict__ slots,
+                                                        int32_t* __restrict__ counts,
+                                                        int32_t* __restrict__ overflow) {
+  __shared__ Cand hits[SCAN_CAP];
+  __shared__ int32_t nh;
+  const int64_t base = (int64_t)blockIdx.x * SCAN_CHUNK;
+  if (threadIdx.x == 0) nh = 0;
+  __syncthreads();
+  for (int it = 0; it < SCAN_CHUNK / 4096; it++) {
+    int64_t off = base + (int64_t)it * 4096 + threadIdx.x * 16;
+    if (off >= n) break;
+    // bytes off .. off+19 (C is padded by >= 64 bytes)
+    const uint4 v = *reinterpret_cast<const uint4*>(C + off);
+    const uint32_t nx = *reinterpret_cast<const uint32_t*>(C + off + 16);
+    uint32_t w[5] = {v.x, v.y, v.z, v.w, nx};
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      int wi = k >> 2, sb = (k & 3) * 8;
+      uint32_t win = sb ? (uint32_t)((((uint64_t)w[wi + 1] << 32) | w[wi]) >> sb) : w[wi];
+      if (win == BGZF_MAGIC) {
+        int64_t q = off + k;
+        if (q + 4 <= L && q < n) {
+          int32_t cs = 0, us = 0;
+          int r = guesser_at(C, q, L, &cs, &us);
+          int slot = atomicAdd(&nh, 1);
+          if (slot < SCAN_CAP) {
+            Cand c;
+            c.pos = q;
+            c.csize = cs;
+            c.usize = us;
+            c.valid = r == 1 ? 1 : (r == 2 ? 2 : 0);
+            c.pad = 0;
+            hits[slot] = c;
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  int32_t m = nh;
+  if (m > SCAN_CAP) {
+    if (threadIdx.x == 0) {
+      *overflow = 1;
+      counts[blockIdx.x] = 0;
+    }
+    return;
+  }
+  // rank sort by position
+  for (int i = threadIdx.x; i < m; i += 256) {
+    Cand c = hits[i];
+    int rank = 0;
+    for (int j = 0; j < m; j++) rank += hits[j].pos < c.pos;
+    slots[(int64_t)blockIdx.x * SCAN_CAP + rank] = c;
+  }
+  if (threadIdx.x == 0) counts[blockIdx.x] = m;
+}
+
+__global__ void gather_slots_kernel(const Cand* __restrict__ slots, const int32_t* __restrict__ counts,
+                                    const int64_t* __restrict__ offs, int64_t nchunks,
+                                    Cand* __restrict__ out, int64_t cap) {
+  int64_t ch = blockIdx.x;
+  if (ch >= nchunks) return;
+  int32_t m = counts[ch];
+  int64_t o = offs[ch];
+  for (int i = threadIdx.x; i < m; i += blockDim.x)
+    if (o + i < cap) out[o + i] = slots[ch * SCAN_CAP + i];
+}
+
+// ------------------------------------------------------------------ scans
+// Block-level exclusive scan of 1024 elements per block, then a recursive pass on block sums.
+template <typename T>
+__global__ __launch_bounds__(1024) void scan_block_kernel(const T* __restrict__ in, int64_t* out,
+                                                          int64_t n, int64_t* __restrict__ sums) {
+  __shared__ int64_t s[1024];
+  int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x;
+  int64_t v = i < n ? (int64_t)in[i] : 0;
+  s[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    int64_t t = threadIdx.x >= o ? s[threadIdx.x - o] : 0;
+    __syncthreads();
+    s[threadIdx.x] += t;
+    __syncthreads();
+  }
+  if (i < n) out[i] = s[threadIdx.x] - v;
+  if (threadIdx.x == 1023) sums[blockIdx.x] = s[1023];
+}
+
+__global__ void scan_add_kernel(int64_t* out, int64_t n, const int64_t* __restrict__ sums_scanned) {
+  int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x;
+  if (i < n) out[i] += sums_scanned[blockIdx.x];
+}
+
+template <typename T>
+void exclusive_scan(const T* in, int64_t* out, int64_t n, int64_t* tmp, hipStream_t s) {
+  // out has n + 1 entries; out[n] = total.  tmp needs >= 2 * ceil(n/1024) + 64 entries.
+  if (n <= 0) {
+    hipMemsetAsync(out, 0, sizeof(int64_t), s);
+    return;
+  }
+  int64_t nb = (n + 1023) / 1024;
+  int64_t* sums = tmp;
+  int64_t* sums_sc = tmp + nb + 1;
+  hipLaunchKernelGGL(scan_block_kernel<T>, dim3((unsigned)nb), dim3(1024), 0, s, in, out, n, sums);
+  if (nb > 1) {
+    exclusive_scan<int64_t>(sums, sums_sc, nb, tmp + 2 * nb + 2, s);
+    hipLaunchKernelGGL(scan_add_kernel, dim3((unsigned)nb), dim3(1024), 0, s, out, n, sums_sc);
+    // total = sums_sc[nb]
+    hipMemcpyAsync(out + n, sums_sc + nb, sizeof(int64_t), hipMemcpyDeviceToDevice, s);
+  } else {
+    hipMemcpyAsync(out + n, sums, sizeof(int64_t), hipMemcpyDeviceToDevice, s);
+  }
+}
+
+// ------------------------------------------------------------------ chain
+// htsjdk reads blocks one after another by BSIZE at header offset 16 and requires XLEN == 6
+// (BlockGunzipper.unzipBlock).  Valid guesser candidates must form exactly that chain.
+__device__ inline int htsjdk_block(const uint8_t* C, int64_t p, int64_t L, int32_t* cs) {
+  if (p + 18 > L) return 0;
+  if ((uint32_t)ld32(C, p) != BGZF_MAGIC || ld16(C, p + 10) != 6) return 0;
+  int32_t c = (int32_t)ld16(C, p + 16) + 1;
+  if (c < 26 || p + c > L) return 0;
+  *cs = c;
+  return 1;
+}
+
+__global__ void valid_flags_kernel(const Cand* __restrict__ cand, const int64_t* __restrict__ ncand,
+                                   int32_t* __restrict__ flags) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < *ncand) flags[i] = cand[i].valid == 1;
+}
+
+__global__ void chain_kernel(const uint8_t* __restrict__ C, int64_t L, const Cand* __restrict__ cand,
+                             const int64_t* __restrict__ ncand, const int64_t* __restrict__ voff,
+                             int64_t* __restrict__ blk_pos, int32_t* __restrict__ blk_csize,
+                             int32_t* __restrict__ blk_usize, int64_t cap, int64_t* d_nblk,
+                             int32_t* d_broken, int32_t eof_in_buf) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t nc = *ncand;
+  int64_t nv = voff[nc];
+  if (i == 0) *d_nblk = nv;
+  if (i >= nc || cand[i].valid != 1) return;
+  int64_t k = voff[i];
+  if (k >= cap) {
+    *d_broken = 1;
+    return;
+  }
+  const Cand c = cand[i];
+  int32_t cs;
+  if (!htsjdk_block(C, c.pos, L, &cs) || cs != c.csize) {
+    *d_broken = 1;
+    return;
+  }
+  blk_pos[k] = c.pos;
+  blk_csize[k] = cs;
+  blk_usize[k] = c.usize;
+  // link to the next valid candidate
+  int64_t nextpos = -1;
+  for (int64_t j = i + 1; j < nc; j++)
+    if (cand[j].valid == 1) {
+      nextpos = cand[j].pos;
+      break;
+    }
+  if (nextpos >= 0) {
+    if (c.pos + cs != nextpos) *d_broken = 1;
+  } else if (eof_in_buf && c.pos + cs != L) {
+    *d_broken = 1;
+  }
+}
+
+__global__ void chain_serial_kernel(const uint8_t* __restrict__ C, int64_t L, int64_t start,
+                                    int64_t* __restrict__ blk_pos, int32_t* __restrict__ blk_csize,
+                                    int32_t* __restrict__ blk_usize, int64_t cap, int64_t* d_nblk,
+                                    int32_t* d_status) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int64_t p = start, n = 0;
+  while (p < L) {
+    int32_t cs;
+    if (!htsjdk_block(C, p, L, &cs)) break;
+    if (n >= cap) {
+      *d_status = ST_BAD_HEADER;
+      break;
+    }
+    blk_pos[n] = p;
+    blk_csize[n] = cs;
+    blk_usize[n] = ld32(C, p + cs - 4);
+    n++;
+    p += cs;
+  }
+  *d_nblk = n;
+}
+
+// ------------------------------------------------------------------ CRC32
+__constant__ uint32_t c_crc_tab[256];
+
+__device__ inline uint32_t gf2_mulmod(uint32_t a, uint32_t b) {  // reflected, poly 0xEDB88320
+  uint32_t m = 1u << 31, p = 0;
+  if (a == 0) return 0;
+  for (;;) {
+    if (a & m) {
+      p ^= b;
+      if ((a & (m - 1)) == 0) break;
+    }
+    m >>= 1;
+    b = b & 1 ? (b >> 1) ^ 0xEDB88320u : b >> 1;
+  }
+  return p;
+}
+// x^(8n) mod P (reflected), square-and-multiply over the bits of n using x^(2^k) powers.
+__constant__ uint32_t c_x2n[32];
+__device__ inline uint32_t x8nmodp(uint64_t n) {
+  uint32_t p = 1u << 31;  // x^0
+  int k = 3;
+  while (n) {
+    if (n & 1) p = gf2_mulmod(c_x2n[k & 31], p);
+    n >>= 1;
+    k++;
+  }
+  return p;
+}
+
+// One wave per block: lane l hashes bytes [l*S, (l+1)*S) with the byte table, then the lane
+// CRCs are combined with x^(8n) shifts (CRC linearity) and compared with the gzip trailer.
+__global__ __launch_bounds__(64) void crc_kernel(const uint8_t* __restrict__ C, const int64_t* __restrict__ blk_pos,
+                                                 const int32_t* __restrict__ blk_csize,
+                                                 const int32_t* __restrict__ blk_usize,
+                                                 const int64_t* __restrict__ uoff, int64_t nblk,
+                                                 const uint8_t* __restrict__ U,
+                                                 int32_t* __restrict__ status) {
+  __shared__ uint32_t tab[256];
+  for (int i = threadIdx.x; i < 256; i += 64) tab[i] = c_crc_tab[i];
+  __syncthreads();
+  int64_t b = blockIdx.x;
+  if (b >= nblk) return;
+  if (status[b] != ST_OK) return;
+  const int lane = threadIdx.x;
+  const int32_t n = blk_usize[b];
+  const uint8_t* src = U + uoff[b];
+  const int32_t S = (n + 63) / 64;
+  int32_t lo = min(n, lane * S), hi = min(n, lo + S);
+  uint32_t c = 0;  // raw register, zero init
+  for (int32_t i = lo; i < hi; i++) c = tab[(c ^ src[i]) & 0xff] ^ (c >> 8);
+  // shift by the bytes after this lane's segment
+  uint32_t sh = x8nmodp((uint64_t)(n - hi));
+  c = gf2_mulmod(sh, c);
+  for (int o = 32; o >= 1; o >>= 1) c ^= __shfl_xor(c, o, 64);
+  if (lane == 0) {
+    // standard CRC-32: init 0xffffffff, final xor 0xffffffff
+    uint32_t init = gf2_mulmod(0xffffffffu, x8nmodp((uint64_t)n));
+    uint32_t crc = (c ^ init) ^ 0xffffffffu;
+    int64_t p = blk_pos[b] + blk_csize[b] - 8;
+    uint32_t want = (uint32_t)ld32(C, p);
+    if (crc != want) status[b] = ST_CRC;
+  }
+}
+
+// ------------------------------------------------------------------ record guesser
+// BamRecordGuesser.checkRecordStartInternal (BamRecordGuesser.java:79-194) on the linear stream.
+// Returns 1 (start; *next set), 0 (no start), 3 (EOF), 4 (need data beyond the buffer).
+__device__ inline int rd_ok(int64_t p, int64_t n, int64_t ulen, int u_is_eof) {
+  if (p + n <= ulen) return 0;
+  return u_is_eof ? 3 : 4;
+}
+
+__device__ int check_internal(const uint8_t* U, int64_t ulen, int u_is_eof, const int32_t* ref_len,
+                              int32_t n_ref, int64_t v, int64_t* next) {
+  int e;
+  if ((e = rd_ok(v, 36, ulen, u_is_eof))) return e;
+  int32_t remaining = ld32(U, v);
+  int32_t id = ld32(U, v + 4), pos = ld32(U, v + 8);
+  if (id < -1 || id >= n_ref || pos < -1) return 0;
+  if (id >= 0 && pos > ref_len[id]) return 0;
+  int32_t nid = ld32(U, v + 24), npos = ld32(U, v + 28);
+  if (nid < -1 || nid >= n_ref || npos < -1) return 0;
+  if (nid >= 0 && npos > ref_len[nid]) return 0;
+  int32_t name_len = ld32(U, v + 12) & 0xff;
+  if (name_len < 2) return 0;
+  uint32_t flag_nc = (uint32_t)ld32(U, v + 16);
+  int32_t flags = (int32_t)(flag_nc >> 16);
+  int32_t n_cig = (int32_t)(flag_nc & 0xffff);
+  int32_t cig_len = (int32_t)((uint32_t)n_cig * 4u);
+  int32_t l_seq = ld32(U, v + 20);
+  int32_t seq_len = (int32_t)((uint32_t)l_seq + (uint32_t)((int32_t)((uint32_t)l_seq + 1u) / 2));
+  if ((flags & 4) == 0 && (seq_len == 0 || n_cig == 0)) return 0;
+  if ((e = rd_ok(v + 36, name_len, ulen, u_is_eof))) return e;
+  if (U[v + 36 + name_len - 1] != 0) return 0;
+  for (int i = 0; i < name_len - 1; i++) {
+    int8_t b = (int8_t)U[v + 36 + i];
+    if (!((b >= '!' && b <= '?') || (b >= 'A' && b <= '~'))) return 0;
+  }
+  int64_t cp = v + 36 + name_len;
+  for (int i = 0; i < n_cig; i++) {
+    if ((e = rd_ok(cp, 4, ulen, u_is_eof))) return e;
+    int32_t op = ld32(U, cp);
+    if (op == -1) return 3;
+    if ((op & 0xf) > 8) return 0;
+    cp += 4;
+  }
+  int32_t zero_min =
+      (int32_t)((uint32_t)32 + (uint32_t)name_len + (uint32_t)cig_len + (uint32_t)seq_len);
+  if (remaining >= zero_min) {
+    int32_t skip = (int32_t)(4u + (uint32_t)remaining);
+    int64_t nv = v;
+    if (skip > 0) {
+      if (v + skip > ulen) return u_is_eof ? 3 : 4;
+      nv = v + skip;
+    }
+    *next = nv;
+    return 1;
+  }
+  return 0;
+}
+
+// checkRecordStart (BamRecordGuesser.java:34-52): 1 true, 0 false, 4 need more data.
+__device__ int check_record_start(const uint8_t* U, int64_t ulen, int u_is_eof,
+                                  const int32_t* ref_len, int32_t n_ref, int64_t v) {
+  for (int k = 0; k < 10; k++) {
+    int64_t nv = 0;
+    int r = check_internal(U, ulen, u_is_eof, ref_len, n_ref, v, &nv);
+    if (r == 1) {
+      v = nv;
+      continue;
+    }
+    if (r == 0) return 0;
+    if (r == 3) return k > 0 ? 1 : 0;
+    return 4;
+  }
+  return 1;
+}
+
+// ------------------------------------------------------------------ planning
+__device__ inline int64_t lower_bound_cand(const Cand* c, int64_t n, int64_t p) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (c[mid].pos < p) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+__device__ inline int64_t lower_bound_i64(const int64_t* a, int64_t n, int64_t v) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+__device__ inline int64_t lower_bound_u64(const uint64_t* a, int64_t n, uint64_t v) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+// block containing linear offset x: largest j with uoff[j] <= x among blocks with data.
+__device__ inline int64_t block_of(const int64_t* uoff, int64_t nblk, int64_t x) {
+  int64_t lo = 0, hi = nblk - 1;
+  while (lo < hi) {
+    int64_t mid = (lo + hi + 1) >> 1;
+    if (uoff[mid] <= x) lo = mid;
+    else hi = mid - 1;
+  }
+  // skip back over trailing empty blocks sharing the offset: take the last block whose range
+  // contains x (uoff[j] <= x < uoff[j+1]).
+  while (lo > 0 && uoff[lo] > x) lo--;
+  return lo;
+}
+
+// guessNextBGZFPos(p, end) over the candidate list (magic positions, in order), then the
+// BgzfBlockSource chain of the split: blocks [first, last] with pos <= split end.
+__global__ void plan_blocks_kernel(const Cand* __restrict__ cand, const int64_t* __restrict__ ncand,
+                                   const int64_t* __restrict__ blk_pos,
+                                   const int32_t* __restrict__ blk_usize,
+                                   const int64_t* __restrict__ uoff, const int64_t* __restrict__ d_nblk,
+                                   SplitPlan* __restrict__ plans, int64_t nsplit) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nsplit) return;
+  SplitPlan& P = plans[i];
+  const int64_t nc = *ncand, nb = *d_nblk;
+  P.first_blk = -1;
+  P.rec_lin = -1;
+  P.status = 0;
+  const int64_t s = P.split_start, e = P.split_end;
+  int64_t p = s;
+  int64_t found = -1;
+  for (;;) {
+    int64_t k = lower_bound_cand(cand, nc, p);
+    if (k >= nc) break;             // scan runs off the data -> null
+    const Cand c = cand[k];
+    if (c.pos != p && c.pos >= e) break;  // :91 end check (skipped for the first position)
+    if (c.valid == 1) {
+      found = c.pos;
+      break;
+    }
+    if (c.valid == 2) break;        // IOException -> null
+    p = c.pos + 4;                  // :144, tested without an end check
+  }
+  if (found < 0) return;
+  int64_t j = lower_bound_i64(blk_pos, nb, found);
+  if (j >= nb || blk_pos[j] != found) {
+    P.status = ST_BAD_HEADER;  // guessed block is not on the BGZF chain
+    return;
+  }
+  // BgzfBlockSource: blocks while start <= split end
+  int64_t jl = j;
+  while (jl + 1 < nb && blk_pos[jl + 1] <= e) jl++;
+  P.first_blk = j;
+  P.u_lo = uoff[j];
+  P.u_hi = uoff[jl] + blk_usize[jl];
+}
+
+// BamSource.getFirstReadInPartition: first position (<= 10,000,000 scanned) where the guesser
+// fires.  One workgroup per split, 256 positions per step, first hit by ballot + LDS min.
+__global__ __launch_bounds__(256) void first_record_kernel(
+    const uint8_t* __restrict__ U, int64_t ulen, int32_t u_is_eof, const int32_t* __restrict__ ref_len,
+    int32_t n_ref, const int64_t* __restrict__ blk_pos, const int64_t* __restrict__ uoff,
+    const int64_t* __restrict__ d_nblk, SplitPlan* __restrict__ plans, int64_t nsplit) {
+  __shared__ int64_t best;
+  __shared__ int32_t need;
+  int64_t i = blockIdx.x;
+  if (i >= nsplit) return;
+  SplitPlan& P = plans[i];
+  if (P.first_blk < 0 || P.status != 0) return;
+  const int64_t lo = P.u_lo;
+  const int64_t hi = min(P.u_hi, lo + (int64_t)10000000);
+  if (threadIdx.x == 0) {
+    best = INT64_MAX;
+    need = 0;
+  }
+  __syncthreads();
+  for (int64_t b = lo; b < hi; b += 256) {
+    int64_t v = b + threadIdx.x;
+    if (v < hi) {
+      int r = check_record_start(U, ulen, u_is_eof, ref_len, n_ref, v);
+      if (r == 1) atomicMin((unsigned long long*)&best, (unsigned long long)v);
+      if (r == 4) atomicMin((unsigned long long*)&best, (unsigned long long)v), need = 1;
+    }
+    __syncthreads();
+    if (best != INT64_MAX) break;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (best != INT64_MAX) {
+      // a "need more data" at the minimum position means the answer is unknown here
+      int64_t v = best;
+      if (need && check_record_start(U, ulen, u_is_eof, ref_len, n_ref, v) == 4) {
+        P.status = 100;  // caller must extend the buffer
+        return;
+      }
+      int64_t nb = *d_nblk;
+      int64_t j = block_of(uoff, nb, v);
+      P.rec_lin = v;
+      P.vstart = ((uint64_t)blk_pos[j] << 16) | (uint64_t)(v - uoff[j]);
+    }
+    P.vend = ((uint64_t)P.split_end << 16) | 0xffff;
+  }
+}
+
+// ------------------------------------------------------------------ Kernel 3: record chain
+// Records are walked with next = p + 4 + block_size (htsjdk BAMRecordCodec.decode reads
+// block_size, then block_size bytes).  Segment speculation uses the guesser; a segment whose
+// speculated start differs from its predecessor's exit is re-walked from that exit, so the
+// result is the exact sequential chain regardless of speculation quality.
+constexpr int64_t END_CHAIN = INT64_MAX;
+
+// Walk from `start` while p < seg_end.  Returns exit position (>= seg_end, or END_CHAIN), count.
+__device__ int walk(const uint8_t* U, int64_t ulen, int u_is_eof, int64_t start, int64_t seg_end,
+                    int64_t* exit, int64_t* count) {
+  int64_t p = start, n = 0;
+  while (p < seg_end) {
+    if (p + 4 > ulen) {
+      if (u_is_eof) {
+        *exit = END_CHAIN;
+        *count = n;
+        return 0;
+      }
+      return 4;
+    }
+    int32_t bs = ld32(U, p);
+    if (bs < 32) return ST_BAD_CODE;  // "Invalid record length" (SAMFormatException)
+    n++;
+    p += 4 + (int64_t)bs;
+  }
+  *exit = p;
+  *count = n;
+  return 0;
+}
+
+__global__ __launch_bounds__(64) void seg_spec_kernel(const uint8_t* __restrict__ U, int64_t ulen,
+                                                      int32_t u_is_eof,
+                                                      const int32_t* __restrict__ ref_len,
+                                                      int32_t n_ref, Seg* __restrict__ segs,
+                                                      int64_t nseg, int64_t seg_bytes,
+                                                      int64_t start_lin) {
+  int64_t s = blockIdx.x;
+  if (s >= nseg) return;
+  const int64_t sb = start_lin + s * seg_bytes;
+  const int64_t se = min(ulen, sb + seg_bytes);
+  __shared__ int64_t best;
+  if (threadIdx.x == 0) best = INT64_MAX;
+  __syncthreads();
+  if (s == 0) {
+    if (threadIdx.x == 0) best = start_lin;
+  } else {
+    for (int64_t b = sb; b < se; b += 64) {
+      int64_t v = b + threadIdx.x;
+      bool hit = v < se && check_record_start(U, ulen, u_is_eof, ref_len, n_ref, v) == 1;
+      uint64_t m = __ballot(hit);
+      if (m) {
+        if (threadIdx.x == 0) best = b + __builtin_ctzll(m);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Seg g;
+    g.exact = s == 0;
+    g.status = 0;
+    g.start = best == INT64_MAX ? -1 : best;  // -1: no start speculated in this segment
+    g.exit = -1;
+    g.count = 0;
+    if (g.start >= 0) {
+      int64_t ex, cnt;
+      int r = walk(U, ulen, u_is_eof, g.start, se, &ex, &cnt);
+      g.status = r;
+      if (r == 0) {
+        g.exit = ex;
+        g.count = cnt;
+      }
+    }
+    segs[s] = g;
+  }
+}
+
+// Serial link check + repair (one lane).  Segments are few (one per 1 MiB of U); each link is
+// O(1) unless a speculation was wrong, in which case that segment is re-walked from the exact
+// incoming position.
+__global__ void seg_fix_kernel(const uint8_t* __restrict__ U, int64_t ulen, int32_t u_is_eof,
+                               Seg* __restrict__ segs, int64_t nseg, int64_t seg_bytes,
+                               int64_t start_lin, int32_t* d_status) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int64_t in = segs[0].exit;
+  if (segs[0].status) {
+    *d_status = segs[0].status;
+    return;
+  }
+  for (int64_t s = 1; s < nseg; s++) {
+    Seg& g = segs[s];
+    const int64_t sb = start_lin + s * seg_bytes;
+    const int64_t se = min(ulen, sb + seg_bytes);
+    if (in == END_CHAIN || in >= se) {  // no record starts inside this segment
+      g.start = in;
+      g.exit = in;
+      g.count = 0;
+      g.exact = 1;
+      g.status = 0;
+      continue;
+    }
+    if (g.start != in || g.status != 0) {
+      int64_t ex = -1, cnt = 0;
+      int r = walk(U, ulen, u_is_eof, in, se, &ex, &cnt);
+      g.start = in;
+      g.status = r;
+      g.exit = ex;
+      g.count = cnt;
+      if (r) {
+        *d_status = r;
+        return;
+      }
+    }
+    g.exact = 1;
+    in = g.exit;
+  }
+}
+
+// Parallel link check: segment s is consistent when the exit of the last earlier segment that
+// has a start equals s's speculated start (or passes beyond s when s has none).
+__global__ void seg_link_kernel(const Seg* __restrict__ segs, int64_t nseg, int64_t seg_bytes,
+                                int64_t start_lin, int64_t ulen, int32_t* d_broken) {
+  int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nseg) return;
+  const Seg g = segs[s];
+  if (g.status != 0) {
+    *d_broken = 1;
+    return;
+  }
+  if (s == 0) return;
+  int64_t t = s - 1;
+  while (t > 0 && segs[t].start < 0) t--;
+  const int64_t in = segs[t].exit;
+  const int64_t se = min(ulen, start_lin + (s + 1) * seg_bytes);
+  bool ok = g.start < 0 ? (in == END_CHAIN || in >= se) : (in == g.start);
+  if (!ok) *d_broken = 1;
+}
+
+__global__ void seg_counts_kernel(const Seg* __restrict__ segs, int64_t nseg, int64_t* counts) {
+  int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < nseg) counts[s] = segs[s].count;
+}
+
+__global__ void seg_emit_kernel(const uint8_t* __restrict__ U, const Seg* __restrict__ segs,
+                                const int64_t* __restrict__ base, int64_t nseg,
+                                int64_t* __restrict__ rec_lin) {
+  int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nseg) return;
+  const Seg g = segs[s];
+  int64_t p = g.start, o = base[s];
+  for (int64_t k = 0; k < g.count; k++) {
+    rec_lin[o + k] = p;
+    p += 4 + (int64_t)ld32(U, p);
+  }
+}
+
+// ------------------------------------------------------------------ decode + hash
+__device__ inline uint32_t ldw(const uint32_t* U32, int64_t wi) { return U32[wi]; }
+
+// One lane per record: fixed fields into SoA, htsjdk start pointer, and the raw-byte hash
+// (8-byte little-endian words, zero padded) read as aligned dwords.
+__global__ __launch_bounds__(256) void decode_records_kernel(
+    const uint8_t* __restrict__ U, int64_t ulen, const int64_t* __restrict__ rec_lin, int64_t nrec,
+    const int64_t* __restrict__ blk_pos, const int32_t* __restrict__ blk_csize,
+    const int64_t* __restrict__ uoff, int64_t nblk, RecSoA soa, int32_t* d_status) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nrec) return;
+  const int64_t p = rec_lin[i];
+  const int32_t bs = ld32(U, p);
+  const int64_t n = 4 + (int64_t)bs;
+  if (p + n > ulen) {
+    *d_status = ST_SHORT;
+    return;
+  }
+  soa.block_size[i] = bs;
+  soa.ref_id[i] = ld32(U, p + 4);
+  soa.pos[i] = ld32(U, p + 8);
+  uint32_t bmn = (uint32_t)ld32(U, p + 12);
+  soa.l_read_name[i] = (uint8_t)(bmn & 0xff);
+  soa.mapq[i] = (uint8_t)((bmn >> 8) & 0xff);
+  soa.bin[i] = (uint16_t)(bmn >> 16);
+  uint32_t fnc = (uint32_t)ld32(U, p + 16);
+  soa.n_cigar[i] = (uint16_t)(fnc & 0xffff);
+  soa.flag[i] = (uint16_t)(fnc >> 16);
+  soa.l_seq[i] = ld32(U, p + 20);
+  soa.next_ref_id[i] = ld32(U, p + 24);
+  soa.next_pos[i] = ld32(U, p + 28);
+  soa.tlen[i] = ld32(U, p + 32);
+  int64_t j = block_of(uoff, nblk, p);
+  soa.voffset[i] = ((uint64_t)blk_pos[j] << 16) | (uint64_t)(p - uoff[j]);
+  // hash
+  const uint32_t* U32 = reinterpret_cast<const uint32_t*>(U);
+  const int sh = (int)(p & 3) * 8;
+  int64_t wi = p >> 2;
+  uint32_t w0 = ldw(U32, wi);
+  uint64_t h = (uint64_t)n * DQ_K_LEN;
+  const int64_t nw = (n + 7) / 8;
+  for (int64_t k = 0; k < nw; k++) {
+    uint32_t w1 = ldw(U32, wi + 1), w2 = ldw(U32, wi + 2);
+    uint32_t lo = sh ? (uint32_t)((((uint64_t)w1 << 32) | w0) >> sh) : w0;
+    uint32_t hi = sh ? (uint32_t)((((uint64_t)w2 << 32) | w1) >> sh) : w1;
+    uint64_t w = ((uint64_t)hi << 32) | lo;
+    int64_t rem = n - 8 * k;
+    if (rem < 8) w &= (1ull << (8 * rem)) - 1;
+    h += dq_mix64(w ^ ((uint64_t)(k + 1) * DQ_K_WORD));
+    w0 = w2;
+    wi += 2;
+  }
+  soa.hash[i] = dq_mix64(h);
+}
+
+// ------------------------------------------------------------------ partitions
+// BAMFileIndexIterator over Chunk(vstart, vend): records from the guesser's start while the
+// start pointer < vend (H/BAMFileReader2.java:1082-1095).
+__global__ void partition_ranges_kernel(const SplitPlan* __restrict__ plans, int64_t nsplit,
+                                        const int64_t* __restrict__ rec_lin,
+                                        const uint64_t* __restrict__ voffset, int64_t nrec,
+                                        PartRange* __restrict__ parts, int32_t* d_status) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nsplit) return;
+  const SplitPlan P = plans[i];
+  PartRange r;
+  r.begin = r.end = 0;
+  r.digest = 0;
+  if (P.rec_lin >= 0) {
+    int64_t b = lower_bound_i64(rec_lin, nrec, P.rec_lin);
+    if (b >= nrec || rec_lin[b] != P.rec_lin) {
+      *d_status = 101;  // guesser start not on the record chain (misfire)
+    } else {
+      int64_t e = lower_bound_u64(voffset, nrec, P.vend);
+      r.begin = b;
+      r.end = e < b ? b : e;
+    }
+  }
+  parts[i] = r;
+}
+
+__global__ __launch_bounds__(256) void partition_digest_kernel(const uint64_t* __restrict__ hash,
+                                                               PartRange* __restrict__ parts,
+                                                               int64_t nparts) {
+  __shared__ uint64_t red[256];
+  int64_t i = blockIdx.x;
+  if (i >= nparts) return;
+  const PartRange r = parts[i];
+  uint64_t acc = 0;
+  for (int64_t k = r.begin + threadIdx.x; k < r.end; k += 256)
+    acc += dq_mix64(hash[k] + (uint64_t)(k - r.begin + 1) * DQ_K_LEN);
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) parts[i].digest = red[0];
+}
+
+// ------------------------------------------------------------------ Kernel 4: interval filter
+// BAMQueryMultipleIntervalsIteratorFilter.compareIntervalToRecord with contained=false on
+// optimized (sorted, merged) QueryIntervals: a record matches iff an interval on its reference
+// has start <= alignmentEnd and end >= alignmentStart.  alignmentEnd = pos + refLen(CIGAR
+// M/D/N/=/X) for mapped reads, alignmentStart for unmapped reads with a position, 0 otherwise.
+__global__ __launch_bounds__(256) void interval_filter_kernel(
+    const uint8_t* __restrict__ U, const int64_t* __restrict__ rec_lin, RecSoA soa,
+    const int64_t* __restrict__ idx, int64_t n, const int32_t* __restrict__ iv_ref,
+    const int32_t* __restrict__ iv_start, const int32_t* __restrict__ iv_end,
+    const int32_t* __restrict__ ref_iv_begin, int32_t n_ref, uint8_t* __restrict__ keep) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int64_t i = idx ? idx[t] : t;
+  const int32_t ref = soa.ref_id[i];
+  uint8_t k = 0;
+  if (ref >= 0 && ref < n_ref) {
+    const int32_t astart = soa.pos[i] + 1;
+    const uint16_t flag = soa.flag[i];
+    int32_t aend;
+    if (flag & 4) {
+      aend = astart != 0 ? astart : 0;
+    } else {
+      const int64_t p = rec_lin[i];
+      const int64_t cp = p + 36 + soa.l_read_name[i];
+      const int nc = soa.n_cigar[i];
+      int32_t rl = 0;
+      if (32 + (int64_t)soa.l_read_name[i] + 4 * (int64_t)nc <= soa.block_size[i]) {
+        for (int c = 0; c < nc; c++) {
+          uint32_t op = (uint32_t)ld32(U, cp + 4 * c);
+          uint32_t o = op & 0xf;
+          if (o == 0 || o == 2 || o == 3 || o == 7 || o == 8) rl += (int32_t)(op >> 4);
+        }
+      }
+      aend = astart + rl - 1;
+    }
+    int32_t lo = ref_iv_begin[ref], hi = ref_iv_begin[ref + 1];
+    // last interval with start <= aend (intervals on one reference are sorted and disjoint)
+    int32_t a = lo, b = hi;
+    while (a < b) {
+      int32_t m = (a + b) >> 1;
+      if (iv_start[m] <= aend) a = m + 1;
+      else b = m;
+    }
+    if (a > lo) {
+      int32_t e = iv_end[a - 1];
+      if (e <= 0) e = INT32_MAX;
+      if (e >= astart) k = 1;
+    }
+  }
+  keep[t] = k;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ launchers
+void launch_bgzf_scan(const uint8_t* C, int64_t n, int64_t L, Cand* slots_out, int64_t cap,
+                      int32_t* chunk_counts, int64_t n_chunks, int64_t* d_count,
+                      int32_t* d_overflow, hipStream_t s) {
+  (void)cap;
+  (void)d_count;
+  hipLaunchKernelGGL(bgzf_scan_kernel, dim3((unsigned)n_chunks), dim3(256), 0, s, C, n, L,
+                     slots_out, chunk_counts, d_overflow);
+}
+
+void launch_gather_slots(const Cand* slots, const int32_t* counts, const int64_t* offs,
+                         int64_t nchunks, Cand* out, int64_t cap, hipStream_t s) {
+  hipLaunchKernelGGL(gather_slots_kernel, dim3((unsigned)nchunks), dim3(64), 0, s, slots, counts,
+                     offs, nchunks, out, cap);
+}
+
+void launch_exclusive_scan_i32(const int32_t* in, int64_t* out, int64_t n, int64_t* tmp,
+                               hipStream_t s) {
+  exclusive_scan<int32_t>(in, out, n, tmp, s);
+}
+void launch_exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* tmp,
+                               hipStream_t s) {
+  exclusive_scan<int64_t>(in, out, n, tmp, s);
+}
+
+void launch_valid_flags(const Cand* cand, const int64_t* ncand, int64_t cap, int32_t* flags,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(valid_flags_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, s,
+                     cand, ncand, flags);
+}
+
+void launch_chain2(const uint8_t* C, int64_t L, const Cand* cand, const int64_t* ncand, int64_t cap,
+                   const int64_t* voff, int64_t* blk_pos, int32_t* blk_csize, int32_t* blk_usize,
+                   int64_t blk_cap, int64_t* d_nblk, int32_t* d_broken, int32_t eof_in_buf,
+                   hipStream_t s) {
+  hipLaunchKernelGGL(chain_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, s, C, L, cand,
+                     ncand, voff, blk_pos, blk_csize, blk_usize, blk_cap, d_nblk, d_broken,
+                     eof_in_buf);
+}
+
+void launch_chain_serial(const uint8_t* C, int64_t clen, int64_t start, int64_t* blk_pos,
+                         int32_t* blk_csize, int32_t* blk_usize, int64_t cap, int64_t* d_nblk,
+                         int32_t* d_status, hipStream_t s) {
+  hipLaunchKernelGGL(chain_serial_kernel, dim3(1), dim3(64), 0, s, C, clen, start, blk_pos,
+                     blk_csize, blk_usize, cap, d_nblk, d_status);
+}
+
+static uint32_t host_gf2_mulmod(uint32_t a, uint32_t b) {
+  uint32_t m = 1u << 31, p = 0;
+  for (;;) {
+    if (a & m) {
+      p ^= b;
+      if ((a & (m - 1)) == 0) break;
+    }
+    m >>= 1;
+    b = b & 1 ? (b >> 1) ^ 0xEDB88320u : b >> 1;
+  }
+  return p;
+}
+
+void init_crc_tables() {
+  static bool done = false;
+  if (done) return;
+  uint32_t tab[256];
+  for (uint32_t i = 0; i < 256; i++) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; k++) c = c & 1 ? (c >> 1) ^ 0xEDB88320u : c >> 1;
+    tab[i] = c;
+  }
+  uint32_t x2n[32];
+  uint32_t p = 1u << 30;  // x^1
+  x2n[0] = p;
+  for (int k = 1; k < 32; k++) x2n[k] = p = host_gf2_mulmod(p, p);
+  hipMemcpyToSymbol(HIP_SYMBOL(c_crc_tab), tab, sizeof tab);
+  hipMemcpyToSymbol(HIP_SYMBOL(c_x2n), x2n, sizeof x2n);
+  done = true;
+}
+
+void launch_crc_check(const uint8_t* C, const int64_t* blk_pos, const int32_t* blk_csize,
+                      const int32_t* blk_usize, const int64_t* uoff, int64_t nblk,
+                      const uint8_t* U, int32_t* status, hipStream_t s) {
+  if (nblk <= 0) return;
+  init_crc_tables();
+  hipLaunchKernelGGL(crc_kernel, dim3((unsigned)nblk), dim3(64), 0, s, C, blk_pos, blk_csize,
+                     blk_usize, uoff, nblk, U, status);
+}
+
+void launch_plan_blocks(const Cand* cand, const int64_t* d_ncand, const int64_t* blk_pos,
+                        const int32_t* blk_usize, const int64_t* uoff, const int64_t* d_nblk,
+                        SplitPlan* plans, int64_t nsplit, hipStream_t s) {
+  if (nsplit <= 0) return;
+  hipLaunchKernelGGL(plan_blocks_kernel, dim3((unsigned)((nsplit + 63) / 64)), dim3(64), 0, s,
+                     cand, d_ncand, blk_pos, blk_usize, uoff, d_nblk, plans, nsplit);
+}
+
+void launch_first_record(const uint8_t* U, int64_t ulen, int32_t u_is_eof, const int32_t* ref_len,
+                         int32_t n_ref, const int64_t* blk_pos, const int64_t* uoff,
+                         const int64_t* d_nblk, SplitPlan* plans, int64_t nsplit, hipStream_t s) {
+  if (nsplit <= 0) return;
+  hipLaunchKernelGGL(first_record_kernel, dim3((unsigned)nsplit), dim3(256), 0, s, U, ulen,
+                     u_is_eof, ref_len, n_ref, blk_pos, uoff, d_nblk, plans, nsplit);
+}
+
+void launch_seg_spec(const uint8_t* U, int64_t ulen, int32_t u_is_eof, const int32_t* ref_len,
+                     int32_t n_ref, Seg* segs, int64_t nseg, int64_t seg_bytes, int64_t start_lin,
+                     hipStream_t s) {
+  if (nseg <= 0) return;
+  hipLaunchKernelGGL(seg_spec_kernel, dim3((unsigned)nseg), dim3(64), 0, s, U, ulen, u_is_eof,
+                     ref_len, n_ref, segs, nseg, seg_bytes, start_lin);
+}
+
+void launch_seg_fix2(const uint8_t* U, int64_t ulen, int32_t u_is_eof, Seg* segs, int64_t nseg,
+                     int64_t seg_bytes, int64_t start_lin, int32_t* d_status, hipStream_t s) {
+  hipLaunchKernelGGL(seg_fix_kernel, dim3(1), dim3(64), 0, s, U, ulen, u_is_eof, segs, nseg,
+                     seg_bytes, start_lin, d_status);
+}
+
+void launch_seg_link(const Seg* segs, int64_t nseg, int64_t seg_bytes, int64_t start_lin,
+                     int64_t ulen, int32_t* d_broken, hipStream_t s) {
+  if (nseg <= 0) return;
+  hipLaunchKernelGGL(seg_link_kernel, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, segs,
+                     nseg, seg_bytes, start_lin, ulen, d_broken);
+}
+
+void launch_seg_counts(const Seg* segs, int64_t nseg, int64_t* counts, hipStream_t s) {
+  hipLaunchKernelGGL(seg_counts_kernel, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s,
+                     segs, nseg, counts);
+}
+
+void launch_seg_emit2(const uint8_t* U, const Seg* segs, const int64_t* base, int64_t nseg,
+                      int64_t* rec_lin, hipStream_t s) {
+  hipLaunchKernelGGL(seg_emit_kernel, dim3((unsigned)((nseg + 63) / 64)), dim3(64), 0, s, U, segs,
+                     base, nseg, rec_lin);
+}
+
+void launch_decode_records(const uint8_t* U, int64_t ulen, const int64_t* rec_lin, int64_t nrec,
+                           const int64_t* blk_pos, const int32_t* blk_csize, const int64_t* uoff,
+                           int64_t nblk, RecSoA soa, int32_t* d_status, hipStream_t s) {
+  if (nrec <= 0) return;
+  hipLaunchKernelGGL(decode_records_kernel, dim3((unsigned)((nrec + 255) / 256)), dim3(256), 0, s,
+                     U, ulen, rec_lin, nrec, blk_pos, blk_csize, uoff, nblk, soa, d_status);
+}
+
+void launch_partition_ranges(const SplitPlan* plans, int64_t nsplit, const int64_t* rec_lin,
+                             const uint64_t* voffset, int64_t nrec, PartRange* parts,
+                             int32_t* d_status, hipStream_t s) {
+  if (nsplit <= 0) return;
+  hipLaunchKernelGGL(partition_ranges_kernel, dim3((unsigned)((nsplit + 63) / 64)), dim3(64), 0, s,
+                     plans, nsplit, rec_lin, voffset, nrec, parts, d_status);
+}
+
+void launch_partition_digest2(const uint64_t* hash, PartRange* parts, int64_t nparts, hipStream_t s) {
+  if (nparts <= 0) return;
+  hipLaunchKernelGGL(partition_digest_kernel, dim3((unsigned)nparts), dim3(256), 0, s, hash, parts,
+                     nparts);
+}
+
+void launch_interval_filter(const uint8_t* U, const int64_t* rec_lin, const RecSoA soa,
+                            const int64_t* idx, int64_t n, const int32_t* iv_ref,
+                            const int32_t* iv_start, const int32_t* iv_end,
+                            const int32_t* ref_iv_begin, int32_t n_ref, uint8_t* keep,
+                            hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(interval_filter_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, U,
+                     rec_lin, soa, idx, n, iv_ref, iv_start, iv_end, ref_iv_begin, n_ref, keep);
+}
+
+}  // namespace dq

@@ -1,0 +1,253 @@
+"""Host-side mirror of Disq's reads API over the MI355X path.
+
+Mirrors, with the same names, argument meaning and error behaviour:
+  HtsjdkReadsRddStorage      D/HtsjdkReadsRddStorage.java:17-131 (read side)
+  HtsjdkReadsRdd             D/HtsjdkReadsRdd.java:16-38
+  HtsjdkReadsTraversalParameters  D/HtsjdkReadsTraversalParameters.java:13-30
+  getReads (AbstractBinarySamSource.java:42-136) with BamSource's planning/iteration
+  (BamSource.java:61-182) executed by libdisq_gpu.so.
+
+There is no Spark here: the "RDD" is the ordered list of partitions Spark would hold, each a
+structure-of-arrays batch of records (plus each record's raw 4 + block_size bytes).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+
+
+class ValidationStringency:
+    STRICT = 0
+    LENIENT = 1
+    SILENT = 2
+    DEFAULT_STRINGENCY = STRICT
+
+
+@dataclass(frozen=True)
+class Interval:
+    """htsjdk.samtools.util.Interval (1-based, closed)."""
+    contig: str
+    start: int
+    end: int
+
+    def getContig(self):
+        return self.contig
+
+    def getStart(self):
+        return self.start
+
+    def getEnd(self):
+        return self.end
+
+
+class HtsjdkReadsTraversalParameters:
+    def __init__(self, intervalsForTraversal: Optional[Sequence[Interval]],
+                 traverseUnplacedUnmapped: bool):
+        self._intervals = None if intervalsForTraversal is None else list(intervalsForTraversal)
+        self._unplaced = bool(traverseUnplacedUnmapped)
+
+    def getIntervalsForTraversal(self):
+        return self._intervals
+
+    def getTraverseUnplacedUnmapped(self):
+        return self._unplaced
+
+
+@dataclass
+class SAMFileHeader:
+    text: str
+    sequences: List[tuple]  # (name, length)
+
+    def getSequenceDictionary(self):
+        return self.sequences
+
+    def getSequenceIndex(self, name):
+        for i, (n, _) in enumerate(self.sequences):
+            if n == name:
+                return i
+        return -1
+
+
+@dataclass
+class ReadsPartition:
+    """Records of one Spark partition, as structure-of-arrays."""
+    fields: dict
+    raw: Optional[np.ndarray]
+    digest: int
+    path: str = ""
+
+    def __len__(self):
+        return len(self.fields["voffset"])
+
+    def record_bytes(self, i):
+        o = int(self.fields["raw_offset"][i])
+        n = 4 + int(self.fields["block_size"][i])
+        return bytes(self.raw[o:o + n])
+
+
+@dataclass
+class ReadsRDD:
+    partitions: List[ReadsPartition] = field(default_factory=list)
+
+    def count(self):
+        return sum(len(p) for p in self.partitions)
+
+    def getNumPartitions(self):
+        return len(self.partitions)
+
+    def field(self, name):
+        arrs = [p.fields[name] for p in self.partitions]
+        return np.concatenate(arrs) if arrs else np.zeros(0)
+
+    def hashes(self):
+        return self.field("hash").astype(np.uint64)
+
+
+class HtsjdkReadsRdd:
+    def __init__(self, header: SAMFileHeader, reads: ReadsRDD):
+        self._header = header
+        self._reads = reads
+
+    def getHeader(self):
+        return self._header
+
+    def getReads(self):
+        return self._reads
+
+
+def _parse_header(raw: bytes) -> SAMFileHeader:
+    import struct
+    l_text = struct.unpack_from("<i", raw, 4)[0]
+    text = raw[8:8 + l_text].decode(errors="replace")
+    p = 8 + l_text
+    n_ref = struct.unpack_from("<i", raw, p)[0]
+    p += 4
+    seqs = []
+    for _ in range(n_ref):
+        ln = struct.unpack_from("<i", raw, p)[0]
+        name = raw[p + 4:p + 4 + ln - 1].decode()
+        length = struct.unpack_from("<i", raw, p + 4 + ln)[0]
+        seqs.append((name, length))
+        p += 8 + ln
+    return SAMFileHeader(text, seqs)
+
+
+def _is_hidden(name):  # HiddenFileFilter (D/impl/file/HiddenFileFilter.java)
+    return name.startswith("_") or name.startswith(".")
+
+
+class HtsjdkReadsRddStorage:
+    """Builder + read() of Disq's reads entry point, backed by libdisq_gpu.so."""
+
+    def __init__(self, device: int = 0):
+        self._split_size = 0
+        self._stringency = ValidationStringency.DEFAULT_STRINGENCY
+        self._use_nio = False
+        self._reference = None
+        self._device = device
+        self._verify_crc = False
+
+    @staticmethod
+    def makeDefault(device: int = 0) -> "HtsjdkReadsRddStorage":
+        return HtsjdkReadsRddStorage(device)
+
+    def splitSize(self, splitSize: int):
+        self._split_size = int(splitSize)
+        return self
+
+    def validationStringency(self, s: int):
+        self._stringency = s
+        return self
+
+    def useNio(self, useNio: bool):
+        self._use_nio = bool(useNio)
+        return self
+
+    def referenceSourcePath(self, p):
+        self._reference = p
+        return self
+
+    def verifyCrc(self, v: bool):
+        """Extension: check every BGZF block's CRC32 (htsjdk's default does not)."""
+        self._verify_crc = bool(v)
+        return self
+
+    def _files(self, path):
+        if os.path.isdir(path):
+            names = sorted(n for n in os.listdir(path) if not _is_hidden(n))
+            return [os.path.join(path, n) for n in names]
+        return [path]
+
+    def read(self, path: str, traversalParameters: Optional[HtsjdkReadsTraversalParameters] = None
+             ) -> HtsjdkReadsRdd:
+        files = self._files(path)
+        if not files:
+            raise ValueError(f"No files found in {path}")
+        first = files[0]
+        if not first.endswith(".bam"):
+            raise ValueError(f"Cannot find format extension for {path}")
+        tp = traversalParameters
+        if tp is not None and tp.getIntervalsForTraversal() is None and \
+                not tp.getTraverseUnplacedUnmapped():
+            # AbstractBinarySamSource.java:50-54
+            raise ValueError("Traversing mapped reads only is not supported.")
+        header = None
+        parts: List[ReadsPartition] = []
+        for f in files:
+            with _lib.Context(split_size=self._split_size, use_nio=self._use_nio,
+                              verify_crc=self._verify_crc, device=self._device,
+                              stringency=self._stringency) as ctx:
+                ctx.open_path(f)
+                _, hraw = ctx.header()
+                h = _parse_header(hraw)
+                if header is None:
+                    header = h
+                trav = None
+                if tp is not None:
+                    bai = self._find_index(f)
+                    if bai is None:
+                        raise ValueError(f"Intervals set but no index file found for {f}")
+                    with open(bai, "rb") as fh:
+                        ctx.set_index(fh.read())
+                    ivs = tp.getIntervalsForTraversal()
+                    conv = None
+                    if ivs is not None:
+                        conv = []
+                        for iv in ivs:  # BoundedTraversalUtil.convertSimpleIntervalToQueryInterval
+                            if iv is None:
+                                raise ValueError("interval may not be null")
+                            idx = h.getSequenceIndex(iv.getContig())
+                            if idx == -1:
+                                raise ValueError(f"Contig {iv.getContig()} not present in reads "
+                                                 "sequence dictionary")
+                            conv.append((idx, iv.getStart(), iv.getEnd()))
+                    trav = (conv, tp.getTraverseUnplacedUnmapped())
+                b = ctx.read(with_raw=True, traversal=trav)
+                po = b["part_offset"]
+                for p in range(len(po) - 1):
+                    lo, hi = int(po[p]), int(po[p + 1])
+                    fields = {k: b[k][lo:hi] for k, _ in _lib.FIELDS}
+                    raw = None
+                    if b["raw"] is not None and hi > lo:
+                        r0 = int(fields["raw_offset"][0])
+                        r1 = int(fields["raw_offset"][-1]) + 4 + int(fields["block_size"][-1])
+                        raw = b["raw"][r0:r1]
+                        fields["raw_offset"] = fields["raw_offset"] - r0
+                    parts.append(ReadsPartition(fields, raw, int(b["part_digest"][p]), f))
+        return HtsjdkReadsRdd(header, ReadsRDD(parts))
+
+    @staticmethod
+    def _find_index(path):
+        # AbstractSamSource.findIndex (D/impl/formats/sam/AbstractSamSource.java:92-108)
+        cand = [path + ".bai"]
+        if path.endswith(".bam"):
+            cand.append(path[: -len(".bam")] + ".bai")
+        for c in cand:
+            if os.path.exists(c):
+                return c
+        return None

@@ -1,0 +1,178 @@
+/*
+ * disq_gpu.h -- C ABI of libdisq_gpu.so, the MI355X (gfx950) BAM read path for Disq.
+ *
+ * Drop-in boundary.  A JNI / Panama shim implements the three
+ * template methods of D/impl/formats/sam/AbstractBinarySamSource.java:138-150 on top of these
+ * calls; callers of HtsjdkReadsRddStorage.read() (D/HtsjdkReadsRddStorage.java:83-131) are
+ * unchanged.  No HIP or torch types cross this boundary: plain pointers and sizes only.
+ *
+ *   reference interface                                         replaced by
+ *   ---------------------------------------------------------   -------------------------------
+ *   BamSource.getPathChunks (D/impl/formats/bam/BamSource.java:61-104)
+ *     = PathSplitSource.getPathSplits (D/impl/file/PathSplitSource.java:26-64)
+ *     + BgzfBlockSource/BgzfBlockGuesser (D/impl/formats/bgzf/BgzfBlockSource.java:34-84,
+ *       BgzfBlockGuesser.java:76-149)
+ *     + getFirstReadInPartition/BamRecordGuesser (BamSource.java:110-153,
+ *       D/impl/formats/bam/BamRecordGuesser.java:34-194)                    dq_plan
+ *   BamSource.getIterator(SamReader, SAMFileSpan) (BamSource.java:172-175)  dq_decode
+ *   BamSource.createIndexIterator + queryUnmapped tail
+ *     (BamSource.java:177-182; AbstractBinarySamSource.java:86-134)       dq_decode_filtered
+ *   AbstractBinarySamSource.getReads, whole RDD (AbstractBinarySamSource.java:42-136)  dq_read
+ *   AbstractSamSource.getFileHeader (D/impl/formats/sam/AbstractSamSource.java:32-49)
+ *                                                                           dq_read_header
+ *
+ * Error mapping (Java side): DQ_EIO -> IOException; DQ_EFORMAT -> htsjdk SAMFormatException;
+ * DQ_EINVAL -> IllegalArgumentException; DQ_EDEVICE / DQ_ENOMEM -> RuntimeException.
+ * Threading: a dq_ctx is used by one thread at a time (one per Spark task thread); each ctx owns
+ * its own HIP stream.  Every call is synchronous with respect to its results.
+ */
+#ifndef DISQ_GPU_H
+#define DISQ_GPU_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DQ_OK 0
+#define DQ_EIO (-1)
+#define DQ_EFORMAT (-2)
+#define DQ_EINVAL (-3)
+#define DQ_EDEVICE (-4)
+#define DQ_ENOMEM (-5)
+
+/* ValidationStringency (htsjdk); recorded, see DESIGN.md "STRICT validation". */
+#define DQ_STRINGENCY_STRICT 0
+#define DQ_STRINGENCY_LENIENT 1
+#define DQ_STRINGENCY_SILENT 2
+
+typedef struct dq_ctx dq_ctx;
+
+/* HtsjdkReadsRddStorage builder state (D/HtsjdkReadsRddStorage.java:19-73) + device knobs. */
+typedef struct dq_opts {
+  int32_t device;            /* HIP device ordinal */
+  int32_t split_size;        /* splitSize(int); 0 = Hadoop default (one split per block) */
+  int32_t use_nio;           /* useNio(boolean): NIO ceil(len/splitSize) splits */
+  int32_t verify_crc;        /* check each BGZF block's CRC32 (stricter than htsjdk default) */
+  int32_t stringency;        /* validationStringency (recorded) */
+  int32_t reserved;
+  int64_t hadoop_block_size; /* fs.local.block.size; 0 = 32 MiB */
+} dq_opts;
+
+/* One Spark partition of the BAM read plan: a PathChunk (D/impl/file/PathChunk.java). */
+typedef struct dq_chunk {
+  int64_t split_start;  /* PathSplit [start, end) */
+  int64_t split_end;
+  uint64_t vstart;      /* Chunk virtual start (first record found by the guesser) */
+  uint64_t vend;        /* Chunk virtual end = (split_end << 16) | 0xffff */
+  int32_t has_chunk;    /* 0: getFirstReadInPartition returned null (empty partition) */
+  int32_t reserved;
+} dq_chunk;
+
+/* Records as structure-of-arrays (fixed BAM fields, SAMv1 §4.2), host memory owned by the
+ * library.  raw holds each record's 4 + block_size bytes (what htsjdk's
+ * SAMRecordFactory.createBAMRecord needs as restOfData) at raw_offset[i]. */
+typedef struct dq_batch {
+  int64_t n_records;
+  uint64_t* voffset;     /* htsjdk start file pointer of the record */
+  int32_t* block_size;
+  int32_t* ref_id;
+  int32_t* pos;          /* 0-based as stored; SAMRecord alignmentStart = pos + 1 */
+  int32_t* l_seq;
+  int32_t* next_ref_id;
+  int32_t* next_pos;
+  int32_t* tlen;
+  uint16_t* flag;
+  uint16_t* bin;
+  uint16_t* n_cigar;
+  uint8_t* mapq;
+  uint8_t* l_read_name;
+  uint64_t* hash;        /* per-record raw-byte hash */
+  int64_t* raw_offset;
+  uint8_t* raw;          /* may be NULL when the caller asked for fields only */
+  int64_t raw_len;
+  int64_t n_partitions;
+  int64_t* part_offset;  /* n_partitions + 1 entries: partition p = [part_offset[p], [p+1]) */
+  uint64_t* part_digest; /* ordered digest of each partition's record hashes */
+} dq_batch;
+
+/* Interval traversal (HtsjdkReadsTraversalParameters, D/HtsjdkReadsTraversalParameters.java):
+ * intervals already converted to (reference index, 1-based start, 1-based end) as in
+ * BoundedTraversalUtil.convertSimpleIntervalToQueryInterval (BoundedTraversalUtil.java:36-53).
+ * intervals == NULL means getIntervalsForTraversal() == null. */
+typedef struct dq_traversal {
+  const int32_t* ref;
+  const int32_t* start;
+  const int32_t* end;
+  int64_t n;
+  int32_t has_intervals;            /* 0: null interval list */
+  int32_t traverse_unplaced_unmapped;
+} dq_traversal;
+
+typedef struct dq_header_info {
+  int32_t n_ref;
+  int32_t reserved;
+  uint64_t first_record_voffset;
+  int64_t header_bytes;   /* l_text etc. total, uncompressed */
+} dq_header_info;
+
+/* Timings / counters of the last pipeline run on the device (for benchmarks). */
+typedef struct dq_stats {
+  int64_t compressed_bytes;
+  int64_t decompressed_bytes;
+  int64_t n_blocks;
+  int64_t n_records;        /* records emitted over all partitions (duplicates included) */
+  int64_t n_partitions;
+  double ms_total;          /* device time of the whole pipeline (HIP events) */
+  double ms_scan;           /* kernel 1: BGZF scan + chain */
+  double ms_inflate;        /* kernel 2: inflate (+CRC) */
+  double ms_records;        /* kernel 3: record starts + SoA decode + hash */
+  double ms_filter;         /* kernel 4: interval filter */
+  double ms_plan;           /* split planning (guesser) */
+  uint64_t digest;          /* digest over partition digests, in partition order */
+} dq_stats;
+
+int dq_ctx_create(dq_ctx** out, const dq_opts* opts);
+void dq_ctx_destroy(dq_ctx* ctx);
+const char* dq_last_error(const dq_ctx* ctx);
+const char* dq_version(void);
+
+/* Open a BAM from host memory (copied to HBM) or from a path.  The resident file is used by
+ * every call below until the next open. */
+int dq_open_memory(dq_ctx* ctx, const uint8_t* bam, int64_t len);
+int dq_open_path(dq_ctx* ctx, const char* path);
+
+/* .bai bytes for interval traversal (AbstractSamSource.findIndex: path.bai or .bam->.bai). */
+int dq_set_index(dq_ctx* ctx, const uint8_t* bai, int64_t len);
+
+int dq_read_header(dq_ctx* ctx, dq_header_info* info, uint8_t* header_bytes, int64_t cap);
+
+/* getPathChunks: all splits of the open file, in Disq partition order.  *chunks is
+ * library-allocated; free with dq_free. */
+int dq_plan(dq_ctx* ctx, dq_chunk** chunks, int64_t* n);
+
+/* getIterator(span): the records of one chunk (start pointer < vend), in file order. */
+int dq_decode(dq_ctx* ctx, uint64_t vstart, uint64_t vend, int32_t with_raw, dq_batch** out);
+
+/* createIndexIterator(intervals, contained=false) over one chunk, plus the unplaced-unmapped
+ * tail when the chunk contains the .bai's start of the last linear bin. */
+int dq_decode_filtered(dq_ctx* ctx, uint64_t vstart, uint64_t vend, const dq_traversal* tr,
+                       int32_t with_raw, dq_batch** out);
+
+/* getReads for the whole file: every partition, in order (tr may be NULL). */
+int dq_read(dq_ctx* ctx, const dq_traversal* tr, int32_t with_raw, dq_batch** out);
+
+/* Run the whole device pipeline on the resident file without copying records back (records
+ * stay in HBM); fills stats.  This is the benchmark entry point. */
+int dq_run_resident(dq_ctx* ctx, const dq_traversal* tr, dq_stats* stats);
+
+/* Device pointer of the resident decompressed stream (for tests), and its length. */
+int dq_debug_inflated(dq_ctx* ctx, uint8_t* host_out, int64_t cap, int64_t* len);
+
+void dq_batch_free(dq_batch* b);
+void dq_free(void* p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
