@@ -66,7 +66,7 @@ class DqStats(C.Structure):
                 ("n_blocks", C.c_int64), ("n_records", C.c_int64), ("n_partitions", C.c_int64),
                 ("ms_total", C.c_double), ("ms_scan", C.c_double), ("ms_inflate", C.c_double),
                 ("ms_records", C.c_double), ("ms_filter", C.c_double), ("ms_plan", C.c_double),
-                ("digest", C.c_uint64)]
+                ("digest", C.c_uint64), ("ms_crc", C.c_double), ("deflate_bytes", C.c_int64)]
 
 
 # Every symbol include/disq_gpu.h declares.

@@ -63,7 +63,8 @@ struct dq_ctx {
   DevBuf slots, counts, offs, cand, flags, voff, scal, tmp;
   int64_t ncand = 0;
   // chain + inflate
-  DevBuf blk_pos, blk_cs, blk_us, uoff, status, U;
+  DevBuf blk_pos, blk_cs, blk_us, uoff, status, U, tok, tokcnt;
+  int n_cu = 256;
   int64_t nblk = 0, ulen = 0;
   // header
   int32_t n_ref = 0;
@@ -398,13 +399,14 @@ static int run_pipeline(dq_ctx* ctx) {
   if ((rc = ensure_all(ctx, ctx->status, sizeof(int32_t) * (size_t)(nblk + 1)))) return rc;
   HIPCHK(hipMemsetAsync(ctx->status.p, 0, sizeof(int32_t) * (size_t)(nblk + 1), s));
   HIPCHK(hipMemsetAsync(ctx->U.as<uint8_t>() + ulen, 0, 256, s));
-  launch_inflate(ctx->C.as<uint8_t>(), ctx->blk_pos.as<int64_t>(), ctx->blk_cs.as<int32_t>(),
-                 ctx->blk_us.as<int32_t>(), ctx->uoff.as<int64_t>(), nblk, ctx->U.as<uint8_t>(),
-                 ctx->status.as<int32_t>(), s);
-  if (ctx->o.verify_crc)
-    launch_crc_check(ctx->C.as<uint8_t>(), ctx->blk_pos.as<int64_t>(), ctx->blk_cs.as<int32_t>(),
-                     ctx->blk_us.as<int32_t>(), ctx->uoff.as<int64_t>(), nblk,
-                     ctx->U.as<uint8_t>(), ctx->status.as<int32_t>(), s);
+  if ((rc = ensure_all(ctx, ctx->tok, (size_t)token_bytes(ulen, nblk)))) return rc;
+  if ((rc = ensure_all(ctx, ctx->tokcnt, sizeof(int32_t) * (size_t)(nblk + 1)))) return rc;
+  init_inflate_tables();
+  HIPCHK(hipEventRecord(ctx->ev[5], s));
+  launch_inflate2(ctx->C.as<uint8_t>(), ctx->blk_pos.as<int64_t>(), ctx->blk_cs.as<int32_t>(),
+                  ctx->blk_us.as<int32_t>(), ctx->uoff.as<int64_t>(), nblk, ctx->tok.as<uint16_t>(),
+                  ctx->tokcnt.as<int32_t>(), d_stat + 8, ctx->U.as<uint8_t>(),
+                  ctx->status.as<int32_t>(), ctx->o.verify_crc, ctx->n_cu, ctx->ev[6], s);
   dbg(s, "inflate", nblk, ulen);
   HIPCHK(hipEventRecord(ctx->ev[2], s));
   {
@@ -541,7 +543,16 @@ static int run_pipeline(dq_ctx* ctx) {
   S.n_records = emitted;
   S.digest = dg;
   S.ms_scan = ev_ms(ctx->ev[0], ctx->ev[1]);
-  S.ms_inflate = ev_ms(ctx->ev[1], ctx->ev[2]);
+  S.ms_inflate = ev_ms(ctx->ev[5], ctx->ev[2]);  // K2a + K2b (CRC fused into K2b)
+  S.ms_crc = ev_ms(ctx->ev[6], ctx->ev[2]);  // K2b alone (resolve + CRC + store)
+  {
+    // DEFLATE payload bytes = sum over blocks of (BSIZE + 1 - 26): csize - 18 header - 8 trailer
+    std::vector<int32_t> cs((size_t)nblk);
+    if (nblk) HIPCHK(hipMemcpy(cs.data(), ctx->blk_cs.p, 4 * (size_t)nblk, hipMemcpyDeviceToHost));
+    int64_t db = 0;
+    for (int32_t c : cs) db += c - 26;
+    S.deflate_bytes = db;
+  }
   S.ms_plan = ev_ms(ctx->ev[2], ctx->ev[3]);
   S.ms_records = ev_ms(ctx->ev[3], ctx->ev[4]);
   S.ms_total = ev_ms(ctx->ev[0], ctx->ev[4]);
@@ -764,6 +775,11 @@ int dq_ctx_create(dq_ctx** out, const dq_opts* opts) {
   }
   HIPCHK(hipSetDevice(ctx->o.device));
   HIPCHK(hipStreamCreateWithFlags(&ctx->s, hipStreamNonBlocking));
+  {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, ctx->o.device) == hipSuccess && prop.multiProcessorCount > 0)
+      ctx->n_cu = prop.multiProcessorCount;
+  }
   for (auto& e : ctx->ev) HIPCHK(hipEventCreate(&e));
   *out = ctx;
   return 0;

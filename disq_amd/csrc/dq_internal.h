@@ -71,13 +71,14 @@ void launch_exclusive_scan_i32(const int32_t* in, int64_t* out, int64_t n, int64
 void launch_exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* tmp,
                                hipStream_t s);
 
-// Kernel 2: inflate every chain block into U at uoff[b]; status per block; optional CRC check.
-void launch_inflate(const uint8_t* C, const int64_t* blk_pos, const int32_t* blk_csize,
-                    const int32_t* blk_usize, const int64_t* uoff, int64_t nblk, uint8_t* U,
-                    int32_t* status, hipStream_t s);
-void launch_crc_check(const uint8_t* C, const int64_t* blk_pos, const int32_t* blk_csize,
-                      const int32_t* blk_usize, const int64_t* uoff, int64_t nblk,
-                      const uint8_t* U, int32_t* status, hipStream_t s);
+// Kernel 2: inflate every chain block into U at uoff[b] (K2a Huffman decode to a u16 token
+// stream, event `mid`, K2b LZ77 resolve + CRC32 in LDS); status per block.
+int64_t token_bytes(int64_t uoff_total, int64_t nblk);
+void init_inflate_tables();
+void launch_inflate2(const uint8_t* C, const int64_t* blk_pos, const int32_t* blk_csize,
+                     const int32_t* blk_usize, const int64_t* uoff, int64_t nblk, uint16_t* tok,
+                     int32_t* tok_count, int32_t* counter, uint8_t* U, int32_t* status,
+                     int32_t verify_crc, int n_cu, hipEvent_t mid, hipStream_t s);
 
 // Split planning (a2-a4).
 struct SplitPlan {

@@ -253,70 +253,6 @@ __global__ void chain_serial_kernel(const uint8_t* __restrict__ C, int64_t L, in
   *d_nblk = n;
 }
 
-// ------------------------------------------------------------------ CRC32
-__constant__ uint32_t c_crc_tab[256];
-
-__device__ inline uint32_t gf2_mulmod(uint32_t a, uint32_t b) {  // reflected, poly 0xEDB88320
-  uint32_t m = 1u << 31, p = 0;
-  if (a == 0) return 0;
-  for (;;) {
-    if (a & m) {
-      p ^= b;
-      if ((a & (m - 1)) == 0) break;
-    }
-    m >>= 1;
-    b = b & 1 ? (b >> 1) ^ 0xEDB88320u : b >> 1;
-  }
-  return p;
-}
-// x^(8n) mod P (reflected), square-and-multiply over the bits of n using x^(2^k) powers.
-__constant__ uint32_t c_x2n[32];
-__device__ inline uint32_t x8nmodp(uint64_t n) {
-  uint32_t p = 1u << 31;  // x^0
-  int k = 3;
-  while (n) {
-    if (n & 1) p = gf2_mulmod(c_x2n[k & 31], p);
-    n >>= 1;
-    k++;
-  }
-  return p;
-}
-
-// One wave per block: lane l hashes bytes [l*S, (l+1)*S) with the byte table, then the lane
-// CRCs are combined with x^(8n) shifts (CRC linearity) and compared with the gzip trailer.
-__global__ __launch_bounds__(64) void crc_kernel(const uint8_t* __restrict__ C, const int64_t* __restrict__ blk_pos,
-                                                 const int32_t* __restrict__ blk_csize,
-                                                 const int32_t* __restrict__ blk_usize,
-                                                 const int64_t* __restrict__ uoff, int64_t nblk,
-                                                 const uint8_t* __restrict__ U,
-                                                 int32_t* __restrict__ status) {
-  __shared__ uint32_t tab[256];
-  for (int i = threadIdx.x; i < 256; i += 64) tab[i] = c_crc_tab[i];
-  __syncthreads();
-  int64_t b = blockIdx.x;
-  if (b >= nblk) return;
-  if (status[b] != ST_OK) return;
-  const int lane = threadIdx.x;
-  const int32_t n = blk_usize[b];
-  const uint8_t* src = U + uoff[b];
-  const int32_t S = (n + 63) / 64;
-  int32_t lo = min(n, lane * S), hi = min(n, lo + S);
-  uint32_t c = 0;  // raw register, zero init
-  for (int32_t i = lo; i < hi; i++) c = tab[(c ^ src[i]) & 0xff] ^ (c >> 8);
-  // shift by the bytes after this lane's segment
-  uint32_t sh = x8nmodp((uint64_t)(n - hi));
-  c = gf2_mulmod(sh, c);
-  for (int o = 32; o >= 1; o >>= 1) c ^= __shfl_xor(c, o, 64);
-  if (lane == 0) {
-    // standard CRC-32: init 0xffffffff, final xor 0xffffffff
-    uint32_t init = gf2_mulmod(0xffffffffu, x8nmodp((uint64_t)n));
-    uint32_t crc = (c ^ init) ^ 0xffffffffu;
-    int64_t p = blk_pos[b] + blk_csize[b] - 8;
-    uint32_t want = (uint32_t)ld32(C, p);
-    if (crc != want) status[b] = ST_CRC;
-  }
-}
-
 // ------------------------------------------------------------------ record guesser
 // BamRecordGuesser.checkRecordStartInternal (BamRecordGuesser.java:79-194) on the linear stream.
 // Returns 1 (start; *next set), 0 (no start), 3 (EOF), 4 (need data beyond the buffer).
@@ -878,46 +814,6 @@ void launch_chain_serial(const uint8_t* C, int64_t clen, int64_t start, int64_t*
                          int32_t* d_status, hipStream_t s) {
   hipLaunchKernelGGL(chain_serial_kernel, dim3(1), dim3(64), 0, s, C, clen, start, blk_pos,
                      blk_csize, blk_usize, cap, d_nblk, d_status);
-}
-
-static uint32_t host_gf2_mulmod(uint32_t a, uint32_t b) {
-  uint32_t m = 1u << 31, p = 0;
-  for (;;) {
-    if (a & m) {
-      p ^= b;
-      if ((a & (m - 1)) == 0) break;
-    }
-    m >>= 1;
-    b = b & 1 ? (b >> 1) ^ 0xEDB88320u : b >> 1;
-  }
-  return p;
-}
-
-void init_crc_tables() {
-  static bool done = false;
-  if (done) return;
-  uint32_t tab[256];
-  for (uint32_t i = 0; i < 256; i++) {
-    uint32_t c = i;
-    for (int k = 0; k < 8; k++) c = c & 1 ? (c >> 1) ^ 0xEDB88320u : c >> 1;
-    tab[i] = c;
-  }
-  uint32_t x2n[32];
-  uint32_t p = 1u << 30;  // x^1
-  x2n[0] = p;
-  for (int k = 1; k < 32; k++) x2n[k] = p = host_gf2_mulmod(p, p);
-  hipMemcpyToSymbol(HIP_SYMBOL(c_crc_tab), tab, sizeof tab);
-  hipMemcpyToSymbol(HIP_SYMBOL(c_x2n), x2n, sizeof x2n);
-  done = true;
-}
-
-void launch_crc_check(const uint8_t* C, const int64_t* blk_pos, const int32_t* blk_csize,
-                      const int32_t* blk_usize, const int64_t* uoff, int64_t nblk,
-                      const uint8_t* U, int32_t* status, hipStream_t s) {
-  if (nblk <= 0) return;
-  init_crc_tables();
-  hipLaunchKernelGGL(crc_kernel, dim3((unsigned)nblk), dim3(64), 0, s, C, blk_pos, blk_csize,
-                     blk_usize, uoff, nblk, U, status);
 }
 
 void launch_plan_blocks(const Cand* cand, const int64_t* d_ncand, const int64_t* blk_pos,

@@ -569,12 +569,19 @@ int dq_synth_bam(const dq_synth_opts* opts, dq_synth_result* res) {
   if (g.o.shape == DQ_SYNTH_LONGREAD && opts->records_per_chunk <= 0) g.per_chunk = 2000;
   g.n_chunks = std::max<int64_t>(1, (g.total_records + g.per_chunk - 1) / g.per_chunk);
   std::vector<Chunk> chunks((size_t)g.n_chunks);
-  std::atomic<int64_t> next{0};
+  std::atomic<int64_t> next{0}, finished{0};
+  const bool progress = getenv("DQ_SYNTH_PROGRESS") != nullptr;
+  const int64_t step = std::max<int64_t>(1, g.n_chunks / 20);
   auto work = [&]() {
     for (;;) {
       int64_t k = next++;
       if (k >= g.n_chunks) break;
       make_chunk(g, k, chunks[(size_t)k], index);
+      int64_t f = ++finished;
+      if (progress && f % step == 0) {
+        fprintf(stderr, "[synth] %lld/%lld chunks\n", (long long)f, (long long)g.n_chunks);
+        fflush(stderr);
+      }
     }
   };
   std::vector<std::thread> th;

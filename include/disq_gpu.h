@@ -125,11 +125,13 @@ typedef struct dq_stats {
   int64_t n_partitions;
   double ms_total;          /* device time of the whole pipeline (HIP events) */
   double ms_scan;           /* kernel 1: BGZF scan + chain */
-  double ms_inflate;        /* kernel 2: inflate (+CRC) */
+  double ms_inflate;        /* kernel 2: the inflate kernel alone */
   double ms_records;        /* kernel 3: record starts + SoA decode + hash */
   double ms_filter;         /* kernel 4: interval filter */
   double ms_plan;           /* split planning (guesser) */
   uint64_t digest;          /* digest over partition digests, in partition order */
+  double ms_crc;            /* CRC32 verification kernel */
+  int64_t deflate_bytes;    /* compressed DEFLATE payload bytes (sum of BSIZE + 1 - 26) */
 } dq_stats;
 
 int dq_ctx_create(dq_ctx** out, const dq_opts* opts);
