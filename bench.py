@@ -78,7 +78,10 @@ def main():
     cpu_data = None
     if rank == 0 and args.cpu_seconds > 0:
         import ctypes
-        cpu_data = ctypes.string_at(res.bam, clen)
+
+        import numpy as np
+        # ctypes.string_at takes a C int length: copy through numpy for files > 2 GiB
+        cpu_data = np.ctypeslib.as_array((ctypes.c_uint8 * clen).from_address(res.bam)).copy()
     free()
 
     def barrier():
