@@ -179,7 +179,7 @@ const char* status_name(int32_t st) {
     case ST_OVERREAD: return "deflate data overrun";
     case ST_CRC: return "CRC mismatch";
     case ST_ISIZE: return "ISIZE out of range";
-    default: return "format error";
+    default: { static char b[32]; snprintf(b, sizeof b, "format error %d", st); return b; }
   }
 }
 
@@ -399,14 +399,42 @@ static int run_pipeline(dq_ctx* ctx) {
   if ((rc = ensure_all(ctx, ctx->status, sizeof(int32_t) * (size_t)(nblk + 1)))) return rc;
   HIPCHK(hipMemsetAsync(ctx->status.p, 0, sizeof(int32_t) * (size_t)(nblk + 1), s));
   HIPCHK(hipMemsetAsync(ctx->U.as<uint8_t>() + ulen, 0, 256, s));
-  if ((rc = ensure_all(ctx, ctx->tok, (size_t)token_bytes(ulen, nblk)))) return rc;
-  if ((rc = ensure_all(ctx, ctx->tokcnt, sizeof(int32_t) * (size_t)(nblk + 1)))) return rc;
-  init_inflate_tables();
-  HIPCHK(hipEventRecord(ctx->ev[5], s));
-  launch_inflate2(ctx->C.as<uint8_t>(), ctx->blk_pos.as<int64_t>(), ctx->blk_cs.as<int32_t>(),
-                  ctx->blk_us.as<int32_t>(), ctx->uoff.as<int64_t>(), nblk, ctx->tok.as<uint16_t>(),
-                  ctx->tokcnt.as<int32_t>(), d_stat + 8, ctx->U.as<uint8_t>(),
-                  ctx->status.as<int32_t>(), ctx->o.verify_crc, ctx->n_cu, ctx->ev[6], s);
+  static const int infl_ver = getenv("DQ_INFLATE") ? atoi(getenv("DQ_INFLATE")) : 3;
+  if (infl_ver == 2) {
+    if ((rc = ensure_all(ctx, ctx->tok, (size_t)token_bytes(ulen, nblk)))) return rc;
+    if ((rc = ensure_all(ctx, ctx->tokcnt, sizeof(int32_t) * (size_t)(nblk + 1)))) return rc;
+    init_inflate_tables();
+    HIPCHK(hipEventRecord(ctx->ev[5], s));
+    launch_inflate2(ctx->C.as<uint8_t>(), ctx->blk_pos.as<int64_t>(), ctx->blk_cs.as<int32_t>(),
+                    ctx->blk_us.as<int32_t>(), ctx->uoff.as<int64_t>(), nblk, ctx->tok.as<uint16_t>(),
+                    ctx->tokcnt.as<int32_t>(), d_stat + 8, ctx->U.as<uint8_t>(),
+                    ctx->status.as<int32_t>(), ctx->o.verify_crc, ctx->n_cu, ctx->ev[6], s);
+  } else {
+    init_inflate3_tables();
+    static const bool timing = getenv("DQ_TIMING") != nullptr;
+    uint64_t* tim = nullptr;
+    if (timing) HIPCHK(hipMalloc(&tim, sizeof(uint64_t) * 12 * (size_t)std::max<int64_t>(1, nblk)));
+    HIPCHK(hipEventRecord(ctx->ev[5], s));
+    launch_inflate3(ctx->C.as<uint8_t>(), ctx->blk_pos.as<int64_t>(), ctx->blk_cs.as<int32_t>(),
+                    ctx->blk_us.as<int32_t>(), ctx->uoff.as<int64_t>(), nblk, ctx->U.as<uint8_t>(),
+                    ctx->status.as<int32_t>(), ctx->o.verify_crc, tim, s);
+    HIPCHK(hipEventRecord(ctx->ev[6], s));
+    if (timing) {
+      std::vector<uint64_t> h(12 * (size_t)nblk);
+      HIPCHK(hipMemcpyAsync(h.data(), tim, 8 * h.size(), hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      (void)hipFree(tim);
+      double acc[12] = {0};
+      for (int64_t i = 0; i < nblk; i++)
+        for (int k = 0; k < 12; k++) acc[k] += (double)h[12 * (size_t)i + k];
+      static const char* nm[12] = {"header", "tables", "spec", "rounds", "scan", "emit",
+                                   "resolve+store", "crc", "-", "-", "n_rounds", "n_dblocks"};
+      fprintf(stderr, "[dq] inflate3 phase cycles per BGZF block (thread 0, s_memtime):");
+      for (int k = 0; k < 12; k++)
+        if (nm[k][0] != '-') fprintf(stderr, " %s=%.0f", nm[k], acc[k] / (double)std::max<int64_t>(1, nblk));
+      fprintf(stderr, "\n");
+    }
+  }
   dbg(s, "inflate", nblk, ulen);
   HIPCHK(hipEventRecord(ctx->ev[2], s));
   {

@@ -1,0 +1,1025 @@
+// dq_inflate3.hip -- Kernel 2 (v3): fused BGZF block inflate + CRC32, one workgroup per block.
+//
+// Replaces htsjdk BlockCompressedInputStream / BlockGunzipper.unzipBlock (htsjdk 2.16.0, reached
+// from D/impl/formats/bam/BamSource.java:172-175) -> java.util.zip.Inflater, plus the CRC32 check
+// that htsjdk leaves off by default.
+//
+// A BGZF block is an independent raw-DEFLATE stream of <= 64 KiB output, so blocks are decoded
+// independently: one 512-thread workgroup per block, the whole output image in LDS (two
+// workgroups per CU: 80 KiB of LDS each).  Per deflate block of the stream:
+//   1. header   -- thread 0 reads BFINAL/BTYPE/HLIT/HDIST/HCLEN; 19 threads read the code-length
+//                  code lengths; 128 threads fill its 7-bit decode table; wave 0 decodes the
+//                  code-length sequence 64 bit offsets at a time (every lane decodes the symbol
+//                  at its offset, the true path is walked with readlane, runs are placed by a
+//                  wave scan).
+//   2. tables   -- canonical codes are assigned in parallel (per-wave ballots give each symbol
+//                  its rank among equal lengths); 10-bit litlen / 8-bit distance root tables of
+//                  16-bit entries (sym << 4 | length) plus 32 / 128-entry second-level tables for
+//                  longer codes, so every code decodes with at most two LDS reads.
+//   3. spec     -- the bit range is cut into NDEC segments; lane t starts decoding at the first
+//                  bit of segment t (an arbitrary bit) and records its EXIT: the first litlen-mode
+//                  symbol boundary at or past the start of segment t+1.  Huffman codes
+//                  self-synchronise, so an exit is almost always on the true symbol path.
+//   4. rounds   -- lane t re-decodes from lane t-1's exit, counting output bytes; a lane whose
+//                  exit changed triggers a re-decode of its successor (Jacobi iteration: lane 0
+//                  starts on the true path, so round r has verified lanes 0..r).
+//   5. emit     -- an exclusive scan of the per-lane byte counts gives every lane its output
+//                  offset; lanes decode once more, writing literals into the LDS image and, for
+//                  each match, a 3-byte descriptor (dist-1 | len-3 << 15) at its first byte plus a
+//                  bit in a match-start bitmap.
+// Then, for the whole BGZF block:
+//   6. resolve  -- lastStart[w] = last match start at or before the end of bitmap word w (a max
+//                  scan), so the owner of any byte is found in O(1).  2 KiB chunks in order: each
+//                  thread resolves 4 bytes by following copy sources (start - dist + (offset mod
+//                  dist)) until a literal or an earlier (already resolved) chunk; resolved 16-byte
+//                  lines are stored to U while the next chunk is resolved.
+//   7. CRC32    -- slice-by-4 per thread over a 128-byte slice, combined across threads by
+//                  multiplying with x^(8n) mod P (precomputed per slice index); compared with the
+//                  gzip trailer.
+// Output stops at ISIZE (Inflater.inflate(buf, 0, ISIZE) semantics); fewer bytes is an error.
+#include "dq_inflate_core.h"
+#include "dq_internal.h"
+
+#include <vector>
+
+namespace dq {
+namespace {
+
+using namespace dqi;
+
+constexpr int WG = 512;           // threads per workgroup
+constexpr int NDEC_MAX = 512;     // speculative decode lanes (<= WG)
+constexpr uint32_t OV = 96;       // speculative warm-up bits before each segment
+constexpr int OUTCAP = 65536 + 20;  // + alignment shift (<= 15) + descriptor overhang
+
+// 16-bit decode table layout: [litlen root | litlen subtables | dist root | dist subtables]
+constexpr int LR = 10, DR = 8;            // root bits
+constexpr int LSB = 15 - LR, DSB = 15 - DR;  // second-level index bits
+constexpr int LSLOTS = 16, DSLOTS = 4;    // second-level tables available
+constexpr int T_LSUB = 1 << LR;
+constexpr int T_DROOT = T_LSUB + LSLOTS * (1 << LSB);
+constexpr int T_DSUB = T_DROOT + (1 << DR);
+constexpr int T_END = T_DSUB + DSLOTS * (1 << DSB);
+constexpr int HB_WORDS = 160;             // staged dynamic-header words (aliases T)
+constexpr uint16_t E_LINK = 0x8000;  // | slot: second-level table
+constexpr uint16_t E_SLOW = 0x4000;  // no second-level table left: canonical decode
+
+enum : int32_t { F_EXIT = 0, F_EOB = 1, F_ERR = 2, F_END = 3 };
+
+struct alignas(16) LdsI {
+  uint8_t out[OUTCAP];            // output image: byte x at out[sh + x]
+  uint32_t bm[2048];              // match-start bitmap
+  union {
+    struct {
+      uint16_t T[T_END];
+      HuffCanon hl, hd;           // canonical descriptions (E_SLOW fallback)
+      uint16_t lsym[288];
+      uint8_t dsym[32];
+      union {
+        struct {
+          uint8_t lens[320];      // litlen lengths [0, 288), distance lengths [288, 320)
+          uint8_t clen[20];
+          uint16_t clt[128];      // code-length code: sym << 3 | len (len 0 = invalid)
+          int32_t cntw[8][16];    // per-wave counts of each code length
+          uint16_t pref[320];     // root prefix of each long code, by canonical position
+          uint8_t slotq[320];     // second-level table of each long code, by canonical position
+        } h;
+      } x;
+    } d;
+    uint16_t last_start[2048];    // resolve: last match start <= end of bitmap word (0xffff none)
+    uint32_t crc4[4][256];
+  } u;
+  int32_t misc[24];
+  int32_t wsum[16];
+  int32_t small[8 * 5];           // per-lane arrays when the image tail is too short
+  uint32_t ltab[29];              // length symbols 257..285: base | extra bits << 16
+  uint32_t dtab[30];              // distance symbols: base | extra bits << 16
+};
+static_assert(sizeof(LdsI) <= 81920, "two workgroups per CU");
+static_assert(HB_WORDS * 4 <= T_END * 2, "header staging fits the decode table");
+
+__constant__ uint32_t c_crc4[4][256];
+__constant__ uint32_t c_slice_shift[WG];  // x^(8 * 128 * k) mod P, k = 0..511
+__constant__ uint8_t c_clorder3[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+// misc slots
+enum { M_ERR = 0, M_BFINAL, M_BTYPE, M_POS, M_A, M_LAST, M_MORE, M_MORE1, M_STLEN, M_STSRC,
+       M_CARRY_MS, M_CARRY_DESC, M_NLEN, M_NDIST, M_NCODE, M_LQ0, M_LQN, M_DQ0, M_DQN, M_NEXT,
+       M_LASTF };
+
+__device__ __attribute__((always_inline)) inline void set_err(LdsI& L, int32_t code) { atomicCAS(&L.misc[M_ERR], 0, code); }
+
+struct BitR {
+  uint64_t bb;
+  uint32_t bc;
+  uint32_t ip;    // index of the next word to merge
+  uint32_t nxt;   // prefetched word W[ip]
+  uint32_t nxt2;  // prefetched word W[ip + 1]
+};
+
+#define DQ_AI __device__ __attribute__((always_inline)) inline
+
+DQ_AI void br_init(BitR& r, const uint32_t* __restrict__ W, uint32_t bitpos) {
+  const uint32_t wi = bitpos >> 5;
+  const uint64_t lo = W[wi], hi = W[wi + 1];
+  const uint32_t sh = bitpos & 31;
+  r.bb = ((hi << 32) | lo) >> sh;
+  r.bc = 64 - sh;
+  r.ip = wi + 2;
+  r.nxt = W[r.ip];
+  r.nxt2 = W[r.ip + 1];
+}
+DQ_AI void br_refill(BitR& r, const uint32_t* __restrict__ W) {
+  if (r.bc <= 32) {
+    r.bb |= (uint64_t)r.nxt << r.bc;
+    r.bc += 32;
+    r.ip++;
+    r.nxt = r.nxt2;
+    r.nxt2 = W[r.ip + 1];
+  }
+}
+DQ_AI uint32_t br_pos(const BitR& r) { return r.ip * 32 - r.bc; }
+DQ_AI uint32_t br_take(BitR& r, uint32_t n) {
+  const uint32_t v = (uint32_t)(r.bb & ((1ull << n) - 1));
+  r.bb >>= n;
+  r.bc -= n;
+  return v;
+}
+// n (<= 25) bits at an arbitrary bit position
+DQ_AI uint32_t peek_bits(const uint32_t* __restrict__ W, uint32_t pos, uint32_t n) {
+  const uint32_t wi = pos >> 5;
+  const uint64_t v = ((uint64_t)W[wi + 1] << 32) | W[wi];
+  return (uint32_t)(v >> (pos & 31)) & ((1u << n) - 1);
+}
+
+enum : int { S_NONE = 0, S_LIT = 1, S_MATCH = 2, S_EOB = 3, S_ERR = 4 };
+
+// 3-byte match descriptor at image byte `a` via two aligned dword reads.
+DQ_AI uint32_t load_desc(const LdsI& L, int a) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(L.out + (a & ~3));
+  const uint64_t v = ((uint64_t)w[1] << 32) | w[0];
+  return (uint32_t)(v >> (8 * (a & 3))) & 0xffffffu;
+}
+
+// Second-level / canonical lookup for a root entry flagged E_LINK or E_SLOW.
+DQ_AI uint32_t ll_second(const LdsI& L, uint32_t e, uint32_t bb) {
+  if (e & E_LINK)
+    return L.u.d.T[T_LSUB + ((e & 15) << LSB) + ((bb >> LR) & ((1u << LSB) - 1))];
+  int l = 0;
+  const int k = canon_decode(bb, L.u.d.hl, LR + 1, &l);
+  return k < 0 ? 0u : (((uint32_t)L.u.d.lsym[k] << 4) | (uint32_t)l);
+}
+DQ_AI uint32_t d_second(const LdsI& L, uint32_t e, uint32_t bb) {
+  if (e & E_LINK)
+    return L.u.d.T[T_DSUB + ((e & 15) << DSB) + ((bb >> DR) & ((1u << DSB) - 1))];
+  int l = 0;
+  const int k = canon_decode(bb, L.u.d.hd, DR + 1, &l);
+  return k < 0 ? 0u : (((uint32_t)L.u.d.dsym[k] << 4) | (uint32_t)l);
+}
+
+// One full symbol: a literal (value in len), a match (len, dist) or EOB.  Straight-line: every
+// lane does the litlen and the distance lookup (a literal lane consumes no distance bits), so a
+// wave mixing literals and matches does not execute both paths one after the other.
+DQ_AI int dsym(BitR& r, const uint32_t* __restrict__ W, const LdsI& L, uint32_t& len,
+               uint32_t& dist) {
+  br_refill(r, W);  // >= 33 bits: a litlen code + its extra bits (<= 20)
+  uint32_t bb = (uint32_t)r.bb;
+  uint32_t e = L.u.d.T[bb & ((1u << LR) - 1)];
+  if (e & (E_LINK | E_SLOW)) e = ll_second(L, e, bb);
+  const uint32_t nb = e & 15, sym = e >> 4;
+  const bool is_len = sym - 257u < 29u;
+  const uint32_t lt = L.ltab[min(sym - 257u, 28u)];
+  const uint32_t lx = is_len ? (lt >> 16) : 0u;
+  len = is_len ? (lt & 0xffffu) + ((bb >> nb) & ((1u << lx) - 1)) : sym;
+  br_take(r, nb + lx);
+  br_refill(r, W);  // >= 33 bits: a distance code + its extra bits (<= 28)
+  bb = (uint32_t)r.bb;
+  uint32_t e2 = L.u.d.T[T_DROOT + (bb & ((1u << DR) - 1))];
+  if (is_len && (e2 & (E_LINK | E_SLOW))) e2 = d_second(L, e2, bb);
+  const uint32_t nb2 = e2 & 15, ds = e2 >> 4;
+  const uint32_t dt = L.dtab[min(ds, 29u)];
+  const uint32_t dx = dt >> 16;
+  dist = (dt & 0xffffu) + ((bb >> nb2) & ((1u << dx) - 1));
+  br_take(r, is_len ? nb2 + dx : 0u);
+  if (nb == 0 || sym > 285) return S_ERR;
+  if (sym < 256) return S_LIT;
+  if (sym == 256) return S_EOB;
+  if (nb2 == 0 || ds >= 30) return S_ERR;
+  return S_MATCH;
+}
+
+enum : int32_t { F_DEAD = 4 };  // speculative path found no boundary >= sB (garbage)
+
+// Decode from `start`; output is counted from the first symbol boundary >= sB (*Bp) and the
+// run stops at the first boundary >= sE (*Ep).  Returns F_EXIT / F_EOB (*Ep = bit after EOB) /
+// F_ERR / F_END (ran off the data) / F_DEAD (no boundary >= sB before an error, EOB or the end).
+DQ_AI int run_seg(const uint32_t* __restrict__ W, const LdsI& L, uint32_t start, uint32_t sB,
+                  uint32_t sE, uint32_t endbits, int32_t* Bp, int32_t* Ep, int32_t* cntp) {
+  BitR r;
+  br_init(r, W, start);
+  bool counting = false;
+  int32_t cnt = 0, B = -1;
+  int f;
+  for (;;) {
+    const uint32_t p = br_pos(r);
+    const bool nc = !counting && p >= sB;
+    B = nc ? (int32_t)p : B;
+    counting = counting || nc;
+    if ((counting && p >= sE) || p >= endbits) {
+      *Ep = (int32_t)p;
+      f = p >= sE && counting ? F_EXIT : (counting ? F_END : F_DEAD);
+      break;
+    }
+    uint32_t len = 0, dist = 0;
+    const int k = dsym(r, W, L, len, dist);
+    if (k > S_MATCH) {
+      *Ep = (int32_t)(k == S_EOB ? br_pos(r) : p);
+      f = !counting ? F_DEAD : (k == S_EOB ? F_EOB : F_ERR);
+      break;
+    }
+    cnt += counting ? (k == S_MATCH ? (int32_t)len : 1) : 0;
+  }
+  *Bp = B;
+  *cntp = cnt;
+  return f;
+}
+
+// Emit from the verified boundary `start` to the first boundary >= target, output starting at
+// absolute position p; stops at isize.
+DQ_AI void emit_seg(const uint32_t* __restrict__ W, LdsI& L, uint32_t start, uint32_t target,
+                    uint32_t endbits, int32_t p, int32_t isize, int sh) {
+  BitR r;
+  br_init(r, W, start);
+  for (;;) {
+    const uint32_t q = br_pos(r);
+    if (q >= target || q >= endbits || p >= isize) return;
+    uint32_t len = 0, dist = 0;
+    const int k = dsym(r, W, L, len, dist);
+    if (k == S_LIT) {
+      L.out[sh + p] = (uint8_t)len;
+      p++;
+    } else if (k == S_MATCH) {
+      if ((int32_t)dist > p) {
+        set_err(L, ST_BAD_DIST);
+        return;
+      }
+      const uint32_t desc = (dist - 1) | ((len - 3) << 15);
+      volatile uint8_t* o = L.out + sh + p;  // byte stores: a merged unaligned b16 store stalls
+      o[0] = (uint8_t)desc;
+      o[1] = (uint8_t)(desc >> 8);
+      o[2] = (uint8_t)(desc >> 16);
+      atomicOr(&L.bm[p >> 5], 1u << (p & 31));
+      p += (int32_t)len;
+    } else {
+      return;  // EOB / error: already accounted for by the rounds
+    }
+  }
+}
+
+__device__ inline uint32_t gf2_mulmod(uint32_t a, uint32_t b) {  // reflected, poly 0xEDB88320
+  uint32_t m = 1u << 31, p = 0;
+  if (a == 0) return 0;
+  for (;;) {
+    if (a & m) {
+      p ^= b;
+      if ((a & (m - 1)) == 0) break;
+    }
+    m >>= 1;
+    b = b & 1 ? (b >> 1) ^ 0xEDB88320u : b >> 1;
+  }
+  return p;
+}
+
+DQ_AI int wave_incl_scan(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(v, o, 64);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+DQ_AI uint64_t lanes_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
+
+// Canonical description of one alphabet from the per-wave length counts (one thread).
+// Returns 0, or ST_BAD_TABLE for an over-subscribed or (except a single code) incomplete code.
+DQ_AI int canon_from_counts(LdsI& L, int w0, int nw, HuffCanon& h) {
+  int left = 1, maxl = 0;
+  uint32_t code = 0, off = 0;
+  h.first[0] = 0;
+  h.count[0] = 0;
+  h.offs[0] = 0;
+  for (int l = 1; l <= 15; l++) {
+    int c = 0;
+    for (int w = w0; w < w0 + nw; w++) c += L.u.d.x.h.cntw[w][l];
+    left = (left << 1) - c;
+    if (left < 0) return ST_BAD_TABLE;
+    if (c) maxl = l;
+    h.first[l] = (uint16_t)code;
+    h.count[l] = (uint16_t)c;
+    h.offs[l] = (uint16_t)off;
+    off += c;
+    code = (code + c) << 1;
+  }
+  if (maxl > 0 && left > 0 && maxl != 1) return ST_BAD_TABLE;  // zlib inflate_table rule
+  return 0;
+}
+
+// Build both decode tables from L.u.d.x.h.lens (all threads; barriers inside).
+// Litlen symbols are handled by threads 0..319 (waves 0-4), distance symbols by wave 5.
+DQ_AI void build_tables(LdsI& L, int nlen, int ndist) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  for (int i = t; i < T_END; i += WG) L.u.d.T[i] = 0;
+  const bool isl = t < 320, isd = t >= 320 && t < 352;
+  const int sym = isl ? t : t - 320;
+  const int len = isl ? (sym < nlen ? L.u.d.x.h.lens[sym] : 0)
+                      : (isd && sym < ndist ? L.u.d.x.h.lens[288 + sym] : 0);
+  // rank among equal lengths inside the wave
+  int rank = 0;
+  if (wv < 6) {
+    for (int l = 1; l <= 15; l++) {
+      const uint64_t m = __ballot(len == l);
+      if (len == l) rank = __popcll(m & lanes_below(lane));
+      if (lane == 0) L.u.d.x.h.cntw[wv][l] = __popcll(m);
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    const int e = canon_from_counts(L, 0, 5, L.u.d.hl);
+    if (e) set_err(L, e);
+  }
+  if (t == 320) {
+    const int e = canon_from_counts(L, 5, 1, L.u.d.hd);
+    if (e) set_err(L, e);
+  }
+  __syncthreads();
+  if (L.misc[M_ERR]) return;
+  const HuffCanon& H = isl ? L.u.d.hl : L.u.d.hd;
+  const int R = isl ? LR : DR;
+  int q = -1;  // canonical position
+  uint32_t code = 0;
+  if (len) {
+    if (isl) for (int w = 0; w < wv; w++) rank += L.u.d.x.h.cntw[w][len];
+    code = H.first[len] + (uint32_t)rank;
+    q = H.offs[len] + rank;
+    if (isl) L.u.d.lsym[q] = (uint16_t)sym;
+    else L.u.d.dsym[q] = (uint8_t)sym;
+    const uint16_t ent = (uint16_t)((sym << 4) | len);
+    if (len <= R) {
+      const uint32_t rv = bitrev(code, len);
+      uint16_t* root = L.u.d.T + (isl ? 0 : T_DROOT);
+      for (uint32_t k = 0; k < (1u << (R - len)); k++) root[rv | (k << len)] = ent;
+    } else {
+      L.u.d.x.h.pref[(isl ? 0 : 288) + q] = (uint16_t)(code >> (len - R));
+    }
+  }
+  // first canonical position of a long code / number of codes, per alphabet
+  if (t == 0) {
+    int n = 0, q0 = 0;
+    for (int l = 1; l <= 15; l++) n += L.u.d.hl.count[l];
+    for (int l = 1; l <= LR; l++) q0 += L.u.d.hl.count[l];
+    L.misc[M_LQ0] = q0;
+    L.misc[M_LQN] = n;
+  }
+  if (t == 320) {
+    int n = 0, q0 = 0;
+    for (int l = 1; l <= 15; l++) n += L.u.d.hd.count[l];
+    for (int l = 1; l <= DR; l++) q0 += L.u.d.hd.count[l];
+    L.misc[M_DQ0] = q0;
+    L.misc[M_DQN] = n;
+  }
+  __syncthreads();
+  // second-level tables: thread t handles canonical position t of each alphabet
+  {
+    const int q0 = isl ? L.misc[M_LQ0] : L.misc[M_DQ0];
+    const int qn = isl ? L.misc[M_LQN] : L.misc[M_DQN];
+    const int base = isl ? 0 : 288;
+    const bool lng = (isl || isd) && sym >= q0 && sym < qn;  // here `sym` = canonical position
+    const uint16_t pf = lng ? L.u.d.x.h.pref[base + sym] : 0;
+    const bool start = lng && (sym == q0 || L.u.d.x.h.pref[base + sym - 1] != pf);
+    const uint64_t sm = __ballot(start);
+    int slot = __popcll(sm & lanes_below(lane)) + (start ? 1 : 0);  // inclusive
+    if (wv < 6 && lane == 0) L.u.d.x.h.cntw[wv][0] = __popcll(sm);
+    __syncthreads();
+    if (isl)
+      for (int w = 0; w < wv; w++) slot += L.u.d.x.h.cntw[w][0];
+    slot -= 1;
+    if (lng) {
+      const int cap = isl ? LSLOTS : DSLOTS;
+      L.u.d.x.h.slotq[base + sym] = (uint8_t)min(slot, 255);
+      if (start) {
+        const int R2 = isl ? LR : DR;
+        const uint32_t ridx = bitrev(pf, R2) + (isl ? 0 : T_DROOT);
+        L.u.d.T[ridx] = slot < cap ? (uint16_t)(E_LINK | slot) : E_SLOW;
+      }
+    }
+  }
+  __syncthreads();
+  if (len > R) {
+    const int slot = L.u.d.x.h.slotq[(isl ? 0 : 288) + q];
+    const int cap = isl ? LSLOTS : DSLOTS;
+    if (slot < cap) {
+      const int sb = isl ? LSB : DSB;
+      const int m = len - R;
+      const uint32_t tail = bitrev(code & ((1u << m) - 1), m);
+      uint16_t* sub = L.u.d.T + (isl ? T_LSUB : T_DSUB) + (slot << sb);
+      const uint16_t ent = (uint16_t)((sym << 4) | len);
+      for (uint32_t k = 0; k < (1u << (sb - m)); k++) sub[tail | (k << m)] = ent;
+    }
+  }
+  __syncthreads();
+}
+
+// Dynamic header: decode the code-length sequence (wave 0) into L.u.d.x.h.lens.
+// Returns the bit position after the header, or sets M_ERR.
+DQ_AI uint32_t read_lengths(const uint32_t* __restrict__ W, LdsI& L, uint32_t P, int nlen,
+                                 int ndist, uint32_t endbits, uint32_t hbase) {
+  // the header's compressed words were staged in the (not yet built) decode table: HB_WORDS
+  // words cover the longest possible header (17 + 57 + 320 * 14 bits)
+  const uint32_t* hb = reinterpret_cast<const uint32_t*>(L.u.d.T);
+  auto word = [&](uint32_t i) -> uint32_t { return hb[min(i - hbase, (uint32_t)HB_WORDS - 1)]; };
+  const int lane = threadIdx.x & 63;
+  const int total = nlen + ndist;
+  int have = 0, prev = -1;
+  for (int iter = 0; iter < 400 && have < total; iter++) {
+    if (P > endbits) {
+      set_err(L, ST_OVERREAD);
+      return P;
+    }
+    const uint32_t wi = P >> 5, off = P & 31;
+    const uint64_t lo = ((uint64_t)word(wi + 1) << 32) | word(wi);
+    const uint64_t hi = ((uint64_t)word(wi + 3) << 32) | word(wi + 2);
+    const uint32_t o = off + (uint32_t)lane;  // <= 94
+    const uint64_t x = o < 64 ? ((lo >> o) | (o ? hi << (64 - o) : 0ull)) : (hi >> (o - 64));
+    const uint32_t bits = (uint32_t)x;
+    const uint32_t ent = L.u.d.x.h.clt[bits & 127];
+    const uint32_t cl = ent & 7, s = ent >> 3;
+    const uint32_t ex = s == 16 ? 2u : s == 17 ? 3u : s == 18 ? 7u : 0u;
+    const uint32_t xv = (bits >> cl) & ((1u << ex) - 1);
+    const int rep = s < 16 ? 1 : s == 16 ? 3 + (int)xv : s == 17 ? 3 + (int)xv : 11 + (int)xv;
+    const int adv = cl ? (int)(cl + ex) : 0;
+    // walk the true symbol path through this window (uniform)
+    uint64_t mark = 0;
+    int j = 0, cum = have;
+    bool bad = false;
+    while (j < 64 && cum < total) {
+      const int a = __builtin_amdgcn_readlane(adv, j);
+      if (a == 0) {
+        bad = true;
+        break;
+      }
+      mark |= 1ull << j;
+      cum += __builtin_amdgcn_readlane(rep, j);
+      j += a;
+    }
+    if (bad || cum > total) {
+      set_err(L, ST_BAD_TABLE);
+      return P;
+    }
+    const bool on = (mark >> lane) & 1;
+    // value written by each symbol: 0-15 literal length, 17/18 zero, 16 the previous value
+    const int v0 = s < 16 ? (int)s : 0;
+    const uint64_t nonrep = mark & __ballot(on && s != 16);
+    // (all lanes shuffle: ds_bpermute returns 0 from inactive source lanes)
+    const uint64_t mb = nonrep & lanes_below(lane);
+    const int pv = __shfl(v0, mb ? 63 - __clzll(mb) : 0, 64);
+    const int val = (on && s == 16) ? (mb ? pv : prev) : v0;
+    if (__any(on && s == 16 && val < 0)) {
+      set_err(L, ST_BAD_TABLE);
+      return P;
+    }
+    const int r = on ? rep : 0;
+    const int incl = wave_incl_scan(r, lane);
+    if (on) {
+      for (int i = have + incl - r; i < have + incl; i++)
+        L.u.d.x.h.lens[i < nlen ? i : 288 + i - nlen] = (uint8_t)val;
+    }
+    const int lastlane = 63 - __clzll(mark);
+    prev = __shfl(val, lastlane, 64);
+    have = cum;
+    P += (uint32_t)j;
+  }
+  if (have < total) set_err(L, ST_BAD_TABLE);
+  return P;
+}
+
+template <bool TIMING, int NDEC, int BPT>
+__global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
+    const uint8_t* __restrict__ C, const int64_t* __restrict__ blk_pos,
+    const int32_t* __restrict__ blk_csize, const int32_t* __restrict__ blk_usize,
+    const int64_t* __restrict__ uoff, int64_t nblk, uint8_t* __restrict__ U,
+    int32_t* __restrict__ status, int32_t verify_crc, const uint32_t* __restrict__ crc_init,
+    uint64_t* __restrict__ tim) {
+  __shared__ LdsI L;
+  // DQ_TIMING: thread 0 accumulates s_memtime cycles per phase (tim != nullptr only then)
+  uint64_t tacc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t tlast = TIMING ? __builtin_amdgcn_s_memtime() : 0;
+#define TST(i)                                            \
+  do {                                                    \
+    if (TIMING && threadIdx.x == 0) {                     \
+      const uint64_t now_ = __builtin_amdgcn_s_memtime(); \
+      tacc[i] += now_ - tlast;                            \
+      tlast = now_;                                       \
+    }                                                     \
+  } while (0)
+#define TCOUNT(i) do { if (TIMING && threadIdx.x == 0) tacc[i] += 1; } while (0)
+  const int64_t b = blockIdx.x;
+  if (b >= nblk) return;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t cpos = blk_pos[b];
+  const int32_t csize = blk_csize[b];
+  const int32_t isize = blk_usize[b];
+  const int64_t ub = uoff[b];
+  const int sh = (int)(ub & 15);
+  // deflate data: bytes [cpos + 18, cpos + csize - 8); bit positions relative to the aligned base
+  // (pointer arithmetic on C keeps the global address space: an integer round trip would turn
+  // every load into a FLAT load, which the compiler must wait for with vmcnt(0) lgkmcnt(0))
+  const uint8_t* dp = C + cpos + 18;
+  const int mis = (int)(reinterpret_cast<uintptr_t>(dp) & 3);
+  const uint32_t* W =
+      reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(dp - mis, 4));
+  const uint32_t a0 = 8u * (uint32_t)mis;
+  const int32_t dbytes = csize - 26;
+  const uint32_t endbits = a0 + 8u * (uint32_t)max(dbytes, 0);
+
+  for (int i = t; i < 2048; i += WG) L.bm[i] = 0;
+  if (t < 24) L.misc[t] = 0;
+  if (t < 29) L.ltab[t] = len_base((uint32_t)t) | (len_extra((uint32_t)t) << 16);
+  if (t >= 64 && t < 94) L.dtab[t - 64] = dist_base((uint32_t)(t - 64)) | (dist_extra((uint32_t)(t - 64)) << 16);
+  if (t == 0) {
+    if (isize < 0 || isize > 65536) L.misc[M_ERR] = ST_ISIZE;
+    else if (dbytes < 0) L.misc[M_ERR] = ST_OVERREAD;
+    L.misc[M_POS] = (int32_t)a0;
+  }
+  __syncthreads();
+  int32_t produced = 0;
+  while (L.misc[M_ERR] == 0 && produced < isize) {
+    // ---- 1. block header
+    if (t == 0) {
+      const uint32_t pos = (uint32_t)L.misc[M_POS];
+      const uint32_t h = peek_bits(W, pos, 17);
+      const int32_t bfinal = (int32_t)(h & 1), btype = (int32_t)((h >> 1) & 3);
+      L.misc[M_BFINAL] = bfinal;
+      L.misc[M_BTYPE] = btype;
+      if (pos + 3 > endbits) {
+        L.misc[M_ERR] = ST_OVERREAD;
+      } else if (btype == 0) {
+        const uint32_t q = (pos + 3 + 7) & ~7u;  // byte boundary
+        const uint8_t* bp = reinterpret_cast<const uint8_t*>(W) + q / 8;
+        const uint32_t len = bp[0] | ((uint32_t)bp[1] << 8), nlen = bp[2] | ((uint32_t)bp[3] << 8);
+        if ((len ^ 0xffffu) != nlen) L.misc[M_ERR] = ST_BAD_STORED;
+        else if (q + 32 + 8 * len > endbits) L.misc[M_ERR] = ST_OVERREAD;
+        L.misc[M_STLEN] = (int32_t)len;
+        L.misc[M_STSRC] = (int32_t)(q / 8 + 4);
+        L.misc[M_POS] = (int32_t)(q + 32 + 8 * len);
+      } else if (btype == 3) {
+        L.misc[M_ERR] = ST_BAD_BLOCKTYPE;
+      } else if (btype == 1) {
+        L.misc[M_NLEN] = 288;
+        L.misc[M_NDIST] = 32;
+        L.misc[M_A] = (int32_t)(pos + 3);
+      } else {
+        const int nlen = (int)((h >> 3) & 31) + 257, ndist = (int)((h >> 8) & 31) + 1;
+        const int ncode = (int)((h >> 13) & 15) + 4;
+        if (nlen > 286 || ndist > 30) L.misc[M_ERR] = ST_BAD_TABLE;
+        L.misc[M_NLEN] = nlen;
+        L.misc[M_NDIST] = ndist;
+        L.misc[M_NCODE] = ncode;
+        L.misc[M_A] = (int32_t)(pos + 17);  // code-length code lengths
+      }
+    }
+    __syncthreads();
+    if (L.misc[M_ERR]) break;
+    const int btype = L.misc[M_BTYPE];
+    if (btype == 0) {  // stored block: copy
+      const int32_t len = L.misc[M_STLEN], src = L.misc[M_STSRC];
+      const uint8_t* sp = reinterpret_cast<const uint8_t*>(W) + src;
+      const int32_t n = min(len, isize - produced);
+      for (int i = t; i < n; i += WG) L.out[sh + produced + i] = sp[i];
+      produced += n;
+      const int32_t fin = L.misc[M_BFINAL];
+      __syncthreads();
+      if (fin) break;
+      continue;
+    }
+    const int nlen = L.misc[M_NLEN], ndist = L.misc[M_NDIST];
+    if (btype == 1) {
+      for (int i = t; i < 320; i += WG) L.u.d.x.h.lens[i] = fixed_len(i);
+      __syncthreads();
+    } else {
+      const int ncode = L.misc[M_NCODE];
+      const uint32_t clpos = (uint32_t)L.misc[M_A];
+      for (int i = t; i < 320; i += WG) L.u.d.x.h.lens[i] = 0;
+      const uint32_t hbase = clpos >> 5;
+      if (t < HB_WORDS) reinterpret_cast<uint32_t*>(L.u.d.T)[t] = W[hbase + t];
+      if (t < 19) L.u.d.x.h.clen[c_clorder3[t]] = t < ncode ? (uint8_t)peek_bits(W, clpos + 3 * t, 3) : 0;
+      __syncthreads();
+      // code-length code: 7-bit table, one entry per thread (canonical decode over 19 lengths)
+      if (t < 128) {
+        int cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        uint8_t cl[19];
+#pragma unroll
+        for (int s = 0; s < 19; s++) cl[s] = L.u.d.x.h.clen[s];
+#pragma unroll
+        for (int s = 0; s < 19; s++)
+#pragma unroll
+          for (int l = 1; l <= 7; l++) cnt[l] += cl[s] == l;
+        int left = 1, code = 0, first = 0;
+        bool ok = true;
+        uint16_t ent = 0;
+        const uint32_t rv = bitrev((uint32_t)t, 7);
+#pragma unroll
+        for (int l = 1; l <= 7; l++) {
+          left = (left << 1) - cnt[l];
+          if (left < 0) ok = false;
+          first = code;
+          code = (code + cnt[l]) << 1;
+          const int c = (int)(rv >> (7 - l));
+          if (ent == 0 && c - first >= 0 && c - first < cnt[l]) {
+            int k = c - first, s2 = 0;
+#pragma unroll
+            for (int s = 0; s < 19; s++)
+              if (cl[s] == l) {
+                if (k == 0) s2 = s;
+                k--;
+              }
+            ent = (uint16_t)((s2 << 3) | l);
+          }
+        }
+        if (left != 0) ok = false;  // the code-length code must be complete
+        L.u.d.x.h.clt[t] = ent;
+        if (t == 0 && !ok) set_err(L, ST_BAD_TABLE);
+      }
+      __syncthreads();
+      if (L.misc[M_ERR]) break;
+      if (wv == 0) {
+        const uint32_t a = read_lengths(W, L, clpos + 3 * (uint32_t)ncode, nlen, ndist, endbits, hbase);
+        if (t == 0) L.misc[M_A] = (int32_t)a;
+      }
+      __syncthreads();
+      if (t == 0 && L.misc[M_ERR] == 0 && L.u.d.x.h.lens[256] == 0) set_err(L, ST_BAD_TABLE);
+      __syncthreads();
+      if (L.misc[M_ERR]) break;
+    }
+    TST(0);
+    // ---- 2. tables
+    build_tables(L, nlen, ndist);
+    TST(1);
+    if (L.misc[M_ERR]) break;
+    const uint32_t a = (uint32_t)L.misc[M_A];
+    if (a > endbits) {
+      if (t == 0) L.misc[M_ERR] = ST_OVERREAD;
+      break;
+    }
+    const uint32_t span = endbits - a;
+    // per-lane arrays live in the not-yet-written tail of the output image
+    const int ob = (sh + produced + 3) & ~3;
+    const int cap = (sh + isize - ob) / 20;
+    int32_t* AB;  // verified start (first boundary >= segment start), -1 none
+    int32_t* AE;  // exit << 3 | flag
+    int32_t* AC;  // output bytes in [B, E)
+    int32_t* LS;  // redo list: lane
+    int32_t* ST;  // redo list: start
+    int nl = (int)max(1u, min((uint32_t)NDEC, span / 128u));
+    if (cap >= 8) {
+      nl = min(nl, cap);
+      AB = reinterpret_cast<int32_t*>(L.out + ob);
+    } else {
+      nl = min(nl, 8);
+      AB = L.small;
+    }
+    AE = AB + nl;
+    AC = AE + nl;
+    LS = AC + nl;
+    ST = LS + nl;
+    const uint32_t seg = (span + nl - 1) / nl;
+    // ---- 3. speculative pass: from OV bits before the segment, counting from its first boundary
+    if (t < nl) {
+      const uint32_t sB = a + (uint32_t)t * seg;
+      const uint32_t start = t == 0 ? a : (sB > a + OV ? sB - OV : a);
+      const uint32_t sE = t == nl - 1 ? 0xffffffffu : a + (uint32_t)(t + 1) * seg;
+      int32_t B = -1, E = 0, c = 0;
+      const int f = run_seg(W, L, start, sB, sE, endbits, &B, &E, &c);
+      AB[t] = B;
+      AE[t] = (E << 3) | f;
+      AC[t] = c;
+    }
+    __syncthreads();
+    TST(2);
+    // ---- 4. rounds: lanes whose first boundary differs from the predecessor's exit re-decode
+    //      from that exit (compacted onto the first threads); repeat until consistent
+    for (int round = 0; round <= nl; round++) {
+      bool need = false;
+      int32_t st = 0;
+      if (t > 0 && t < nl) {
+        const int32_t pe = AE[t - 1];
+        st = pe >> 3;
+        need = (pe & 7) == F_EXIT && AB[t] != st;
+      }
+      const uint64_t nm = __ballot(need);
+      if (lane == 0) L.wsum[wv] = __popcll(nm);
+      __syncthreads();
+      int off = 0, nneed = 0;
+      for (int w = 0; w < WG / 64; w++) {
+        const int c = L.wsum[w];
+        off += w < wv ? c : 0;
+        nneed += c;
+      }
+      if (need) {
+        const int r = off + __popcll(nm & lanes_below(lane));
+        LS[r] = t;
+        ST[r] = st;
+      }
+      __syncthreads();
+      TCOUNT(10);
+      if (nneed == 0) break;
+      if (t < nneed) {
+        const int lt = LS[t];
+        const uint32_t s0 = (uint32_t)ST[t];
+        const uint32_t sE = lt == nl - 1 ? 0xffffffffu : a + (uint32_t)(lt + 1) * seg;
+        int32_t B = -1, E = 0, c = 0;
+        const int f = run_seg(W, L, s0, s0, sE, endbits, &B, &E, &c);
+        AB[lt] = B;
+        AE[lt] = (E << 3) | f;
+        AC[lt] = c;
+      }
+      __syncthreads();
+    }
+    TST(3);
+    TCOUNT(11);
+    // ---- 5. counts -> offsets (the first non-exit lane ends the deflate block)
+    int32_t myB = 0, myE = 0, myF = F_DEAD, myC = 0;
+    if (t < nl) {
+      myB = AB[t];
+      myE = AE[t] >> 3;
+      myF = AE[t] & 7;
+      myC = AC[t];
+    }
+    if (t == 0) L.misc[M_LAST] = nl - 1;
+    __syncthreads();
+    if (t < nl && myF != F_EXIT) atomicMin(&L.misc[M_LAST], t);
+    __syncthreads();
+    const int last = L.misc[M_LAST];
+    const int32_t cv = t <= last ? myC : 0;
+    const int32_t incl = wave_incl_scan(cv, lane);
+    if (lane == 63) L.wsum[wv] = incl;
+    if (t == last) {
+      L.misc[M_NEXT] = myE;
+      L.misc[M_LASTF] = myF;
+    }
+    __syncthreads();
+    int32_t woff = 0;
+    for (int w = 0; w < wv; w++) woff += L.wsum[w];
+    const int32_t myoff = produced + woff + incl - cv;  // absolute output offset of lane t
+    int32_t total = 0;
+    for (int w = 0; w < WG / 64; w++) total += L.wsum[w];
+    // ISIZE: the lane that reaches isize ends the stream (Inflater stops filling its buffer)
+    const bool full = produced + total >= isize;
+    const int32_t fl = L.misc[M_LASTF];
+    if (!full && fl != F_EOB && t == 0) L.misc[M_ERR] = fl == F_ERR ? ST_BAD_CODE : ST_SHORT;
+    __syncthreads();  // the arrays are dead from here: emit overwrites them
+    TST(4);
+    if (L.misc[M_ERR]) break;
+    // ---- emit
+    if (t <= last && myoff < isize) {
+      const uint32_t sE = t == nl - 1 ? 0xffffffffu : a + (uint32_t)(t + 1) * seg;
+      emit_seg(W, L, (uint32_t)myB, sE, endbits, myoff, isize, sh);
+    }
+    const int32_t nextpos = L.misc[M_NEXT];
+    const int32_t fin = L.misc[M_BFINAL];
+    __syncthreads();
+    TST(5);
+    produced = min(isize, produced + total);
+    if (full || fin) break;
+    if (t == 0) L.misc[M_POS] = nextpos;
+    __syncthreads();
+  }
+  __syncthreads();
+  int32_t err = L.misc[M_ERR];
+  if (!err && produced != isize) err = ST_SHORT;
+  if (err) {
+    if (t == 0) status[b] = err;
+    return;
+  }
+  // ---- 6. resolve matches, chunk by chunk
+  {  // last_start: max-scan over bitmap words (4 words per thread)
+    int ls[4];
+    int run = -1;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t m = L.bm[4 * t + k];
+      if (m) run = 32 * (4 * t + k) + 31 - __builtin_clz(m);
+      ls[k] = run;
+    }
+    int wm = run;  // wave inclusive max-scan of the thread's last value
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u2 = __shfl_up(wm, o, 64);
+      if (lane >= o) wm = max(wm, u2);
+    }
+    if (lane == 63) L.wsum[wv] = wm;
+    int ex = __shfl_up(wm, 1, 64);
+    if (lane == 0) ex = -1;
+    __syncthreads();
+    for (int w = 0; w < wv; w++) ex = max(ex, L.wsum[w]);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int v = max(ex, ls[k]);
+      L.u.last_start[4 * t + k] = v < 0 ? (uint16_t)0xffff : (uint16_t)v;
+    }
+    if (t == 0) L.misc[M_CARRY_MS] = -1;
+    __syncthreads();
+  }
+  uint8_t* dstU = U + ub;
+  const uint8_t* O = L.out + sh;
+  const int head = min((16 - sh) & 15, isize);  // bytes before the first 16-byte U boundary
+  int32_t lines_done = 0;                       // 16-byte lines [head + 16k, +16) stored
+  constexpr int CHUNK = BPT * WG;
+  for (int32_t c0 = 0; c0 < isize; c0 += CHUNK) {
+    const int32_t carry_ms = L.misc[M_CARRY_MS];
+    const uint32_t carry_desc = (uint32_t)L.misc[M_CARRY_DESC];
+    const int32_t x0 = c0 + BPT * t;
+    uint32_t word = 0;
+    int32_t next_ms = -1;
+    uint32_t next_desc = 0;
+    for (int k = 0; k < BPT; k++) {
+      int32_t x = x0 + k;
+      if (x >= isize) break;
+      uint8_t val = 0;
+      for (int hop = 0; hop < CHUNK + 2; hop++) {
+        // owner: last match start <= x
+        const int w = x >> 5;
+        const uint32_t m = L.bm[w] & (0xffffffffu >> (31 - (x & 31)));
+        int32_t ms;
+        if (m) ms = w * 32 + 31 - __builtin_clz(m);
+        else ms = w ? (int32_t)L.u.last_start[w - 1] : 0xffff;
+        uint32_t desc;
+        if (ms == 0xffff) {
+          val = O[x];
+          break;
+        }
+        if (ms >= c0) {
+          desc = load_desc(L, sh + ms);
+        } else if (ms == carry_ms) {
+          desc = carry_desc;
+        } else {
+          val = O[x];  // that match ended before this chunk: x is a literal
+          break;
+        }
+        const int32_t len = (int32_t)(desc >> 15) + 3, D = (int32_t)(desc & 0x7fff) + 1;
+        if (hop == 0 && x == c0 + CHUNK - 1 && ms + len > c0 + CHUNK) {
+          next_ms = ms;
+          next_desc = desc;
+        }
+        if (x >= ms + len) {
+          val = O[x];
+          break;
+        }
+        const int32_t j = x - ms;
+        const int32_t src = j < D ? x - D : ms - D + (j % D);
+        if (src < c0) {
+          val = O[src];
+          break;
+        }
+        x = src;
+      }
+      word |= (uint32_t)val << (8 * k);
+    }
+    __syncthreads();
+    for (int k = 0; k < BPT; k++)
+      if (x0 + k < isize) L.out[sh + x0 + k] = (uint8_t)(word >> (8 * k));
+    if (t == WG - 1) {
+      L.misc[M_CARRY_MS] = next_ms;
+      L.misc[M_CARRY_DESC] = (int32_t)next_desc;
+    }
+    __syncthreads();
+    // store the 16-byte U lines completed by this chunk (overlaps the next chunk's resolve)
+    const int32_t c1 = min(isize, c0 + CHUNK);
+    const int32_t lines_to = c1 >= head ? (c1 - head) / 16 : 0;
+    for (int32_t k = lines_done + t; k < lines_to; k += WG)
+      *reinterpret_cast<uint4*>(dstU + head + 16 * k) = *reinterpret_cast<const uint4*>(O + head + 16 * k);
+    lines_done = lines_to;
+  }
+  for (int x = t; x < head; x += WG) dstU[x] = O[x];
+  for (int x = head + 16 * lines_done + t; x < isize; x += WG) dstU[x] = O[x];
+  TST(6);
+  // ---- 7. CRC32: thread t hashes the 128-byte slice ending (511 - t) * 128 bytes before isize
+  if (verify_crc) {
+    __syncthreads();  // last_start is dead: the CRC tables reuse it
+    for (int i = t; i < 1024; i += WG) (&L.u.crc4[0][0])[i] = (&c_crc4[0][0])[i];
+    __syncthreads();
+    const int32_t e = isize - (WG - 1 - t) * 128;
+    const int32_t s0 = max(0, e - 128);
+    uint32_t cr = 0;
+    if (e > 0) {
+      int32_t x = s0;
+      while (x < e && ((sh + x) & 3)) cr = L.u.crc4[0][(cr ^ O[x++]) & 0xff] ^ (cr >> 8);
+      for (; x + 4 <= e; x += 4) {
+        const uint32_t v = cr ^ *reinterpret_cast<const uint32_t*>(O + x);
+        cr = L.u.crc4[3][v & 0xff] ^ L.u.crc4[2][(v >> 8) & 0xff] ^ L.u.crc4[1][(v >> 16) & 0xff] ^
+             L.u.crc4[0][v >> 24];
+      }
+      while (x < e) cr = L.u.crc4[0][(cr ^ O[x++]) & 0xff] ^ (cr >> 8);
+      cr = gf2_mulmod(c_slice_shift[WG - 1 - t], cr);
+    }
+    for (int o = 32; o >= 1; o >>= 1) cr ^= __shfl_xor(cr, o, 64);
+    if (lane == 0) L.wsum[wv] = (int32_t)cr;
+    __syncthreads();
+    if (t == 0) {
+      uint32_t x = 0;
+      for (int w = 0; w < WG / 64; w++) x ^= (uint32_t)L.wsum[w];
+      const uint32_t init = crc_init[isize];  // x^(8 isize) * 0xffffffff mod P
+      const uint32_t crc = (x ^ init) ^ 0xffffffffu;
+      const uint8_t* tr = C + cpos + csize - 8;
+      const uint32_t want = (uint32_t)tr[0] | ((uint32_t)tr[1] << 8) | ((uint32_t)tr[2] << 16) |
+                            ((uint32_t)tr[3] << 24);
+      if (crc != want) status[b] = ST_CRC;
+    }
+  }
+  TST(7);
+  if (TIMING && t == 0)
+    for (int i = 0; i < 12; i++) tim[b * 12 + i] = tacc[i];
+}
+
+uint32_t h_mul(uint32_t a, uint32_t b) {
+  uint32_t m = 1u << 31, p = 0;
+  for (;;) {
+    if (a & m) {
+      p ^= b;
+      if ((a & (m - 1)) == 0) break;
+    }
+    m >>= 1;
+    b = b & 1 ? (b >> 1) ^ 0xEDB88320u : b >> 1;
+  }
+  return p;
+}
+
+uint32_t* g_crc_init = nullptr;
+
+}  // namespace
+
+void init_inflate3_tables() {
+  static bool done = false;
+  if (done) return;
+  uint32_t tab[4][256];
+  for (uint32_t i = 0; i < 256; i++) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; k++) c = c & 1 ? (c >> 1) ^ 0xEDB88320u : c >> 1;
+    tab[0][i] = c;
+  }
+  for (int j = 1; j < 4; j++)
+    for (uint32_t i = 0; i < 256; i++) tab[j][i] = (tab[j - 1][i] >> 8) ^ tab[0][tab[j - 1][i] & 0xff];
+  uint32_t x2n[32];
+  uint32_t p = 1u << 30;  // x^1
+  x2n[0] = p;
+  for (int k = 1; k < 32; k++) x2n[k] = p = h_mul(p, p);
+  // x^(8 * 128 * k) mod P: x^1024 = x2n[10]; powers by repeated multiplication
+  uint32_t sl[WG];
+  sl[0] = 1u << 31;  // x^0
+  for (int k = 1; k < WG; k++) sl[k] = h_mul(sl[k - 1], x2n[10]);
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(c_crc4), tab, sizeof tab);
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(c_slice_shift), sl, sizeof sl);
+  // CRC of n zero bytes with initial register ~0, for every ISIZE n in [0, 65536]
+  std::vector<uint32_t> ini(65537);
+  uint32_t x8 = 1u << 31;  // x^0
+  const uint32_t x8step = x2n[3];  // x^8
+  for (int n = 0; n <= 65536; n++) {
+    ini[(size_t)n] = h_mul(x8, 0xffffffffu);
+    x8 = h_mul(x8, x8step);
+  }
+  (void)hipMalloc(&g_crc_init, sizeof(uint32_t) * ini.size());
+  (void)hipMemcpy(g_crc_init, ini.data(), sizeof(uint32_t) * ini.size(), hipMemcpyHostToDevice);
+  done = true;
+}
+
+void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* blk_csize,
+                     const int32_t* blk_usize, const int64_t* uoff, int64_t nblk, uint8_t* U,
+                     int32_t* status, int32_t verify_crc, uint64_t* tim, hipStream_t s) {
+  if (nblk <= 0) return;
+  static int cfg = -1;
+  if (cfg < 0) {  // DQ_CFG="ndec,bpt" (tuning experiments); default 256,1
+    int nd = 256, bp = 1;
+    if (const char* e = getenv("DQ_CFG")) sscanf(e, "%d,%d", &nd, &bp);
+    cfg = (nd == 512 ? 3 : 0) + (bp == 2 ? 1 : bp == 4 ? 2 : 0);
+  }
+#define DQ_LAUNCH(TM, ND, BP)                                                                  \
+  hipLaunchKernelGGL((inflate_block_kernel<TM, ND, BP>), dim3((unsigned)nblk), dim3(WG), 0, s, C, \
+                     blk_pos, blk_csize, blk_usize, uoff, nblk, U, status, verify_crc, g_crc_init, tim)
+#define DQ_CFGS(TM)                       \
+  switch (cfg) {                          \
+    case 0: DQ_LAUNCH(TM, 256, 1); break; \
+    case 1: DQ_LAUNCH(TM, 256, 2); break; \
+    case 2: DQ_LAUNCH(TM, 256, 4); break; \
+    case 3: DQ_LAUNCH(TM, 512, 1); break; \
+    case 4: DQ_LAUNCH(TM, 512, 2); break; \
+    default: DQ_LAUNCH(TM, 512, 4); break; \
+  }
+  if (tim) {
+    DQ_CFGS(true)
+  } else {
+    DQ_CFGS(false)
+  }
+#undef DQ_CFGS
+#undef DQ_LAUNCH
+}
+
+}  // namespace dq

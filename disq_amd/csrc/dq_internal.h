@@ -80,6 +80,12 @@ void launch_inflate2(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
                      int32_t* tok_count, int32_t* counter, uint8_t* U, int32_t* status,
                      int32_t verify_crc, int n_cu, hipEvent_t mid, hipStream_t s);
 
+// Kernel 2 (v3): fused inflate + CRC32, one workgroup per block (dq_inflate3.hip).
+void init_inflate3_tables();
+void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* blk_csize,
+                     const int32_t* blk_usize, const int64_t* uoff, int64_t nblk, uint8_t* U,
+                     int32_t* status, int32_t verify_crc, uint64_t* tim, hipStream_t s);
+
 // Split planning (a2-a4).
 struct SplitPlan {
   int64_t split_start, split_end;
