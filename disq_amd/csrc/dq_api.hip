@@ -428,7 +428,7 @@ static int run_pipeline(dq_ctx* ctx) {
       for (int64_t i = 0; i < nblk; i++)
         for (int k = 0; k < 12; k++) acc[k] += (double)h[12 * (size_t)i + k];
       static const char* nm[12] = {"header", "tables", "spec", "rounds", "scan", "emit",
-                                   "resolve+store", "crc", "-", "-", "n_rounds", "n_dblocks"};
+                                   "resolve+store", "crc", "spec_iters_sum", "spec_iters_max", "n_rounds", "n_dblocks"};
       fprintf(stderr, "[dq] inflate3 phase cycles per BGZF block (thread 0, s_memtime):");
       for (int k = 0; k < 12; k++)
         if (nm[k][0] != '-') fprintf(stderr, " %s=%.0f", nm[k], acc[k] / (double)std::max<int64_t>(1, nblk));

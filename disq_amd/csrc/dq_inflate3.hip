@@ -109,12 +109,17 @@ enum { M_ERR = 0, M_BFINAL, M_BTYPE, M_POS, M_A, M_LAST, M_MORE, M_MORE1, M_STLE
 
 __device__ __attribute__((always_inline)) inline void set_err(LdsI& L, int32_t code) { atomicCAS(&L.misc[M_ERR], 0, code); }
 
+// Bit reader: a 64-bit LSB-first buffer refilled 32 bits at a time from a 4-word staging
+// queue q0, with the following 4 words already in flight in q1.  A refill never touches a word
+// loaded less than a queue length (~14 symbols) earlier, so its s_waitcnt rarely stalls (moving a
+// just-loaded word between registers would force an immediate vmcnt(0) wait on every refill).
 struct BitR {
   uint64_t bb;
   uint32_t bc;
-  uint32_t ip;    // index of the next word to merge
-  uint32_t nxt;   // prefetched word W[ip]
-  uint32_t nxt2;  // prefetched word W[ip + 1]
+  uint32_t wp;    // word index of the next word to enter bb (br_pos = 32 * wp - bc)
+  uint32_t qn;    // words of q0 consumed
+  uint32_t q0[4];
+  uint32_t q1[4];
 };
 
 #define DQ_AI __device__ __attribute__((always_inline)) inline
@@ -125,20 +130,31 @@ DQ_AI void br_init(BitR& r, const uint32_t* __restrict__ W, uint32_t bitpos) {
   const uint32_t sh = bitpos & 31;
   r.bb = ((hi << 32) | lo) >> sh;
   r.bc = 64 - sh;
-  r.ip = wi + 2;
-  r.nxt = W[r.ip];
-  r.nxt2 = W[r.ip + 1];
+  r.wp = wi + 2;
+  r.qn = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) r.q0[k] = W[wi + 2 + k];
+#pragma unroll
+  for (int k = 0; k < 4; k++) r.q1[k] = W[wi + 6 + k];
 }
 DQ_AI void br_refill(BitR& r, const uint32_t* __restrict__ W) {
   if (r.bc <= 32) {
-    r.bb |= (uint64_t)r.nxt << r.bc;
+    r.bb |= (uint64_t)r.q0[0] << r.bc;
     r.bc += 32;
-    r.ip++;
-    r.nxt = r.nxt2;
-    r.nxt2 = W[r.ip + 1];
+    r.wp++;
+    r.q0[0] = r.q0[1];
+    r.q0[1] = r.q0[2];
+    r.q0[2] = r.q0[3];
+    if (++r.qn == 4) {
+#pragma unroll
+      for (int k = 0; k < 4; k++) r.q0[k] = r.q1[k];
+#pragma unroll
+      for (int k = 0; k < 4; k++) r.q1[k] = W[r.wp + 4 + k];
+      r.qn = 0;
+    }
   }
 }
-DQ_AI uint32_t br_pos(const BitR& r) { return r.ip * 32 - r.bc; }
+DQ_AI uint32_t br_pos(const BitR& r) { return r.wp * 32 - r.bc; }
 DQ_AI uint32_t br_take(BitR& r, uint32_t n) {
   const uint32_t v = (uint32_t)(r.bb & ((1ull << n) - 1));
   r.bb >>= n;
@@ -214,13 +230,14 @@ enum : int32_t { F_DEAD = 4 };  // speculative path found no boundary >= sB (gar
 // run stops at the first boundary >= sE (*Ep).  Returns F_EXIT / F_EOB (*Ep = bit after EOB) /
 // F_ERR / F_END (ran off the data) / F_DEAD (no boundary >= sB before an error, EOB or the end).
 DQ_AI int run_seg(const uint32_t* __restrict__ W, const LdsI& L, uint32_t start, uint32_t sB,
-                  uint32_t sE, uint32_t endbits, int32_t* Bp, int32_t* Ep, int32_t* cntp) {
+                  uint32_t sE, uint32_t endbits, int32_t* Bp, int32_t* Ep, int32_t* cntp,
+                  int32_t* itp = nullptr) {
   BitR r;
   br_init(r, W, start);
   bool counting = false;
-  int32_t cnt = 0, B = -1;
+  int32_t cnt = 0, B = -1, it = 0;
   int f;
-  for (;;) {
+  for (;; it++) {
     const uint32_t p = br_pos(r);
     const bool nc = !counting && p >= sB;
     B = nc ? (int32_t)p : B;
@@ -241,6 +258,7 @@ DQ_AI int run_seg(const uint32_t* __restrict__ W, const LdsI& L, uint32_t start,
   }
   *Bp = B;
   *cntp = cnt;
+  if (itp) *itp = it;
   return f;
 }
 
@@ -698,13 +716,24 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       const uint32_t start = t == 0 ? a : (sB > a + OV ? sB - OV : a);
       const uint32_t sE = t == nl - 1 ? 0xffffffffu : a + (uint32_t)(t + 1) * seg;
       int32_t B = -1, E = 0, c = 0;
-      const int f = run_seg(W, L, start, sB, sE, endbits, &B, &E, &c);
+      int32_t its = 0;
+      const int f = run_seg(W, L, start, sB, sE, endbits, &B, &E, &c, TIMING ? &its : nullptr);
+      if (TIMING) {
+        atomicAdd(&L.misc[21], its);
+        atomicMax(&L.misc[22], its);
+      }
       AB[t] = B;
       AE[t] = (E << 3) | f;
       AC[t] = c;
     }
     __syncthreads();
     TST(2);
+    if (TIMING && t == 0) {
+      tacc[8] += (uint64_t)L.misc[21];
+      tacc[9] += (uint64_t)L.misc[22];
+      L.misc[21] = 0;
+      L.misc[22] = 0;
+    }
     // ---- 4. rounds: lanes whose first boundary differs from the predecessor's exit re-decode
     //      from that exit (compacted onto the first threads); repeat until consistent
     for (int round = 0; round <= nl; round++) {
@@ -838,51 +867,64 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     const int32_t carry_ms = L.misc[M_CARRY_MS];
     const uint32_t carry_desc = (uint32_t)L.misc[M_CARRY_DESC];
     const int32_t x0 = c0 + BPT * t;
-    uint32_t word = 0;
+    // the thread's BPT bytes follow their copy chains together (independent LDS reads overlap)
+    int32_t xs[BPT];
+    uint32_t word = 0, pending = 0;
+#pragma unroll
+    for (int k = 0; k < BPT; k++) {
+      xs[k] = x0 + k;
+      if (x0 + k < isize) pending |= 1u << k;
+    }
     int32_t next_ms = -1;
     uint32_t next_desc = 0;
-    for (int k = 0; k < BPT; k++) {
-      int32_t x = x0 + k;
-      if (x >= isize) break;
-      uint8_t val = 0;
-      for (int hop = 0; hop < CHUNK + 2; hop++) {
-        // owner: last match start <= x
-        const int w = x >> 5;
-        const uint32_t m = L.bm[w] & (0xffffffffu >> (31 - (x & 31)));
-        int32_t ms;
-        if (m) ms = w * 32 + 31 - __builtin_clz(m);
-        else ms = w ? (int32_t)L.u.last_start[w - 1] : 0xffff;
-        uint32_t desc;
-        if (ms == 0xffff) {
-          val = O[x];
-          break;
-        }
-        if (ms >= c0) {
-          desc = load_desc(L, sh + ms);
-        } else if (ms == carry_ms) {
-          desc = carry_desc;
-        } else {
-          val = O[x];  // that match ended before this chunk: x is a literal
-          break;
-        }
-        const int32_t len = (int32_t)(desc >> 15) + 3, D = (int32_t)(desc & 0x7fff) + 1;
-        if (hop == 0 && x == c0 + CHUNK - 1 && ms + len > c0 + CHUNK) {
-          next_ms = ms;
-          next_desc = desc;
-        }
-        if (x >= ms + len) {
-          val = O[x];
-          break;
-        }
-        const int32_t j = x - ms;
-        const int32_t src = j < D ? x - D : ms - D + (j % D);
-        if (src < c0) {
-          val = O[src];
-          break;
-        }
-        x = src;
+    for (int hop = 0; pending != 0 && hop < CHUNK + 2; hop++) {
+      uint32_t mk[BPT], lk[BPT];
+#pragma unroll
+      for (int k = 0; k < BPT; k++) {  // owner lookups: bitmap word + last start before it
+        const int w = xs[k] >> 5;
+        mk[k] = L.bm[w] & (0xffffffffu >> (31 - (xs[k] & 31)));
+        lk[k] = w ? L.u.last_start[w - 1] : 0xffffu;
       }
-      word |= (uint32_t)val << (8 * k);
+      int32_t msk[BPT];
+      uint32_t dk[BPT];
+#pragma unroll
+      for (int k = 0; k < BPT; k++) {
+        const int w = xs[k] >> 5;
+        msk[k] = mk[k] ? w * 32 + 31 - __builtin_clz(mk[k]) : (int32_t)lk[k];
+        dk[k] = load_desc(L, sh + min(max(msk[k], c0), 65535));
+      }
+#pragma unroll
+      for (int k = 0; k < BPT; k++) {
+        if (!((pending >> k) & 1)) continue;
+        const int32_t x = xs[k], ms = msk[k];
+        int32_t from = -1;  // final byte position to read, or -1 to hop on
+        uint32_t desc = dk[k];
+        if (ms == 0xffff) {
+          from = x;
+        } else if (ms < c0) {
+          if (ms == carry_ms) desc = carry_desc;
+          else from = x;  // that match ended before this chunk: x is a literal
+        }
+        if (from < 0) {
+          const int32_t len = (int32_t)(desc >> 15) + 3, D = (int32_t)(desc & 0x7fff) + 1;
+          if (hop == 0 && x == c0 + CHUNK - 1 && ms + len > c0 + CHUNK) {
+            next_ms = ms;
+            next_desc = desc;
+          }
+          if (x >= ms + len) {
+            from = x;
+          } else {
+            const int32_t jj = x - ms;
+            const int32_t src = jj < D ? x - D : ms - D + (jj % D);
+            if (src < c0) from = src;
+            else xs[k] = src;
+          }
+        }
+        if (from >= 0) {
+          word |= (uint32_t)O[from] << (8 * k);
+          pending &= ~(1u << k);
+        }
+      }
     }
     __syncthreads();
     for (int k = 0; k < BPT; k++)
@@ -996,8 +1038,8 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
                      int32_t* status, int32_t verify_crc, uint64_t* tim, hipStream_t s) {
   if (nblk <= 0) return;
   static int cfg = -1;
-  if (cfg < 0) {  // DQ_CFG="ndec,bpt" (tuning experiments); default 256,1
-    int nd = 256, bp = 1;
+  if (cfg < 0) {  // DQ_CFG="ndec,bpt" (tuning experiments); default 512,1
+    int nd = 512, bp = 1;
     if (const char* e = getenv("DQ_CFG")) sscanf(e, "%d,%d", &nd, &bp);
     cfg = (nd == 512 ? 3 : 0) + (bp == 2 ? 1 : bp == 4 ? 2 : 0);
   }
