@@ -73,7 +73,7 @@ class DqStats(C.Structure):
 EXPORTS = ("dq_ctx_create", "dq_ctx_destroy", "dq_last_error", "dq_version", "dq_open_memory",
            "dq_open_path", "dq_set_index", "dq_read_header", "dq_plan", "dq_decode",
            "dq_decode_filtered", "dq_read", "dq_run_resident", "dq_debug_inflated",
-           "dq_batch_free", "dq_free")
+           "dq_batch_free", "dq_free", "dq_open_shard", "dq_header_from_prefix")
 
 _lib = None
 _lock = threading.Lock()
@@ -96,6 +96,9 @@ def lib():
         L.dq_open_memory.argtypes = [vp, vp, C.c_int64]
         L.dq_open_path.argtypes = [vp, C.c_char_p]
         L.dq_set_index.argtypes = [vp, vp, C.c_int64]
+        L.dq_open_shard.argtypes = [vp, vp, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
+                                    vp, C.c_int64]
+        L.dq_header_from_prefix.argtypes = [vp, vp, C.c_int64, vp, C.c_int64, P(C.c_int64)]
         L.dq_read_header.argtypes = [vp, P(DqHeaderInfo), vp, C.c_int64]
         L.dq_plan.argtypes = [vp, P(P(DqChunk)), P(C.c_int64)]
         L.dq_decode.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_int32, P(P(DqBatch))]
@@ -185,6 +188,27 @@ class Context:
     def open_bytes(self, data):
         buf = np.frombuffer(data, np.uint8)
         check(self._h, lib().dq_open_memory(self._h, buf.ctypes.data, len(buf)))
+
+    def open_shard(self, data, base, file_len, p0, p1, header):
+        """Byte-range shard [base, base + len(data)) owning partitions [p0, p1) (dq_open_shard)."""
+        self._shard = np.frombuffer(data, np.uint8)
+        self._hdr = np.frombuffer(header, np.uint8).copy()
+        check(self._h, lib().dq_open_shard(self._h, self._shard.ctypes.data, len(self._shard),
+                                           base, file_len, p0, p1, self._hdr.ctypes.data,
+                                           len(self._hdr)))
+
+    def header_from_prefix(self, data):
+        """Decompressed BAM header from the first bytes of a file (dq_header_from_prefix)."""
+        buf = np.frombuffer(data, np.uint8)
+        n = C.c_int64()
+        out = np.zeros(1 << 20, np.uint8)
+        check(self._h, lib().dq_header_from_prefix(self._h, buf.ctypes.data, len(buf),
+                                                   out.ctypes.data, len(out), C.byref(n)))
+        if n.value > len(out):
+            out = np.zeros(n.value, np.uint8)
+            check(self._h, lib().dq_header_from_prefix(self._h, buf.ctypes.data, len(buf),
+                                                       out.ctypes.data, len(out), C.byref(n)))
+        return bytes(out[: n.value])
 
     def open_path(self, path):
         check(self._h, lib().dq_open_path(self._h, path.encode()))

@@ -55,10 +55,15 @@ struct dq_ctx {
   hipStream_t s = nullptr;
   hipEvent_t ev[8] = {};
   std::string err;
-  // resident file
+  // resident file (or byte-range shard of one: DESIGN.md §8)
   int64_t flen = 0;
   DevBuf C;
   bool have_file = false;
+  bool shard = false;        // C holds file bytes [base, base + flen) of a file_len-byte file
+  int64_t base = 0, file_len = 0;
+  int64_t p0 = 0, p1 = 0;    // Disq partitions owned by the shard
+  std::vector<uint8_t> hdr;  // shard: the decompressed BAM header, supplied by the caller
+  bool header_only = false;  // dq_header_from_prefix: stop after the header
   // kernel 1
   DevBuf slots, counts, offs, cand, flags, voff, scal, tmp;
   int64_t ncand = 0;
@@ -183,51 +188,54 @@ const char* status_name(int32_t st) {
   }
 }
 
-// Parse the BAM header from the front of U (BAMFileReader2.readHeader, H/BAMFileReader2.java:
-// 747-801; readSequenceRecord :807-821).
+// Parse a BAM header (BAMFileReader2.readHeader, H/BAMFileReader2.java:747-801;
+// readSequenceRecord :807-821) from the first n bytes of the decompressed stream.  Returns 0,
+// 1 when more bytes are needed, or a DQ_ error.
+int parse_header_bytes(dq_ctx* ctx, const uint8_t* h, int64_t n) {
+  int64_t p = 0;
+  auto need = [&](int64_t k) { return p + k <= n; };
+  if (!need(8)) return 1;
+  if (memcmp(h, "BAM\1", 4) != 0) RET(DQ_EFORMAT, "Invalid BAM file header");
+  int32_t l_text = rd32(&h[4]);
+  if (l_text < 0) RET(DQ_EFORMAT, "Invalid BAM header text length");
+  p = 8 + (int64_t)l_text;
+  if (!need(4)) return 1;
+  int32_t nr = rd32(&h[(size_t)p]);
+  p += 4;
+  if (nr < 0) RET(DQ_EFORMAT, "Invalid reference count");
+  std::vector<int32_t> lens;
+  std::vector<std::string> names;
+  for (int32_t i = 0; i < nr; i++) {
+    if (!need(4)) return 1;
+    int32_t ln = rd32(&h[(size_t)p]);
+    if (ln <= 1) RET(DQ_EFORMAT, "Invalid BAM file header: missing sequence name");
+    if (!need(4 + (int64_t)ln + 4)) return 1;
+    names.emplace_back((const char*)&h[(size_t)p + 4], (size_t)ln - 1);
+    lens.push_back(rd32(&h[(size_t)(p + 4 + ln)]));
+    p += 8 + ln;
+  }
+  ctx->n_ref = nr;
+  ctx->ref_len = lens;
+  ctx->ref_name = names;
+  ctx->header_bytes = p;
+  return 0;
+}
+
+// The header from the front of U (a shard uses the header bytes its caller supplied).
 int parse_header(dq_ctx* ctx) {
+  if (ctx->shard && !ctx->header_only) {
+    const int rc = parse_header_bytes(ctx, ctx->hdr.data(), (int64_t)ctx->hdr.size());
+    if (rc == 1) RET(DQ_EINVAL, "truncated BAM header given to dq_open_shard");
+    return rc;
+  }
   int64_t want = std::min<int64_t>(ctx->ulen, 1 << 20);
   std::vector<uint8_t> h;
   for (;;) {
     h.resize((size_t)want);
     HIPCHK(hipMemcpy(h.data(), ctx->U.p, (size_t)want, hipMemcpyDeviceToHost));
-    int64_t p = 0;
-    auto need = [&](int64_t n) { return p + n <= want; };
-    bool more = false;
-    if (!need(8)) {
-      more = true;
-    } else {
-      if (memcmp(h.data(), "BAM\1", 4) != 0) RET(DQ_EFORMAT, "Invalid BAM file header");
-      int32_t l_text = rd32(&h[4]);
-      if (l_text < 0) RET(DQ_EFORMAT, "Invalid BAM header text length");
-      p = 8 + (int64_t)l_text;
-      if (!need(4)) {
-        more = true;
-      } else {
-        int32_t nr = rd32(&h[(size_t)p]);
-        p += 4;
-        if (nr < 0) RET(DQ_EFORMAT, "Invalid reference count");
-        std::vector<int32_t> lens;
-        std::vector<std::string> names;
-        for (int32_t i = 0; i < nr && !more; i++) {
-          if (!need(4)) { more = true; break; }
-          int32_t ln = rd32(&h[(size_t)p]);
-          if (ln <= 1) RET(DQ_EFORMAT, "Invalid BAM file header: missing sequence name");
-          if (!need(4 + (int64_t)ln + 4)) { more = true; break; }
-          names.emplace_back((const char*)&h[(size_t)p + 4], (size_t)ln - 1);
-          lens.push_back(rd32(&h[(size_t)(p + 4 + ln)]));
-          p += 8 + ln;
-        }
-        if (!more) {
-          ctx->n_ref = nr;
-          ctx->ref_len = lens;
-          ctx->ref_name = names;
-          ctx->header_bytes = p;
-          return 0;
-        }
-      }
-    }
-    if (!more || want >= ctx->ulen) RET(DQ_EFORMAT, "truncated BAM header");
+    const int rc = parse_header_bytes(ctx, h.data(), want);
+    if (rc != 1) return rc;
+    if (want >= ctx->ulen) RET(DQ_EFORMAT, "truncated BAM header");
     want = std::min<int64_t>(ctx->ulen, want * 4);
   }
 }
@@ -361,26 +369,40 @@ static int run_pipeline(dq_ctx* ctx) {
   if ((rc = ensure_all(ctx, ctx->blk_pos, sizeof(int64_t) * (size_t)capb))) return rc;
   if ((rc = ensure_all(ctx, ctx->blk_cs, sizeof(int32_t) * (size_t)capb))) return rc;
   if ((rc = ensure_all(ctx, ctx->blk_us, sizeof(int32_t) * (size_t)capb))) return rc;
+  // a shard's bytes end inside the file: the end of the buffer is not EOF
+  const int32_t is_eof = (!ctx->shard || ctx->base + L >= ctx->file_len) ? 1 : 0;
   if (ncand > 0)
     launch_chain2(ctx->C.as<uint8_t>(), L, ctx->cand.as<Cand>(), d_ncand, ncand,
                   ctx->voff.as<int64_t>(), ctx->blk_pos.as<int64_t>(), ctx->blk_cs.as<int32_t>(),
-                  ctx->blk_us.as<int32_t>(), capb, d_nblk, d_broken, 1, s);
+                  ctx->blk_us.as<int32_t>(), capb, d_nblk, d_broken, is_eof, s);
   int64_t nblk = 0;
   if ((rc = get_i64(ctx, d_nblk, &nblk))) return rc;
   int32_t broken = 0;
   HIPCHK(hipMemcpy(&broken, d_broken, 4, hipMemcpyDeviceToHost));
-  // The chain must start at the file start (htsjdk reads from block 0).
+  // The chain must start at the file start (htsjdk reads from block 0); a shard's chain starts
+  // at the guesser's first block in its first split (the first valid candidate).
+  int64_t chain_start = 0;
+  if (ctx->shard && ncand > 0) {
+    std::vector<Cand> ch((size_t)ncand);
+    HIPCHK(hipMemcpy(ch.data(), ctx->cand.p, sizeof(Cand) * (size_t)ncand, hipMemcpyDeviceToHost));
+    chain_start = L;
+    for (const Cand& c : ch)
+      if (c.valid == 1) {
+        chain_start = c.pos;
+        break;
+      }
+  }
   if (!broken && ncand > 0) {
     int64_t p0 = 0;
     HIPCHK(hipMemcpy(&p0, ctx->blk_pos.p, sizeof(int64_t), hipMemcpyDeviceToHost));
-    if (p0 != 0) broken = 1;
+    if (p0 != chain_start) broken = 1;
   }
-  if (broken) {  // walk htsjdk headers from 0 (false-positive or non-BC headers present)
+  if (broken) {  // walk htsjdk headers from the start (false-positive or non-BC headers present)
     int64_t capw = L / 26 + 2;
     if ((rc = ensure_all(ctx, ctx->blk_pos, sizeof(int64_t) * (size_t)capw))) return rc;
     if ((rc = ensure_all(ctx, ctx->blk_cs, sizeof(int32_t) * (size_t)capw))) return rc;
     if ((rc = ensure_all(ctx, ctx->blk_us, sizeof(int32_t) * (size_t)capw))) return rc;
-    launch_chain_serial(ctx->C.as<uint8_t>(), L, 0, ctx->blk_pos.as<int64_t>(),
+    launch_chain_serial(ctx->C.as<uint8_t>(), L, chain_start, ctx->blk_pos.as<int64_t>(),
                         ctx->blk_cs.as<int32_t>(), ctx->blk_us.as<int32_t>(), capw, d_nblk, d_stat, s);
     if ((rc = get_i64(ctx, d_nblk, &nblk))) return rc;
   }
@@ -454,13 +476,24 @@ static int run_pipeline(dq_ctx* ctx) {
   }
   // ---- header (n_ref, reference lengths for the guesser)
   if ((rc = parse_header(ctx))) return rc;
+  if (ctx->header_only) return 0;
   if ((rc = ensure_all(ctx, ctx->d_ref_len, sizeof(int32_t) * (size_t)(ctx->n_ref + 1)))) return rc;
   if (ctx->n_ref)
     HIPCHK(hipMemcpyAsync(ctx->d_ref_len.p, ctx->ref_len.data(), sizeof(int32_t) * ctx->n_ref,
                           hipMemcpyHostToDevice, s));
   // ---- planning (a1-a5)
   std::vector<std::pair<int64_t, int64_t>> splits;
-  if (path_splits(ctx->o, L, splits)) RET(DQ_EINVAL, "splitSize must be > 0 with useNio");
+  if (path_splits(ctx->o, ctx->shard ? ctx->file_len : L, splits))
+    RET(DQ_EINVAL, "splitSize must be > 0 with useNio");
+  if (ctx->shard) {  // the shard's partitions, in shard coordinates
+    if (ctx->p0 < 0 || ctx->p1 > (int64_t)splits.size() || ctx->p0 >= ctx->p1)
+      RET(DQ_EINVAL, "shard partition range out of bounds");
+    std::vector<std::pair<int64_t, int64_t>> mine;
+    for (int64_t i = ctx->p0; i < ctx->p1; i++)
+      mine.push_back({splits[(size_t)i].first - ctx->base, splits[(size_t)i].second - ctx->base});
+    if (mine.front().first < 0) RET(DQ_EINVAL, "shard bytes start after its first split");
+    splits.swap(mine);
+  }
   const int64_t nsplit = (int64_t)splits.size();
   ctx->plans_h.assign((size_t)nsplit, SplitPlan{});
   for (int64_t i = 0; i < nsplit; i++) {
@@ -474,7 +507,7 @@ static int run_pipeline(dq_ctx* ctx) {
   launch_plan_blocks(ctx->cand.as<Cand>(), d_ncand, ctx->blk_pos.as<int64_t>(),
                      ctx->blk_us.as<int32_t>(), ctx->uoff.as<int64_t>(), d_nblk,
                      ctx->plans.as<SplitPlan>(), nsplit, s);
-  launch_first_record(ctx->U.as<uint8_t>(), ulen, 1, ctx->d_ref_len.as<int32_t>(), ctx->n_ref,
+  launch_first_record(ctx->U.as<uint8_t>(), ulen, is_eof, ctx->d_ref_len.as<int32_t>(), ctx->n_ref,
                       ctx->blk_pos.as<int64_t>(), ctx->uoff.as<int64_t>(), d_nblk,
                       ctx->plans.as<SplitPlan>(), nsplit, s);
   HIPCHK(hipMemcpyAsync(ctx->plans_h.data(), ctx->plans.p, sizeof(SplitPlan) * (size_t)nsplit,
@@ -484,6 +517,8 @@ static int run_pipeline(dq_ctx* ctx) {
   dbg(s, "plan", nsplit);
   int64_t start_lin = -1;
   for (auto& P : ctx->plans_h) {
+    if (P.status == 100 && ctx->shard && !is_eof)
+      RET(DQ_EFORMAT, "shard halo too small: the record guesser needs bytes past the shard");
     if (P.status != 0) {
       char msg[160];
       snprintf(msg, sizeof msg, "split planning failed (code %d) for split [%lld, %lld)", P.status,
@@ -495,24 +530,35 @@ static int run_pipeline(dq_ctx* ctx) {
   // ---- Kernel 3: record chain, SoA decode, hashes
   int64_t nrec = 0;
   const int64_t SEG = 256 * 1024;
-  if (start_lin >= 0) {
-    const int64_t nseg = (ulen - start_lin + SEG - 1) / SEG;
+  // record starts wanted: all of U, or (shard) those in blocks at or before the last split end
+  int64_t chain_end = ulen;
+  if (ctx->shard && !is_eof && nblk > 0) {
+    std::vector<int64_t> bp((size_t)nblk);
+    HIPCHK(hipMemcpy(bp.data(), ctx->blk_pos.p, 8 * (size_t)nblk, hipMemcpyDeviceToHost));
+    const int64_t last_end = splits.back().second;
+    const int64_t j = std::upper_bound(bp.begin(), bp.end(), last_end) - bp.begin();
+    if (j >= nblk) RET(DQ_EFORMAT, "shard halo too small: no BGZF block after the last split");
+    HIPCHK(hipMemcpy(&chain_end, ctx->uoff.as<int64_t>() + j, 8, hipMemcpyDeviceToHost));
+  }
+  if (start_lin >= 0 && start_lin < chain_end) {
+    const int64_t nseg = (chain_end - start_lin + SEG - 1) / SEG;
     if ((rc = ensure_all(ctx, ctx->segs, sizeof(Seg) * (size_t)(nseg + 1)))) return rc;
     if ((rc = ensure_all(ctx, ctx->segcnt, sizeof(int64_t) * (size_t)(nseg + 1)))) return rc;
     if ((rc = ensure_all(ctx, ctx->segbase, sizeof(int64_t) * (size_t)(nseg + 1)))) return rc;
     HIPCHK(hipMemsetAsync(d_broken, 0, 8, s));
-    launch_seg_spec(ctx->U.as<uint8_t>(), ulen, 1, ctx->d_ref_len.as<int32_t>(), ctx->n_ref,
+    launch_seg_spec(ctx->U.as<uint8_t>(), ulen, is_eof, chain_end, ctx->d_ref_len.as<int32_t>(), ctx->n_ref,
                     ctx->segs.as<Seg>(), nseg, SEG, start_lin, s);
-    launch_seg_link(ctx->segs.as<Seg>(), nseg, SEG, start_lin, ulen, d_broken, s);
+    launch_seg_link(ctx->segs.as<Seg>(), nseg, SEG, start_lin, chain_end, d_broken, s);
     int32_t br = 0;
     HIPCHK(hipMemcpyAsync(&br, d_broken, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     if (br) {
-      launch_seg_fix2(ctx->U.as<uint8_t>(), ulen, 1, ctx->segs.as<Seg>(), nseg, SEG, start_lin,
+      launch_seg_fix2(ctx->U.as<uint8_t>(), ulen, is_eof, chain_end, ctx->segs.as<Seg>(), nseg, SEG, start_lin,
                       d_stat, s);
       int32_t st = 0;
       HIPCHK(hipMemcpyAsync(&st, d_stat, 4, hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
+      if (st == 4) RET(DQ_EFORMAT, "shard halo too small: the record chain runs past the shard bytes");
       if (st) RET(DQ_EFORMAT, st == ST_BAD_CODE ? "Invalid record length" : "truncated record chain");
     }
     dbg(s, "segs", nseg, br);
@@ -553,6 +599,7 @@ static int run_pipeline(dq_ctx* ctx) {
   HIPCHK(hipMemcpyAsync(&st, d_stat, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   if (st == 101) RET(DQ_EFORMAT, "record guesser start is not on the record chain");
+  if (st && ctx->shard && !is_eof) RET(DQ_EFORMAT, "shard halo too small: a record ends past the shard bytes");
   if (st) RET(DQ_EFORMAT, "truncated BAM record");
   // stats
   dq_stats& S = ctx->stats;
@@ -653,6 +700,8 @@ static int make_batch(dq_ctx* ctx, const std::vector<std::pair<int64_t, int64_t>
     dq_batch_free(b);
     return rc;
   }
+  if (ctx->base)
+    for (int64_t i = 0; i < n; i++) b->voffset[i] += (uint64_t)ctx->base << 16;
   int64_t raw_len = 0;
   for (int64_t i = 0; i < n; i++) {
     b->raw_offset[i] = raw_len;
@@ -701,6 +750,9 @@ static int make_batch(dq_ctx* ctx, const std::vector<std::pair<int64_t, int64_t>
 static int chunk_range(dq_ctx* ctx, uint64_t vstart, uint64_t vend, int64_t* b, int64_t* e) {
   int rc;
   if ((rc = fetch_index(ctx))) return rc;
+  const uint64_t vb = (uint64_t)ctx->base << 16;  // file coordinates -> shard coordinates
+  vstart = vstart >= vb ? vstart - vb : 0;
+  vend = vend >= vb ? vend - vb : 0;
   auto& v = ctx->voff_h;
   auto it = std::lower_bound(v.begin(), v.end(), vstart);
   if (it == v.end() || *it != vstart) {
@@ -764,11 +816,13 @@ static int filtered_indices(dq_ctx* ctx, uint64_t vstart, uint64_t vend, int64_t
     for (int64_t k = 0; k < n; k++)
       if (keep[(size_t)k]) out.push_back(b + k);
   }
+  const uint64_t vb = (uint64_t)ctx->base << 16;
+  const uint64_t solb = ctx->solb >= 0 && (uint64_t)ctx->solb >= vb ? (uint64_t)ctx->solb - vb : 0;
   if (tr->traverse_unplaced_unmapped && ctx->solb != -1 && ctx->ncc >= 1 &&
-      vstart <= (uint64_t)ctx->solb && (uint64_t)ctx->solb < vend) {
+      (uint64_t)ctx->solb >= vb && vstart <= solb && solb < vend) {
     if ((rc = fetch_index(ctx))) return rc;
     auto& v = ctx->voff_h;
-    auto it = std::lower_bound(v.begin(), v.end(), (uint64_t)ctx->solb);
+    auto it = std::lower_bound(v.begin(), v.end(), solb);
     int64_t k = it - v.begin();
     if (k < ctx->nrec) {
       std::vector<int32_t> refs((size_t)(ctx->nrec - k));
@@ -835,6 +889,27 @@ int dq_open_memory(dq_ctx* ctx, const uint8_t* bam, int64_t len) {
   ctx->flen = len;
   ctx->have_file = true;
   ctx->have_pipeline = false;
+  ctx->shard = false;
+  ctx->base = 0;
+  ctx->file_len = len;
+  ctx->p0 = 0;
+  ctx->p1 = 0;
+  return 0;
+}
+
+int dq_open_shard(dq_ctx* ctx, const uint8_t* bytes, int64_t len, int64_t base, int64_t file_len,
+                  int64_t p0, int64_t p1, const uint8_t* header, int64_t header_len) {
+  if (!ctx || (!bytes && len > 0) || len < 0 || base < 0 || base + len > file_len || p0 < 0 ||
+      p1 <= p0 || !header || header_len <= 0)
+    return DQ_EINVAL;
+  const int rc = dq_open_memory(ctx, bytes, len);
+  if (rc) return rc;
+  ctx->shard = true;
+  ctx->base = base;
+  ctx->file_len = file_len;
+  ctx->p0 = p0;
+  ctx->p1 = p1;
+  ctx->hdr.assign(header, header + header_len);
   return 0;
 }
 
@@ -850,6 +925,25 @@ int dq_open_path(dq_ctx* ctx, const char* path) {
   fclose(f);
   if ((int64_t)got != len) RET(DQ_EIO, std::string("short read on ") + path);
   return dq_open_memory(ctx, buf.data(), len);
+}
+
+int dq_header_from_prefix(dq_ctx* ctx, const uint8_t* bytes, int64_t len, uint8_t* out,
+                          int64_t cap, int64_t* out_len) {
+  if (!ctx || !bytes || len <= 0) return DQ_EINVAL;
+  int rc = dq_open_memory(ctx, bytes, len);
+  if (rc) return rc;
+  ctx->shard = true;  // the prefix is not the whole file: its end is not EOF
+  ctx->file_len = INT64_MAX / 4;
+  ctx->header_only = true;
+  rc = run_pipeline(ctx);
+  ctx->header_only = false;
+  ctx->have_pipeline = false;
+  ctx->have_file = false;  // the prefix is not a usable file
+  if (rc) return rc;
+  if (out_len) *out_len = ctx->header_bytes;
+  if (out && cap > 0)
+    HIPCHK(hipMemcpy(out, ctx->U.p, (size_t)std::min(cap, ctx->header_bytes), hipMemcpyDeviceToHost));
+  return 0;
 }
 
 int dq_set_index(dq_ctx* ctx, const uint8_t* bai, int64_t len) {
@@ -877,12 +971,13 @@ int dq_read_header(dq_ctx* ctx, dq_header_info* info, uint8_t* header_bytes, int
     if (ctx->nrec) {
       uint64_t v;
       HIPCHK(hipMemcpy(&v, ctx->f_voff.p, 8, hipMemcpyDeviceToHost));
-      info->first_record_voffset = v;
+      info->first_record_voffset = v + ((uint64_t)ctx->base << 16);
     }
   }
   if (header_bytes && cap > 0) {
     int64_t n = std::min(cap, ctx->header_bytes);
-    HIPCHK(hipMemcpy(header_bytes, ctx->U.p, (size_t)n, hipMemcpyDeviceToHost));
+    if (ctx->shard) memcpy(header_bytes, ctx->hdr.data(), (size_t)n);
+    else HIPCHK(hipMemcpy(header_bytes, ctx->U.p, (size_t)n, hipMemcpyDeviceToHost));
   }
   return 0;
 }
@@ -895,11 +990,12 @@ int dq_plan(dq_ctx* ctx, dq_chunk** chunks, int64_t* n) {
   dq_chunk* c = (dq_chunk*)calloc((size_t)std::max<int64_t>(1, *n), sizeof(dq_chunk));
   for (int64_t i = 0; i < *n; i++) {
     const SplitPlan& P = ctx->plans_h[(size_t)i];
-    c[i].split_start = P.split_start;
-    c[i].split_end = P.split_end;
+    const uint64_t vb = (uint64_t)ctx->base << 16;  // shard coordinates -> file coordinates
+    c[i].split_start = P.split_start + ctx->base;
+    c[i].split_end = P.split_end + ctx->base;
     c[i].has_chunk = P.rec_lin >= 0;
-    c[i].vstart = P.rec_lin >= 0 ? P.vstart : 0;
-    c[i].vend = P.vend;
+    c[i].vstart = P.rec_lin >= 0 ? P.vstart + vb : 0;
+    c[i].vend = P.vend + vb;
   }
   *chunks = c;
   return 0;
@@ -923,8 +1019,11 @@ int dq_decode_filtered(dq_ctx* ctx, uint64_t vstart, uint64_t vend, const dq_tra
   if (rc) return rc;
   int64_t b, e;
   if ((rc = chunk_range(ctx, vstart, vend, &b, &e))) return rc;
+  const uint64_t vb = (uint64_t)ctx->base << 16;
   std::vector<int64_t> idx;
-  if ((rc = filtered_indices(ctx, vstart, vend, b, e, tr, idx))) return rc;
+  if ((rc = filtered_indices(ctx, vstart >= vb ? vstart - vb : 0, vend >= vb ? vend - vb : 0, b, e,
+                             tr, idx)))
+    return rc;
   return make_batch(ctx, {}, &idx, with_raw, {0, (int64_t)idx.size()}, out);
 }
 

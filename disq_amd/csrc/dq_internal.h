@@ -111,12 +111,14 @@ struct Seg {
   int32_t exact;
   int32_t status;
 };
-void launch_seg_spec(const uint8_t* U, int64_t ulen, int32_t u_is_eof, const int32_t* ref_len,
-                     int32_t n_ref, Seg* segs, int64_t nseg, int64_t seg_bytes, int64_t start_lin,
-                     hipStream_t s);
+// Segments cover [start_lin, chain_end) (record starts wanted); ulen bounds the readable bytes.
+void launch_seg_spec(const uint8_t* U, int64_t ulen, int32_t u_is_eof, int64_t chain_end,
+                     const int32_t* ref_len, int32_t n_ref, Seg* segs, int64_t nseg,
+                     int64_t seg_bytes, int64_t start_lin, hipStream_t s);
 void launch_seg_link(const Seg* segs, int64_t nseg, int64_t seg_bytes, int64_t start_lin,
                      int64_t ulen, int32_t* d_broken, hipStream_t s);
-void launch_seg_fix2(const uint8_t* U, int64_t ulen, int32_t u_is_eof, Seg* segs, int64_t nseg,
+void launch_seg_fix2(const uint8_t* U, int64_t ulen, int32_t u_is_eof, int64_t chain_end,
+                     Seg* segs, int64_t nseg,
                      int64_t seg_bytes, int64_t start_lin, int32_t* d_status, hipStream_t s);
 void launch_seg_counts(const Seg* segs, int64_t nseg, int64_t* counts, hipStream_t s);
 void launch_seg_emit2(const uint8_t* U, const Seg* segs, const int64_t* base, int64_t nseg,

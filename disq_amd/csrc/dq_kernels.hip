@@ -494,11 +494,11 @@ __global__ __launch_bounds__(64) void seg_spec_kernel(const uint8_t* __restrict_
                                                       const int32_t* __restrict__ ref_len,
                                                       int32_t n_ref, Seg* __restrict__ segs,
                                                       int64_t nseg, int64_t seg_bytes,
-                                                      int64_t start_lin) {
+                                                      int64_t start_lin, int64_t chain_end) {
   int64_t s = blockIdx.x;
   if (s >= nseg) return;
   const int64_t sb = start_lin + s * seg_bytes;
-  const int64_t se = min(ulen, sb + seg_bytes);
+  const int64_t se = min(chain_end, sb + seg_bytes);
   __shared__ int64_t best;
   if (threadIdx.x == 0) best = INT64_MAX;
   __syncthreads();
@@ -541,7 +541,7 @@ __global__ __launch_bounds__(64) void seg_spec_kernel(const uint8_t* __restrict_
 // incoming position.
 __global__ void seg_fix_kernel(const uint8_t* __restrict__ U, int64_t ulen, int32_t u_is_eof,
                                Seg* __restrict__ segs, int64_t nseg, int64_t seg_bytes,
-                               int64_t start_lin, int32_t* d_status) {
+                               int64_t start_lin, int64_t chain_end, int32_t* d_status) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   int64_t in = segs[0].exit;
   if (segs[0].status) {
@@ -551,7 +551,7 @@ __global__ void seg_fix_kernel(const uint8_t* __restrict__ U, int64_t ulen, int3
   for (int64_t s = 1; s < nseg; s++) {
     Seg& g = segs[s];
     const int64_t sb = start_lin + s * seg_bytes;
-    const int64_t se = min(ulen, sb + seg_bytes);
+    const int64_t se = min(chain_end, sb + seg_bytes);
     if (in == END_CHAIN || in >= se) {  // no record starts inside this segment
       g.start = in;
       g.exit = in;
@@ -832,18 +832,20 @@ void launch_first_record(const uint8_t* U, int64_t ulen, int32_t u_is_eof, const
                      u_is_eof, ref_len, n_ref, blk_pos, uoff, d_nblk, plans, nsplit);
 }
 
-void launch_seg_spec(const uint8_t* U, int64_t ulen, int32_t u_is_eof, const int32_t* ref_len,
+void launch_seg_spec(const uint8_t* U, int64_t ulen, int32_t u_is_eof, int64_t chain_end,
+                     const int32_t* ref_len,
                      int32_t n_ref, Seg* segs, int64_t nseg, int64_t seg_bytes, int64_t start_lin,
                      hipStream_t s) {
   if (nseg <= 0) return;
   hipLaunchKernelGGL(seg_spec_kernel, dim3((unsigned)nseg), dim3(64), 0, s, U, ulen, u_is_eof,
-                     ref_len, n_ref, segs, nseg, seg_bytes, start_lin);
+                     ref_len, n_ref, segs, nseg, seg_bytes, start_lin, chain_end);
 }
 
-void launch_seg_fix2(const uint8_t* U, int64_t ulen, int32_t u_is_eof, Seg* segs, int64_t nseg,
-                     int64_t seg_bytes, int64_t start_lin, int32_t* d_status, hipStream_t s) {
+void launch_seg_fix2(const uint8_t* U, int64_t ulen, int32_t u_is_eof, int64_t chain_end,
+                     Seg* segs, int64_t nseg, int64_t seg_bytes, int64_t start_lin,
+                     int32_t* d_status, hipStream_t s) {
   hipLaunchKernelGGL(seg_fix_kernel, dim3(1), dim3(64), 0, s, U, ulen, u_is_eof, segs, nseg,
-                     seg_bytes, start_lin, d_status);
+                     seg_bytes, start_lin, chain_end, d_status);
 }
 
 void launch_seg_link(const Seg* segs, int64_t nseg, int64_t seg_bytes, int64_t start_lin,

@@ -144,6 +144,24 @@ const char* dq_version(void);
 int dq_open_memory(dq_ctx* ctx, const uint8_t* bam, int64_t len);
 int dq_open_path(dq_ctx* ctx, const char* path);
 
+/* Byte-range shard of one file (multi-GPU): `bytes` are the file's bytes
+ * [base, base + len) -- from the start of split p0 through the end of split p1 - 1, plus a halo
+ * long enough to hold the last partition's straddling record (the end of the halo may cut a
+ * BGZF block).  `file_len` is the whole file's length (split arithmetic) and the shard owns Disq
+ * partitions [p0, p1).  `header` is the decompressed BAM header (dq_read_header of the file's
+ * first bytes), which the record guesser needs.  Every later call reports file coordinates
+ * (split offsets and virtual offsets), exactly as for the whole file.  A halo that is too short
+ * fails with DQ_EFORMAT "shard halo too small" (retry with more bytes). */
+int dq_open_shard(dq_ctx* ctx, const uint8_t* bytes, int64_t len, int64_t base, int64_t file_len,
+                  int64_t p0, int64_t p1, const uint8_t* header, int64_t header_len);
+
+/* The decompressed BAM header (AbstractSamSource.getFileHeader, D/impl/formats/sam/
+ * AbstractSamSource.java:32-49) from the first `len` bytes of a file: enough BGZF blocks to hold
+ * it (the last one may be cut).  Writes up to cap bytes to out; *out_len = header length.  Used
+ * by the multi-GPU path: one rank reads it and broadcasts it to the others' dq_open_shard. */
+int dq_header_from_prefix(dq_ctx* ctx, const uint8_t* bytes, int64_t len, uint8_t* out,
+                          int64_t cap, int64_t* out_len);
+
 /* .bai bytes for interval traversal (AbstractSamSource.findIndex: path.bai or .bam->.bai). */
 int dq_set_index(dq_ctx* ctx, const uint8_t* bai, int64_t len);
 

@@ -1,0 +1,205 @@
+"""Multi-GPU path (disq_amd/parallel.py): shard planning, descriptor exchange and shard parity.
+
+CPU tests run the collective orchestration with world_size 2 on gloo, using the oracle as each
+rank's decoder (the GPU decoder is exercised by the -m gpu tests below, one shard at a time on a
+single device: every shard of a file must reproduce the whole-file decode bit for bit).
+"""
+import multiprocessing as mp
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from disq_amd import parallel as P
+from oracle import oracle as O
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _bam1():
+    return open(os.path.join(GOLDEN, "1.bam"), "rb").read()
+
+
+@pytest.mark.parametrize("n,split,nio", [(597482, 128 * 1024, False), (597482, 40000, False),
+                                         (597482, 0, False), (105, 100, False), (111, 100, False),
+                                         (597482, 65536, True), (10 * 2 ** 30, 0, False)])
+def test_path_splits_match_oracle(n, split, nio):
+    assert P.path_splits(n, split, nio) == O.path_splits(n, split, nio)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("n,split", [(597482, 40000), (597482, 14146), (10 * 2 ** 30, 0),
+                                     (597482, 0)])
+def test_shard_plan_tiles_the_partitions(world, n, split):
+    plan = P.shard_plan(n, world, split_size=split)
+    splits = P.path_splits(n, split)
+    owned = [p for s in plan for p in range(s.p0, s.p1)]
+    assert owned == list(range(len(splits)))            # each partition once, in order
+    for s in plan:
+        if not s.empty:
+            assert (s.lo, s.hi) == (splits[s.p0][0], splits[s.p1 - 1][1])
+    if len(splits) >= world:
+        sizes = [s.hi - s.lo for s in plan]
+        assert min(sizes) > 0
+        assert max(sizes) - min(sizes) <= 2 * max(e - b for b, e in splits)
+
+
+def test_fold_digest_definition():
+    d = [5, 0, 7]
+    want = sum(P.mix64(x ^ ((i + 1) * P.K_WORD) & P.M64) for i, x in enumerate(d)) & P.M64
+    assert P.fold_digest(d) == want
+    assert P.fold_digest(d[1:], first_index=1) + P.mix64(5 ^ P.K_WORD) & P.M64 == want
+
+
+def _oracle_decoder(full: bytes, split: int):
+    ob = O.OracleBam(full)
+    plan = ob.plan(split)
+
+    def decode(data, base, file_len, shard, header, with_raw):
+        assert data == full[base:base + len(data)] and file_len == len(full)
+        assert header == bytes(_oracle_header(full))
+        idx, po, pd = [], [0], []
+        for p in range(shard.p0, shard.p1):
+            ch = plan[p][2]
+            if ch is None:
+                continue
+            recs = ob.read_chunk(*ch)
+            idx.append(p)
+            po.append(po[-1] + len(recs))
+            pd.append(O.stream_digest(recs["hash"]))
+        return {"part_offset": np.array(po, np.int64), "part_digest": np.array(pd, np.uint64)}, idx
+
+    return decode
+
+
+def _oracle_header(full: bytes) -> bytes:
+    u = O.OracleBam(full).inflate_all()
+    l_text = int.from_bytes(bytes(u[4:8]), "little")
+    p = 8 + l_text
+    n_ref = int.from_bytes(bytes(u[p:p + 4]), "little")
+    p += 4
+    for _ in range(n_ref):
+        ln = int.from_bytes(bytes(u[p:p + 4]), "little")
+        p += 8 + ln
+    return bytes(u[:p])
+
+
+def _worker(rank, world, port, split, q):
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        full = _bam1()
+        mine, summary = P.sharded_read(full, split_size=split, decoder=_oracle_decoder(full, split),
+                                       header_reader=lambda prefix: _oracle_header(full))
+        q.put((rank, mine.shard.p0, mine.shard.p1, summary))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world,split", [(2, 40000), (2, 14146), (3, 128 * 1024)])
+def test_sharded_read_gloo(world, split):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, split, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    full = _bam1()
+    parts = O.OracleBam(full).read_partitions(split)
+    plan = O.OracleBam(full).plan(split)
+    digests, k = [], 0
+    for s, e, ch in plan:
+        if ch is None:
+            digests.append(0)
+        else:
+            digests.append(O.stream_digest(parts[k]["hash"]))
+            k += 1
+    want = P.fold_digest(digests)
+    summaries = [r[3] for r in sorted(res)]
+    for s in summaries:   # identical on every rank
+        assert s["digest"] == want
+        assert s["n_records"] == sum(len(p) for p in parts)
+    owned = sorted((r[1], r[2]) for r in res)
+    assert owned[0][0] == 0 and owned[-1][1] == len(plan)
+
+
+# ---------------------------------------------------------------------------- GPU
+FIELDS = ("voffset", "block_size", "ref_id", "pos", "l_seq", "next_ref_id", "next_pos", "tlen",
+          "flag", "bin", "n_cigar", "mapq", "l_read_name", "hash")
+
+
+def _gpu_whole(data, split):
+    from disq_amd import _lib
+    with _lib.Context(split_size=split, verify_crc=True) as c:
+        c.open_bytes(data)
+        b = c.read(with_raw=True)
+        st = c.run_resident()
+    return b, st
+
+
+def _check_shards(data, split, world, halo):
+    from disq_amd import _lib  # noqa: F401
+    whole, st = _gpu_whole(data, split)
+    dec = P.gpu_shard_decoder({"split_size": split}, device=0)
+    hdr_ctx = _lib.Context()
+    header = hdr_ctx.header_from_prefix(data[:1 << 20])
+    hdr_ctx.close()
+    plan = P.shard_plan(len(data), world, split_size=split)
+    got = {f: [] for f in FIELDS}
+    raw = []
+    digests = []
+    for s in plan:
+        r = P.read_shard(lambda a, b: data[a:b], len(data), s, header, dec, halo=halo,
+                         with_raw=True)
+        digests += r.digests
+        if s.empty:
+            continue
+        for f in FIELDS:
+            got[f].append(r.batch[f])
+        raw.append(r.batch["raw"] if r.batch["raw"] is not None else np.zeros(0, np.uint8))
+    for f in FIELDS:
+        assert np.array_equal(np.concatenate(got[f]), whole[f]), f
+    assert np.array_equal(np.concatenate(raw), whole["raw"])
+    assert P.fold_digest(digests) == st.digest
+    return plan
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("split,world", [(128 * 1024, 2), (40000, 3), (40000, 5), (14146, 4),
+                                         (65536, 2)])
+def test_1bam_shards_equal_whole_file(split, world):
+    _check_shards(_bam1(), split, world, halo=16 * 1024)
+
+
+@pytest.mark.gpu
+def test_synthetic_shards_equal_whole_file():
+    from disq_amd import synth
+    r = synth.generate(150000, seed=7, nthreads=8)
+    _check_shards(r.bam, 1 << 20, 4, halo=8 * 1024)
+
+
+@pytest.mark.gpu
+def test_long_read_shards_grow_the_halo():
+    from disq_amd import synth
+    r = synth.generate(400, seed=5, shape=synth.LONGREAD, nthreads=8)
+    _check_shards(r.bam, 256 * 1024, 3, halo=4 * 1024)
+
+
+@pytest.mark.gpu
+def test_sharded_read_single_rank():
+    data = _bam1()
+    mine, summary = P.sharded_read(data, split_size=40000)
+    _, st = _gpu_whole(data, 40000)
+    assert summary["digest"] == st.digest and summary["n_records"] == st.n_records
