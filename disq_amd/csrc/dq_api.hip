@@ -435,24 +435,25 @@ static int run_pipeline(dq_ctx* ctx) {
     init_inflate3_tables();
     static const bool timing = getenv("DQ_TIMING") != nullptr;
     uint64_t* tim = nullptr;
-    if (timing) HIPCHK(hipMalloc(&tim, sizeof(uint64_t) * 12 * (size_t)std::max<int64_t>(1, nblk)));
+    if (timing) HIPCHK(hipMalloc(&tim, sizeof(uint64_t) * 16 * (size_t)std::max<int64_t>(1, nblk)));
     HIPCHK(hipEventRecord(ctx->ev[5], s));
     launch_inflate3(ctx->C.as<uint8_t>(), ctx->blk_pos.as<int64_t>(), ctx->blk_cs.as<int32_t>(),
                     ctx->blk_us.as<int32_t>(), ctx->uoff.as<int64_t>(), nblk, ctx->U.as<uint8_t>(),
                     ctx->status.as<int32_t>(), ctx->o.verify_crc, tim, s);
     HIPCHK(hipEventRecord(ctx->ev[6], s));
     if (timing) {
-      std::vector<uint64_t> h(12 * (size_t)nblk);
+      std::vector<uint64_t> h(16 * (size_t)nblk);
       HIPCHK(hipMemcpyAsync(h.data(), tim, 8 * h.size(), hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
       (void)hipFree(tim);
-      double acc[12] = {0};
+      double acc[16] = {0};
       for (int64_t i = 0; i < nblk; i++)
-        for (int k = 0; k < 12; k++) acc[k] += (double)h[12 * (size_t)i + k];
-      static const char* nm[12] = {"header", "tables", "spec", "rounds", "scan", "emit",
-                                   "resolve+store", "crc", "spec_iters_sum", "spec_iters_max", "n_rounds", "n_dblocks"};
+        for (int k = 0; k < 16; k++) acc[k] += (double)h[16 * (size_t)i + k];
+      static const char* nm[16] = {"header", "tables", "spec", "rounds", "scan", "emit",
+                                   "resolve+store", "crc", "hdr_read_lengths", "res_trips_t0", "hdr_iters", "res_chains_t0",
+                                   "wave0_trips_sum", "wgmax_trips_sum", "res_store", "res_batches"};
       fprintf(stderr, "[dq] inflate3 phase cycles per BGZF block (thread 0, s_memtime):");
-      for (int k = 0; k < 12; k++)
+      for (int k = 0; k < 16; k++)
         if (nm[k][0] != '-') fprintf(stderr, " %s=%.0f", nm[k], acc[k] / (double)std::max<int64_t>(1, nblk));
       fprintf(stderr, "\n");
     }

@@ -29,10 +29,12 @@
 //                  bit in a match-start bitmap.
 // Then, for the whole BGZF block:
 //   6. resolve  -- lastStart[w] = last match start at or before the end of bitmap word w (a max
-//                  scan), so the owner of any byte is found in O(1).  2 KiB chunks in order: each
-//                  thread resolves 4 bytes by following copy sources (start - dist + (offset mod
-//                  dist)) until a literal or an earlier (already resolved) chunk; resolved 16-byte
-//                  lines are stored to U while the next chunk is resolved.
+//                  scan), so the owner of any byte is found in O(1).  Batches of NB chunks of 512
+//                  bytes: (a) every byte follows its copy chain (start - dist + (offset mod dist))
+//                  through static data only until it reaches a literal or a byte of an earlier
+//                  chunk -- the NB chains of a thread advance together, no barriers; (b) chunk by
+//                  chunk, one LDS read + write per byte and one barrier; (c) the batch's 16-byte
+//                  lines are stored to U while the next batch follows its chains.
 //   7. CRC32    -- slice-by-4 per thread over a 128-byte slice, combined across threads by
 //                  multiplying with x^(8n) mod P (precomputed per slice index); compared with the
 //                  gzip trailer.
@@ -48,7 +50,7 @@ namespace {
 using namespace dqi;
 
 constexpr int WG = 512;           // threads per workgroup
-constexpr int NDEC_MAX = 512;     // speculative decode lanes (<= WG)
+constexpr int NDEC = 512;         // speculative decode lanes (<= WG)
 constexpr uint32_t OV = 96;       // speculative warm-up bits before each segment
 constexpr int OUTCAP = 65536 + 20;  // + alignment shift (<= 15) + descriptor overhang
 
@@ -308,12 +310,24 @@ __device__ inline uint32_t gf2_mulmod(uint32_t a, uint32_t b) {  // reflected, p
   return p;
 }
 
-DQ_AI int wave_incl_scan(int v, int lane) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int u = __shfl_up(v, o, 64);
-    if (lane >= o) v += u;
-  }
+// Inclusive wave scans by DPP (row_shr 1/2/4/8 inside rows of 16, then row_bcast 15/31 across
+// rows): a few cycles per step instead of a ds_bpermute round trip.  All 64 lanes must be active.
+DQ_AI int wave_incl_scan(int v, int) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+  return v;
+}
+DQ_AI int wave_incl_max(int v) {  // values >= -1
+  v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x111, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x112, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x114, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x118, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x142, 0xa, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x143, 0xc, 0xf, false));
   return v;
 }
 DQ_AI uint64_t lanes_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
@@ -450,7 +464,8 @@ DQ_AI void build_tables(LdsI& L, int nlen, int ndist) {
 // Dynamic header: decode the code-length sequence (wave 0) into L.u.d.x.h.lens.
 // Returns the bit position after the header, or sets M_ERR.
 DQ_AI uint32_t read_lengths(const uint32_t* __restrict__ W, LdsI& L, uint32_t P, int nlen,
-                                 int ndist, uint32_t endbits, uint32_t hbase) {
+                                 int ndist, uint32_t endbits, uint32_t hbase, int& nit,
+                                 uint64_t* tp = nullptr) {
   // the header's compressed words were staged in the (not yet built) decode table: HB_WORDS
   // words cover the longest possible header (17 + 57 + 320 * 14 bits)
   const uint32_t* hb = reinterpret_cast<const uint32_t*>(L.u.d.T);
@@ -459,6 +474,7 @@ DQ_AI uint32_t read_lengths(const uint32_t* __restrict__ W, LdsI& L, uint32_t P,
   const int total = nlen + ndist;
   int have = 0, prev = -1;
   for (int iter = 0; iter < 400 && have < total; iter++) {
+    nit++;
     if (P > endbits) {
       set_err(L, ST_OVERREAD);
       return P;
@@ -469,6 +485,7 @@ DQ_AI uint32_t read_lengths(const uint32_t* __restrict__ W, LdsI& L, uint32_t P,
     const uint32_t o = off + (uint32_t)lane;  // <= 94
     const uint64_t x = o < 64 ? ((lo >> o) | (o ? hi << (64 - o) : 0ull)) : (hi >> (o - 64));
     const uint32_t bits = (uint32_t)x;
+    uint64_t q0 = tp ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t ent = L.u.d.x.h.clt[bits & 127];
     const uint32_t cl = ent & 7, s = ent >> 3;
     const uint32_t ex = s == 16 ? 2u : s == 17 ? 3u : s == 18 ? 7u : 0u;
@@ -476,6 +493,7 @@ DQ_AI uint32_t read_lengths(const uint32_t* __restrict__ W, LdsI& L, uint32_t P,
     const int rep = s < 16 ? 1 : s == 16 ? 3 + (int)xv : s == 17 ? 3 + (int)xv : 11 + (int)xv;
     const int adv = cl ? (int)(cl + ex) : 0;
     // walk the true symbol path through this window (uniform)
+    uint64_t q1 = tp ? __builtin_amdgcn_s_memtime() : 0;
     uint64_t mark = 0;
     int j = 0, cum = have;
     bool bad = false;
@@ -493,26 +511,32 @@ DQ_AI uint32_t read_lengths(const uint32_t* __restrict__ W, LdsI& L, uint32_t P,
       set_err(L, ST_BAD_TABLE);
       return P;
     }
+    uint64_t q2 = tp ? __builtin_amdgcn_s_memtime() : 0;
     const bool on = (mark >> lane) & 1;
     // value written by each symbol: 0-15 literal length, 17/18 zero, 16 the previous value
     const int v0 = s < 16 ? (int)s : 0;
-    const uint64_t nonrep = mark & __ballot(on && s != 16);
-    // (all lanes shuffle: ds_bpermute returns 0 from inactive source lanes)
-    const uint64_t mb = nonrep & lanes_below(lane);
-    const int pv = __shfl(v0, mb ? 63 - __clzll(mb) : 0, 64);
-    const int val = (on && s == 16) ? (mb ? pv : prev) : v0;
+    // a repeat (16) takes the value of the nearest on-path non-repeat symbol below it, else the
+    // last value of the previous window: forward fill by a max-scan of (lane + 1) << 5 | value
+    const int key = wave_incl_max(on && s != 16 ? ((lane + 1) << 5) | v0 : 0);
+    const int val = (on && s == 16) ? (key > 0 ? (key & 31) : prev) : v0;
     if (__any(on && s == 16 && val < 0)) {
       set_err(L, ST_BAD_TABLE);
       return P;
     }
     const int r = on ? rep : 0;
     const int incl = wave_incl_scan(r, lane);
-    if (on) {
+    if (on && val != 0) {  // lens is zero-filled: zero runs (up to 138) need no stores
       for (int i = have + incl - r; i < have + incl; i++)
         L.u.d.x.h.lens[i < nlen ? i : 288 + i - nlen] = (uint8_t)val;
     }
     const int lastlane = 63 - __clzll(mark);
-    prev = __shfl(val, lastlane, 64);
+    prev = __builtin_amdgcn_readlane(val, lastlane);
+    if (tp) {
+      uint64_t q3 = __builtin_amdgcn_s_memtime();
+      tp[12] += q1 - q0;
+      tp[13] += q2 - q1;
+      tp[14] += q3 - q2;
+    }
     have = cum;
     P += (uint32_t)j;
   }
@@ -520,7 +544,7 @@ DQ_AI uint32_t read_lengths(const uint32_t* __restrict__ W, LdsI& L, uint32_t P,
   return P;
 }
 
-template <bool TIMING, int NDEC, int BPT>
+template <bool TIMING, int NB, int G>
 __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     const uint8_t* __restrict__ C, const int64_t* __restrict__ blk_pos,
     const int32_t* __restrict__ blk_csize, const int32_t* __restrict__ blk_usize,
@@ -529,7 +553,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     uint64_t* __restrict__ tim) {
   __shared__ LdsI L;
   // DQ_TIMING: thread 0 accumulates s_memtime cycles per phase (tim != nullptr only then)
-  uint64_t tacc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t tacc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t tlast = TIMING ? __builtin_amdgcn_s_memtime() : 0;
 #define TST(i)                                            \
   do {                                                    \
@@ -670,8 +694,16 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       __syncthreads();
       if (L.misc[M_ERR]) break;
       if (wv == 0) {
-        const uint32_t a = read_lengths(W, L, clpos + 3 * (uint32_t)ncode, nlen, ndist, endbits, hbase);
+        // the serial critical path of the block: win issue arbitration against the other
+        // workgroup's waves on this SIMD (the guard must be provably wave-uniform)
+        if (__builtin_amdgcn_readfirstlane(t) < 64) __builtin_amdgcn_s_setprio(3);
+        const uint64_t tr0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
+        int nit = 0;
+        const uint32_t a = read_lengths(W, L, clpos + 3 * (uint32_t)ncode, nlen, ndist, endbits, hbase, nit);
+        if (TIMING && t == 0) tacc[10] += (uint64_t)nit;
         if (t == 0) L.misc[M_A] = (int32_t)a;
+        if (TIMING && t == 0) tacc[8] += __builtin_amdgcn_s_memtime() - tr0;
+        if (__builtin_amdgcn_readfirstlane(t) < 64) __builtin_amdgcn_s_setprio(0);
       }
       __syncthreads();
       if (t == 0 && L.misc[M_ERR] == 0 && L.u.d.x.h.lens[256] == 0) set_err(L, ST_BAD_TABLE);
@@ -716,24 +748,13 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       const uint32_t start = t == 0 ? a : (sB > a + OV ? sB - OV : a);
       const uint32_t sE = t == nl - 1 ? 0xffffffffu : a + (uint32_t)(t + 1) * seg;
       int32_t B = -1, E = 0, c = 0;
-      int32_t its = 0;
-      const int f = run_seg(W, L, start, sB, sE, endbits, &B, &E, &c, TIMING ? &its : nullptr);
-      if (TIMING) {
-        atomicAdd(&L.misc[21], its);
-        atomicMax(&L.misc[22], its);
-      }
+      const int f = run_seg(W, L, start, sB, sE, endbits, &B, &E, &c);
       AB[t] = B;
       AE[t] = (E << 3) | f;
       AC[t] = c;
     }
     __syncthreads();
     TST(2);
-    if (TIMING && t == 0) {
-      tacc[8] += (uint64_t)L.misc[21];
-      tacc[9] += (uint64_t)L.misc[22];
-      L.misc[21] = 0;
-      L.misc[22] = 0;
-    }
     // ---- 4. rounds: lanes whose first boundary differs from the predecessor's exit re-decode
     //      from that exit (compacted onto the first threads); repeat until consistent
     for (int round = 0; round <= nl; round++) {
@@ -759,8 +780,9 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
         ST[r] = st;
       }
       __syncthreads();
-      TCOUNT(10);
       if (nneed == 0) break;
+      const bool hi = __builtin_amdgcn_readfirstlane(t) < __builtin_amdgcn_readfirstlane(nneed);  // the few waves re-decoding
+      if (hi) __builtin_amdgcn_s_setprio(3);
       if (t < nneed) {
         const int lt = LS[t];
         const uint32_t s0 = (uint32_t)ST[t];
@@ -771,10 +793,11 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
         AE[lt] = (E << 3) | f;
         AC[lt] = c;
       }
+      if (hi) __builtin_amdgcn_s_setprio(0);
       __syncthreads();
     }
     TST(3);
-    TCOUNT(11);
+
     // ---- 5. counts -> offsets (the first non-exit lane ends the deflate block)
     int32_t myB = 0, myE = 0, myF = F_DEAD, myC = 0;
     if (t < nl) {
@@ -839,12 +862,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       if (m) run = 32 * (4 * t + k) + 31 - __builtin_clz(m);
       ls[k] = run;
     }
-    int wm = run;  // wave inclusive max-scan of the thread's last value
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int u2 = __shfl_up(wm, o, 64);
-      if (lane >= o) wm = max(wm, u2);
-    }
+    const int wm = wave_incl_max(run);  // wave inclusive max-scan of the thread's last value
     if (lane == 63) L.wsum[wv] = wm;
     int ex = __shfl_up(wm, 1, 64);
     if (lane == 0) ex = -1;
@@ -862,84 +880,183 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   const uint8_t* O = L.out + sh;
   const int head = min((16 - sh) & 15, isize);  // bytes before the first 16-byte U boundary
   int32_t lines_done = 0;                       // 16-byte lines [head + 16k, +16) stored
-  constexpr int CHUNK = BPT * WG;
-  for (int32_t c0 = 0; c0 < isize; c0 += CHUNK) {
+  // chunks of CH = G * WG bytes, thread t owns bytes [G t, G t + G) of each; NB chunks per batch;
+  // a byte's chain may stop at any byte before its 512-byte step (the unit of the barriers in (b))
+  constexpr int CH = G * WG;
+  constexpr int BATCH = NB * CH;
+  constexpr int NE = NB * G;
+  for (int32_t bs = 0; bs < isize; bs += BATCH) {
+    const uint64_t tb0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
     const int32_t carry_ms = L.misc[M_CARRY_MS];
     const uint32_t carry_desc = (uint32_t)L.misc[M_CARRY_DESC];
-    const int32_t x0 = c0 + BPT * t;
-    // the thread's BPT bytes follow their copy chains together (independent LDS reads overlap)
-    int32_t xs[BPT];
-    uint32_t word = 0, pending = 0;
-#pragma unroll
-    for (int k = 0; k < BPT; k++) {
-      xs[k] = x0 + k;
-      if (x0 + k < isize) pending |= 1u << k;
-    }
+    // the match covering the batch's last byte continues into the next batch, whose chains can
+    // no longer read its descriptor (overwritten in (b)): keep it aside
     int32_t next_ms = -1;
     uint32_t next_desc = 0;
-    for (int hop = 0; pending != 0 && hop < CHUNK + 2; hop++) {
-      uint32_t mk[BPT], lk[BPT];
-#pragma unroll
-      for (int k = 0; k < BPT; k++) {  // owner lookups: bitmap word + last start before it
-        const int w = xs[k] >> 5;
-        mk[k] = L.bm[w] & (0xffffffffu >> (31 - (xs[k] & 31)));
-        lk[k] = w ? L.u.last_start[w - 1] : 0xffffu;
+    if (t == WG - 1 && bs + BATCH < isize) {
+      const int32_t x = bs + BATCH - 1;
+      const uint32_t m = L.bm[x >> 5];  // bit 31 of the last word: every bit is at or before x
+      const int32_t ms = m ? (x | 31) - (int32_t)__builtin_clz(m) : (int32_t)L.u.last_start[(x >> 5) - 1];
+      if (ms != 0xffff) {
+        const uint32_t desc = ms < bs ? carry_desc : load_desc(L, sh + ms);
+        if ((ms >= bs || ms == carry_ms) && ms + (int32_t)(desc >> 15) + 3 > bs + BATCH) {
+          next_ms = ms;
+          next_desc = desc;
+        }
       }
-      int32_t msk[BPT];
-      uint32_t dk[BPT];
+    }
+    // (a) sources: every byte follows its copy chain until a literal or a byte before its step.
+    //     Only the bitmap, last_start and the descriptors of this batch are read (all static
+    //     until (b) writes), so a thread's chains advance together, without barriers.
+    //     First hop per group: one bitmap word, one last_start and two descriptors (G <= 4 bytes
+    //     have at most two owners: matches are >= 3 bytes long).
+    int32_t xs[NE], fr[NE], sbk[NB];
+    uint32_t pending = 0;
+    {
+      uint32_t mw[NB];
+      int32_t lsv[NB];
 #pragma unroll
-      for (int k = 0; k < BPT; k++) {
-        const int w = xs[k] >> 5;
-        msk[k] = mk[k] ? w * 32 + 31 - __builtin_clz(mk[k]) : (int32_t)lk[k];
-        dk[k] = load_desc(L, sh + min(max(msk[k], c0), 65535));
+      for (int k = 0; k < NB; k++) {
+        const int32_t g0 = bs + k * CH + G * t;
+        const int w = min(g0 >> 5, 2047);  // bytes past isize: read anything, copy = false
+        mw[k] = L.bm[w];
+        lsv[k] = w ? (int32_t)L.u.last_start[w - 1] : 0xffff;
+      }
+      int32_t msv[NE];
+      uint32_t da[NB], db[NB];
+#pragma unroll
+      for (int k = 0; k < NB; k++) {
+        const int32_t g0 = bs + k * CH + G * t;
+#pragma unroll
+        for (int i = 0; i < G; i++) {
+          const uint32_t mi = mw[k] & (0xffffffffu >> (31 - ((g0 + i) & 31)));
+          msv[k * G + i] = mi ? (g0 | 31) - (int32_t)__builtin_clz(mi) : lsv[k];
+        }
+        da[k] = load_desc(L, sh + min(max(msv[k * G], bs), 65535));
+        db[k] = G > 1 ? load_desc(L, sh + min(max(msv[k * G + G - 1], bs), 65535)) : da[k];
       }
 #pragma unroll
-      for (int k = 0; k < BPT; k++) {
-        if (!((pending >> k) & 1)) continue;
-        const int32_t x = xs[k], ms = msk[k];
+      for (int k = 0; k < NB; k++) {
+        const int32_t g0 = bs + k * CH + G * t;
+        sbk[k] = bs + k * CH + ((G * t) & ~511);
+#pragma unroll
+        for (int i = 0; i < G; i++) {
+          const int e = k * G + i;
+          const int32_t x = g0 + i, ms = msv[e];
+          const bool before = ms < bs;  // descriptors before the batch are overwritten: the carry
+          const uint32_t desc = before ? carry_desc : (ms == msv[k * G + G - 1] ? db[k] : da[k]);
+          const int32_t len = (int32_t)(desc >> 15) + 3, D = (int32_t)(desc & 0x7fff) + 1;
+          const bool copy = x < isize && ms != 0xffff && (!before || ms == carry_ms) && x < ms + len;
+          // src = ms - D + (x - ms) mod D; x - ms <= 257: a float reciprocal + one fix-up is exact
+          const int32_t jj = x - ms;
+          const int32_t q = (int32_t)((float)jj * __builtin_amdgcn_rcpf((float)D));
+          int32_t r = jj - q * D;
+          r = r >= D ? r - D : r;
+          const int32_t src = ms - D + r;
+          const bool done = !copy || src < sbk[k];
+          fr[e] = copy ? src : x;
+          xs[e] = src;
+          pending |= done ? 0u : 1u << e;
+        }
+      }
+    }
+    // further hops (chains inside a step): per byte
+    int hop = 1;
+    for (; pending != 0 && hop < WG + 2; hop++) {
+      uint32_t mk[NE], lk[NE];
+#pragma unroll
+      for (int e = 0; e < NE; e++) {  // owner lookups: bitmap word + last start before it
+        if (!((pending >> e) & 1)) continue;
+        const int w = xs[e] >> 5;
+        mk[e] = L.bm[w] & (0xffffffffu >> (31 - (xs[e] & 31)));
+        lk[e] = L.u.last_start[max(w - 1, 0)];
+      }
+      int32_t msk[NE];
+      uint32_t dk[NE];
+#pragma unroll
+      for (int e = 0; e < NE; e++) {
+        if (!((pending >> e) & 1)) continue;
+        msk[e] = mk[e] ? (xs[e] | 31) - (int32_t)__builtin_clz(mk[e])
+                       : (xs[e] >= 32 ? (int32_t)lk[e] : 0xffff);
+        dk[e] = load_desc(L, sh + min(max(msk[e], bs), 65535));
+      }
+#pragma unroll
+      for (int e = 0; e < NE; e++) {
+        if (!((pending >> e) & 1)) continue;
+        const int32_t x = xs[e], ms = msk[e];
         int32_t from = -1;  // final byte position to read, or -1 to hop on
-        uint32_t desc = dk[k];
+        uint32_t desc = dk[e];
         if (ms == 0xffff) {
           from = x;
-        } else if (ms < c0) {
+        } else if (ms < bs) {
           if (ms == carry_ms) desc = carry_desc;
-          else from = x;  // that match ended before this chunk: x is a literal
+          else from = x;  // that match ended before this batch: x is a literal
         }
         if (from < 0) {
           const int32_t len = (int32_t)(desc >> 15) + 3, D = (int32_t)(desc & 0x7fff) + 1;
-          if (hop == 0 && x == c0 + CHUNK - 1 && ms + len > c0 + CHUNK) {
-            next_ms = ms;
-            next_desc = desc;
-          }
           if (x >= ms + len) {
             from = x;
           } else {
             const int32_t jj = x - ms;
-            const int32_t src = jj < D ? x - D : ms - D + (jj % D);
-            if (src < c0) from = src;
-            else xs[k] = src;
+            const int32_t q = (int32_t)((float)jj * __builtin_amdgcn_rcpf((float)D));
+            int32_t r = jj - q * D;
+            r = r >= D ? r - D : r;
+            const int32_t src = ms - D + r;
+            if (src < sbk[e / G]) from = src;
+            else xs[e] = src;
           }
         }
         if (from >= 0) {
-          word |= (uint32_t)O[from] << (8 * k);
-          pending &= ~(1u << k);
+          fr[e] = from;
+          pending &= ~(1u << e);
         }
       }
     }
-    __syncthreads();
-    for (int k = 0; k < BPT; k++)
-      if (x0 + k < isize) L.out[sh + x0 + k] = (uint8_t)(word >> (8 * k));
-    if (t == WG - 1) {
-      L.misc[M_CARRY_MS] = next_ms;
-      L.misc[M_CARRY_DESC] = (int32_t)next_desc;
+    const uint64_t tb1 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
+    if (TIMING) {
+      const int wmax = __builtin_amdgcn_readlane(wave_incl_max(hop), 63);
+      if (lane == 0) {
+        if (wv == 0) atomicAdd(&L.misc[21], wmax);
+        atomicMax(&L.misc[22], wmax);
+      }
     }
-    __syncthreads();
-    // store the 16-byte U lines completed by this chunk (overlaps the next chunk's resolve)
-    const int32_t c1 = min(isize, c0 + CHUNK);
+    __syncthreads();  // every chain has read its descriptors before (b) overwrites them
+    const int wgm = TIMING ? L.misc[22] : 0;
+    // (b) 512-byte steps in order: one LDS read + write per copied byte, one barrier per step
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+#pragma unroll
+      for (int j = 0; j < G; j++) {
+        if (((G * t) >> 9) == j) {
+          const int32_t g0 = bs + k * CH + G * t;
+          uint8_t v[G];
+#pragma unroll
+          for (int i = 0; i < G; i++) v[i] = O[min(fr[k * G + i], 65535)];
+#pragma unroll
+          for (int i = 0; i < G; i++)
+            if (g0 + i < isize && fr[k * G + i] != g0 + i) L.out[sh + g0 + i] = v[i];
+        }
+        if (TIMING && k == 0 && j == 0 && t == 0) L.misc[22] = 0;
+        if (k == NB - 1 && j == G - 1 && t == WG - 1) {  // the old carry was read before step 0
+          L.misc[M_CARRY_MS] = next_ms;
+          L.misc[M_CARRY_DESC] = (int32_t)next_desc;
+        }
+        __syncthreads();
+      }
+    }
+    // (c) store the 16-byte U lines this batch completed (overlaps the next batch's chains)
+    const int32_t c1 = min(isize, bs + BATCH);
     const int32_t lines_to = c1 >= head ? (c1 - head) / 16 : 0;
     for (int32_t k = lines_done + t; k < lines_to; k += WG)
       *reinterpret_cast<uint4*>(dstU + head + 16 * k) = *reinterpret_cast<const uint4*>(O + head + 16 * k);
     lines_done = lines_to;
+    if (TIMING && t == 0) {
+      tacc[9] += (uint64_t)hop;
+      tacc[12] = (uint64_t)L.misc[21];
+      tacc[13] += (uint64_t)wgm;
+      tacc[11] += tb1 - tb0;
+      tacc[15] += 1;
+    }
   }
   for (int x = t; x < head; x += WG) dstU[x] = O[x];
   for (int x = head + 16 * lines_done + t; x < isize; x += WG) dstU[x] = O[x];
@@ -979,7 +1096,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   }
   TST(7);
   if (TIMING && t == 0)
-    for (int i = 0; i < 12; i++) tim[b * 12 + i] = tacc[i];
+    for (int i = 0; i < 16; i++) tim[b * 16 + i] = tacc[i];
 }
 
 uint32_t h_mul(uint32_t a, uint32_t b) {
@@ -1038,22 +1155,20 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
                      int32_t* status, int32_t verify_crc, uint64_t* tim, hipStream_t s) {
   if (nblk <= 0) return;
   static int cfg = -1;
-  if (cfg < 0) {  // DQ_CFG="ndec,bpt" (tuning experiments); default 512,1
-    int nd = 512, bp = 1;
-    if (const char* e = getenv("DQ_CFG")) sscanf(e, "%d,%d", &nd, &bp);
-    cfg = (nd == 512 ? 3 : 0) + (bp == 2 ? 1 : bp == 4 ? 2 : 0);
+  if (cfg < 0) {  // DQ_CFG="nb,g" (tuning experiments); default 4,1
+    int nb = 4, g = 1;
+    if (const char* e = getenv("DQ_CFG")) sscanf(e, "%d,%d", &nb, &g);
+    cfg = g != 4 ? 0 : nb == 1 ? 1 : nb == 4 ? 3 : 2;
   }
-#define DQ_LAUNCH(TM, ND, BP)                                                                  \
-  hipLaunchKernelGGL((inflate_block_kernel<TM, ND, BP>), dim3((unsigned)nblk), dim3(WG), 0, s, C, \
+#define DQ_LAUNCH(TM, NBT, GT)                                                                  \
+  hipLaunchKernelGGL((inflate_block_kernel<TM, NBT, GT>), dim3((unsigned)nblk), dim3(WG), 0, s, C, \
                      blk_pos, blk_csize, blk_usize, uoff, nblk, U, status, verify_crc, g_crc_init, tim)
 #define DQ_CFGS(TM)                       \
   switch (cfg) {                          \
-    case 0: DQ_LAUNCH(TM, 256, 1); break; \
-    case 1: DQ_LAUNCH(TM, 256, 2); break; \
-    case 2: DQ_LAUNCH(TM, 256, 4); break; \
-    case 3: DQ_LAUNCH(TM, 512, 1); break; \
-    case 4: DQ_LAUNCH(TM, 512, 2); break; \
-    default: DQ_LAUNCH(TM, 512, 4); break; \
+    case 1: DQ_LAUNCH(TM, 1, 4); break;   \
+    case 2: DQ_LAUNCH(TM, 2, 4); break;   \
+    case 3: DQ_LAUNCH(TM, 4, 4); break;   \
+    default: DQ_LAUNCH(TM, 4, 1); break;  \
   }
   if (tim) {
     DQ_CFGS(true)
