@@ -450,8 +450,8 @@ static int run_pipeline(dq_ctx* ctx) {
       for (int64_t i = 0; i < nblk; i++)
         for (int k = 0; k < 16; k++) acc[k] += (double)h[16 * (size_t)i + k];
       static const char* nm[16] = {"header", "tables", "spec", "rounds", "scan", "emit",
-                                   "resolve+store", "crc", "hdr_read_lengths", "res_trips_t0", "hdr_iters", "res_chains_t0",
-                                   "wave0_trips_sum", "wgmax_trips_sum", "res_store", "res_batches"};
+                                   "resolve+store", "crc", "hdr_read_lengths", "unmerged_spec_err_eob", "redo_rounds", "unmerged_other",
+                                   "unmerged_spec_exit", "merge_j_sum", "redo_merged", "res_batches"};
       fprintf(stderr, "[dq] inflate3 phase cycles per BGZF block (thread 0, s_memtime):");
       for (int k = 0; k < 16; k++)
         if (nm[k][0] != '-') fprintf(stderr, " %s=%.0f", nm[k], acc[k] / (double)std::max<int64_t>(1, nblk));

@@ -51,7 +51,7 @@ using namespace dqi;
 
 constexpr int WG = 512;           // threads per workgroup
 constexpr int NDEC = 512;         // speculative decode lanes (<= WG)
-constexpr uint32_t OV = 96;       // speculative warm-up bits before each segment
+constexpr uint32_t OV_DEFAULT = 96;  // speculative warm-up bits before each segment
 constexpr int OUTCAP = 65536 + 20;  // + alignment shift (<= 15) + descriptor overhang
 
 // 16-bit decode table layout: [litlen root | litlen subtables | dist root | dist subtables]
@@ -91,9 +91,9 @@ struct alignas(16) LdsI {
     uint16_t last_start[2048];    // resolve: last match start <= end of bitmap word (0xffff none)
     uint32_t crc4[4][256];
   } u;
-  int32_t misc[24];
+  int32_t misc[32];
   int32_t wsum[16];
-  int32_t small[8 * 5];           // per-lane arrays when the image tail is too short
+  int32_t small[8 * 7];           // per-lane arrays when the image tail is too short
   uint32_t ltab[29];              // length symbols 257..285: base | extra bits << 16
   uint32_t dtab[30];              // distance symbols: base | extra bits << 16
 };
@@ -231,19 +231,33 @@ enum : int32_t { F_DEAD = 4 };  // speculative path found no boundary >= sB (gar
 // Decode from `start`; output is counted from the first symbol boundary >= sB (*Bp) and the
 // run stops at the first boundary >= sE (*Ep).  Returns F_EXIT / F_EOB (*Ep = bit after EOB) /
 // F_ERR / F_END (ran off the data) / F_DEAD (no boundary >= sB before an error, EOB or the end).
+constexpr int NCK = 8;          // checkpoints per speculative lane
+constexpr uint32_t CKI = 48;    // checkpoint spacing in bits (>= the longest symbol: a symbol
+                                // crosses at most one threshold; most paths re-synchronise
+                                // within ~100 bits, segments are ~160-1000 bits)
+
+// Speculative lanes also record checkpoints: the first symbol boundary at or past sB + CKI * (j+1)
+// (offset from sB << 16 | bytes counted so far), j < NCK, at ck[j * ckstride] (nullptr: none).
 DQ_AI int run_seg(const uint32_t* __restrict__ W, const LdsI& L, uint32_t start, uint32_t sB,
                   uint32_t sE, uint32_t endbits, int32_t* Bp, int32_t* Ep, int32_t* cntp,
-                  int32_t* itp = nullptr) {
+                  uint32_t* ck = nullptr, int ckstride = 0) {
   BitR r;
   br_init(r, W, start);
   bool counting = false;
-  int32_t cnt = 0, B = -1, it = 0;
+  int32_t cnt = 0, B = -1;
   int f;
-  for (;; it++) {
+  uint32_t thr = ck ? sB + CKI : 0xffffffffu;
+  int j = 0;
+  for (;;) {
     const uint32_t p = br_pos(r);
     const bool nc = !counting && p >= sB;
     B = nc ? (int32_t)p : B;
     counting = counting || nc;
+    if (p >= thr) {  // rare: a checkpoint
+      ck[j * ckstride] = ((p - sB) << 16) | (uint32_t)cnt;
+      j++;
+      thr = j < NCK ? thr + CKI : 0xffffffffu;
+    }
     if ((counting && p >= sE) || p >= endbits) {
       *Ep = (int32_t)p;
       f = p >= sE && counting ? F_EXIT : (counting ? F_END : F_DEAD);
@@ -260,7 +274,52 @@ DQ_AI int run_seg(const uint32_t* __restrict__ W, const LdsI& L, uint32_t start,
   }
   *Bp = B;
   *cntp = cnt;
-  if (itp) *itp = it;
+  return f;
+}
+
+// Re-decode of lane `lt` from its verified start s0 (a boundary >= sB).  At each checkpoint
+// threshold the path is compared with the speculative one: the same boundary means the same
+// decoder state, so the rest of the segment is the speculative run's (exit `se` = E << 3 | flag,
+// `sc` bytes from its first boundary) and the decode stops there.
+DQ_AI int run_redo(const uint32_t* __restrict__ W, const LdsI& L, uint32_t s0, uint32_t sB,
+                   uint32_t sE, uint32_t endbits, const uint32_t* ck, int ckstride, int32_t se,
+                   int32_t sc, int32_t* Ep, int32_t* cntp, int* jm = nullptr) {
+  BitR r;
+  br_init(r, W, s0);
+  int32_t cnt = 0;
+  int f;
+  uint32_t thr = ck ? sB + CKI : 0xffffffffu;
+  uint32_t cur = ck ? ck[0] : 0xffffffffu;
+  int j = 0;
+  for (;;) {
+    const uint32_t p = br_pos(r);
+    if (p >= sE || p >= endbits) {
+      *Ep = (int32_t)p;
+      f = p >= sE ? F_EXIT : F_END;
+      break;
+    }
+    if (p >= thr) {  // rare: compare with the speculative checkpoint
+      if ((cur >> 16) == p - sB) {
+        *Ep = se >> 3;
+        f = se & 7;
+        cnt += sc - (int32_t)(cur & 0xffffu);
+        if (jm) *jm = j;
+        break;
+      }
+      j++;
+      thr = j < NCK ? thr + CKI : 0xffffffffu;
+      cur = j < NCK ? ck[j * ckstride] : 0xffffffffu;
+    }
+    uint32_t len = 0, dist = 0;
+    const int k = dsym(r, W, L, len, dist);
+    if (k > S_MATCH) {
+      *Ep = (int32_t)(k == S_EOB ? br_pos(r) : p);
+      f = k == S_EOB ? F_EOB : F_ERR;
+      break;
+    }
+    cnt += k == S_MATCH ? (int32_t)len : 1;
+  }
+  *cntp = cnt;
   return f;
 }
 
@@ -550,7 +609,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     const int32_t* __restrict__ blk_csize, const int32_t* __restrict__ blk_usize,
     const int64_t* __restrict__ uoff, int64_t nblk, uint8_t* __restrict__ U,
     int32_t* __restrict__ status, int32_t verify_crc, const uint32_t* __restrict__ crc_init,
-    uint64_t* __restrict__ tim) {
+    uint64_t* __restrict__ tim, uint32_t OV) {
   __shared__ LdsI L;
   // DQ_TIMING: thread 0 accumulates s_memtime cycles per phase (tim != nullptr only then)
   uint64_t tacc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -584,7 +643,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   const uint32_t endbits = a0 + 8u * (uint32_t)max(dbytes, 0);
 
   for (int i = t; i < 2048; i += WG) L.bm[i] = 0;
-  if (t < 24) L.misc[t] = 0;
+  if (t < 32) L.misc[t] = 0;
   if (t < 29) L.ltab[t] = len_base((uint32_t)t) | (len_extra((uint32_t)t) << 16);
   if (t >= 64 && t < 94) L.dtab[t - 64] = dist_base((uint32_t)(t - 64)) | (dist_extra((uint32_t)(t - 64)) << 16);
   if (t == 0) {
@@ -700,7 +759,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
         const uint64_t tr0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
         int nit = 0;
         const uint32_t a = read_lengths(W, L, clpos + 3 * (uint32_t)ncode, nlen, ndist, endbits, hbase, nit);
-        if (TIMING && t == 0) tacc[10] += (uint64_t)nit;
+        (void)nit;
         if (t == 0) L.misc[M_A] = (int32_t)a;
         if (TIMING && t == 0) tacc[8] += __builtin_amdgcn_s_memtime() - tr0;
         if (__builtin_amdgcn_readfirstlane(t) < 64) __builtin_amdgcn_s_setprio(0);
@@ -723,17 +782,20 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     const uint32_t span = endbits - a;
     // per-lane arrays live in the not-yet-written tail of the output image
     const int ob = (sh + produced + 3) & ~3;
-    const int cap = (sh + isize - ob) / 20;
+    const int cap = (sh + isize - ob) / (4 * (7 + NCK));
     int32_t* AB;  // verified start (first boundary >= segment start), -1 none
     int32_t* AE;  // exit << 3 | flag
     int32_t* AC;  // output bytes in [B, E)
     int32_t* LS;  // redo list: lane
     int32_t* ST;  // redo list: start
+    int32_t* SE;  // speculative exit << 3 | flag
+    int32_t* SC;  // speculative byte count
+    uint32_t* CK = nullptr;  // checkpoints, [j * nl + lane]
     int nl = (int)max(1u, min((uint32_t)NDEC, span / 128u));
     if (cap >= 8) {
       nl = min(nl, cap);
       AB = reinterpret_cast<int32_t*>(L.out + ob);
-    } else {
+    } else {  // a short image tail: at most 8 lanes, no checkpoints
       nl = min(nl, 8);
       AB = L.small;
     }
@@ -741,6 +803,9 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     AC = AE + nl;
     LS = AC + nl;
     ST = LS + nl;
+    SE = ST + nl;
+    SC = SE + nl;
+    if (cap >= 8) CK = reinterpret_cast<uint32_t*>(SC + nl);
     const uint32_t seg = (span + nl - 1) / nl;
     // ---- 3. speculative pass: from OV bits before the segment, counting from its first boundary
     if (t < nl) {
@@ -748,10 +813,14 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       const uint32_t start = t == 0 ? a : (sB > a + OV ? sB - OV : a);
       const uint32_t sE = t == nl - 1 ? 0xffffffffu : a + (uint32_t)(t + 1) * seg;
       int32_t B = -1, E = 0, c = 0;
-      const int f = run_seg(W, L, start, sB, sE, endbits, &B, &E, &c);
+      if (CK)
+        for (int j = 0; j < NCK; j++) CK[j * nl + t] = 0xffffffffu;
+      const int f = run_seg(W, L, start, sB, sE, endbits, &B, &E, &c, CK ? CK + t : nullptr, nl);
       AB[t] = B;
       AE[t] = (E << 3) | f;
       AC[t] = c;
+      SE[t] = (E << 3) | f;
+      SC[t] = c;
     }
     __syncthreads();
     TST(2);
@@ -781,17 +850,31 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       }
       __syncthreads();
       if (nneed == 0) break;
+      TCOUNT(10);
       const bool hi = __builtin_amdgcn_readfirstlane(t) < __builtin_amdgcn_readfirstlane(nneed);  // the few waves re-decoding
       if (hi) __builtin_amdgcn_s_setprio(3);
       if (t < nneed) {
         const int lt = LS[t];
         const uint32_t s0 = (uint32_t)ST[t];
         const uint32_t sE = lt == nl - 1 ? 0xffffffffu : a + (uint32_t)(lt + 1) * seg;
-        int32_t B = -1, E = 0, c = 0;
-        const int f = run_seg(W, L, s0, s0, sE, endbits, &B, &E, &c);
-        AB[lt] = B;
+        int32_t E = 0, c = 0;
+        int jmerge = -1;
+        const uint32_t sB = a + (uint32_t)lt * seg;
+        // a speculative lane that found no boundary (F_DEAD) recorded no checkpoints
+        const int f = run_redo(W, L, s0, sB, sE, endbits, CK ? CK + lt : nullptr, nl, SE[lt],
+                               SC[lt], &E, &c, TIMING ? &jmerge : nullptr);
+        AB[lt] = (int32_t)s0;
         AE[lt] = (E << 3) | f;
         AC[lt] = c;
+        if (TIMING) {
+          if (jmerge >= 0) {
+            atomicAdd(&L.misc[23], 1);
+            atomicAdd(&L.misc[24], jmerge);
+          } else {
+            const int sf = SE[lt] & 7;
+            atomicAdd(&L.misc[sf == F_ERR || sf == F_EOB ? 25 : sf == F_EXIT ? 26 : 27], 1);
+          }
+        }
       }
       if (hi) __builtin_amdgcn_s_setprio(0);
       __syncthreads();
@@ -1051,12 +1134,17 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       *reinterpret_cast<uint4*>(dstU + head + 16 * k) = *reinterpret_cast<const uint4*>(O + head + 16 * k);
     lines_done = lines_to;
     if (TIMING && t == 0) {
-      tacc[9] += (uint64_t)hop;
-      tacc[12] = (uint64_t)L.misc[21];
-      tacc[13] += (uint64_t)wgm;
-      tacc[11] += tb1 - tb0;
+      (void)wgm;
+      (void)tb0; (void)tb1;
       tacc[15] += 1;
     }
+  }
+  if (TIMING && t == 0) {
+    tacc[14] = (uint64_t)L.misc[23];
+    tacc[13] = (uint64_t)L.misc[24];
+    tacc[9] = (uint64_t)L.misc[25];
+    tacc[12] = (uint64_t)L.misc[26];
+    tacc[11] = (uint64_t)L.misc[27];
   }
   for (int x = t; x < head; x += WG) dstU[x] = O[x];
   for (int x = head + 16 * lines_done + t; x < isize; x += WG) dstU[x] = O[x];
@@ -1154,6 +1242,7 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
                      const int32_t* blk_usize, const int64_t* uoff, int64_t nblk, uint8_t* U,
                      int32_t* status, int32_t verify_crc, uint64_t* tim, hipStream_t s) {
   if (nblk <= 0) return;
+  static const uint32_t ov = getenv("DQ_OV") ? (uint32_t)atoi(getenv("DQ_OV")) : OV_DEFAULT;
   static int cfg = -1;
   if (cfg < 0) {  // DQ_CFG="nb,g" (tuning experiments); default 4,1
     int nb = 4, g = 1;
@@ -1162,7 +1251,7 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
   }
 #define DQ_LAUNCH(TM, NBT, GT)                                                                  \
   hipLaunchKernelGGL((inflate_block_kernel<TM, NBT, GT>), dim3((unsigned)nblk), dim3(WG), 0, s, C, \
-                     blk_pos, blk_csize, blk_usize, uoff, nblk, U, status, verify_crc, g_crc_init, tim)
+                     blk_pos, blk_csize, blk_usize, uoff, nblk, U, status, verify_crc, g_crc_init, tim, ov)
 #define DQ_CFGS(TM)                       \
   switch (cfg) {                          \
     case 1: DQ_LAUNCH(TM, 1, 4); break;   \
