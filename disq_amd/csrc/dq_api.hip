@@ -82,7 +82,7 @@ struct dq_ctx {
   DevBuf plans;
   std::vector<SplitPlan> plans_h;
   // records
-  DevBuf segs, segcnt, segbase, rec_lin;
+  DevBuf segs, segcnt, segbase, rec_lin, pages;
   DevBuf f_voff, f_bs, f_ref, f_pos, f_lseq, f_nref, f_npos, f_tlen, f_flag, f_bin, f_ncig, f_mapq,
       f_lrn, f_hash;
   int64_t nrec = 0;
@@ -530,7 +530,7 @@ static int run_pipeline(dq_ctx* ctx) {
   }
   // ---- Kernel 3: record chain, SoA decode, hashes
   int64_t nrec = 0;
-  const int64_t SEG = 256 * 1024;
+  const int64_t SEG = 64 * 1024;  // record-chain segment: one wave walks it
   // record starts wanted: all of U, or (shard) those in blocks at or before the last split end
   int64_t chain_end = ulen;
   if (ctx->shard && !is_eof && nblk > 0) {
@@ -569,8 +569,8 @@ static int run_pipeline(dq_ctx* ctx) {
     if ((rc = get_i64(ctx, ctx->segbase.as<int64_t>() + nseg, &nrec))) return rc;
     const size_t nr = (size_t)std::max<int64_t>(1, nrec);
     if ((rc = ensure_all(ctx, ctx->rec_lin, 8 * nr))) return rc;
-    launch_seg_emit2(ctx->U.as<uint8_t>(), ctx->segs.as<Seg>(), ctx->segbase.as<int64_t>(), nseg,
-                     ctx->rec_lin.as<int64_t>(), s);
+    launch_seg_emit2(ctx->U.as<uint8_t>(), ulen, ctx->segs.as<Seg>(), ctx->segbase.as<int64_t>(),
+                     nseg, ctx->rec_lin.as<int64_t>(), s);
     DevBuf* b8[] = {&ctx->f_voff, &ctx->f_hash};
     DevBuf* b4[] = {&ctx->f_bs, &ctx->f_ref, &ctx->f_pos, &ctx->f_lseq, &ctx->f_nref, &ctx->f_npos,
                     &ctx->f_tlen};
@@ -580,10 +580,11 @@ static int run_pipeline(dq_ctx* ctx) {
     for (auto* b : b4) if ((rc = ensure_all(ctx, *b, 4 * nr))) return rc;
     for (auto* b : b2) if ((rc = ensure_all(ctx, *b, 2 * nr))) return rc;
     for (auto* b : b1) if ((rc = ensure_all(ctx, *b, nr))) return rc;
+    if ((rc = ensure_all(ctx, ctx->pages, 4 * (size_t)((ulen >> 16) + 1)))) return rc;
     HIPCHK(hipMemsetAsync(d_stat, 0, 4, s));
     launch_decode_records(ctx->U.as<uint8_t>(), ulen, ctx->rec_lin.as<int64_t>(), nrec,
-                          ctx->blk_pos.as<int64_t>(), ctx->blk_cs.as<int32_t>(),
-                          ctx->uoff.as<int64_t>(), nblk, ctx->soa(), d_stat, s);
+                          ctx->blk_pos.as<int64_t>(), ctx->uoff.as<int64_t>(), nblk,
+                          ctx->pages.as<int32_t>(), ctx->soa(), d_stat, s);
   }
   dbg(s, "decode", nrec);
   ctx->nrec = nrec;

@@ -121,8 +121,8 @@ void launch_seg_fix2(const uint8_t* U, int64_t ulen, int32_t u_is_eof, int64_t c
                      Seg* segs, int64_t nseg,
                      int64_t seg_bytes, int64_t start_lin, int32_t* d_status, hipStream_t s);
 void launch_seg_counts(const Seg* segs, int64_t nseg, int64_t* counts, hipStream_t s);
-void launch_seg_emit2(const uint8_t* U, const Seg* segs, const int64_t* base, int64_t nseg,
-                      int64_t* rec_lin, hipStream_t s);
+void launch_seg_emit2(const uint8_t* U, int64_t ulen, const Seg* segs, const int64_t* base,
+                      int64_t nseg, int64_t* rec_lin, hipStream_t s);
 
 struct RecSoA {
   uint64_t* voffset;
@@ -140,9 +140,10 @@ struct RecSoA {
   uint8_t* l_read_name;
   uint64_t* hash;
 };
+// pt: (ulen >> 16) + 1 int32 scratch (block page table)
 void launch_decode_records(const uint8_t* U, int64_t ulen, const int64_t* rec_lin, int64_t nrec,
-                           const int64_t* blk_pos, const int32_t* blk_csize, const int64_t* uoff,
-                           int64_t nblk, RecSoA soa, int32_t* d_status, hipStream_t s);
+                           const int64_t* blk_pos, const int64_t* uoff, int64_t nblk, int32_t* pt,
+                           RecSoA soa, int32_t* d_status, hipStream_t s);
 
 struct PartRange {
   int64_t begin, end;   // record index range in the chain

@@ -158,7 +158,7 @@ template <typename T>
 void exclusive_scan(const T* in, int64_t* out, int64_t n, int64_t* tmp, hipStream_t s) {
   // out has n + 1 entries; out[n] = total.  tmp needs >= 2 * ceil(n/1024) + 64 entries.
   if (n <= 0) {
-    hipMemsetAsync(out, 0, sizeof(int64_t), s);
+    (void)hipMemsetAsync(out, 0, sizeof(int64_t), s);
     return;
   }
   int64_t nb = (n + 1023) / 1024;
@@ -169,9 +169,9 @@ void exclusive_scan(const T* in, int64_t* out, int64_t n, int64_t* tmp, hipStrea
     exclusive_scan<int64_t>(sums, sums_sc, nb, tmp + 2 * nb + 2, s);
     hipLaunchKernelGGL(scan_add_kernel, dim3((unsigned)nb), dim3(1024), 0, s, out, n, sums_sc);
     // total = sums_sc[nb]
-    hipMemcpyAsync(out + n, sums_sc + nb, sizeof(int64_t), hipMemcpyDeviceToDevice, s);
+    (void)hipMemcpyAsync(out + n, sums_sc + nb, sizeof(int64_t), hipMemcpyDeviceToDevice, s);
   } else {
-    hipMemcpyAsync(out + n, sums, sizeof(int64_t), hipMemcpyDeviceToDevice, s);
+    (void)hipMemcpyAsync(out + n, sums, sizeof(int64_t), hipMemcpyDeviceToDevice, s);
   }
 }
 
@@ -489,6 +489,50 @@ __device__ int walk(const uint8_t* U, int64_t ulen, int u_is_eof, int64_t start,
   return 0;
 }
 
+// The same walk by a whole wave: the wave copies 4 KiB windows of U into LDS with coalesced
+// loads and walks the block_size chain through LDS (one global round trip per ~12 records instead
+// of one per record).  p, the count and the result are wave-uniform.
+constexpr int WALK_WIN = 4096;
+__device__ int walk_wave(const uint8_t* U, int64_t ulen, int u_is_eof, int64_t start,
+                         int64_t seg_end, int64_t* exit, int64_t* count, uint4* win4,
+                         int64_t* out = nullptr, int64_t out_max = 0) {
+  const uint8_t* win = reinterpret_cast<const uint8_t*>(win4);
+  const int lane = threadIdx.x;
+  int64_t p = start, n = 0;
+  int64_t wb = -1;  // window base (16-byte aligned), -1 none
+  while (p < seg_end && (!out || n < out_max)) {
+    if (p + 4 > ulen) {
+      if (u_is_eof) {
+        *exit = END_CHAIN;
+        *count = n;
+        return 0;
+      }
+      return 4;
+    }
+    if (wb < 0 || p + 4 > wb + WALK_WIN) {
+      __syncthreads();  // every lane is done with the old window
+      wb = p & ~(int64_t)15;
+      const uint4* src = reinterpret_cast<const uint4*>(U + wb);
+#pragma unroll
+      for (int k = 0; k < WALK_WIN / 16 / 64; k++) {  // U is padded by 256 zero bytes
+        const int c = lane + 64 * k;
+        win4[c] = wb + 16 * (c + 1) <= ulen + 256 ? src[c] : make_uint4(0, 0, 0, 0);
+      }
+      __syncthreads();
+    }
+    const int64_t o = p - wb;
+    const int32_t bs = (int32_t)(win[o] | (win[o + 1] << 8) | (win[o + 2] << 16) |
+                                 ((uint32_t)win[o + 3] << 24));
+    if (bs < 32) return ST_BAD_CODE;  // "Invalid record length" (SAMFormatException)
+    if (out && lane == 0 && n < out_max) out[n] = p;
+    n++;
+    p += 4 + (int64_t)bs;
+  }
+  *exit = p;
+  *count = n;
+  return 0;
+}
+
 __global__ __launch_bounds__(64) void seg_spec_kernel(const uint8_t* __restrict__ U, int64_t ulen,
                                                       int32_t u_is_eof,
                                                       const int32_t* __restrict__ ref_len,
@@ -516,24 +560,23 @@ __global__ __launch_bounds__(64) void seg_spec_kernel(const uint8_t* __restrict_
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    Seg g;
-    g.exact = s == 0;
-    g.status = 0;
-    g.start = best == INT64_MAX ? -1 : best;  // -1: no start speculated in this segment
-    g.exit = -1;
-    g.count = 0;
-    if (g.start >= 0) {
-      int64_t ex, cnt;
-      int r = walk(U, ulen, u_is_eof, g.start, se, &ex, &cnt);
-      g.status = r;
-      if (r == 0) {
-        g.exit = ex;
-        g.count = cnt;
-      }
+  __shared__ uint4 win4[WALK_WIN / 16];
+  Seg g;
+  g.exact = s == 0;
+  g.status = 0;
+  g.start = best == INT64_MAX ? -1 : best;  // -1: no start speculated in this segment
+  g.exit = -1;
+  g.count = 0;
+  if (g.start >= 0) {
+    int64_t ex, cnt;
+    const int r = walk_wave(U, ulen, u_is_eof, g.start, se, &ex, &cnt, win4);
+    g.status = r;
+    if (r == 0) {
+      g.exit = ex;
+      g.count = cnt;
     }
-    segs[s] = g;
   }
+  if (threadIdx.x == 0) segs[s] = g;
 }
 
 // Serial link check + repair (one lane).  Segments are few (one per 1 MiB of U); each link is
@@ -602,66 +645,115 @@ __global__ void seg_counts_kernel(const Seg* __restrict__ segs, int64_t nseg, in
   if (s < nseg) counts[s] = segs[s].count;
 }
 
-__global__ void seg_emit_kernel(const uint8_t* __restrict__ U, const Seg* __restrict__ segs,
-                                const int64_t* __restrict__ base, int64_t nseg,
-                                int64_t* __restrict__ rec_lin) {
-  int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// One wave per segment: the record starts of the (exact) chain, walked through LDS windows.
+__global__ __launch_bounds__(64) void seg_emit_kernel(const uint8_t* __restrict__ U, int64_t ulen,
+                                                      const Seg* __restrict__ segs,
+                                                      const int64_t* __restrict__ base, int64_t nseg,
+                                                      int64_t* __restrict__ rec_lin) {
+  __shared__ uint4 win4[WALK_WIN / 16];
+  const int64_t s = blockIdx.x;
   if (s >= nseg) return;
   const Seg g = segs[s];
-  int64_t p = g.start, o = base[s];
-  for (int64_t k = 0; k < g.count; k++) {
-    rec_lin[o + k] = p;
-    p += 4 + (int64_t)ld32(U, p);
-  }
+  if (g.count <= 0) return;
+  int64_t ex, cnt;
+  // the chain was validated by seg_spec / seg_fix: walk exactly g.count records
+  walk_wave(U, ulen, 1, g.start, INT64_MAX, &ex, &cnt, win4, rec_lin + base[s], g.count);
 }
 
 // ------------------------------------------------------------------ decode + hash
-__device__ inline uint32_t ldw(const uint32_t* U32, int64_t wi) { return U32[wi]; }
+// Page table for block_of: pt[g] = the last block whose first byte is <= g * 64 KiB, so the block
+// of a record start is pt[p >> 16] plus a short forward walk (htsjdk blocks hold <= 64 KiB).
+__global__ void block_pages_kernel(const int64_t* __restrict__ uoff, int64_t nblk, int32_t* pt,
+                                   int64_t npages) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < npages) pt[g] = (int32_t)block_of(uoff, nblk, g << 16);
+}
 
-// One lane per record: fixed fields into SoA, htsjdk start pointer, and the raw-byte hash
-// (8-byte little-endian words, zero padded) read as aligned dwords.
-__global__ __launch_bounds__(256) void decode_records_kernel(
+__device__ inline uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t sh) {  // (hi:lo) >> 8 sh
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * sh));
+}
+
+// One wave per 64 consecutive records (the chain is contiguous in U).  The wave first copies the
+// records' bytes into LDS with coalesced 16-byte loads, then lane r decodes record r: fixed fields
+// into the SoA, the htsjdk start pointer (block via the page table) and the raw-byte hash
+// (8-byte little-endian words, zero padded; DESIGN.md section "hash") from LDS.  Runs of records
+// longer than the staging buffer (long reads) are read straight from U.
+constexpr int REC_WAVE = 64;
+constexpr int REC_STAGE = 24576;  // 64 short-read records (~21 KB); 6 waves per CU
+
+__global__ __launch_bounds__(64) void decode_records_kernel(
     const uint8_t* __restrict__ U, int64_t ulen, const int64_t* __restrict__ rec_lin, int64_t nrec,
-    const int64_t* __restrict__ blk_pos, const int32_t* __restrict__ blk_csize,
-    const int64_t* __restrict__ uoff, int64_t nblk, RecSoA soa, int32_t* d_status) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nrec) return;
-  const int64_t p = rec_lin[i];
-  const int32_t bs = ld32(U, p);
+    const int64_t* __restrict__ blk_pos, const int64_t* __restrict__ uoff, int64_t nblk,
+    const int32_t* __restrict__ pt, RecSoA soa, int32_t* d_status) {
+  __shared__ uint4 stage4[REC_STAGE / 16 + 1];
+  const int lane = threadIdx.x;
+  const int64_t i0 = (int64_t)blockIdx.x * REC_WAVE;
+  const int nact = (int)min((int64_t)REC_WAVE, nrec - i0);
+  const int64_t i = i0 + lane;
+  const bool act = lane < nact;
+  const int64_t p = act ? rec_lin[i] : rec_lin[i0];
+  // block_size of every record: two aligned dwords (U is padded by 256 zero bytes)
+  const uint32_t* U32 = reinterpret_cast<const uint32_t*>(U);
+  const int32_t bs = (int32_t)funnel(U32[p >> 2], U32[(p >> 2) + 1], (uint32_t)(p & 3));
   const int64_t n = 4 + (int64_t)bs;
-  if (p + n > ulen) {
-    *d_status = ST_SHORT;
+  const bool bad = act && p + n > ulen;
+  if (__any(bad)) {
+    if (bad) *d_status = ST_SHORT;
     return;
   }
+  const int64_t first = rec_lin[i0];
+  const int64_t lastp = rec_lin[i0 + nact - 1];
+  const int32_t lastbs = (int32_t)funnel(U32[lastp >> 2], U32[(lastp >> 2) + 1], (uint32_t)(lastp & 3));
+  const int64_t base = first & ~(int64_t)15;
+  const int64_t len = lastp + 4 + (int64_t)lastbs - base;
+  const uint32_t* W;  // dword view of the record bytes
+  int64_t off;        // byte offset of this record in W
+  if (len + 32 <= REC_STAGE) {  // the hash reads up to 12 bytes past the last record
+    const uint4* src = reinterpret_cast<const uint4*>(U + base);
+    for (int64_t o = lane; o * 16 < len + 16; o += REC_WAVE) stage4[o] = src[o];
+    __syncthreads();
+    W = reinterpret_cast<const uint32_t*>(stage4);
+    off = p - base;
+  } else {
+    W = U32;
+    off = p;
+  }
+  if (!act) return;
+  const int64_t wi0 = off >> 2;
+  const uint32_t sh = (uint32_t)(off & 3);
+  uint32_t f[10];
+  {
+    uint32_t w[10];
+#pragma unroll
+    for (int k = 0; k < 10; k++) w[k] = W[wi0 + k];
+#pragma unroll
+    for (int k = 0; k < 9; k++) f[k] = funnel(w[k], w[k + 1], sh);
+  }
   soa.block_size[i] = bs;
-  soa.ref_id[i] = ld32(U, p + 4);
-  soa.pos[i] = ld32(U, p + 8);
-  uint32_t bmn = (uint32_t)ld32(U, p + 12);
-  soa.l_read_name[i] = (uint8_t)(bmn & 0xff);
-  soa.mapq[i] = (uint8_t)((bmn >> 8) & 0xff);
-  soa.bin[i] = (uint16_t)(bmn >> 16);
-  uint32_t fnc = (uint32_t)ld32(U, p + 16);
-  soa.n_cigar[i] = (uint16_t)(fnc & 0xffff);
-  soa.flag[i] = (uint16_t)(fnc >> 16);
-  soa.l_seq[i] = ld32(U, p + 20);
-  soa.next_ref_id[i] = ld32(U, p + 24);
-  soa.next_pos[i] = ld32(U, p + 28);
-  soa.tlen[i] = ld32(U, p + 32);
-  int64_t j = block_of(uoff, nblk, p);
+  soa.ref_id[i] = (int32_t)f[1];
+  soa.pos[i] = (int32_t)f[2];
+  soa.l_read_name[i] = (uint8_t)(f[3] & 0xff);
+  soa.mapq[i] = (uint8_t)((f[3] >> 8) & 0xff);
+  soa.bin[i] = (uint16_t)(f[3] >> 16);
+  soa.n_cigar[i] = (uint16_t)(f[4] & 0xffff);
+  soa.flag[i] = (uint16_t)(f[4] >> 16);
+  soa.l_seq[i] = (int32_t)f[5];
+  soa.next_ref_id[i] = (int32_t)f[6];
+  soa.next_pos[i] = (int32_t)f[7];
+  soa.tlen[i] = (int32_t)f[8];
+  int64_t j = pt[p >> 16];
+  while (j + 1 < nblk && uoff[j + 1] <= p) j++;
   soa.voffset[i] = ((uint64_t)blk_pos[j] << 16) | (uint64_t)(p - uoff[j]);
   // hash
-  const uint32_t* U32 = reinterpret_cast<const uint32_t*>(U);
-  const int sh = (int)(p & 3) * 8;
-  int64_t wi = p >> 2;
-  uint32_t w0 = ldw(U32, wi);
   uint64_t h = (uint64_t)n * DQ_K_LEN;
   const int64_t nw = (n + 7) / 8;
+  int64_t wi = wi0;
+  uint32_t w0 = W[wi];
   for (int64_t k = 0; k < nw; k++) {
-    uint32_t w1 = ldw(U32, wi + 1), w2 = ldw(U32, wi + 2);
-    uint32_t lo = sh ? (uint32_t)((((uint64_t)w1 << 32) | w0) >> sh) : w0;
-    uint32_t hi = sh ? (uint32_t)((((uint64_t)w2 << 32) | w1) >> sh) : w1;
+    const uint32_t w1 = W[wi + 1], w2 = W[wi + 2];
+    const uint32_t lo = funnel(w0, w1, sh), hi = funnel(w1, w2, sh);
     uint64_t w = ((uint64_t)hi << 32) | lo;
-    int64_t rem = n - 8 * k;
+    const int64_t rem = n - 8 * k;
     if (rem < 8) w &= (1ull << (8 * rem)) - 1;
     h += dq_mix64(w ^ ((uint64_t)(k + 1) * DQ_K_WORD));
     w0 = w2;
@@ -696,15 +788,19 @@ __global__ void partition_ranges_kernel(const SplitPlan* __restrict__ plans, int
   parts[i] = r;
 }
 
+// grid (partition, DIG_SPLIT): block y of partition x sums every DIG_SPLIT-th group of 256 records
+// and adds its sum to the partition digest (zeroed by partition_ranges_kernel)
+constexpr int DIG_SPLIT = 64;
 __global__ __launch_bounds__(256) void partition_digest_kernel(const uint64_t* __restrict__ hash,
                                                                PartRange* __restrict__ parts,
                                                                int64_t nparts) {
   __shared__ uint64_t red[256];
-  int64_t i = blockIdx.x;
+  const int64_t i = blockIdx.x;
   if (i >= nparts) return;
   const PartRange r = parts[i];
   uint64_t acc = 0;
-  for (int64_t k = r.begin + threadIdx.x; k < r.end; k += 256)
+  for (int64_t k = r.begin + (int64_t)blockIdx.y * 256 + threadIdx.x; k < r.end;
+       k += 256 * DIG_SPLIT)
     acc += dq_mix64(hash[k] + (uint64_t)(k - r.begin + 1) * DQ_K_LEN);
   red[threadIdx.x] = acc;
   __syncthreads();
@@ -712,7 +808,8 @@ __global__ __launch_bounds__(256) void partition_digest_kernel(const uint64_t* _
     if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
     __syncthreads();
   }
-  if (threadIdx.x == 0) parts[i].digest = red[0];
+  if (threadIdx.x == 0 && red[0]) atomicAdd(reinterpret_cast<unsigned long long*>(&parts[i].digest),
+                                            (unsigned long long)red[0]);
 }
 
 // ------------------------------------------------------------------ Kernel 4: interval filter
@@ -860,18 +957,22 @@ void launch_seg_counts(const Seg* segs, int64_t nseg, int64_t* counts, hipStream
                      segs, nseg, counts);
 }
 
-void launch_seg_emit2(const uint8_t* U, const Seg* segs, const int64_t* base, int64_t nseg,
-                      int64_t* rec_lin, hipStream_t s) {
-  hipLaunchKernelGGL(seg_emit_kernel, dim3((unsigned)((nseg + 63) / 64)), dim3(64), 0, s, U, segs,
-                     base, nseg, rec_lin);
+void launch_seg_emit2(const uint8_t* U, int64_t ulen, const Seg* segs, const int64_t* base,
+                      int64_t nseg, int64_t* rec_lin, hipStream_t s) {
+  hipLaunchKernelGGL(seg_emit_kernel, dim3((unsigned)nseg), dim3(64), 0, s, U, ulen, segs, base,
+                     nseg, rec_lin);
 }
 
 void launch_decode_records(const uint8_t* U, int64_t ulen, const int64_t* rec_lin, int64_t nrec,
-                           const int64_t* blk_pos, const int32_t* blk_csize, const int64_t* uoff,
-                           int64_t nblk, RecSoA soa, int32_t* d_status, hipStream_t s) {
-  if (nrec <= 0) return;
-  hipLaunchKernelGGL(decode_records_kernel, dim3((unsigned)((nrec + 255) / 256)), dim3(256), 0, s,
-                     U, ulen, rec_lin, nrec, blk_pos, blk_csize, uoff, nblk, soa, d_status);
+                           const int64_t* blk_pos, const int64_t* uoff, int64_t nblk, int32_t* pt,
+                           RecSoA soa, int32_t* d_status, hipStream_t s) {
+  if (nrec <= 0 || nblk <= 0) return;
+  const int64_t npages = (ulen >> 16) + 1;
+  hipLaunchKernelGGL(block_pages_kernel, dim3((unsigned)((npages + 255) / 256)), dim3(256), 0, s,
+                     uoff, nblk, pt, npages);
+  hipLaunchKernelGGL(decode_records_kernel, dim3((unsigned)((nrec + REC_WAVE - 1) / REC_WAVE)),
+                     dim3(REC_WAVE), 0, s, U, ulen, rec_lin, nrec, blk_pos, uoff, nblk, pt, soa,
+                     d_status);
 }
 
 void launch_partition_ranges(const SplitPlan* plans, int64_t nsplit, const int64_t* rec_lin,
@@ -884,8 +985,8 @@ void launch_partition_ranges(const SplitPlan* plans, int64_t nsplit, const int64
 
 void launch_partition_digest2(const uint64_t* hash, PartRange* parts, int64_t nparts, hipStream_t s) {
   if (nparts <= 0) return;
-  hipLaunchKernelGGL(partition_digest_kernel, dim3((unsigned)nparts), dim3(256), 0, s, hash, parts,
-                     nparts);
+  hipLaunchKernelGGL(partition_digest_kernel, dim3((unsigned)nparts, DIG_SPLIT), dim3(256), 0, s,
+                     hash, parts, nparts);
 }
 
 void launch_interval_filter(const uint8_t* U, const int64_t* rec_lin, const RecSoA soa,
