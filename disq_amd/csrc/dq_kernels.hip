@@ -489,99 +489,67 @@ __device__ int walk(const uint8_t* U, int64_t ulen, int u_is_eof, int64_t start,
   return 0;
 }
 
-// The same walk by a whole wave: the wave copies 4 KiB windows of U into LDS with coalesced
-// loads and walks the block_size chain through LDS (one global round trip per ~12 records instead
-// of one per record).  p, the count and the result are wave-uniform.
-constexpr int WALK_WIN = 4096;
-__device__ int walk_wave(const uint8_t* U, int64_t ulen, int u_is_eof, int64_t start,
-                         int64_t seg_end, int64_t* exit, int64_t* count, uint4* win4,
-                         int64_t* out = nullptr, int64_t out_max = 0) {
-  const uint8_t* win = reinterpret_cast<const uint8_t*>(win4);
-  const int lane = threadIdx.x;
-  int64_t p = start, n = 0;
-  int64_t wb = -1;  // window base (16-byte aligned), -1 none
-  while (p < seg_end && (!out || n < out_max)) {
-    if (p + 4 > ulen) {
-      if (u_is_eof) {
-        *exit = END_CHAIN;
-        *count = n;
-        return 0;
-      }
-      return 4;
-    }
-    if (wb < 0 || p + 4 > wb + WALK_WIN) {
-      __syncthreads();  // every lane is done with the old window
-      wb = p & ~(int64_t)15;
-      const uint4* src = reinterpret_cast<const uint4*>(U + wb);
-#pragma unroll
-      for (int k = 0; k < WALK_WIN / 16 / 64; k++) {  // U is padded by 256 zero bytes
-        const int c = lane + 64 * k;
-        win4[c] = wb + 16 * (c + 1) <= ulen + 256 ? src[c] : make_uint4(0, 0, 0, 0);
-      }
-      __syncthreads();
-    }
-    const int64_t o = p - wb;
-    const int32_t bs = (int32_t)(win[o] | (win[o + 1] << 8) | (win[o + 2] << 16) |
-                                 ((uint32_t)win[o + 3] << 24));
-    if (bs < 32) return ST_BAD_CODE;  // "Invalid record length" (SAMFormatException)
-    if (out && lane == 0 && n < out_max) out[n] = p;
-    n++;
-    p += 4 + (int64_t)bs;
-  }
-  *exit = p;
-  *count = n;
-  return 0;
-}
-
+// One wave per segment (grid-stride: a few thousand resident waves instead of one dispatch per
+// segment): the first guesser hit at or after the segment start, 64 positions per step.
 __global__ __launch_bounds__(64) void seg_spec_kernel(const uint8_t* __restrict__ U, int64_t ulen,
                                                       int32_t u_is_eof,
                                                       const int32_t* __restrict__ ref_len,
                                                       int32_t n_ref, Seg* __restrict__ segs,
                                                       int64_t nseg, int64_t seg_bytes,
                                                       int64_t start_lin, int64_t chain_end) {
-  int64_t s = blockIdx.x;
-  if (s >= nseg) return;
-  const int64_t sb = start_lin + s * seg_bytes;
-  const int64_t se = min(chain_end, sb + seg_bytes);
-  __shared__ int64_t best;
-  if (threadIdx.x == 0) best = INT64_MAX;
-  __syncthreads();
-  if (s == 0) {
-    if (threadIdx.x == 0) best = start_lin;
-  } else {
-    for (int64_t b = sb; b < se; b += 64) {
-      int64_t v = b + threadIdx.x;
-      bool hit = v < se && check_record_start(U, ulen, u_is_eof, ref_len, n_ref, v) == 1;
-      uint64_t m = __ballot(hit);
-      if (m) {
-        if (threadIdx.x == 0) best = b + __builtin_ctzll(m);
-        break;
+  for (int64_t s = blockIdx.x; s < nseg; s += gridDim.x) {
+    const int64_t sb = start_lin + s * seg_bytes;
+    const int64_t se = min(chain_end, sb + seg_bytes);
+    int64_t best = INT64_MAX;
+    if (s == 0) {
+      best = start_lin;
+    } else {
+      for (int64_t b = sb; b < se; b += 64) {
+        const int64_t v = b + threadIdx.x;
+        const bool hit = v < se && check_record_start(U, ulen, u_is_eof, ref_len, n_ref, v) == 1;
+        const uint64_t m = __ballot(hit);
+        if (m) {
+          best = b + __builtin_ctzll(m);
+          break;
+        }
       }
     }
-  }
-  __syncthreads();
-  __shared__ uint4 win4[WALK_WIN / 16];
-  Seg g;
-  g.exact = s == 0;
-  g.status = 0;
-  g.start = best == INT64_MAX ? -1 : best;  // -1: no start speculated in this segment
-  g.exit = -1;
-  g.count = 0;
-  if (g.start >= 0) {
-    int64_t ex, cnt;
-    const int r = walk_wave(U, ulen, u_is_eof, g.start, se, &ex, &cnt, win4);
-    g.status = r;
-    if (r == 0) {
-      g.exit = ex;
-      g.count = cnt;
+    if (threadIdx.x == 0) {
+      Seg g;
+      g.exact = s == 0;
+      g.status = 0;
+      g.start = best == INT64_MAX ? -1 : best;  // -1: no start speculated in this segment
+      g.exit = -1;
+      g.count = 0;
+      segs[s] = g;
     }
   }
-  if (threadIdx.x == 0) segs[s] = g;
 }
 
-// Serial link check + repair (one lane).  Segments are few (one per 1 MiB of U); each link is
-// O(1) unless a speculation was wrong, in which case that segment is re-walked from the exact
-// incoming position.
+// The walks of all segments, one lane each (a walk is a chain of dependent loads: many walks per
+// wave keep many in flight).
+__global__ __launch_bounds__(256) void seg_walk_kernel(const uint8_t* __restrict__ U, int64_t ulen,
+                                                       int32_t u_is_eof, Seg* __restrict__ segs,
+                                                       int64_t nseg, int64_t seg_bytes,
+                                                       int64_t start_lin, int64_t chain_end) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nseg) return;
+  Seg g = segs[s];
+  if (g.start < 0) return;
+  const int64_t se = min(chain_end, start_lin + (s + 1) * seg_bytes);
+  int64_t ex, cnt;
+  const int r = walk(U, ulen, u_is_eof, g.start, se, &ex, &cnt);
+  g.status = r;
+  if (r == 0) {
+    g.exit = ex;
+    g.count = cnt;
+  }
+  segs[s] = g;
+}
+
+// Serial link check + repair (one lane), run only when seg_link found a broken link (a guesser
+// false positive): each link is O(1) unless a speculation was wrong, in which case that segment is
+// re-walked from the exact incoming position.
 __global__ void seg_fix_kernel(const uint8_t* __restrict__ U, int64_t ulen, int32_t u_is_eof,
                                Seg* __restrict__ segs, int64_t nseg, int64_t seg_bytes,
                                int64_t start_lin, int64_t chain_end, int32_t* d_status) {
@@ -645,19 +613,17 @@ __global__ void seg_counts_kernel(const Seg* __restrict__ segs, int64_t nseg, in
   if (s < nseg) counts[s] = segs[s].count;
 }
 
-// One wave per segment: the record starts of the (exact) chain, walked through LDS windows.
-__global__ __launch_bounds__(64) void seg_emit_kernel(const uint8_t* __restrict__ U, int64_t ulen,
-                                                      const Seg* __restrict__ segs,
-                                                      const int64_t* __restrict__ base, int64_t nseg,
-                                                      int64_t* __restrict__ rec_lin) {
-  __shared__ uint4 win4[WALK_WIN / 16];
-  const int64_t s = blockIdx.x;
+__global__ void seg_emit_kernel(const uint8_t* __restrict__ U, const Seg* __restrict__ segs,
+                                const int64_t* __restrict__ base, int64_t nseg,
+                                int64_t* __restrict__ rec_lin) {
+  int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nseg) return;
   const Seg g = segs[s];
-  if (g.count <= 0) return;
-  int64_t ex, cnt;
-  // the chain was validated by seg_spec / seg_fix: walk exactly g.count records
-  walk_wave(U, ulen, 1, g.start, INT64_MAX, &ex, &cnt, win4, rec_lin + base[s], g.count);
+  int64_t p = g.start, o = base[s];
+  for (int64_t k = 0; k < g.count; k++) {
+    rec_lin[o + k] = p;
+    p += 4 + (int64_t)ld32(U, p);
+  }
 }
 
 // ------------------------------------------------------------------ decode + hash
@@ -681,13 +647,12 @@ __device__ inline uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t sh) {  // (
 constexpr int REC_WAVE = 64;
 constexpr int REC_STAGE = 24576;  // 64 short-read records (~21 KB); 6 waves per CU
 
-__global__ __launch_bounds__(64) void decode_records_kernel(
-    const uint8_t* __restrict__ U, int64_t ulen, const int64_t* __restrict__ rec_lin, int64_t nrec,
-    const int64_t* __restrict__ blk_pos, const int64_t* __restrict__ uoff, int64_t nblk,
-    const int32_t* __restrict__ pt, RecSoA soa, int32_t* d_status) {
-  __shared__ uint4 stage4[REC_STAGE / 16 + 1];
+__device__ void decode_group(const uint8_t* __restrict__ U, int64_t ulen,
+                             const int64_t* __restrict__ rec_lin, int64_t nrec,
+                             const int64_t* __restrict__ blk_pos, const int64_t* __restrict__ uoff,
+                             int64_t nblk, const int32_t* __restrict__ pt, const RecSoA& soa,
+                             int32_t* d_status, int64_t i0, uint4* stage4) {
   const int lane = threadIdx.x;
-  const int64_t i0 = (int64_t)blockIdx.x * REC_WAVE;
   const int nact = (int)min((int64_t)REC_WAVE, nrec - i0);
   const int64_t i = i0 + lane;
   const bool act = lane < nact;
@@ -709,8 +674,15 @@ __global__ __launch_bounds__(64) void decode_records_kernel(
   const uint32_t* W;  // dword view of the record bytes
   int64_t off;        // byte offset of this record in W
   if (len + 32 <= REC_STAGE) {  // the hash reads up to 12 bytes past the last record
+    // LDS-DMA: every 16-byte piece in flight at once (a register-staged loop waits per piece)
     const uint4* src = reinterpret_cast<const uint4*>(U + base);
-    for (int64_t o = lane; o * 16 < len + 16; o += REC_WAVE) stage4[o] = src[o];
+    const int npiece = (int)((len + 31) / 16);
+    for (int c0 = 0; c0 < npiece; c0 += REC_WAVE)
+      if (c0 + lane < npiece)
+        __builtin_amdgcn_global_load_lds(
+            static_cast<const void*>(src + c0 + lane),
+            (__attribute__((address_space(3))) void*)(stage4 + c0), 16, 0, 0);
+    __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     W = reinterpret_cast<const uint32_t*>(stage4);
     off = p - base;
@@ -760,6 +732,19 @@ __global__ __launch_bounds__(64) void decode_records_kernel(
     wi += 2;
   }
   soa.hash[i] = dq_mix64(h);
+}
+
+// Grid-stride over groups of 64 records: a few thousand resident waves, not one dispatch per group.
+__global__ __launch_bounds__(64) void decode_records_kernel(
+    const uint8_t* __restrict__ U, int64_t ulen, const int64_t* __restrict__ rec_lin, int64_t nrec,
+    const int64_t* __restrict__ blk_pos, const int64_t* __restrict__ uoff, int64_t nblk,
+    const int32_t* __restrict__ pt, RecSoA soa, int32_t* d_status) {
+  __shared__ uint4 stage4[REC_STAGE / 16 + 1];
+  for (int64_t g = blockIdx.x; g * REC_WAVE < nrec; g += gridDim.x) {
+    decode_group(U, ulen, rec_lin, nrec, blk_pos, uoff, nblk, pt, soa, d_status, g * REC_WAVE,
+                 stage4);
+    __syncthreads();  // this group is done with the staging buffer
+  }
 }
 
 // ------------------------------------------------------------------ partitions
@@ -934,8 +919,10 @@ void launch_seg_spec(const uint8_t* U, int64_t ulen, int32_t u_is_eof, int64_t c
                      int32_t n_ref, Seg* segs, int64_t nseg, int64_t seg_bytes, int64_t start_lin,
                      hipStream_t s) {
   if (nseg <= 0) return;
-  hipLaunchKernelGGL(seg_spec_kernel, dim3((unsigned)nseg), dim3(64), 0, s, U, ulen, u_is_eof,
+  hipLaunchKernelGGL(seg_spec_kernel, dim3((unsigned)std::min<int64_t>(nseg, 16384)), dim3(64), 0, s, U, ulen, u_is_eof,
                      ref_len, n_ref, segs, nseg, seg_bytes, start_lin, chain_end);
+  hipLaunchKernelGGL(seg_walk_kernel, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, U, ulen,
+                     u_is_eof, segs, nseg, seg_bytes, start_lin, chain_end);
 }
 
 void launch_seg_fix2(const uint8_t* U, int64_t ulen, int32_t u_is_eof, int64_t chain_end,
@@ -957,10 +944,10 @@ void launch_seg_counts(const Seg* segs, int64_t nseg, int64_t* counts, hipStream
                      segs, nseg, counts);
 }
 
-void launch_seg_emit2(const uint8_t* U, int64_t ulen, const Seg* segs, const int64_t* base,
+void launch_seg_emit2(const uint8_t* U, int64_t, const Seg* segs, const int64_t* base,
                       int64_t nseg, int64_t* rec_lin, hipStream_t s) {
-  hipLaunchKernelGGL(seg_emit_kernel, dim3((unsigned)nseg), dim3(64), 0, s, U, ulen, segs, base,
-                     nseg, rec_lin);
+  hipLaunchKernelGGL(seg_emit_kernel, dim3((unsigned)((nseg + 63) / 64)), dim3(64), 0, s, U, segs,
+                     base, nseg, rec_lin);
 }
 
 void launch_decode_records(const uint8_t* U, int64_t ulen, const int64_t* rec_lin, int64_t nrec,
@@ -970,7 +957,8 @@ void launch_decode_records(const uint8_t* U, int64_t ulen, const int64_t* rec_li
   const int64_t npages = (ulen >> 16) + 1;
   hipLaunchKernelGGL(block_pages_kernel, dim3((unsigned)((npages + 255) / 256)), dim3(256), 0, s,
                      uoff, nblk, pt, npages);
-  hipLaunchKernelGGL(decode_records_kernel, dim3((unsigned)((nrec + REC_WAVE - 1) / REC_WAVE)),
+  hipLaunchKernelGGL(decode_records_kernel,
+                     dim3((unsigned)std::min<int64_t>((nrec + REC_WAVE - 1) / REC_WAVE, 8192)),
                      dim3(REC_WAVE), 0, s, U, ulen, rec_lin, nrec, blk_pos, uoff, nblk, pt, soa,
                      d_status);
 }
