@@ -380,6 +380,15 @@ DQ_AI int wave_incl_scan(int v, int) {
   v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
   return v;
 }
+DQ_AI int wave_incl_or(int v) {
+  v |= __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+  v |= __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
+  v |= __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
+  v |= __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
+  v |= __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+  v |= __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+  return v;
+}
 DQ_AI int wave_incl_max(int v) {  // values >= -1
   v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x111, 0xf, 0xf, false));
   v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x112, 0xf, 0xf, false));
@@ -523,8 +532,7 @@ DQ_AI void build_tables(LdsI& L, int nlen, int ndist) {
 // Dynamic header: decode the code-length sequence (wave 0) into L.u.d.x.h.lens.
 // Returns the bit position after the header, or sets M_ERR.
 DQ_AI uint32_t read_lengths(const uint32_t* __restrict__ W, LdsI& L, uint32_t P, int nlen,
-                                 int ndist, uint32_t endbits, uint32_t hbase, int& nit,
-                                 uint64_t* tp = nullptr) {
+                                 int ndist, uint32_t endbits, uint32_t hbase, int& nit) {
   // the header's compressed words were staged in the (not yet built) decode table: HB_WORDS
   // words cover the longest possible header (17 + 57 + 320 * 14 bits)
   const uint32_t* hb = reinterpret_cast<const uint32_t*>(L.u.d.T);
@@ -544,33 +552,44 @@ DQ_AI uint32_t read_lengths(const uint32_t* __restrict__ W, LdsI& L, uint32_t P,
     const uint32_t o = off + (uint32_t)lane;  // <= 94
     const uint64_t x = o < 64 ? ((lo >> o) | (o ? hi << (64 - o) : 0ull)) : (hi >> (o - 64));
     const uint32_t bits = (uint32_t)x;
-    uint64_t q0 = tp ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t ent = L.u.d.x.h.clt[bits & 127];
     const uint32_t cl = ent & 7, s = ent >> 3;
     const uint32_t ex = s == 16 ? 2u : s == 17 ? 3u : s == 18 ? 7u : 0u;
     const uint32_t xv = (bits >> cl) & ((1u << ex) - 1);
     const int rep = s < 16 ? 1 : s == 16 ? 3 + (int)xv : s == 17 ? 3 + (int)xv : 11 + (int)xv;
     const int adv = cl ? (int)(cl + ex) : 0;
-    // walk the true symbol path through this window (uniform)
-    uint64_t q1 = tp ? __builtin_amdgcn_s_memtime() : 0;
-    uint64_t mark = 0;
-    int j = 0, cum = have;
-    bool bad = false;
-    while (j < 64 && cum < total) {
-      const int a = __builtin_amdgcn_readlane(adv, j);
-      if (a == 0) {
-        bad = true;
-        break;
-      }
-      mark |= 1ull << j;
-      cum += __builtin_amdgcn_readlane(rep, j);
-      j += a;
+    // the true symbol path through this window, by pointer doubling: J_b = successor^(2^b)
+    // (lane + adv; an invalid code is a self-loop, leaving the window is 64), then lane k finds the
+    // k-th symbol of the path from lane 0 -- 11 lane shuffles instead of a serial readlane walk
+    int Jb[6];
+    Jb[0] = adv ? min(lane + adv, 64) : lane;
+#pragma unroll
+    for (int b = 1; b < 6; b++) {
+      const int y = __shfl(Jb[b - 1], min(Jb[b - 1], 63), 64);
+      Jb[b] = Jb[b - 1] >= 64 ? 64 : y;
     }
-    if (bad || cum > total) {
+    int pk = 0;  // start lane of the lane-th symbol of the path
+#pragma unroll
+    for (int b = 0; b < 6; b++) {
+      const int y = __shfl(Jb[b], min(pk, 63), 64);
+      if ((lane >> b) & 1) pk = pk >= 64 ? 64 : y;
+    }
+    const uint64_t pbit = pk < 64 ? 1ull << pk : 0ull;
+    const uint64_t path = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(wave_incl_or((int)(uint32_t)(pbit >> 32)), 63) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane(wave_incl_or((int)(uint32_t)pbit), 63);
+    // take path symbols while the lengths read so far are < total
+    const bool onp = (path >> lane) & 1;
+    const int rp = onp ? rep : 0;
+    const int rinc = wave_incl_scan(rp, lane);
+    const bool take = onp && have + rinc - rp < total;
+    const uint64_t mark = __ballot(take);
+    const int lastl = 63 - __clzll(mark);  // lane 0 is always taken (have < total)
+    const int cum = have + __builtin_amdgcn_readlane(rinc, lastl);
+    const int j = lastl + __builtin_amdgcn_readlane(adv, lastl);
+    if (__any(take && adv == 0) || cum > total) {
       set_err(L, ST_BAD_TABLE);
       return P;
     }
-    uint64_t q2 = tp ? __builtin_amdgcn_s_memtime() : 0;
     const bool on = (mark >> lane) & 1;
     // value written by each symbol: 0-15 literal length, 17/18 zero, 16 the previous value
     const int v0 = s < 16 ? (int)s : 0;
@@ -583,19 +602,13 @@ DQ_AI uint32_t read_lengths(const uint32_t* __restrict__ W, LdsI& L, uint32_t P,
       return P;
     }
     const int r = on ? rep : 0;
-    const int incl = wave_incl_scan(r, lane);
+    const int incl = rinc;  // taken lanes precede the untaken ones on the path
     if (on && val != 0) {  // lens is zero-filled: zero runs (up to 138) need no stores
       for (int i = have + incl - r; i < have + incl; i++)
         L.u.d.x.h.lens[i < nlen ? i : 288 + i - nlen] = (uint8_t)val;
     }
     const int lastlane = 63 - __clzll(mark);
     prev = __builtin_amdgcn_readlane(val, lastlane);
-    if (tp) {
-      uint64_t q3 = __builtin_amdgcn_s_memtime();
-      tp[12] += q1 - q0;
-      tp[13] += q2 - q1;
-      tp[14] += q3 - q2;
-    }
     have = cum;
     P += (uint32_t)j;
   }
