@@ -400,26 +400,42 @@ DQ_AI int wave_incl_max(int v) {  // values >= -1
 }
 DQ_AI uint64_t lanes_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
 
-// Canonical description of one alphabet from the per-wave length counts (one thread).
-// Returns 0, or ST_BAD_TABLE for an over-subscribed or (except a single code) incomplete code.
-DQ_AI int canon_from_counts(LdsI& L, int w0, int nw, HuffCanon& h) {
-  int left = 1, maxl = 0;
+// Canonical description of one alphabet from the per-wave length counts (one thread; the
+// W * 15 count reads are independent and issued together).  Also stores the number of codes no
+// longer than the root (q0) and of all codes (qn).  Returns 0, or ST_BAD_TABLE for an
+// over-subscribed or (except a single code) incomplete code.
+template <int W0, int NW, int R>
+DQ_AI int canon_from_counts(LdsI& L, HuffCanon& h, int32_t* q0p, int32_t* qnp) {
+  int cnt[16];
+#pragma unroll
+  for (int l = 1; l <= 15; l++) {
+    int c = 0;
+#pragma unroll
+    for (int w = W0; w < W0 + NW; w++) c += L.u.d.x.h.cntw[w][l];
+    cnt[l] = c;
+  }
+  int left = 1, maxl = 0, q0 = 0;
   uint32_t code = 0, off = 0;
+  bool over = false;
   h.first[0] = 0;
   h.count[0] = 0;
   h.offs[0] = 0;
+#pragma unroll
   for (int l = 1; l <= 15; l++) {
-    int c = 0;
-    for (int w = w0; w < w0 + nw; w++) c += L.u.d.x.h.cntw[w][l];
+    const int c = cnt[l];
     left = (left << 1) - c;
-    if (left < 0) return ST_BAD_TABLE;
-    if (c) maxl = l;
+    over = over || left < 0;
+    maxl = c ? l : maxl;
     h.first[l] = (uint16_t)code;
     h.count[l] = (uint16_t)c;
     h.offs[l] = (uint16_t)off;
     off += c;
+    if (l == R) q0 = (int)off;
     code = (code + c) << 1;
   }
+  *q0p = q0;
+  *qnp = (int)off;
+  if (over) return ST_BAD_TABLE;
   if (maxl > 0 && left > 0 && maxl != 1) return ST_BAD_TABLE;  // zlib inflate_table rule
   return 0;
 }
@@ -444,11 +460,11 @@ DQ_AI void build_tables(LdsI& L, int nlen, int ndist) {
   }
   __syncthreads();
   if (t == 0) {
-    const int e = canon_from_counts(L, 0, 5, L.u.d.hl);
+    const int e = canon_from_counts<0, 5, LR>(L, L.u.d.hl, &L.misc[M_LQ0], &L.misc[M_LQN]);
     if (e) set_err(L, e);
   }
   if (t == 320) {
-    const int e = canon_from_counts(L, 5, 1, L.u.d.hd);
+    const int e = canon_from_counts<5, 1, DR>(L, L.u.d.hd, &L.misc[M_DQ0], &L.misc[M_DQN]);
     if (e) set_err(L, e);
   }
   __syncthreads();
@@ -471,21 +487,6 @@ DQ_AI void build_tables(LdsI& L, int nlen, int ndist) {
     } else {
       L.u.d.x.h.pref[(isl ? 0 : 288) + q] = (uint16_t)(code >> (len - R));
     }
-  }
-  // first canonical position of a long code / number of codes, per alphabet
-  if (t == 0) {
-    int n = 0, q0 = 0;
-    for (int l = 1; l <= 15; l++) n += L.u.d.hl.count[l];
-    for (int l = 1; l <= LR; l++) q0 += L.u.d.hl.count[l];
-    L.misc[M_LQ0] = q0;
-    L.misc[M_LQN] = n;
-  }
-  if (t == 320) {
-    int n = 0, q0 = 0;
-    for (int l = 1; l <= 15; l++) n += L.u.d.hd.count[l];
-    for (int l = 1; l <= DR; l++) q0 += L.u.d.hd.count[l];
-    L.misc[M_DQ0] = q0;
-    L.misc[M_DQN] = n;
   }
   __syncthreads();
   // second-level tables: thread t handles canonical position t of each alphabet
