@@ -94,8 +94,6 @@ struct alignas(16) LdsI {
   int32_t misc[32];
   int32_t wsum[16];
   int32_t small[8 * 7];           // per-lane arrays when the image tail is too short
-  uint32_t ltab[29];              // length symbols 257..285: base | extra bits << 16
-  uint32_t dtab[30];              // distance symbols: base | extra bits << 16
 };
 static_assert(sizeof(LdsI) <= 81920, "two workgroups per CU");
 static_assert(HB_WORDS * 4 <= T_END * 2, "header staging fits the decode table");
@@ -195,6 +193,15 @@ DQ_AI uint32_t d_second(const LdsI& L, uint32_t e, uint32_t bb) {
   return k < 0 ? 0u : (((uint32_t)L.u.d.dsym[k] << 4) | (uint32_t)l);
 }
 
+// Length / distance bases and extra bits by arithmetic (RFC 1951 3.2.5): a few ALU ops instead of
+// a dependent LDS table read on the symbol path.  k = length symbol - 257 (0..28), d = 0..29.
+DQ_AI uint32_t lbase(uint32_t k) {
+  return k < 8 ? k + 3 : k == 28 ? 258u : ((4u + ((k - 4) & 3)) << ((k - 4) >> 2)) + 3;
+}
+DQ_AI uint32_t lextra(uint32_t k) { return (k < 8 || k == 28) ? 0u : (k - 4) >> 2; }
+DQ_AI uint32_t dbase(uint32_t d) { return d < 2 ? d + 1 : ((2u + (d & 1)) << ((d >> 1) - 1)) + 1; }
+DQ_AI uint32_t dextra(uint32_t d) { return d < 4 ? 0u : (d - 2) >> 1; }
+
 // One full symbol: a literal (value in len), a match (len, dist) or EOB.  Straight-line: every
 // lane does the litlen and the distance lookup (a literal lane consumes no distance bits), so a
 // wave mixing literals and matches does not execute both paths one after the other.
@@ -206,18 +213,18 @@ DQ_AI int dsym(BitR& r, const uint32_t* __restrict__ W, const LdsI& L, uint32_t&
   if (e & (E_LINK | E_SLOW)) e = ll_second(L, e, bb);
   const uint32_t nb = e & 15, sym = e >> 4;
   const bool is_len = sym - 257u < 29u;
-  const uint32_t lt = L.ltab[min(sym - 257u, 28u)];
-  const uint32_t lx = is_len ? (lt >> 16) : 0u;
-  len = is_len ? (lt & 0xffffu) + ((bb >> nb) & ((1u << lx) - 1)) : sym;
+  const uint32_t lk = min(sym - 257u, 28u);
+  const uint32_t lx = is_len ? lextra(lk) : 0u;
+  len = is_len ? lbase(lk) + ((bb >> nb) & ((1u << lx) - 1)) : sym;
   br_take(r, nb + lx);
   br_refill(r, W);  // >= 33 bits: a distance code + its extra bits (<= 28)
   bb = (uint32_t)r.bb;
   uint32_t e2 = L.u.d.T[T_DROOT + (bb & ((1u << DR) - 1))];
   if (is_len && (e2 & (E_LINK | E_SLOW))) e2 = d_second(L, e2, bb);
   const uint32_t nb2 = e2 & 15, ds = e2 >> 4;
-  const uint32_t dt = L.dtab[min(ds, 29u)];
-  const uint32_t dx = dt >> 16;
-  dist = (dt & 0xffffu) + ((bb >> nb2) & ((1u << dx) - 1));
+  const uint32_t dd = min(ds, 29u);
+  const uint32_t dx = dextra(dd);
+  dist = dbase(dd) + ((bb >> nb2) & ((1u << dx) - 1));
   br_take(r, is_len ? nb2 + dx : 0u);
   if (nb == 0 || sym > 285) return S_ERR;
   if (sym < 256) return S_LIT;
@@ -658,8 +665,6 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
 
   for (int i = t; i < 2048; i += WG) L.bm[i] = 0;
   if (t < 32) L.misc[t] = 0;
-  if (t < 29) L.ltab[t] = len_base((uint32_t)t) | (len_extra((uint32_t)t) << 16);
-  if (t >= 64 && t < 94) L.dtab[t - 64] = dist_base((uint32_t)(t - 64)) | (dist_extra((uint32_t)(t - 64)) << 16);
   if (t == 0) {
     if (isize < 0 || isize > 65536) L.misc[M_ERR] = ST_ISIZE;
     else if (dbytes < 0) L.misc[M_ERR] = ST_OVERREAD;
