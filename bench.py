@@ -22,6 +22,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "decompressed BAM GB/s + reads/sec (whole node) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+TRAFFIC_PROFILE = "r1d_inflate_traffic_pmc.json"
 
 
 def log(*a):
@@ -125,6 +126,16 @@ def main():
     alg_bytes = stats.deflate_bytes + stats.decompressed_bytes
     achieved = alg_bytes / (infl_avg / 1e3) / 1e9
 
+    # HBM traffic of the same launch from the committed PMC passes (tools/pmc_traffic.sh runs this
+    # bench under rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE; a process cannot count itself), used
+    # only when it was taken on this workload
+    traffic, traffic_src = None, None
+    tp = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", TRAFFIC_PROFILE)
+    if os.path.exists(tp) and abs(args.gb - 10.0) < 1e-9 and args.split_size == 0:
+        with open(tp) as f:
+            traffic = json.load(f).get("traffic_bytes_per_launch")
+        traffic_src = "profiles/" + TRAFFIC_PROFILE + " (FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction)"
+
     cpu = None
     if rank == 0 and cpu_data is not None:
         cpu = cpu_baseline(cpu_data, args, threads)
@@ -168,7 +179,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_src": traffic_src,
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_launch_ms": round(infl_avg, 3),
             },

@@ -124,6 +124,12 @@ struct BitR {
 
 #define DQ_AI __device__ __attribute__((always_inline)) inline
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+DQ_AI void st_nt(uint4* d, uint4 v) {  // streaming store (nt): U is not re-read by this kernel
+  u32x4 x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(d));
+}
+
 DQ_AI void br_init(BitR& r, const uint32_t* __restrict__ W, uint32_t bitpos) {
   const uint32_t wi = bitpos >> 5;
   const uint64_t lo = W[wi], hi = W[wi + 1];
@@ -630,7 +636,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     const int32_t* __restrict__ blk_csize, const int32_t* __restrict__ blk_usize,
     const int64_t* __restrict__ uoff, int64_t nblk, uint8_t* __restrict__ U,
     int32_t* __restrict__ status, int32_t verify_crc, const uint32_t* __restrict__ crc_init,
-    uint64_t* __restrict__ tim, uint32_t OV) {
+    uint64_t* __restrict__ tim, uint32_t OV, uint32_t sflags) {
   __shared__ LdsI L;
   // DQ_TIMING: thread 0 accumulates s_memtime cycles per phase (tim != nullptr only then)
   uint64_t tacc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -1149,9 +1155,15 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     // (c) store the 16-byte U lines this batch completed (overlaps the next batch's chains)
     const int32_t c1 = min(isize, bs + BATCH);
     const int32_t lines_to = c1 >= head ? (c1 - head) / 16 : 0;
-    for (int32_t k = lines_done + t; k < lines_to; k += WG)
-      *reinterpret_cast<uint4*>(dstU + head + 16 * k) = *reinterpret_cast<const uint4*>(O + head + 16 * k);
-    lines_done = lines_to;
+    if (!(sflags & 1)) {
+      for (int32_t k = lines_done + t; k < lines_to; k += WG) {
+        const uint4 v = *reinterpret_cast<const uint4*>(O + head + 16 * k);
+        uint4* d = reinterpret_cast<uint4*>(dstU + head + 16 * k);
+        if (sflags & 2) st_nt(d, v);
+        else *d = v;
+      }
+      lines_done = lines_to;
+    }
     if (TIMING && t == 0) {
       (void)wgm;
       (void)tb0; (void)tb1;
@@ -1164,6 +1176,16 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     tacc[9] = (uint64_t)L.misc[25];
     tacc[12] = (uint64_t)L.misc[26];
     tacc[11] = (uint64_t)L.misc[27];
+  }
+  if (sflags & 1) {  // the whole block at the end
+    const int32_t lines_to = isize >= head ? (isize - head) / 16 : 0;
+    for (int32_t k = t; k < lines_to; k += WG) {
+      const uint4 v = *reinterpret_cast<const uint4*>(O + head + 16 * k);
+      uint4* d = reinterpret_cast<uint4*>(dstU + head + 16 * k);
+      if (sflags & 2) st_nt(d, v);
+      else *d = v;
+    }
+    lines_done = lines_to;
   }
   for (int x = t; x < head; x += WG) dstU[x] = O[x];
   for (int x = head + 16 * lines_done + t; x < isize; x += WG) dstU[x] = O[x];
@@ -1262,6 +1284,7 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
                      int32_t* status, int32_t verify_crc, uint64_t* tim, hipStream_t s) {
   if (nblk <= 0) return;
   static const uint32_t ov = getenv("DQ_OV") ? (uint32_t)atoi(getenv("DQ_OV")) : OV_DEFAULT;
+  static const uint32_t sflags = getenv("DQ_STORE") ? (uint32_t)atoi(getenv("DQ_STORE")) : 2;
   static int cfg = -1;
   if (cfg < 0) {  // DQ_CFG="nb,g" (tuning experiments); default 4,1
     int nb = 4, g = 1;
@@ -1270,7 +1293,7 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
   }
 #define DQ_LAUNCH(TM, NBT, GT)                                                                  \
   hipLaunchKernelGGL((inflate_block_kernel<TM, NBT, GT>), dim3((unsigned)nblk), dim3(WG), 0, s, C, \
-                     blk_pos, blk_csize, blk_usize, uoff, nblk, U, status, verify_crc, g_crc_init, tim, ov)
+                     blk_pos, blk_csize, blk_usize, uoff, nblk, U, status, verify_crc, g_crc_init, tim, ov, sflags)
 #define DQ_CFGS(TM)                       \
   switch (cfg) {                          \
     case 1: DQ_LAUNCH(TM, 1, 4); break;   \
