@@ -11,7 +11,15 @@ exchange two small messages:
   * per-partition descriptors (record count, partition digest, first record pointer), all-gathered
     so every rank can fold the whole-file digest in partition order and check that the shards
     tile the file exactly as the single-GPU stream does.
-No record bytes cross ranks: the halo is read from the file, not exchanged.
+Shard boundary stitching (north star): a record that starts in a rank's last
+partition may run into the next rank's bytes.  With `stitch="exchange"` (the default for world > 1)
+every rank reads only its own byte range from the file and the halo is assembled from an
+all_gather of every shard's first `halo` compressed bytes (RCCL over xGMI when the group's backend
+is nccl, gloo on CPU); rank r appends the heads of ranks r+1, r+2, ... until it holds `halo` bytes
+past its end.  When a rank's straddling record (or the guesser's 10-record look-ahead) needs more,
+all ranks agree through a one-int all_reduce and repeat the exchange with a 4x larger window.
+`stitch="file"` reads the halo from the file instead (single rank, or a shared file system where
+re-reading is cheaper than the exchange).
 """
 from __future__ import annotations
 
@@ -142,6 +150,93 @@ def read_shard(read_bytes: Callable[[int, int], bytes], file_len: int, shard: Sh
     return ShardResult(shard, batch, idx, counts, digests, halo)
 
 
+def _halo_from_heads(heads: Sequence[bytes], shards: Sequence[Shard], rank: int, halo: int) -> bytes:
+    """File bytes [hi_rank, hi_rank + halo) from the gathered shard heads: head k holds
+    min(halo, hi_k - lo_k) bytes starting at lo_k, and shards tile the file in rank order."""
+    out, need = [], halo
+    for k in range(rank + 1, len(shards)):
+        if shards[k].empty:
+            continue
+        h = heads[k]
+        out.append(h[:need])
+        need -= min(need, len(h))
+        if need == 0 or len(h) < shards[k].hi - shards[k].lo:
+            break
+    return b"".join(out)
+
+
+def exchange_heads(own: bytes, shards: Sequence[Shard], rank: int, halo: int, group=None,
+                   device: Optional[int] = None) -> bytes:
+    """all_gather of every shard's first `halo` bytes (fixed-size window, one collective); returns
+    this rank's halo.  On an nccl (RCCL) group the window lives in HBM and crosses xGMI."""
+    import torch
+    import torch.distributed as dist
+    world = len(shards)
+    on_gpu = dist.get_backend(group) == "nccl"
+    dev = torch.device("cuda", device if device is not None else torch.cuda.current_device()) \
+        if on_gpu else torch.device("cpu")
+    mine = torch.zeros(halo, dtype=torch.uint8)
+    head = own[:halo]
+    if head:
+        mine[:len(head)] = torch.frombuffer(bytearray(head), dtype=torch.uint8)
+    mine = mine.to(dev)
+    every = torch.empty(world * halo, dtype=torch.uint8, device=dev)
+    dist.all_gather_into_tensor(every, mine, group=group)
+    every = every.cpu().numpy()
+    heads = [every[k * halo:k * halo + min(halo, max(0, s.hi - s.lo))].tobytes()
+             for k, s in enumerate(shards)]
+    return _halo_from_heads(heads, shards, rank, halo)
+
+
+def read_shard_exchange(read_bytes: Callable[[int, int], bytes], file_len: int,
+                        shards: Sequence[Shard], rank: int, header: bytes, decoder,
+                        halo: int = 4 << 20, with_raw: bool = False, group=None,
+                        device: Optional[int] = None) -> ShardResult:
+    """Collective form of read_shard: own bytes from the file, halo from exchange_heads.  Every
+    rank of `group` must call it; the halo grows x4 on all ranks until every shard decodes."""
+    import torch
+    import torch.distributed as dist
+    from ._lib import DqError
+    shard = shards[rank]
+    n = shard.p1 - shard.p0
+    own = read_bytes(shard.lo, shard.hi) if not shard.empty else b""
+    on_gpu = dist.get_backend(group) == "nccl"
+    dev = torch.device("cuda", device if device is not None else torch.cuda.current_device()) \
+        if on_gpu else torch.device("cpu")
+    done, err, result = shard.empty, None, None
+    while True:
+        h = exchange_heads(own, shards, rank, halo, group, device)
+        status = 0
+        if not done:
+            try:
+                result = decoder(own + h, shard.lo, file_len, shard, header, with_raw)
+                done = True
+            except DqError as e:
+                if "halo too small" in str(e) and shard.hi + len(h) < file_len:
+                    status = 1
+                else:
+                    status, err = 2, e
+            except Exception as e:  # noqa: BLE001 -- re-raised below, after the ranks agree
+                status, err = 2, e
+        flag = torch.tensor([status], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+        worst = int(flag.item())
+        if worst == 2:
+            raise err if err is not None else RuntimeError("sharded read failed on another rank")
+        if worst == 0:
+            break
+        halo *= 4
+    if shard.empty:
+        return ShardResult(shard, {}, [], [], [], 0)
+    batch, idx = result
+    counts, digests = [0] * n, [0] * n
+    po, pd = batch["part_offset"], batch["part_digest"]
+    for k, p in enumerate(idx):
+        counts[p - shard.p0] = int(po[k + 1] - po[k])
+        digests[p - shard.p0] = int(pd[k])
+    return ShardResult(shard, batch, idx, counts, digests, halo)
+
+
 def fold_digest(digests: Sequence[int], first_index: int = 0) -> int:
     """Whole-file digest from per-split digests in split order (dq_api.hip run_pipeline)."""
     d = 0
@@ -152,7 +247,8 @@ def fold_digest(digests: Sequence[int], first_index: int = 0) -> int:
 
 def sharded_read(path_or_bytes, split_size: int = 0, use_nio: bool = False,
                  hadoop_block_size: int = 0, device: Optional[int] = None, decoder=None,
-                 header_reader=None, with_raw: bool = False, halo: int = 4 << 20, group=None):
+                 header_reader=None, with_raw: bool = False, halo: int = 4 << 20, group=None,
+                 stitch: str = "exchange"):
     """Collective read of one BAM by all ranks of `group` (torch.distributed).
 
     Returns (ShardResult of this rank, summary) where summary holds the whole-file record count,
@@ -203,7 +299,13 @@ def sharded_read(path_or_bytes, split_size: int = 0, use_nio: bool = False,
     header = hdr[0]
     # 2. this rank's shard
     plan = shard_plan(file_len, world, **split_opts)
-    mine = read_shard(read_bytes, file_len, plan[rank], header, decoder, halo, with_raw)
+    if stitch not in ("exchange", "file"):
+        raise ValueError(f"stitch must be 'exchange' or 'file', not {stitch!r}")
+    if world > 1 and stitch == "exchange":
+        mine = read_shard_exchange(read_bytes, file_len, plan, rank, header, decoder, halo,
+                                   with_raw, group, device)
+    else:
+        mine = read_shard(read_bytes, file_len, plan[rank], header, decoder, halo, with_raw)
     # 3. descriptors of every shard
     desc = (mine.shard.p0, mine.counts, mine.digests)
     every = [None] * world

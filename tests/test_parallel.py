@@ -52,12 +52,17 @@ def test_fold_digest_definition():
     assert P.fold_digest(d[1:], first_index=1) + P.mix64(5 ^ P.K_WORD) & P.M64 == want
 
 
-def _oracle_decoder(full: bytes, split: int):
+def _oracle_decoder(full: bytes, split: int, need: int = 0):
+    """Oracle stand-in for the GPU shard decoder; `need` = halo bytes it demands past the shard
+    end (the library's "shard halo too small" error otherwise), to exercise halo growth."""
     ob = O.OracleBam(full)
     plan = ob.plan(split)
 
     def decode(data, base, file_len, shard, header, with_raw):
+        from disq_amd._lib import DqError
         assert data == full[base:base + len(data)] and file_len == len(full)
+        if base + len(data) < min(file_len, shard.hi + need):
+            raise DqError(-2, "shard halo too small")
         assert header == bytes(_oracle_header(full))
         idx, po, pd = [], [0], []
         for p in range(shard.p0, shard.p1):
@@ -85,15 +90,17 @@ def _oracle_header(full: bytes) -> bytes:
     return bytes(u[:p])
 
 
-def _worker(rank, world, port, split, q):
+def _worker(rank, world, port, split, stitch, need, halo, q):
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
     try:
         full = _bam1()
-        mine, summary = P.sharded_read(full, split_size=split, decoder=_oracle_decoder(full, split),
-                                       header_reader=lambda prefix: _oracle_header(full))
-        q.put((rank, mine.shard.p0, mine.shard.p1, summary))
+        mine, summary = P.sharded_read(full, split_size=split,
+                                       decoder=_oracle_decoder(full, split, need),
+                                       header_reader=lambda prefix: _oracle_header(full),
+                                       stitch=stitch, halo=halo)
+        q.put((rank, mine.shard.p0, mine.shard.p1, summary, mine.halo))
     finally:
         dist.destroy_process_group()
 
@@ -104,12 +111,19 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world,split", [(2, 40000), (2, 14146), (3, 128 * 1024)])
-def test_sharded_read_gloo(world, split):
+@pytest.mark.parametrize("world,split,stitch,need,halo", [
+    (2, 40000, "exchange", 0, 4 << 20), (2, 14146, "exchange", 0, 4 << 20),
+    (3, 128 * 1024, "exchange", 0, 4 << 20), (2, 40000, "file", 0, 4 << 20),
+    # halo growth through repeated exchanges: 1 KiB -> 4 -> 16 -> 64 KiB on every rank
+    (3, 40000, "exchange", 50000, 1024),
+    # more ranks than the halo window spans: the halo is stitched from several ranks' heads
+    (5, 14146, "exchange", 70000, 32768)])
+def test_sharded_read_gloo(world, split, stitch, need, halo):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, split, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, split, stitch, need, halo, q))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]
@@ -133,6 +147,19 @@ def test_sharded_read_gloo(world, split):
         assert s["n_records"] == sum(len(p) for p in parts)
     owned = sorted((r[1], r[2]) for r in res)
     assert owned[0][0] == 0 and owned[-1][1] == len(plan)
+    if need:
+        assert max(r[4] for r in res) >= need   # the window grew to what the decoder demanded
+
+
+def test_halo_from_heads_spans_short_shards():
+    full = bytes(range(256)) * 40
+    shards = [P.Shard(0, 0, 1, 0, 1000), P.Shard(1, 0, 0, 0, 0), P.Shard(2, 1, 2, 1000, 1100),
+              P.Shard(3, 2, 3, 1100, 1500), P.Shard(4, 3, 4, 1500, len(full))]
+    halo = 600
+    heads = [full[s.lo:min(s.hi, s.lo + halo)] if not s.empty else b"" for s in shards]
+    assert P._halo_from_heads(heads, shards, 0, halo) == full[1000:1600]
+    assert P._halo_from_heads(heads, shards, 2, halo) == full[1100:1700]
+    assert P._halo_from_heads(heads, shards, 4, halo) == b""
 
 
 # ---------------------------------------------------------------------------- GPU
@@ -203,3 +230,47 @@ def test_sharded_read_single_rank():
     mine, summary = P.sharded_read(data, split_size=40000)
     _, st = _gpu_whole(data, 40000)
     assert summary["digest"] == st.digest and summary["n_records"] == st.n_records
+
+
+def _gpu_worker(rank, world, port, path, split, halo, q):
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        mine, summary = P.sharded_read(path, split_size=split, device=0, halo=halo,
+                                       stitch="exchange")
+        q.put((rank, summary["digest"], summary["n_records"], mine.halo))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,split,halo", [("1bam", 40000, 16 * 1024),
+                                             ("longread", 256 * 1024, 4 * 1024)])
+def test_sharded_read_exchange_gpu(tmp_path, kind, split, halo):
+    """Two ranks on the one GPU of the box (gloo carries the head exchange; the decode is the HIP
+    library): the stitched shards reproduce the whole-file digest and count."""
+    if kind == "1bam":
+        data = _bam1()
+    else:
+        from disq_amd import synth
+        data = synth.generate(400, seed=5, shape=synth.LONGREAD, nthreads=8).bam
+    path = tmp_path / "in.bam"
+    path.write_bytes(data)
+    _, st = _gpu_whole(data, split)
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, str(path), split, halo, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in procs]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for _, digest, n, _ in res:
+        assert digest == st.digest and n == st.n_records
+    if kind == "longread":
+        assert max(r[3] for r in res) > halo   # the straddling long read forced a larger window
