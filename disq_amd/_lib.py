@@ -73,7 +73,8 @@ class DqStats(C.Structure):
 EXPORTS = ("dq_ctx_create", "dq_ctx_destroy", "dq_last_error", "dq_version", "dq_open_memory",
            "dq_open_path", "dq_set_index", "dq_read_header", "dq_plan", "dq_decode",
            "dq_decode_filtered", "dq_read", "dq_run_resident", "dq_debug_inflated",
-           "dq_batch_free", "dq_free", "dq_open_shard", "dq_header_from_prefix")
+           "dq_batch_free", "dq_free", "dq_open_shard", "dq_header_from_prefix",
+           "dq_set_splitting_index", "dq_write_sbi")
 
 _lib = None
 _lock = threading.Lock()
@@ -96,6 +97,8 @@ def lib():
         L.dq_open_memory.argtypes = [vp, vp, C.c_int64]
         L.dq_open_path.argtypes = [vp, C.c_char_p]
         L.dq_set_index.argtypes = [vp, vp, C.c_int64]
+        L.dq_set_splitting_index.argtypes = [vp, vp, C.c_int64, C.c_int32]
+        L.dq_write_sbi.argtypes = [vp, C.c_int64, P(P(C.c_uint8)), P(C.c_int64)]
         L.dq_open_shard.argtypes = [vp, vp, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
                                     vp, C.c_int64]
         L.dq_header_from_prefix.argtypes = [vp, vp, C.c_int64, vp, C.c_int64, P(C.c_int64)]
@@ -219,6 +222,24 @@ class Context:
             return
         self._bai = np.frombuffer(bai_bytes, np.uint8).copy()
         check(self._h, lib().dq_set_index(self._h, self._bai.ctypes.data, len(self._bai)))
+
+    def set_splitting_index(self, sbi_bytes, use_for_planning=False):
+        """.sbi bytes (dq_set_splitting_index); planning uses them only if use_for_planning."""
+        if sbi_bytes is None:
+            check(self._h, lib().dq_set_splitting_index(self._h, None, 0, 0))
+            return
+        self._sbi = np.frombuffer(sbi_bytes, np.uint8).copy()
+        check(self._h, lib().dq_set_splitting_index(self._h, self._sbi.ctypes.data,
+                                                    len(self._sbi), int(use_for_planning)))
+
+    def write_sbi(self, granularity=4096):
+        """BAMSBIIndexer.createIndex of the open file (dq_write_sbi): the .sbi file's bytes."""
+        p = C.POINTER(C.c_uint8)()
+        n = C.c_int64()
+        check(self._h, lib().dq_write_sbi(self._h, granularity, C.byref(p), C.byref(n)))
+        out = C.string_at(p, n.value)
+        lib().dq_free(C.cast(p, C.c_void_p))
+        return out
 
     def header(self):
         info = DqHeaderInfo()

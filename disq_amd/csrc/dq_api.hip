@@ -92,6 +92,10 @@ struct dq_ctx {
   // host copies for slicing (lazily downloaded)
   std::vector<uint64_t> voff_h;
   std::vector<int64_t> lin_h;
+  // .sbi splitting index (dq_set_splitting_index) and the indexer mode of dq_write_sbi
+  std::vector<uint64_t> sbi;
+  bool sbi_plan = false;   // plan splits from the .sbi (SBIIndex.getChunk) instead of guessing
+  bool index_only = false; // dq_write_sbi: chain from the first record, no partition plans
   // index
   bool have_bai = false;
   int64_t solb = -1, ncc = -1;
@@ -505,6 +509,28 @@ static int run_pipeline(dq_ctx* ctx) {
   HIPCHK(hipMemcpyAsync(ctx->plans.p, ctx->plans_h.data(), sizeof(SplitPlan) * (size_t)nsplit,
                         hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(d_nblk, &ctx->nblk, sizeof(int64_t), hipMemcpyHostToDevice, s));
+  const bool no_guess = ctx->index_only || ctx->sbi_plan;
+  if (no_guess && ctx->shard) RET(DQ_EINVAL, "splitting-index planning and indexing need the whole file");
+  if (no_guess) {
+    // No record guessing: the chain starts at the first record (BAMFileReader2
+    // .findVirtualOffsetOfFirstRecord); .sbi plans are SBIIndex.getChunk (SBIIndex.java:244-277)
+    for (auto& P : ctx->plans_h) {
+      P.first_blk = SPLIT_FROM_SBI;
+      P.rec_lin = -1;
+      if (!ctx->sbi_plan || ctx->index_only || ctx->sbi.empty()) continue;
+      const uint64_t last = ctx->sbi.back();
+      const int64_t max_end = (int64_t)(last >> 16);
+      const uint64_t vs = (uint64_t)std::min(P.split_start, max_end) << 16;
+      const uint64_t ve = (uint64_t)std::min(P.split_end, max_end) << 16;
+      const uint64_t a = *std::lower_bound(ctx->sbi.begin(), ctx->sbi.end(), vs);
+      const uint64_t e = *std::lower_bound(ctx->sbi.begin(), ctx->sbi.end(), ve);
+      P.vstart = a;
+      P.vend = e;
+      if (a != e) P.rec_lin = ctx->header_bytes;  // non-empty (the range is found by pointer)
+    }
+    HIPCHK(hipMemcpyAsync(ctx->plans.p, ctx->plans_h.data(), sizeof(SplitPlan) * (size_t)nsplit,
+                          hipMemcpyHostToDevice, s));
+  } else {
   launch_plan_blocks(ctx->cand.as<Cand>(), d_ncand, ctx->blk_pos.as<int64_t>(),
                      ctx->blk_us.as<int32_t>(), ctx->uoff.as<int64_t>(), d_nblk,
                      ctx->plans.as<SplitPlan>(), nsplit, s);
@@ -513,10 +539,11 @@ static int run_pipeline(dq_ctx* ctx) {
                       ctx->plans.as<SplitPlan>(), nsplit, s);
   HIPCHK(hipMemcpyAsync(ctx->plans_h.data(), ctx->plans.p, sizeof(SplitPlan) * (size_t)nsplit,
                         hipMemcpyDeviceToHost, s));
+  }
   HIPCHK(hipStreamSynchronize(s));
   HIPCHK(hipEventRecord(ctx->ev[3], s));
   dbg(s, "plan", nsplit);
-  int64_t start_lin = -1;
+  int64_t start_lin = no_guess ? ctx->header_bytes : -1;
   for (auto& P : ctx->plans_h) {
     if (P.status == 100 && ctx->shard && !is_eof)
       RET(DQ_EFORMAT, "shard halo too small: the record guesser needs bytes past the shard");
@@ -601,6 +628,7 @@ static int run_pipeline(dq_ctx* ctx) {
   HIPCHK(hipMemcpyAsync(&st, d_stat, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   if (st == 101) RET(DQ_EFORMAT, "record guesser start is not on the record chain");
+  if (st == 102) RET(DQ_EFORMAT, "splitting index offset is not a record start");
   if (st && ctx->shard && !is_eof) RET(DQ_EFORMAT, "shard halo too small: a record ends past the shard bytes");
   if (st) RET(DQ_EFORMAT, "truncated BAM record");
   // stats
@@ -959,6 +987,86 @@ int dq_set_index(dq_ctx* ctx, const uint8_t* bai, int64_t len) {
   ctx->solb = solb;
   ctx->ncc = ncc;
   ctx->have_bai = true;
+  return 0;
+}
+
+int dq_set_splitting_index(dq_ctx* ctx, const uint8_t* sbi, int64_t len, int32_t use_for_planning) {
+  if (!ctx) return DQ_EINVAL;
+  ctx->have_pipeline = false;
+  if (!sbi) {
+    ctx->sbi.clear();
+    ctx->sbi_plan = false;
+    return 0;
+  }
+  // SBIIndex.readIndex / readHeader (M/htsjdk/samtools/SBIIndex.java:123-165)
+  if (len < 68 || memcmp(sbi, "SBI\1", 4) != 0) RET(DQ_EFORMAT, "Invalid file header in SBI");
+  const int64_t n = (int64_t)rd64(sbi + 60);
+  if (n > INT32_MAX) RET(DQ_EFORMAT, "Cannot read SBI with more than 2147483647 offsets.");
+  if (n < 1 || 68 + 8 * n > len) RET(DQ_EFORMAT, "truncated SBI");
+  std::vector<uint64_t> v((size_t)n);
+  for (int64_t i = 0; i < n; i++) {
+    v[(size_t)i] = rd64(sbi + 68 + 8 * i);
+    if (i && (int64_t)v[(size_t)i - 1] > (int64_t)v[(size_t)i]) RET(DQ_EFORMAT, "Invalid SBI; offsets not in order");
+  }
+  ctx->sbi.swap(v);
+  ctx->sbi_plan = use_for_planning != 0;
+  return 0;
+}
+
+int dq_write_sbi(dq_ctx* ctx, int64_t granularity, uint8_t** out, int64_t* out_len) {
+  if (!ctx || !out || !out_len) return DQ_EINVAL;
+  if (granularity <= 0) granularity = 4096;  // SBIIndexWriter.DEFAULT_GRANULARITY
+  if (ctx->shard) RET(DQ_EINVAL, "dq_write_sbi indexes a whole file, not a shard");
+  ctx->have_pipeline = false;
+  ctx->index_only = true;
+  int rc = run_pipeline(ctx);
+  ctx->index_only = false;
+  ctx->have_pipeline = false;  // the next call re-plans with the caller's settings
+  if (rc) return rc;
+  const int64_t nrec = ctx->nrec, nent = (nrec + granularity - 1) / granularity;
+  std::vector<uint64_t> ent((size_t)nent + 1);
+  if (nent) {
+    DevBuf d;
+    HIPCHK(d.ensure(8 * (size_t)nent));
+    launch_sbi_sample(ctx->f_voff.as<uint64_t>(), nrec, granularity, d.as<uint64_t>(), ctx->s);
+    HIPCHK(hipMemcpyAsync(ent.data(), d.p, 8 * (size_t)nent, hipMemcpyDeviceToHost, ctx->s));
+    HIPCHK(hipStreamSynchronize(ctx->s));
+  }
+  // finish(finalVirtualOffset): the file pointer after the last record (or after the header),
+  // normalised as BlockCompressedInputStream.getFilePointer does: a consumed block points to the
+  // next block's start (the EOF block, or the file end)
+  int64_t E = ctx->header_bytes;
+  if (nrec) {
+    int64_t lin = 0;
+    int32_t bs = 0;
+    HIPCHK(hipMemcpy(&lin, ctx->rec_lin.as<int64_t>() + nrec - 1, 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&bs, ctx->f_bs.as<int32_t>() + nrec - 1, 4, hipMemcpyDeviceToHost));
+    E = lin + 4 + (int64_t)bs;
+  }
+  std::vector<int64_t> uo((size_t)ctx->nblk + 1), bp((size_t)ctx->nblk);
+  HIPCHK(hipMemcpy(uo.data(), ctx->uoff.p, 8 * uo.size(), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(bp.data(), ctx->blk_pos.p, 8 * bp.size(), hipMemcpyDeviceToHost));
+  uint64_t fin = (uint64_t)ctx->flen << 16;
+  if (E > 0) {
+    const int64_t j = (int64_t)(std::upper_bound(uo.begin(), uo.end() - 1, E - 1) - uo.begin()) - 1;
+    if (j >= 0 && E < uo[(size_t)j + 1]) fin = ((uint64_t)bp[(size_t)j] << 16) | (uint64_t)(E - uo[(size_t)j]);
+    else if (j + 1 < ctx->nblk) fin = (uint64_t)bp[(size_t)j + 1] << 16;
+  }
+  ent[(size_t)nent] = fin;
+  // SBIIndexWriter.finish (SBIIndexWriter.java:120-151): magic, file length, MD5, UUID, record
+  // count, granularity, offset count, offsets (all little-endian)
+  const int64_t n = 68 + 8 * (int64_t)ent.size();
+  uint8_t* b = (uint8_t*)calloc((size_t)n, 1);
+  if (!b) return DQ_ENOMEM;
+  auto w64 = [&](int64_t at, uint64_t v) { memcpy(b + at, &v, 8); };
+  memcpy(b, "SBI\1", 4);
+  w64(4, (uint64_t)ctx->flen);
+  w64(44, (uint64_t)nrec);
+  w64(52, (uint64_t)granularity);
+  w64(60, (uint64_t)ent.size());
+  for (size_t i = 0; i < ent.size(); i++) w64(68 + 8 * (int64_t)i, ent[i]);
+  *out = b;
+  *out_len = n;
   return 0;
 }
 

@@ -87,6 +87,7 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
                      int32_t* status, int32_t verify_crc, uint64_t* tim, hipStream_t s);
 
 // Split planning (a2-a4).
+constexpr int64_t SPLIT_FROM_SBI = -2;  // SplitPlan.first_blk of a chunk taken from a .sbi
 struct SplitPlan {
   int64_t split_start, split_end;
   int64_t first_blk;     // chain index of the first guessed block (-1 none)
@@ -149,6 +150,8 @@ struct PartRange {
   int64_t begin, end;   // record index range in the chain
   uint64_t digest;
 };
+void launch_sbi_sample(const uint64_t* voffset, int64_t nrec, int64_t g, uint64_t* out,
+                       hipStream_t s);
 void launch_partition_ranges(const SplitPlan* plans, int64_t nsplit, const int64_t* rec_lin,
                              const uint64_t* voffset, int64_t nrec, PartRange* parts,
                              int32_t* d_status, hipStream_t s);

@@ -760,7 +760,16 @@ __global__ void partition_ranges_kernel(const SplitPlan* __restrict__ plans, int
   PartRange r;
   r.begin = r.end = 0;
   r.digest = 0;
-  if (P.rec_lin >= 0) {
+  if (P.rec_lin >= 0 && P.first_blk == SPLIT_FROM_SBI) {  // .sbi chunk: both ends are pointers
+    const int64_t b = lower_bound_u64(voffset, nrec, P.vstart);
+    if (b >= nrec || voffset[b] != P.vstart) {
+      *d_status = 102;  // indexed offset is not a record start
+    } else {
+      const int64_t e = lower_bound_u64(voffset, nrec, P.vend);
+      r.begin = b;
+      r.end = e < b ? b : e;
+    }
+  } else if (P.rec_lin >= 0) {
     int64_t b = lower_bound_i64(rec_lin, nrec, P.rec_lin);
     if (b >= nrec || rec_lin[b] != P.rec_lin) {
       *d_status = 101;  // guesser start not on the record chain (misfire)
@@ -771,6 +780,15 @@ __global__ void partition_ranges_kernel(const SplitPlan* __restrict__ plans, int
     }
   }
   parts[i] = r;
+}
+
+// .sbi entries (SBIIndexWriter.processRecord, M/htsjdk/samtools/SBIIndexWriter.java:84-88):
+// the virtual offset of every g-th record, counted from the first
+__global__ __launch_bounds__(256) void sbi_sample_kernel(const uint64_t* __restrict__ voffset,
+                                                         int64_t nrec, int64_t g,
+                                                         uint64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i * g < nrec) out[i] = voffset[i * g];
 }
 
 // grid (partition, DIG_SPLIT): block y of partition x sums every DIG_SPLIT-th group of 256 records
@@ -985,6 +1003,14 @@ void launch_interval_filter(const uint8_t* U, const int64_t* rec_lin, const RecS
   if (n <= 0) return;
   hipLaunchKernelGGL(interval_filter_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, U,
                      rec_lin, soa, idx, n, iv_ref, iv_start, iv_end, ref_iv_begin, n_ref, keep);
+}
+
+void launch_sbi_sample(const uint64_t* voffset, int64_t nrec, int64_t g, uint64_t* out,
+                       hipStream_t s) {
+  const int64_t n = (nrec + g - 1) / g;
+  if (n <= 0) return;
+  hipLaunchKernelGGL(sbi_sample_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, voffset,
+                     nrec, g, out);
 }
 
 }  // namespace dq

@@ -151,6 +151,7 @@ class HtsjdkReadsRddStorage:
         self._reference = None
         self._device = device
         self._verify_crc = False
+        self._use_sbi = False
 
     @staticmethod
     def makeDefault(device: int = 0) -> "HtsjdkReadsRddStorage":
@@ -175,6 +176,13 @@ class HtsjdkReadsRddStorage:
     def verifyCrc(self, v: bool):
         """Extension: check every BGZF block's CRC32 (htsjdk's default does not)."""
         self._verify_crc = bool(v)
+        return self
+
+    def useSplittingIndex(self, v: bool):
+        """Extension: plan partitions from path.sbi (SBIIndex.getChunk) when it exists.  Disq
+        itself loads the .sbi and discards the result (BamSource.java:69-87), so the default
+        (False) only validates it and plans by record guessing."""
+        self._use_sbi = bool(v)
         return self
 
     def _files(self, path):
@@ -203,6 +211,10 @@ class HtsjdkReadsRddStorage:
                               verify_crc=self._verify_crc, device=self._device,
                               stringency=self._stringency) as ctx:
                 ctx.open_path(f)
+                sbi = f + ".sbi"  # SBIIndex.FILE_EXTENSION, BamSource.java:69-72
+                if os.path.exists(sbi):
+                    with open(sbi, "rb") as fh:
+                        ctx.set_splitting_index(fh.read(), self._use_sbi)
                 _, hraw = ctx.header()
                 h = _parse_header(hraw)
                 if header is None:
@@ -251,3 +263,17 @@ class HtsjdkReadsRddStorage:
             if os.path.exists(c):
                 return c
         return None
+
+
+class BAMSBIIndexer:
+    """htsjdk BAMSBIIndexer (M/htsjdk/samtools/BAMSBIIndexer.java:20-66) on the GPU read path."""
+
+    @staticmethod
+    def createIndex(bamFile: str, granularity: int = 4096, device: int = 0) -> str:
+        with _lib.Context(device=device) as ctx:
+            ctx.open_path(bamFile)
+            data = ctx.write_sbi(granularity)
+        out = bamFile + ".sbi"
+        with open(out, "wb") as fh:
+            fh.write(data)
+        return out

@@ -167,6 +167,21 @@ int dq_set_index(dq_ctx* ctx, const uint8_t* bai, int64_t len);
 
 int dq_read_header(dq_ctx* ctx, dq_header_info* info, uint8_t* header_bytes, int64_t cap);
 
+/* .sbi splitting index bytes (htsjdk SBIIndex.load, M/htsjdk/samtools/SBIIndex.java:117-165:
+ * magic "SBI\1", ascending virtual offsets).  Disq's getPathChunks loads it and then discards the
+ * result (D/impl/formats/bam/BamSource.java:69-87), so with use_for_planning = 0 (Disq-exact,
+ * the default) it is validated and ignored.  With use_for_planning = 1 dq_plan gives each split
+ * the chunk SBIIndex.getChunk(splitStart, splitEnd) returns (SBIIndex.java:244-264: from the
+ * first indexed record at or after the split start to the first at or after the split end) and
+ * no record guessing runs.  NULL clears it. */
+int dq_set_splitting_index(dq_ctx* ctx, const uint8_t* sbi, int64_t len, int32_t use_for_planning);
+
+/* BAMSBIIndexer.createIndex (M/htsjdk/samtools/BAMSBIIndexer.java:45-66) + SBIIndexWriter
+ * (SBIIndexWriter.java:84-151) for the open (whole) file: every granularity-th record's virtual
+ * offset from the first record, then the final pointer; zero MD5 and UUID.  *out is
+ * library-allocated (dq_free); granularity <= 0 means htsjdk's default 4096. */
+int dq_write_sbi(dq_ctx* ctx, int64_t granularity, uint8_t** out, int64_t* out_len);
+
 /* getPathChunks: all splits of the open file, in Disq partition order.  *chunks is
  * library-allocated; free with dq_free. */
 int dq_plan(dq_ctx* ctx, dq_chunk** chunks, int64_t* n);

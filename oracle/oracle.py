@@ -287,6 +287,71 @@ class OracleBam:
         return parts
 
 
+    # SBI (f1): BAMSBIIndexer.createIndex (M/htsjdk/samtools/BAMSBIIndexer.java:45-66)
+    def sbi_final_pointer(self):
+        """BlockCompressedInputStream.getFilePointer after the last record of a well-formed file
+        (the record stream ends at the end of the last non-empty block): the start of the block
+        after it (the EOF block), or the file length (BAMSBIIndexer.java:52-62)."""
+        blocks = self.split_blocks(0, self.len)
+        last = max((i for i, b in enumerate(blocks) if b[2] > 0), default=-1)
+        if last + 1 < len(blocks):
+            return blocks[last + 1][0] << 16
+        return self.len << 16
+
+    def write_sbi(self, granularity=4096):
+        recs = self.read_all()
+        return sbi_write(recs["voffset"], self.sbi_final_pointer(), self.len, granularity)
+
+    # SBI planning: getPathChunks with a .sbi honoured (BamSource.java:69-87 as intended)
+    def plan_sbi(self, sbi_bytes, split_size=0, nio=False,
+                 local_block_size=HADOOP_LOCAL_BLOCK_SIZE):
+        offs = sbi_offsets(sbi_bytes)
+        return [(s, e, sbi_get_chunk(offs, s, e))
+                for s, e in path_splits(self.len, split_size, nio, local_block_size)]
+
+    def read_partitions_sbi(self, sbi_bytes, split_size=0, nio=False,
+                            local_block_size=HADOOP_LOCAL_BLOCK_SIZE):
+        return [self.read_chunk(*ch) for _, _, ch in
+                self.plan_sbi(sbi_bytes, split_size, nio, local_block_size) if ch is not None]
+
+
+def sbi_offsets(sbi_bytes):
+    """SBIIndex.readIndex (M/htsjdk/samtools/SBIIndex.java:123-144): the virtual offsets."""
+    d = bytes(sbi_bytes)
+    if d[:4] != b"SBI\x01":
+        raise OracleError("Invalid file header in SBI")
+    n = int.from_bytes(d[60:68], "little")
+    offs = np.frombuffer(d, "<u8", count=n, offset=68)
+    if n > 1 and np.any(offs[1:].astype(np.int64) < offs[:-1].astype(np.int64)):
+        raise OracleError("Invalid SBI; offsets not in order")
+    return offs
+
+
+def sbi_get_chunk(offs, split_start, split_end):
+    """SBIIndex.getChunk (M/htsjdk/samtools/SBIIndex.java:244-264) with ceiling (:266-280)."""
+    if split_start >= split_end:
+        raise ValueError("Split start must be less than end")
+    max_end = int(offs[-1]) >> 16
+    vs = min(split_start, max_end) << 16
+    ve = min(split_end, max_end) << 16
+    a = int(offs[int(np.searchsorted(offs, np.uint64(vs), side="left"))])
+    b = int(offs[int(np.searchsorted(offs, np.uint64(ve), side="left"))])
+    return None if a == b else (a, b)
+
+
+def sbi_write(voffsets, final_pointer, file_len, granularity=4096):
+    """SBIIndexWriter.processRecord / finish (M/htsjdk/samtools/SBIIndexWriter.java:84-151) with
+    no MD5 and no UUID: every granularity-th record's virtual offset, then the final pointer."""
+    ent = [int(v) for v in np.asarray(voffsets, np.uint64)[::granularity]] + [int(final_pointer)]
+    out = bytearray(b"SBI\x01")
+    out += int(file_len).to_bytes(8, "little") + bytes(32)
+    for x in (len(voffsets), granularity, len(ent)):
+        out += int(x).to_bytes(8, "little")
+    for v in ent:
+        out += v.to_bytes(8, "little")
+    return bytes(out)
+
+
 def bai_info(bai_bytes):
     b = np.frombuffer(bai_bytes, np.uint8)
     nr, solb, ncc = C.c_int32(), C.c_int64(), C.c_int64()
