@@ -66,7 +66,8 @@ class DqStats(C.Structure):
                 ("n_blocks", C.c_int64), ("n_records", C.c_int64), ("n_partitions", C.c_int64),
                 ("ms_total", C.c_double), ("ms_scan", C.c_double), ("ms_inflate", C.c_double),
                 ("ms_records", C.c_double), ("ms_filter", C.c_double), ("ms_plan", C.c_double),
-                ("digest", C.c_uint64), ("ms_crc", C.c_double), ("deflate_bytes", C.c_int64)]
+                ("digest", C.c_uint64), ("ms_crc", C.c_double), ("deflate_bytes", C.c_int64),
+                ("n_filtered", C.c_int64)]
 
 
 # Every symbol include/disq_gpu.h declares.
@@ -290,9 +291,11 @@ class Context:
                                      int(with_raw), C.byref(bp)))
         return batch_to_numpy(bp)
 
-    def run_resident(self):
+    def run_resident(self, traversal=None):
         st = DqStats()
-        check(self._h, lib().dq_run_resident(self._h, None, C.byref(st)))
+        t, keep = self._traversal(traversal)
+        check(self._h, lib().dq_run_resident(self._h, C.byref(t) if t is not None else None,
+                                             C.byref(st)))
         return st
 
     def inflated(self):

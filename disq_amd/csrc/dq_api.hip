@@ -101,6 +101,7 @@ struct dq_ctx {
   int64_t solb = -1, ncc = -1;
   // filter scratch
   DevBuf iv_ref, iv_start, iv_end, iv_begin, idx, keep;
+  int64_t iota_n = -1;  // idx holds 0..iota_n-1 (dq_run_resident's interval filter)
   dq_stats stats{};
 
   RecSoA soa() {
@@ -799,6 +800,36 @@ static int chunk_range(dq_ctx* ctx, uint64_t vstart, uint64_t vend, int64_t* b, 
   return 0;
 }
 
+// QueryInterval.optimizeIntervals of the traversal, uploaded per contig (interval_filter_kernel's
+// layout: sorted intervals + a per-contig begin table).
+static int upload_intervals(dq_ctx* ctx, const dq_traversal* tr) {
+  int rc;
+  std::vector<Interval> iv;
+  for (int64_t i = 0; i < tr->n; i++) {
+    if (tr->ref[i] < 0 || tr->ref[i] >= ctx->n_ref) RET(DQ_EINVAL, "Invalid reference index");
+    iv.push_back({tr->ref[i], tr->start[i], tr->end[i]});
+  }
+  iv = optimize(iv);
+  std::vector<int32_t> r, st, en, beg((size_t)ctx->n_ref + 1, 0);
+  for (auto& x : iv) {
+    r.push_back(x.ref);
+    st.push_back(x.start);
+    en.push_back(x.end);
+  }
+  for (auto& x : iv) beg[(size_t)x.ref + 1]++;
+  for (int32_t k = 0; k < ctx->n_ref; k++) beg[(size_t)k + 1] += beg[(size_t)k];
+  const size_t ni = iv.size();
+  if ((rc = ensure_all(ctx, ctx->iv_ref, 4 * ni + 4)) || (rc = ensure_all(ctx, ctx->iv_start, 4 * ni + 4)) ||
+      (rc = ensure_all(ctx, ctx->iv_end, 4 * ni + 4)) ||
+      (rc = ensure_all(ctx, ctx->iv_begin, 4 * beg.size() + 4)))
+    return rc;
+  HIPCHK(hipMemcpy(ctx->iv_ref.p, r.data(), 4 * ni, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(ctx->iv_start.p, st.data(), 4 * ni, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(ctx->iv_end.p, en.data(), 4 * ni, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(ctx->iv_begin.p, beg.data(), 4 * beg.size(), hipMemcpyHostToDevice));
+  return 0;
+}
+
 // createIndexIterator (contained=false) over [b, e) + the unplaced-unmapped tail
 // (AbstractBinarySamSource.java:86-134).
 static int filtered_indices(dq_ctx* ctx, uint64_t vstart, uint64_t vend, int64_t b, int64_t e,
@@ -807,35 +838,14 @@ static int filtered_indices(dq_ctx* ctx, uint64_t vstart, uint64_t vend, int64_t
   out.clear();
   if (!ctx->have_bai) RET(DQ_EINVAL, "Intervals set but no index file found");
   if (tr->has_intervals && tr->n > 0 && e > b) {
-    std::vector<Interval> iv;
-    for (int64_t i = 0; i < tr->n; i++) {
-      if (tr->ref[i] < 0 || tr->ref[i] >= ctx->n_ref) RET(DQ_EINVAL, "Invalid reference index");
-      iv.push_back({tr->ref[i], tr->start[i], tr->end[i]});
-    }
-    iv = optimize(iv);
-    std::vector<int32_t> r, st, en, beg((size_t)ctx->n_ref + 1, 0);
-    for (auto& x : iv) {
-      r.push_back(x.ref);
-      st.push_back(x.start);
-      en.push_back(x.end);
-    }
-    for (auto& x : iv) beg[(size_t)x.ref + 1]++;
-    for (int32_t k = 0; k < ctx->n_ref; k++) beg[(size_t)k + 1] += beg[(size_t)k];
-    const size_t ni = iv.size();
-    if ((rc = ensure_all(ctx, ctx->iv_ref, 4 * ni + 4)) || (rc = ensure_all(ctx, ctx->iv_start, 4 * ni + 4)) ||
-        (rc = ensure_all(ctx, ctx->iv_end, 4 * ni + 4)) ||
-        (rc = ensure_all(ctx, ctx->iv_begin, 4 * beg.size() + 4)))
-      return rc;
-    HIPCHK(hipMemcpy(ctx->iv_ref.p, r.data(), 4 * ni, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(ctx->iv_start.p, st.data(), 4 * ni, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(ctx->iv_end.p, en.data(), 4 * ni, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(ctx->iv_begin.p, beg.data(), 4 * beg.size(), hipMemcpyHostToDevice));
+    if ((rc = upload_intervals(ctx, tr))) return rc;
     const int64_t n = e - b;
     std::vector<int64_t> idx((size_t)n);
     for (int64_t k = 0; k < n; k++) idx[(size_t)k] = b + k;
     if ((rc = ensure_all(ctx, ctx->idx, 8 * (size_t)n)) || (rc = ensure_all(ctx, ctx->keep, (size_t)n)))
       return rc;
     HIPCHK(hipMemcpy(ctx->idx.p, idx.data(), 8 * (size_t)n, hipMemcpyHostToDevice));
+    ctx->iota_n = -1;
     launch_interval_filter(ctx->U.as<uint8_t>(), ctx->rec_lin.as<int64_t>(), ctx->soa(),
                            ctx->idx.as<int64_t>(), n, ctx->iv_ref.as<int32_t>(),
                            ctx->iv_start.as<int32_t>(), ctx->iv_end.as<int32_t>(),
@@ -1162,11 +1172,42 @@ int dq_read(dq_ctx* ctx, const dq_traversal* tr, int32_t with_raw, dq_batch** ou
 
 int dq_run_resident(dq_ctx* ctx, const dq_traversal* tr, dq_stats* stats) {
   if (!ctx) return DQ_EINVAL;
-  (void)tr;
+  if (tr && !tr->has_intervals && !tr->traverse_unplaced_unmapped)
+    RET(DQ_EINVAL, "Traversing mapped reads only is not supported.");
   ctx->have_pipeline = false;
   int rc = run_pipeline(ctx);
   if (rc) return rc;
-  if (stats) *stats = ctx->stats;
+  dq_stats S = ctx->stats;
+  S.n_filtered = -1;
+  if (tr && tr->has_intervals && tr->n > 0 && ctx->nrec > 0) {
+    // Kernel 4 over every record of the resident stream (the interval filter of all partitions
+    // at once; the unplaced-unmapped tail is a host-side pointer range and is not timed here)
+    if (!ctx->have_bai) RET(DQ_EINVAL, "Intervals set but no index file found");
+    if ((rc = upload_intervals(ctx, tr))) return rc;
+    const int64_t n = ctx->nrec;
+    if (ctx->iota_n != n) {
+      std::vector<int64_t> idx((size_t)n);
+      for (int64_t k = 0; k < n; k++) idx[(size_t)k] = k;
+      if ((rc = ensure_all(ctx, ctx->idx, 8 * (size_t)n)) || (rc = ensure_all(ctx, ctx->keep, (size_t)n)))
+        return rc;
+      HIPCHK(hipMemcpy(ctx->idx.p, idx.data(), 8 * (size_t)n, hipMemcpyHostToDevice));
+      ctx->iota_n = n;
+    }
+    HIPCHK(hipEventRecord(ctx->ev[6], ctx->s));
+    launch_interval_filter(ctx->U.as<uint8_t>(), ctx->rec_lin.as<int64_t>(), ctx->soa(),
+                           ctx->idx.as<int64_t>(), n, ctx->iv_ref.as<int32_t>(),
+                           ctx->iv_start.as<int32_t>(), ctx->iv_end.as<int32_t>(),
+                           ctx->iv_begin.as<int32_t>(), ctx->n_ref, ctx->keep.as<uint8_t>(), ctx->s);
+    HIPCHK(hipEventRecord(ctx->ev[7], ctx->s));
+    HIPCHK(hipEventSynchronize(ctx->ev[7]));
+    S.ms_filter = ev_ms(ctx->ev[6], ctx->ev[7]);
+    std::vector<uint8_t> keep((size_t)n);
+    HIPCHK(hipMemcpy(keep.data(), ctx->keep.p, (size_t)n, hipMemcpyDeviceToHost));
+    int64_t kept = 0;
+    for (int64_t k = 0; k < n; k++) kept += keep[(size_t)k] != 0;
+    S.n_filtered = kept;
+  }
+  if (stats) *stats = S;
   return 0;
 }
 

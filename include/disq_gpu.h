@@ -132,6 +132,7 @@ typedef struct dq_stats {
   uint64_t digest;          /* digest over partition digests, in partition order */
   double ms_crc;            /* CRC32 verification kernel */
   int64_t deflate_bytes;    /* compressed DEFLATE payload bytes (sum of BSIZE + 1 - 26) */
+  int64_t n_filtered;       /* records kernel 4 kept (dq_run_resident with intervals), else -1 */
 } dq_stats;
 
 int dq_ctx_create(dq_ctx** out, const dq_opts* opts);
@@ -198,7 +199,10 @@ int dq_decode_filtered(dq_ctx* ctx, uint64_t vstart, uint64_t vend, const dq_tra
 int dq_read(dq_ctx* ctx, const dq_traversal* tr, int32_t with_raw, dq_batch** out);
 
 /* Run the whole device pipeline on the resident file without copying records back (records
- * stay in HBM); fills stats.  This is the benchmark entry point. */
+ * stay in HBM); fills stats.  This is the benchmark entry point.  With intervals in tr (needs
+ * dq_set_index, as createIndexIterator does), kernel 4 also filters every record against them
+ * (overlap, contained=false; AbstractBinarySamSource.java:86-134) and stats.ms_filter /
+ * stats.n_filtered report it; the kept-record list stays in HBM. */
 int dq_run_resident(dq_ctx* ctx, const dq_traversal* tr, dq_stats* stats);
 
 /* Device pointer of the resident decompressed stream (for tests), and its length. */

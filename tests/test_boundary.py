@@ -44,8 +44,8 @@ def test_unknown_format_rejected(tmp_path):
 
 
 def test_structs_match_header_layout():
-    # dq_opts 32 bytes, dq_chunk 40, dq_traversal 40, dq_stats 112
+    # dq_opts 32 bytes, dq_chunk 40, dq_traversal 40, dq_stats 120
     assert ctypes.sizeof(_lib.DqOpts) == 32
     assert ctypes.sizeof(_lib.DqChunk) == 40
     assert ctypes.sizeof(_lib.DqTraversal) == 40
-    assert ctypes.sizeof(_lib.DqStats) == 112
+    assert ctypes.sizeof(_lib.DqStats) == 120

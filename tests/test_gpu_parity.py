@@ -115,6 +115,35 @@ def test_interval_traversal(anysam, ivs, unplaced, expected, split):
     assert len(b["voffset"]) == expected
 
 
+@pytest.mark.parametrize("ivs,expected", [
+    ([("chr21", 5000, 9999), ("chr21", 20000, 22999)], 16),
+    ([("chr21", 1, 1000135)], 2000),
+    ([("chr21", 20000, 22999), ("chr21", 5000, 9999), ("chr21", 9000, 9500)], 16),
+])
+def test_resident_interval_filter(anysam, ivs, expected):
+    """dq_run_resident with intervals: kernel 4 over the whole resident stream keeps exactly the
+    records the per-partition createIndexIterator path returns (one partition, no unplaced)."""
+    ob = O.OracleBam(anysam.bam)
+    conv = [(ob.ref_index(c), s, e) for c, s, e in ivs]
+    with _lib.Context(split_size=0, verify_crc=True) as c:
+        c.open_bytes(anysam.bam)
+        c.set_index(anysam.bai)
+        st = c.run_resident((conv, False))
+        assert st.n_filtered == expected
+        assert st.ms_filter > 0
+        assert c.run_resident().n_filtered == -1
+        assert c.run_resident((conv, False)).n_filtered == expected
+        assert len(c.read(traversal=(conv, False))["voffset"]) == expected
+        assert c.run_resident((conv, False)).n_filtered == expected
+
+
+def test_resident_interval_filter_needs_index(anysam):
+    with _lib.Context(split_size=0) as c:
+        c.open_bytes(anysam.bam)
+        with pytest.raises(_lib.DqError, match="index"):
+            c.run_resident(([(0, 1, 100)], False))
+
+
 def test_storage_api_mirror(tmp_path, anysam, golden):
     p = str(tmp_path / "anysam.bam")
     anysam.write(p)
