@@ -22,7 +22,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "decompressed BAM GB/s + reads/sec (whole node) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-TRAFFIC_PROFILE = "r1d_inflate_traffic_pmc.json"
+TRAFFIC_PROFILE = "r1k_inflate_traffic_pmc.json"
 
 
 def log(*a):
