@@ -6,6 +6,7 @@ there is no CPU fallback, so a missing or unloadable library raises immediately.
 from __future__ import annotations
 
 import ctypes as C
+import os
 import threading
 
 import numpy as np
@@ -67,7 +68,8 @@ class DqStats(C.Structure):
                 ("ms_total", C.c_double), ("ms_scan", C.c_double), ("ms_inflate", C.c_double),
                 ("ms_records", C.c_double), ("ms_filter", C.c_double), ("ms_plan", C.c_double),
                 ("digest", C.c_uint64), ("ms_crc", C.c_double), ("deflate_bytes", C.c_int64),
-                ("n_filtered", C.c_int64)]
+                ("n_filtered", C.c_int64), ("h2d_bytes", C.c_int64),
+                ("owned_bytes", C.c_int64)]
 
 
 # Every symbol include/disq_gpu.h declares.
@@ -75,7 +77,8 @@ EXPORTS = ("dq_ctx_create", "dq_ctx_destroy", "dq_last_error", "dq_version", "dq
            "dq_open_path", "dq_set_index", "dq_read_header", "dq_plan", "dq_decode",
            "dq_decode_filtered", "dq_read", "dq_run_resident", "dq_debug_inflated",
            "dq_batch_free", "dq_free", "dq_open_shard", "dq_header_from_prefix",
-           "dq_set_splitting_index", "dq_write_sbi")
+           "dq_set_splitting_index", "dq_write_sbi", "dq_open_shard_device", "dq_decode_chunk",
+           "dq_get_stats", "dq_partition_digests")
 
 _lib = None
 _lock = threading.Lock()
@@ -87,6 +90,11 @@ def lib():
     with _lock:
         if _lib is not None:
             return _lib
+        # One HIP runtime per process: torch bundles its own libamdhip64.so.7 (same soname as
+        # /opt/rocm's), and whichever is loaded first serves both.  Loading torch first keeps the
+        # runtime torch was built against, so torch.cuda and this library share devices and
+        # memory (the multi-GPU path hands torch device tensors to dq_open_shard_device).
+        import torch  # noqa: F401
         L = C.CDLL(_build.gpu_lib_path())
         P = C.POINTER
         vp = C.c_void_p
@@ -102,6 +110,13 @@ def lib():
         L.dq_write_sbi.argtypes = [vp, C.c_int64, P(P(C.c_uint8)), P(C.c_int64)]
         L.dq_open_shard.argtypes = [vp, vp, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
                                     vp, C.c_int64]
+        L.dq_open_shard_device.argtypes = [vp, vp, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
+                                           C.c_int64, vp, C.c_int64]
+        L.dq_decode_chunk.argtypes = [vp, C.c_char_p, C.c_uint64, C.c_uint64, C.c_int32,
+                                      P(P(DqBatch))]
+        L.dq_get_stats.argtypes = [vp, P(DqStats)]
+        L.dq_partition_digests.argtypes = [vp, P(C.c_int64), P(C.c_uint64), C.c_int64,
+                                           P(C.c_int64)]
         L.dq_header_from_prefix.argtypes = [vp, vp, C.c_int64, vp, C.c_int64, P(C.c_int64)]
         L.dq_read_header.argtypes = [vp, P(DqHeaderInfo), vp, C.c_int64]
         L.dq_plan.argtypes = [vp, P(P(DqChunk)), P(C.c_int64)]
@@ -200,6 +215,36 @@ class Context:
         check(self._h, lib().dq_open_shard(self._h, self._shard.ctypes.data, len(self._shard),
                                            base, file_len, p0, p1, self._hdr.ctypes.data,
                                            len(self._hdr)))
+
+    def open_shard_device(self, dev_ptr, length, base, file_len, p0, p1, header):
+        """Shard bytes already in device memory (dq_open_shard_device): dev_ptr must stay valid,
+        with 4096 zero bytes after `length`."""
+        self._hdr = np.frombuffer(header, np.uint8).copy()
+        check(self._h, lib().dq_open_shard_device(self._h, dev_ptr, length, base, file_len, p0,
+                                                  p1, self._hdr.ctypes.data, len(self._hdr)))
+
+    def decode_chunk(self, path, vstart, vend, with_raw=True):
+        """BamSource.getIterator for one task: only the chunk's bytes are read (dq_decode_chunk)."""
+        bp = C.POINTER(DqBatch)()
+        check(self._h, lib().dq_decode_chunk(self._h, os.fsencode(path), vstart, vend,
+                                             int(with_raw), C.byref(bp)))
+        return batch_to_numpy(bp)
+
+    def stats(self):
+        st = DqStats()
+        check(self._h, lib().dq_get_stats(self._h, C.byref(st)))
+        return st
+
+    def partition_digests(self):
+        """(counts, digests) per partition of the last pipeline run, in partition order."""
+        n = C.c_int64()
+        check(self._h, lib().dq_partition_digests(self._h, None, None, 0, C.byref(n)))
+        cnt = np.zeros(max(1, n.value), np.int64)
+        dig = np.zeros(max(1, n.value), np.uint64)
+        check(self._h, lib().dq_partition_digests(
+            self._h, cnt.ctypes.data_as(C.POINTER(C.c_int64)),
+            dig.ctypes.data_as(C.POINTER(C.c_uint64)), n.value, C.byref(n)))
+        return cnt[:n.value], dig[:n.value]
 
     def header_from_prefix(self, data):
         """Decompressed BAM header from the first bytes of a file (dq_header_from_prefix)."""

@@ -5,8 +5,12 @@
 // .bai facts read by AbstractBinarySamSource (AbstractBinarySamSource.java:92-94), interval
 // preparation (BoundedTraversalUtil.java:10-27) and the per-chunk record selection of
 // BamSource.getIterator / createIndexIterator.  All byte/bit work runs in the HIP kernels of
-// dq_kernels.hip and dq_inflate.hip; there is no CPU fallback.
+// dq_kernels.hip and dq_inflate3.hip; there is no CPU fallback.
 #include <hip/hip_runtime.h>
+
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -64,11 +68,23 @@ struct dq_ctx {
   int64_t p0 = 0, p1 = 0;    // Disq partitions owned by the shard
   std::vector<uint8_t> hdr;  // shard: the decompressed BAM header, supplied by the caller
   bool header_only = false;  // dq_header_from_prefix: stop after the header
+  const uint8_t* cext = nullptr;  // dq_open_shard_device: caller-owned device bytes instead of C
+  // dq_decode_chunk: the window holds one Chunk [chunk_vs, chunk_ve) (shard coordinates); its
+  // records are walked from the exact start pointer, no split planning or guessing
+  bool chunk_mode = false;
+  uint64_t chunk_vs = 0, chunk_ve = 0;
+  std::string chunk_hdr_path;       // path whose header ctx->hdr holds (dq_decode_chunk cache)
+  // pinned host staging for file reads (dq_open_path, dq_decode_chunk)
+  uint8_t* pin[2] = {nullptr, nullptr};
+  size_t pin_cap = 0;
+  hipEvent_t pin_ev[2] = {nullptr, nullptr};
+  int64_t h2d_bytes = 0;            // compressed bytes copied host -> device by the last open
+  const uint8_t* cbuf() const { return cext ? cext : C.as<uint8_t>(); }
   // kernel 1
   DevBuf slots, counts, offs, cand, flags, voff, scal, tmp;
   int64_t ncand = 0;
   // chain + inflate
-  DevBuf blk_pos, blk_cs, blk_us, uoff, status, U, tok, tokcnt;
+  DevBuf blk_pos, blk_cs, blk_us, uoff, status, U;
   int n_cu = 256;
   int64_t nblk = 0, ulen = 0;
   // header
@@ -89,9 +105,10 @@ struct dq_ctx {
   DevBuf parts;
   std::vector<PartRange> parts_h;
   bool have_pipeline = false;
-  // host copies for slicing (lazily downloaded)
+  // host copy of the record start pointers (chunk lookups; lazily downloaded)
   std::vector<uint64_t> voff_h;
-  std::vector<int64_t> lin_h;
+  // record export scratch (make_batch)
+  DevBuf x_idx, x_rng, x_soa, x_off, x_raw;
   // .sbi splitting index (dq_set_splitting_index) and the indexer mode of dq_write_sbi
   std::vector<uint64_t> sbi;
   bool sbi_plan = false;   // plan splits from the .sbi (SBIIndex.getChunk) instead of guessing
@@ -120,6 +137,15 @@ struct dq_ctx {
       ctx->err = std::string(#x) + ": " + hipGetErrorString(e_);                     \
       return DQ_EDEVICE;                                                              \
     }                                                                                 \
+  } while (0)
+// Every C-ABI entry point runs on the context's device, whatever the calling thread's current
+// device is (one dq_ctx per Spark task thread).
+#define ON_DEVICE(ctx)                                                               \
+  do {                                                                               \
+    if (hipSetDevice((ctx)->o.device) != hipSuccess) {                               \
+      (ctx)->err = "hipSetDevice failed";                                            \
+      return DQ_EDEVICE;                                                             \
+    }                                                                                \
   } while (0)
 #define RET(code, msg)   \
   do {                   \
@@ -347,7 +373,7 @@ static int run_pipeline(dq_ctx* ctx) {
   int32_t* d_stat = d_overflow + 2;
   int64_t* d_nblk = reinterpret_cast<int64_t*>(ctx->scal.as<char>() + 64);
   HIPCHK(hipMemsetAsync(ctx->scal.p, 0, 4096, s));
-  launch_bgzf_scan(ctx->C.as<uint8_t>(), L, L, ctx->slots.as<Cand>(), 0, ctx->counts.as<int32_t>(),
+  launch_bgzf_scan(ctx->cbuf(), L, L, ctx->slots.as<Cand>(), 0, ctx->counts.as<int32_t>(),
                    nch, nullptr, d_overflow, s);
   launch_exclusive_scan_i32(ctx->counts.as<int32_t>(), ctx->offs.as<int64_t>(), nch,
                             ctx->tmp.as<int64_t>(), s);
@@ -377,7 +403,7 @@ static int run_pipeline(dq_ctx* ctx) {
   // a shard's bytes end inside the file: the end of the buffer is not EOF
   const int32_t is_eof = (!ctx->shard || ctx->base + L >= ctx->file_len) ? 1 : 0;
   if (ncand > 0)
-    launch_chain2(ctx->C.as<uint8_t>(), L, ctx->cand.as<Cand>(), d_ncand, ncand,
+    launch_chain2(ctx->cbuf(), L, ctx->cand.as<Cand>(), d_ncand, ncand,
                   ctx->voff.as<int64_t>(), ctx->blk_pos.as<int64_t>(), ctx->blk_cs.as<int32_t>(),
                   ctx->blk_us.as<int32_t>(), capb, d_nblk, d_broken, is_eof, s);
   int64_t nblk = 0;
@@ -387,7 +413,7 @@ static int run_pipeline(dq_ctx* ctx) {
   // The chain must start at the file start (htsjdk reads from block 0); a shard's chain starts
   // at the guesser's first block in its first split (the first valid candidate).
   int64_t chain_start = 0;
-  if (ctx->shard && ncand > 0) {
+  if (ctx->shard && !ctx->chunk_mode && ncand > 0) {
     std::vector<Cand> ch((size_t)ncand);
     HIPCHK(hipMemcpy(ch.data(), ctx->cand.p, sizeof(Cand) * (size_t)ncand, hipMemcpyDeviceToHost));
     chain_start = L;
@@ -407,7 +433,7 @@ static int run_pipeline(dq_ctx* ctx) {
     if ((rc = ensure_all(ctx, ctx->blk_pos, sizeof(int64_t) * (size_t)capw))) return rc;
     if ((rc = ensure_all(ctx, ctx->blk_cs, sizeof(int32_t) * (size_t)capw))) return rc;
     if ((rc = ensure_all(ctx, ctx->blk_us, sizeof(int32_t) * (size_t)capw))) return rc;
-    launch_chain_serial(ctx->C.as<uint8_t>(), L, chain_start, ctx->blk_pos.as<int64_t>(),
+    launch_chain_serial(ctx->cbuf(), L, chain_start, ctx->blk_pos.as<int64_t>(),
                         ctx->blk_cs.as<int32_t>(), ctx->blk_us.as<int32_t>(), capw, d_nblk, d_stat, s);
     if ((rc = get_i64(ctx, d_nblk, &nblk))) return rc;
   }
@@ -426,25 +452,16 @@ static int run_pipeline(dq_ctx* ctx) {
   if ((rc = ensure_all(ctx, ctx->status, sizeof(int32_t) * (size_t)(nblk + 1)))) return rc;
   HIPCHK(hipMemsetAsync(ctx->status.p, 0, sizeof(int32_t) * (size_t)(nblk + 1), s));
   HIPCHK(hipMemsetAsync(ctx->U.as<uint8_t>() + ulen, 0, 256, s));
-  static const int infl_ver = getenv("DQ_INFLATE") ? atoi(getenv("DQ_INFLATE")) : 3;
-  if (infl_ver == 2) {
-    if ((rc = ensure_all(ctx, ctx->tok, (size_t)token_bytes(ulen, nblk)))) return rc;
-    if ((rc = ensure_all(ctx, ctx->tokcnt, sizeof(int32_t) * (size_t)(nblk + 1)))) return rc;
-    init_inflate_tables();
-    HIPCHK(hipEventRecord(ctx->ev[5], s));
-    launch_inflate2(ctx->C.as<uint8_t>(), ctx->blk_pos.as<int64_t>(), ctx->blk_cs.as<int32_t>(),
-                    ctx->blk_us.as<int32_t>(), ctx->uoff.as<int64_t>(), nblk, ctx->tok.as<uint16_t>(),
-                    ctx->tokcnt.as<int32_t>(), d_stat + 8, ctx->U.as<uint8_t>(),
-                    ctx->status.as<int32_t>(), ctx->o.verify_crc, ctx->n_cu, ctx->ev[6], s);
-  } else {
-    init_inflate3_tables();
+  {
+    const uint32_t* crc_init = inflate3_tables(ctx->o.device);
+    if (!crc_init) RET(DQ_EDEVICE, "CRC32 table initialisation failed on this device");
     static const bool timing = getenv("DQ_TIMING") != nullptr;
     uint64_t* tim = nullptr;
     if (timing) HIPCHK(hipMalloc(&tim, sizeof(uint64_t) * 16 * (size_t)std::max<int64_t>(1, nblk)));
     HIPCHK(hipEventRecord(ctx->ev[5], s));
-    launch_inflate3(ctx->C.as<uint8_t>(), ctx->blk_pos.as<int64_t>(), ctx->blk_cs.as<int32_t>(),
+    launch_inflate3(ctx->cbuf(), ctx->blk_pos.as<int64_t>(), ctx->blk_cs.as<int32_t>(),
                     ctx->blk_us.as<int32_t>(), ctx->uoff.as<int64_t>(), nblk, ctx->U.as<uint8_t>(),
-                    ctx->status.as<int32_t>(), ctx->o.verify_crc, tim, s);
+                    ctx->status.as<int32_t>(), ctx->o.verify_crc, crc_init, tim, s);
     HIPCHK(hipEventRecord(ctx->ev[6], s));
     if (timing) {
       std::vector<uint64_t> h(16 * (size_t)nblk);
@@ -489,9 +506,13 @@ static int run_pipeline(dq_ctx* ctx) {
                           hipMemcpyHostToDevice, s));
   // ---- planning (a1-a5)
   std::vector<std::pair<int64_t, int64_t>> splits;
-  if (path_splits(ctx->o, ctx->shard ? ctx->file_len : L, splits))
+  if (ctx->chunk_mode) {
+    // record starts wanted: blocks up to the chunk end's block (chain_end below)
+    splits.push_back({0, (int64_t)(ctx->chunk_ve >> 16)});
+  } else if (path_splits(ctx->o, ctx->shard ? ctx->file_len : L, splits)) {
     RET(DQ_EINVAL, "splitSize must be > 0 with useNio");
-  if (ctx->shard) {  // the shard's partitions, in shard coordinates
+  }
+  if (ctx->shard && !ctx->chunk_mode) {  // the shard's partitions, in shard coordinates
     if (ctx->p0 < 0 || ctx->p1 > (int64_t)splits.size() || ctx->p0 >= ctx->p1)
       RET(DQ_EINVAL, "shard partition range out of bounds");
     std::vector<std::pair<int64_t, int64_t>> mine;
@@ -510,9 +531,20 @@ static int run_pipeline(dq_ctx* ctx) {
   HIPCHK(hipMemcpyAsync(ctx->plans.p, ctx->plans_h.data(), sizeof(SplitPlan) * (size_t)nsplit,
                         hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(d_nblk, &ctx->nblk, sizeof(int64_t), hipMemcpyHostToDevice, s));
-  const bool no_guess = ctx->index_only || ctx->sbi_plan;
-  if (no_guess && ctx->shard) RET(DQ_EINVAL, "splitting-index planning and indexing need the whole file");
-  if (no_guess) {
+  const bool no_guess = ctx->index_only || ctx->sbi_plan || ctx->chunk_mode;
+  if ((ctx->index_only || ctx->sbi_plan) && ctx->shard && !ctx->chunk_mode)
+    RET(DQ_EINVAL, "splitting-index planning and indexing need the whole file");
+  if (ctx->chunk_mode) {
+    // one partition: the caller's Chunk; both ends are pointers (BAMFileIndexIterator limits,
+    // H/BAMFileReader2.java:1082-1095), the start must be a record start
+    SplitPlan& P = ctx->plans_h[0];
+    P.first_blk = SPLIT_FROM_SBI;
+    P.rec_lin = (int64_t)(ctx->chunk_vs & 0xffff);  // window block 0 starts at the chunk's block
+    P.vstart = ctx->chunk_vs;
+    P.vend = ctx->chunk_ve;
+    if ((ctx->chunk_vs >> 16) != 0) RET(DQ_EINVAL, "chunk window must start at the chunk's block");
+    HIPCHK(hipMemcpyAsync(ctx->plans.p, ctx->plans_h.data(), sizeof(SplitPlan), hipMemcpyHostToDevice, s));
+  } else if (no_guess) {
     // No record guessing: the chain starts at the first record (BAMFileReader2
     // .findVirtualOffsetOfFirstRecord); .sbi plans are SBIIndex.getChunk (SBIIndex.java:244-277)
     for (auto& P : ctx->plans_h) {
@@ -544,7 +576,7 @@ static int run_pipeline(dq_ctx* ctx) {
   HIPCHK(hipStreamSynchronize(s));
   HIPCHK(hipEventRecord(ctx->ev[3], s));
   dbg(s, "plan", nsplit);
-  int64_t start_lin = no_guess ? ctx->header_bytes : -1;
+  int64_t start_lin = ctx->chunk_mode ? ctx->plans_h[0].rec_lin : no_guess ? ctx->header_bytes : -1;
   for (auto& P : ctx->plans_h) {
     if (P.status == 100 && ctx->shard && !is_eof)
       RET(DQ_EFORMAT, "shard halo too small: the record guesser needs bytes past the shard");
@@ -629,6 +661,7 @@ static int run_pipeline(dq_ctx* ctx) {
   HIPCHK(hipMemcpyAsync(&st, d_stat, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   if (st == 101) RET(DQ_EFORMAT, "record guesser start is not on the record chain");
+  if (st == 102 && ctx->chunk_mode) RET(DQ_EFORMAT, "chunk start is not a record start");
   if (st == 102) RET(DQ_EFORMAT, "splitting index offset is not a record start");
   if (st && ctx->shard && !is_eof) RET(DQ_EFORMAT, "shard halo too small: a record ends past the shard bytes");
   if (st) RET(DQ_EFORMAT, "truncated BAM record");
@@ -649,22 +682,37 @@ static int run_pipeline(dq_ctx* ctx) {
   S.n_records = emitted;
   S.digest = dg;
   S.ms_scan = ev_ms(ctx->ev[0], ctx->ev[1]);
-  S.ms_inflate = ev_ms(ctx->ev[5], ctx->ev[2]);  // K2a + K2b (CRC fused into K2b)
-  S.ms_crc = ev_ms(ctx->ev[6], ctx->ev[2]);  // K2b alone (resolve + CRC + store)
+  S.ms_inflate = ev_ms(ctx->ev[5], ctx->ev[6]);  // the inflate kernel (CRC32 fused)
+  S.ms_crc = 0;                                   // fused into the inflate kernel
   {
-    // DEFLATE payload bytes = sum over blocks of (BSIZE + 1 - 26): csize - 18 header - 8 trailer
+    // DEFLATE payload bytes = sum over blocks of (BSIZE + 1 - 26): csize - 18 header - 8 trailer;
+    // owned bytes = the decompressed bytes of the blocks that start inside the splits (the
+    // whole stream for a whole file; over the shards of a file they add up to its size)
     std::vector<int32_t> cs((size_t)nblk);
-    if (nblk) HIPCHK(hipMemcpy(cs.data(), ctx->blk_cs.p, 4 * (size_t)nblk, hipMemcpyDeviceToHost));
+    std::vector<int64_t> bp((size_t)nblk);
+    if (nblk) {
+      HIPCHK(hipMemcpyAsync(cs.data(), ctx->blk_cs.p, 4 * (size_t)nblk, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(bp.data(), ctx->blk_pos.p, 8 * (size_t)nblk, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+    }
     int64_t db = 0;
     for (int32_t c : cs) db += c - 26;
     S.deflate_bytes = db;
+    S.owned_bytes = ulen;
+    if (ctx->shard && nblk) {
+      const int64_t last_end = splits.back().second;
+      const int64_t j = std::lower_bound(bp.begin(), bp.end(), last_end) - bp.begin();
+      int64_t u = ulen;
+      if (j < nblk) HIPCHK(hipMemcpy(&u, ctx->uoff.as<int64_t>() + j, 8, hipMemcpyDeviceToHost));
+      S.owned_bytes = u;
+    }
   }
   S.ms_plan = ev_ms(ctx->ev[2], ctx->ev[3]);
   S.ms_records = ev_ms(ctx->ev[3], ctx->ev[4]);
   S.ms_total = ev_ms(ctx->ev[0], ctx->ev[4]);
+  S.h2d_bytes = ctx->h2d_bytes;
   ctx->have_pipeline = true;
   ctx->voff_h.clear();
-  ctx->lin_h.clear();
   return 0;
 }
 
@@ -672,26 +720,29 @@ static int run_pipeline(dq_ctx* ctx) {
 static int fetch_index(dq_ctx* ctx) {
   if ((int64_t)ctx->voff_h.size() == ctx->nrec) return 0;
   ctx->voff_h.resize((size_t)ctx->nrec);
-  ctx->lin_h.resize((size_t)ctx->nrec);
-  if (ctx->nrec) {
+  if (ctx->nrec)
     HIPCHK(hipMemcpy(ctx->voff_h.data(), ctx->f_voff.p, 8 * (size_t)ctx->nrec, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(ctx->lin_h.data(), ctx->rec_lin.p, 8 * (size_t)ctx->nrec, hipMemcpyDeviceToHost));
-  }
   return 0;
 }
 
-// Build a batch from a list of record-index ranges (in order; ranges may repeat records).
-static int make_batch(dq_ctx* ctx, const std::vector<std::pair<int64_t, int64_t>>& ranges,
+// Build a batch from record-index ranges (in order; ranges may repeat records) or an explicit
+// index list.  Only the selected records cross PCIe: one contiguous range is copied straight from
+// the resident arrays, anything else is first gathered into compact device buffers.
+static int make_batch(dq_ctx* ctx, const std::vector<std::pair<int64_t, int64_t>>& ranges_in,
                       const std::vector<int64_t>* explicit_idx, int32_t with_raw,
                       const std::vector<int64_t>& part_bounds, dq_batch** out) {
-  std::vector<int64_t> idx;
-  if (explicit_idx) {
-    idx = *explicit_idx;
-  } else {
-    for (auto& r : ranges)
-      for (int64_t k = r.first; k < r.second; k++) idx.push_back(k);
+  hipStream_t s = ctx->s;
+  // adjacent ranges (consecutive partitions) form one run of the resident arrays
+  std::vector<std::pair<int64_t, int64_t>> ranges;
+  for (auto& r : ranges_in) {
+    if (r.second <= r.first) continue;
+    if (!ranges.empty() && ranges.back().second == r.first) ranges.back().second = r.second;
+    else ranges.push_back(r);
   }
-  const int64_t n = (int64_t)idx.size();
+  int64_t n = 0;
+  if (explicit_idx) n = (int64_t)explicit_idx->size();
+  else
+    for (auto& r : ranges) n += r.second - r.first;
   dq_batch* b = (dq_batch*)calloc(1, sizeof(dq_batch));
   if (!b) RET(DQ_ENOMEM, "out of host memory");
   b->n_records = n;
@@ -711,25 +762,98 @@ static int make_batch(dq_ctx* ctx, const std::vector<std::pair<int64_t, int64_t>
   b->l_read_name = (uint8_t*)malloc(m);
   b->hash = (uint64_t*)malloc(8 * m);
   b->raw_offset = (int64_t*)malloc(8 * m);
-  // The whole-chain SoA is downloaded field by field once, then gathered on the host.
-  auto pull = [&](const DevBuf& d, size_t esz, void* dst) -> int {
-    if (n == 0) return 0;
-    std::vector<uint8_t> all((size_t)ctx->nrec * esz);
-    HIPCHK(hipMemcpy(all.data(), d.p, all.size(), hipMemcpyDeviceToHost));
-    uint8_t* o = (uint8_t*)dst;
-    for (int64_t i = 0; i < n; i++) memcpy(o + (size_t)i * esz, &all[(size_t)idx[(size_t)i] * esz], esz);
-    return 0;
-  };
-  int rc = 0;
-  if ((rc = pull(ctx->f_voff, 8, b->voffset)) || (rc = pull(ctx->f_bs, 4, b->block_size)) ||
-      (rc = pull(ctx->f_ref, 4, b->ref_id)) || (rc = pull(ctx->f_pos, 4, b->pos)) ||
-      (rc = pull(ctx->f_lseq, 4, b->l_seq)) || (rc = pull(ctx->f_nref, 4, b->next_ref_id)) ||
-      (rc = pull(ctx->f_npos, 4, b->next_pos)) || (rc = pull(ctx->f_tlen, 4, b->tlen)) ||
-      (rc = pull(ctx->f_flag, 2, b->flag)) || (rc = pull(ctx->f_bin, 2, b->bin)) ||
-      (rc = pull(ctx->f_ncig, 2, b->n_cigar)) || (rc = pull(ctx->f_mapq, 1, b->mapq)) ||
-      (rc = pull(ctx->f_lrn, 1, b->l_read_name)) || (rc = pull(ctx->f_hash, 8, b->hash))) {
+  if (!b->voffset || !b->block_size || !b->ref_id || !b->pos || !b->l_seq || !b->next_ref_id ||
+      !b->next_pos || !b->tlen || !b->flag || !b->bin || !b->n_cigar || !b->mapq ||
+      !b->l_read_name || !b->hash || !b->raw_offset) {
     dq_batch_free(b);
-    return rc;
+    RET(DQ_ENOMEM, "out of host memory");
+  }
+  int rc = 0;
+  auto fail = [&](int code) {
+    dq_batch_free(b);
+    return code;
+  };
+#define XCHK(x)                                                \
+  do {                                                         \
+    hipError_t e_ = (x);                                       \
+    if (e_ != hipSuccess) {                                    \
+      ctx->err = std::string(#x) + ": " + hipGetErrorString(e_); \
+      return fail(DQ_EDEVICE);                                 \
+    }                                                          \
+  } while (0)
+  const bool direct = !explicit_idx && ranges.size() <= 1;
+  int64_t first = direct && !ranges.empty() ? ranges[0].first : 0;
+  RecSoA rows = ctx->soa();
+  const int64_t* d_idx = nullptr;
+  if (n > 0 && !direct) {
+    if ((rc = ensure_all(ctx, ctx->x_idx, 8 * (size_t)n))) return fail(rc);
+    if (explicit_idx) {
+      XCHK(hipMemcpyAsync(ctx->x_idx.p, explicit_idx->data(), 8 * (size_t)n, hipMemcpyHostToDevice, s));
+    } else {
+      const int64_t nr = (int64_t)ranges.size();
+      std::vector<int64_t> rg((size_t)(2 * nr + 1));
+      int64_t o = 0;
+      for (int64_t r = 0; r < nr; r++) {
+        rg[(size_t)r] = ranges[(size_t)r].first;
+        rg[(size_t)(nr + r)] = o;
+        o += std::max<int64_t>(0, ranges[(size_t)r].second - ranges[(size_t)r].first);
+      }
+      rg[(size_t)(2 * nr)] = o;
+      if ((rc = ensure_all(ctx, ctx->x_rng, 8 * rg.size()))) return fail(rc);
+      XCHK(hipMemcpyAsync(ctx->x_rng.p, rg.data(), 8 * rg.size(), hipMemcpyHostToDevice, s));
+      launch_ranges_to_idx(ctx->x_rng.as<int64_t>(), ctx->x_rng.as<int64_t>() + nr, nr,
+                           ctx->x_idx.as<int64_t>(), s);
+    }
+    d_idx = ctx->x_idx.as<int64_t>();
+    // compact rows: 8-byte fields, then 4-, 2- and 1-byte ones (each array 8-byte aligned)
+    const size_t a8 = ((size_t)n * 8 + 7) & ~(size_t)7, a4 = ((size_t)n * 4 + 7) & ~(size_t)7,
+                 a2 = ((size_t)n * 2 + 7) & ~(size_t)7, a1 = ((size_t)n + 7) & ~(size_t)7;
+    if ((rc = ensure_all(ctx, ctx->x_soa, 2 * a8 + 7 * a4 + 3 * a2 + 2 * a1))) return fail(rc);
+    char* q = ctx->x_soa.as<char>();
+    auto take = [&](size_t bytes) {
+      char* r = q;
+      q += bytes;
+      return r;
+    };
+    RecSoA dst;
+    dst.voffset = (uint64_t*)take(a8);
+    dst.hash = (uint64_t*)take(a8);
+    dst.block_size = (int32_t*)take(a4);
+    dst.ref_id = (int32_t*)take(a4);
+    dst.pos = (int32_t*)take(a4);
+    dst.l_seq = (int32_t*)take(a4);
+    dst.next_ref_id = (int32_t*)take(a4);
+    dst.next_pos = (int32_t*)take(a4);
+    dst.tlen = (int32_t*)take(a4);
+    dst.flag = (uint16_t*)take(a2);
+    dst.bin = (uint16_t*)take(a2);
+    dst.n_cigar = (uint16_t*)take(a2);
+    dst.mapq = (uint8_t*)take(a1);
+    dst.l_read_name = (uint8_t*)take(a1);
+    launch_gather_soa(d_idx, n, ctx->soa(), dst, s);
+    rows = dst;
+    first = 0;
+  }
+  if (n > 0) {
+    auto d2h = [&](const void* dbase, size_t esz, void* dst) {
+      return hipMemcpyAsync(dst, (const char*)dbase + (size_t)first * esz, (size_t)n * esz,
+                            hipMemcpyDeviceToHost, s);
+    };
+    XCHK(d2h(rows.voffset, 8, b->voffset));
+    XCHK(d2h(rows.block_size, 4, b->block_size));
+    XCHK(d2h(rows.ref_id, 4, b->ref_id));
+    XCHK(d2h(rows.pos, 4, b->pos));
+    XCHK(d2h(rows.l_seq, 4, b->l_seq));
+    XCHK(d2h(rows.next_ref_id, 4, b->next_ref_id));
+    XCHK(d2h(rows.next_pos, 4, b->next_pos));
+    XCHK(d2h(rows.tlen, 4, b->tlen));
+    XCHK(d2h(rows.flag, 2, b->flag));
+    XCHK(d2h(rows.bin, 2, b->bin));
+    XCHK(d2h(rows.n_cigar, 2, b->n_cigar));
+    XCHK(d2h(rows.mapq, 1, b->mapq));
+    XCHK(d2h(rows.l_read_name, 1, b->l_read_name));
+    XCHK(d2h(rows.hash, 8, b->hash));
+    XCHK(hipStreamSynchronize(s));
   }
   if (ctx->base)
     for (int64_t i = 0; i < n; i++) b->voffset[i] += (uint64_t)ctx->base << 16;
@@ -740,32 +864,29 @@ static int make_batch(dq_ctx* ctx, const std::vector<std::pair<int64_t, int64_t>
   }
   b->raw_len = raw_len;
   if (with_raw && n > 0) {
-    if ((rc = fetch_index(ctx))) {
-      dq_batch_free(b);
-      return rc;
-    }
     b->raw = (uint8_t*)malloc((size_t)std::max<int64_t>(1, raw_len));
-    // copy contiguous runs of records in one transfer each
-    int64_t i = 0;
-    while (i < n) {
-      int64_t j = i + 1;
-      while (j < n && idx[(size_t)j] == idx[(size_t)j - 1] + 1) j++;
-      int64_t lo = ctx->lin_h[(size_t)idx[(size_t)i]];
-      int64_t hi = ctx->lin_h[(size_t)idx[(size_t)j - 1]] + 4 + b->block_size[j - 1];
-      hipError_t e = hipMemcpy(b->raw + b->raw_offset[i], ctx->U.as<uint8_t>() + lo,
-                               (size_t)(hi - lo), hipMemcpyDeviceToHost);
-      if (e != hipSuccess) {
-        dq_batch_free(b);
-        ctx->err = hipGetErrorString(e);
-        return DQ_EDEVICE;
-      }
-      i = j;
+    if (!b->raw) return fail(DQ_ENOMEM);
+    if (direct) {  // consecutive chain records are contiguous in U
+      int64_t lo = 0;
+      XCHK(hipMemcpy(&lo, ctx->rec_lin.as<int64_t>() + first, 8, hipMemcpyDeviceToHost));
+      XCHK(hipMemcpy(b->raw, ctx->U.as<uint8_t>() + lo, (size_t)raw_len, hipMemcpyDeviceToHost));
+    } else {
+      if ((rc = ensure_all(ctx, ctx->x_off, 8 * (size_t)n)) ||
+          (rc = ensure_all(ctx, ctx->x_raw, (size_t)raw_len)))
+        return fail(rc);
+      XCHK(hipMemcpyAsync(ctx->x_off.p, b->raw_offset, 8 * (size_t)n, hipMemcpyHostToDevice, s));
+      launch_gather_raw(ctx->U.as<uint8_t>(), ctx->rec_lin.as<int64_t>(), ctx->f_bs.as<int32_t>(),
+                        d_idx, 0, n, ctx->x_off.as<int64_t>(), ctx->x_raw.as<uint8_t>(), s);
+      XCHK(hipMemcpyAsync(b->raw, ctx->x_raw.p, (size_t)raw_len, hipMemcpyDeviceToHost, s));
+      XCHK(hipStreamSynchronize(s));
     }
   }
+#undef XCHK
   b->n_partitions = (int64_t)part_bounds.size() - 1;
   if (b->n_partitions < 0) b->n_partitions = 0;
   b->part_offset = (int64_t*)malloc(sizeof(int64_t) * (size_t)(b->n_partitions + 1));
   b->part_digest = (uint64_t*)calloc((size_t)b->n_partitions + 1, sizeof(uint64_t));
+  if (!b->part_offset || !b->part_digest) return fail(DQ_ENOMEM);
   for (int64_t p = 0; p <= b->n_partitions; p++) b->part_offset[p] = part_bounds[(size_t)p];
   for (int64_t p = 0; p < b->n_partitions; p++) {
     uint64_t d = 0;
@@ -875,6 +996,99 @@ static int filtered_indices(dq_ctx* ctx, uint64_t vstart, uint64_t vend, int64_t
   return 0;
 }
 
+// ------------------------------------------------------------------ opening inputs
+static void reset_open(dq_ctx* ctx, int64_t len) {
+  ctx->flen = len;
+  ctx->have_file = true;
+  ctx->have_pipeline = false;
+  ctx->shard = false;
+  ctx->base = 0;
+  ctx->file_len = len;
+  ctx->p0 = 0;
+  ctx->p1 = 0;
+  ctx->cext = nullptr;
+  ctx->chunk_mode = false;
+}
+
+// Bytes [off, off + len) of an open file into C (plus the 4 KiB zero pad): read() into two pinned
+// staging buffers in turn, each copied asynchronously while the next piece is read from the page
+// cache (the role of Disq's 2 x 4 MB NIO prefetcher, SeekableByteChannelPrefetcher.java:45).
+static int upload_file_range(dq_ctx* ctx, int fd, int64_t off, int64_t len) {
+  constexpr size_t PIECE = 32u << 20;
+  int rc;
+  if ((rc = ensure_all(ctx, ctx->C, (size_t)len + 4096))) return rc;
+  if (ctx->pin_cap < PIECE) {
+    for (int k = 0; k < 2; k++) {
+      if (ctx->pin[k]) (void)hipHostFree(ctx->pin[k]);
+      ctx->pin[k] = nullptr;
+      HIPCHK(hipHostMalloc((void**)&ctx->pin[k], PIECE, hipHostMallocDefault));
+      if (!ctx->pin_ev[k]) HIPCHK(hipEventCreateWithFlags(&ctx->pin_ev[k], hipEventDisableTiming));
+    }
+    ctx->pin_cap = PIECE;
+  }
+  bool used[2] = {false, false};
+  int k = 0;
+  for (int64_t done = 0; done < len; k ^= 1) {
+    const size_t n = (size_t)std::min<int64_t>((int64_t)PIECE, len - done);
+    if (used[k]) HIPCHK(hipEventSynchronize(ctx->pin_ev[k]));  // its previous copy is done
+    size_t got = 0;
+    while (got < n) {
+      const ssize_t r = pread(fd, ctx->pin[k] + got, n - got, (off_t)(off + done + (int64_t)got));
+      if (r <= 0) RET(DQ_EIO, "short read");
+      got += (size_t)r;
+    }
+    HIPCHK(hipMemcpyAsync(ctx->C.as<uint8_t>() + done, ctx->pin[k], n, hipMemcpyHostToDevice, ctx->s));
+    HIPCHK(hipEventRecord(ctx->pin_ev[k], ctx->s));
+    used[k] = true;
+    done += (int64_t)n;
+  }
+  HIPCHK(hipMemsetAsync(ctx->C.as<uint8_t>() + len, 0, 4096, ctx->s));
+  HIPCHK(hipStreamSynchronize(ctx->s));
+  reset_open(ctx, len);
+  ctx->h2d_bytes = len;
+  return 0;
+}
+
+struct Fd {
+  int fd = -1;
+  ~Fd() {
+    if (fd >= 0) close(fd);
+  }
+};
+
+static int open_fd(dq_ctx* ctx, const char* path, Fd& f, int64_t* flen) {
+  f.fd = open(path, O_RDONLY);
+  if (f.fd < 0) RET(DQ_EIO, std::string("cannot open ") + path);
+  struct stat st;
+  if (fstat(f.fd, &st) != 0) RET(DQ_EIO, std::string("cannot stat ") + path);
+  *flen = (int64_t)st.st_size;
+  return 0;
+}
+
+// The file's decompressed BAM header into ctx->hdr (AbstractSamSource.getFileHeader): the first
+// bytes of the file, growing the prefix until the header is whole.
+static int load_header(dq_ctx* ctx, int fd, int64_t flen) {
+  int64_t n = std::min<int64_t>(flen, 1 << 20);
+  for (;;) {
+    int rc = upload_file_range(ctx, fd, 0, n);
+    if (rc) return rc;
+    ctx->shard = true;  // a prefix: its end is not EOF unless it is the whole file
+    ctx->file_len = n < flen ? INT64_MAX / 4 : flen;
+    ctx->header_only = true;
+    rc = run_pipeline(ctx);
+    ctx->header_only = false;
+    ctx->have_pipeline = false;
+    ctx->have_file = false;
+    if (rc == 0) {
+      ctx->hdr.resize((size_t)ctx->header_bytes);
+      HIPCHK(hipMemcpy(ctx->hdr.data(), ctx->U.p, (size_t)ctx->header_bytes, hipMemcpyDeviceToHost));
+      return 0;
+    }
+    if (n >= flen) return rc;
+    n = std::min<int64_t>(flen, n * 8);
+  }
+}
+
 // ------------------------------------------------------------------ C ABI
 extern "C" {
 
@@ -913,6 +1127,10 @@ void dq_ctx_destroy(dq_ctx* ctx) {
   if (ctx->s) (void)hipStreamSynchronize(ctx->s);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
+  for (int k = 0; k < 2; k++) {
+    if (ctx->pin_ev[k]) (void)hipEventDestroy(ctx->pin_ev[k]);
+    if (ctx->pin[k]) (void)hipHostFree(ctx->pin[k]);
+  }
   if (ctx->s) (void)hipStreamDestroy(ctx->s);
   delete ctx;
 }
@@ -921,19 +1139,32 @@ const char* dq_last_error(const dq_ctx* ctx) { return ctx ? ctx->err.c_str() : "
 
 int dq_open_memory(dq_ctx* ctx, const uint8_t* bam, int64_t len) {
   if (!ctx || (!bam && len > 0) || len < 0) return DQ_EINVAL;
-  HIPCHK(hipSetDevice(ctx->o.device));
+  ON_DEVICE(ctx);
   int rc;
   if ((rc = ensure_all(ctx, ctx->C, (size_t)len + 4096))) return rc;
   if (len) HIPCHK(hipMemcpy(ctx->C.p, bam, (size_t)len, hipMemcpyHostToDevice));
   HIPCHK(hipMemset(ctx->C.as<uint8_t>() + len, 0, 4096));
-  ctx->flen = len;
-  ctx->have_file = true;
-  ctx->have_pipeline = false;
-  ctx->shard = false;
-  ctx->base = 0;
-  ctx->file_len = len;
-  ctx->p0 = 0;
-  ctx->p1 = 0;
+  reset_open(ctx, len);
+  ctx->h2d_bytes = len;
+  return 0;
+}
+
+int dq_open_shard_device(dq_ctx* ctx, const void* dev_bytes, int64_t len, int64_t base,
+                         int64_t file_len, int64_t p0, int64_t p1, const uint8_t* header,
+                         int64_t header_len) {
+  if (!ctx || !dev_bytes || len <= 0 || base < 0 || base + len > file_len || p0 < 0 || p1 <= p0 ||
+      !header || header_len <= 0)
+    return DQ_EINVAL;
+  ON_DEVICE(ctx);
+  reset_open(ctx, len);
+  ctx->cext = static_cast<const uint8_t*>(dev_bytes);
+  ctx->h2d_bytes = 0;
+  ctx->shard = true;
+  ctx->base = base;
+  ctx->file_len = file_len;
+  ctx->p0 = p0;
+  ctx->p1 = p1;
+  ctx->hdr.assign(header, header + header_len);
   return 0;
 }
 
@@ -955,21 +1186,86 @@ int dq_open_shard(dq_ctx* ctx, const uint8_t* bytes, int64_t len, int64_t base, 
 
 int dq_open_path(dq_ctx* ctx, const char* path) {
   if (!ctx || !path) return DQ_EINVAL;
-  FILE* f = fopen(path, "rb");
-  if (!f) RET(DQ_EIO, std::string("cannot open ") + path);
-  fseek(f, 0, SEEK_END);
-  int64_t len = ftell(f);
-  fseek(f, 0, SEEK_SET);
-  std::vector<uint8_t> buf((size_t)len);
-  size_t got = len ? fread(buf.data(), 1, (size_t)len, f) : 0;
-  fclose(f);
-  if ((int64_t)got != len) RET(DQ_EIO, std::string("short read on ") + path);
-  return dq_open_memory(ctx, buf.data(), len);
+  ON_DEVICE(ctx);
+  Fd f;
+  int64_t len = 0;
+  int rc = open_fd(ctx, path, f, &len);
+  if (rc) return rc;
+  return upload_file_range(ctx, f.fd, 0, len);
+}
+
+int dq_decode_chunk(dq_ctx* ctx, const char* path, uint64_t vstart, uint64_t vend, int32_t with_raw,
+                    dq_batch** out) {
+  if (!ctx || !path || !out) return DQ_EINVAL;
+  ON_DEVICE(ctx);
+  Fd f;
+  int64_t flen = 0;
+  int rc = open_fd(ctx, path, f, &flen);
+  if (rc) return rc;
+  if (ctx->chunk_hdr_path != path) {
+    ctx->chunk_hdr_path.clear();
+    if ((rc = load_header(ctx, f.fd, flen))) return rc;
+    ctx->chunk_hdr_path = path;
+  }
+  const int64_t c0 = (int64_t)(vstart >> 16);
+  if (vend <= vstart || c0 >= flen) return make_batch(ctx, {}, nullptr, with_raw, {0, 0}, out);
+  // the chunk's blocks, then enough to finish its last record: grown x4 while it runs past
+  int64_t extra = 256 << 10, h2d = 0;
+  for (;;) {
+    const int64_t c1 = std::min<int64_t>(flen, (int64_t)(vend >> 16) + extra);
+    if ((rc = upload_file_range(ctx, f.fd, c0, c1 - c0))) return rc;
+    h2d += c1 - c0;
+    ctx->shard = true;
+    ctx->base = c0;
+    ctx->file_len = flen;
+    ctx->p0 = 0;
+    ctx->p1 = 1;
+    ctx->chunk_mode = true;
+    ctx->chunk_vs = vstart - ((uint64_t)c0 << 16);
+    ctx->chunk_ve = vend - ((uint64_t)c0 << 16);
+    ctx->h2d_bytes = h2d;
+    rc = run_pipeline(ctx);
+    if (rc == DQ_EFORMAT && ctx->err.find("halo too small") != std::string::npos && c1 < flen) {
+      extra *= 4;
+      continue;
+    }
+    break;
+  }
+  ctx->chunk_mode = false;
+  if (rc) {
+    ctx->have_file = false;
+    return rc;
+  }
+  const PartRange r = ctx->parts_h[0];
+  rc = make_batch(ctx, {{r.begin, r.end}}, nullptr, with_raw, {0, r.end - r.begin}, out);
+  ctx->have_file = false;  // the window is not a file the other calls can use
+  ctx->have_pipeline = false;
+  return rc;
+}
+
+int dq_get_stats(dq_ctx* ctx, dq_stats* stats) {
+  if (!ctx || !stats) return DQ_EINVAL;
+  *stats = ctx->stats;
+  return 0;
+}
+
+int dq_partition_digests(dq_ctx* ctx, int64_t* counts, uint64_t* digests, int64_t cap,
+                         int64_t* n) {
+  if (!ctx || !n) return DQ_EINVAL;
+  if (!ctx->have_pipeline) RET(DQ_EINVAL, "no pipeline run (call dq_run_resident first)");
+  *n = (int64_t)ctx->parts_h.size();
+  for (int64_t i = 0; i < std::min(cap, *n); i++) {
+    const PartRange& r = ctx->parts_h[(size_t)i];
+    if (counts) counts[i] = r.end - r.begin;
+    if (digests) digests[i] = r.digest;
+  }
+  return 0;
 }
 
 int dq_header_from_prefix(dq_ctx* ctx, const uint8_t* bytes, int64_t len, uint8_t* out,
                           int64_t cap, int64_t* out_len) {
   if (!ctx || !bytes || len <= 0) return DQ_EINVAL;
+  ON_DEVICE(ctx);
   int rc = dq_open_memory(ctx, bytes, len);
   if (rc) return rc;
   ctx->shard = true;  // the prefix is not the whole file: its end is not EOF
@@ -1025,6 +1321,7 @@ int dq_set_splitting_index(dq_ctx* ctx, const uint8_t* sbi, int64_t len, int32_t
 
 int dq_write_sbi(dq_ctx* ctx, int64_t granularity, uint8_t** out, int64_t* out_len) {
   if (!ctx || !out || !out_len) return DQ_EINVAL;
+  ON_DEVICE(ctx);
   if (granularity <= 0) granularity = 4096;  // SBIIndexWriter.DEFAULT_GRANULARITY
   if (ctx->shard) RET(DQ_EINVAL, "dq_write_sbi indexes a whole file, not a shard");
   ctx->have_pipeline = false;
@@ -1082,6 +1379,7 @@ int dq_write_sbi(dq_ctx* ctx, int64_t granularity, uint8_t** out, int64_t* out_l
 
 int dq_read_header(dq_ctx* ctx, dq_header_info* info, uint8_t* header_bytes, int64_t cap) {
   if (!ctx) return DQ_EINVAL;
+  ON_DEVICE(ctx);
   int rc = run_pipeline(ctx);
   if (rc) return rc;
   if (info) {
@@ -1104,6 +1402,7 @@ int dq_read_header(dq_ctx* ctx, dq_header_info* info, uint8_t* header_bytes, int
 
 int dq_plan(dq_ctx* ctx, dq_chunk** chunks, int64_t* n) {
   if (!ctx || !chunks || !n) return DQ_EINVAL;
+  ON_DEVICE(ctx);
   int rc = run_pipeline(ctx);
   if (rc) return rc;
   *n = (int64_t)ctx->plans_h.size();
@@ -1123,6 +1422,7 @@ int dq_plan(dq_ctx* ctx, dq_chunk** chunks, int64_t* n) {
 
 int dq_decode(dq_ctx* ctx, uint64_t vstart, uint64_t vend, int32_t with_raw, dq_batch** out) {
   if (!ctx || !out) return DQ_EINVAL;
+  ON_DEVICE(ctx);
   int rc = run_pipeline(ctx);
   if (rc) return rc;
   int64_t b, e;
@@ -1133,6 +1433,7 @@ int dq_decode(dq_ctx* ctx, uint64_t vstart, uint64_t vend, int32_t with_raw, dq_
 int dq_decode_filtered(dq_ctx* ctx, uint64_t vstart, uint64_t vend, const dq_traversal* tr,
                        int32_t with_raw, dq_batch** out) {
   if (!ctx || !out || !tr) return DQ_EINVAL;
+  ON_DEVICE(ctx);
   if (!tr->has_intervals && !tr->traverse_unplaced_unmapped)
     RET(DQ_EINVAL, "Traversing mapped reads only is not supported.");
   int rc = run_pipeline(ctx);
@@ -1149,29 +1450,39 @@ int dq_decode_filtered(dq_ctx* ctx, uint64_t vstart, uint64_t vend, const dq_tra
 
 int dq_read(dq_ctx* ctx, const dq_traversal* tr, int32_t with_raw, dq_batch** out) {
   if (!ctx || !out) return DQ_EINVAL;
+  ON_DEVICE(ctx);
   if (tr && !tr->has_intervals && !tr->traverse_unplaced_unmapped)
     RET(DQ_EINVAL, "Traversing mapped reads only is not supported.");
   int rc = run_pipeline(ctx);
   if (rc) return rc;
   std::vector<int64_t> idx, bounds{0};
+  std::vector<std::pair<int64_t, int64_t>> ranges;
+  int64_t total = 0;
   for (size_t i = 0; i < ctx->plans_h.size(); i++) {
     const SplitPlan& P = ctx->plans_h[i];
     if (P.rec_lin < 0) continue;  // empty partition (no PathChunk)
     const PartRange& r = ctx->parts_h[i];
     if (!tr) {
-      for (int64_t k = r.begin; k < r.end; k++) idx.push_back(k);
+      ranges.push_back({r.begin, r.end});
+      total += r.end - r.begin;
     } else {
       std::vector<int64_t> f;
       if ((rc = filtered_indices(ctx, P.vstart, P.vend, r.begin, r.end, tr, f))) return rc;
       idx.insert(idx.end(), f.begin(), f.end());
+      total = (int64_t)idx.size();
     }
-    bounds.push_back((int64_t)idx.size());
+    bounds.push_back(total);
+  }
+  if (!tr) {
+    // a single range is copied straight from the resident arrays (ranges.size() <= 1)
+    return make_batch(ctx, ranges, nullptr, with_raw, bounds, out);
   }
   return make_batch(ctx, {}, &idx, with_raw, bounds, out);
 }
 
 int dq_run_resident(dq_ctx* ctx, const dq_traversal* tr, dq_stats* stats) {
   if (!ctx) return DQ_EINVAL;
+  ON_DEVICE(ctx);
   if (tr && !tr->has_intervals && !tr->traverse_unplaced_unmapped)
     RET(DQ_EINVAL, "Traversing mapped reads only is not supported.");
   ctx->have_pipeline = false;
@@ -1213,6 +1524,7 @@ int dq_run_resident(dq_ctx* ctx, const dq_traversal* tr, dq_stats* stats) {
 
 int dq_debug_inflated(dq_ctx* ctx, uint8_t* host_out, int64_t cap, int64_t* len) {
   if (!ctx) return DQ_EINVAL;
+  ON_DEVICE(ctx);
   int rc = run_pipeline(ctx);
   if (rc) return rc;
   if (len) *len = ctx->ulen;

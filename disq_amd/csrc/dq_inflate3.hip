@@ -42,6 +42,7 @@
 #include "dq_inflate_core.h"
 #include "dq_internal.h"
 
+#include <mutex>
 #include <vector>
 
 namespace dq {
@@ -1241,47 +1242,70 @@ uint32_t h_mul(uint32_t a, uint32_t b) {
   return p;
 }
 
-uint32_t* g_crc_init = nullptr;
+// Host-side CRC tables, computed once per process.
+struct HostTables {
+  uint32_t crc4[4][256];
+  uint32_t slice[WG];
+  std::vector<uint32_t> init;  // CRC of n zero bytes with initial register ~0, n = 0..65536
+  HostTables() : init(65537) {
+    for (uint32_t i = 0; i < 256; i++) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; k++) c = c & 1 ? (c >> 1) ^ 0xEDB88320u : c >> 1;
+      crc4[0][i] = c;
+    }
+    for (int j = 1; j < 4; j++)
+      for (uint32_t i = 0; i < 256; i++) crc4[j][i] = (crc4[j - 1][i] >> 8) ^ crc4[0][crc4[j - 1][i] & 0xff];
+    uint32_t x2n[32];
+    uint32_t p = 1u << 30;  // x^1
+    x2n[0] = p;
+    for (int k = 1; k < 32; k++) x2n[k] = p = h_mul(p, p);
+    // x^(8 * 128 * k) mod P: x^1024 = x2n[10]; powers by repeated multiplication
+    slice[0] = 1u << 31;  // x^0
+    for (int k = 1; k < WG; k++) slice[k] = h_mul(slice[k - 1], x2n[10]);
+    uint32_t x8 = 1u << 31;          // x^0
+    const uint32_t x8step = x2n[3];  // x^8
+    for (int n = 0; n <= 65536; n++) {
+      init[(size_t)n] = h_mul(x8, 0xffffffffu);
+      x8 = h_mul(x8, x8step);
+    }
+  }
+};
+
+// Per-device state: the __constant__ tables are per-device copies of the code object, and the
+// init table is device memory, so every device is initialised on its own, once.
+constexpr int kMaxDevices = 64;
+struct DevTables {
+  std::once_flag once;
+  uint32_t* crc_init = nullptr;
+  bool ok = false;
+};
+DevTables g_dev[kMaxDevices];
 
 }  // namespace
 
-void init_inflate3_tables() {
-  static bool done = false;
-  if (done) return;
-  uint32_t tab[4][256];
-  for (uint32_t i = 0; i < 256; i++) {
-    uint32_t c = i;
-    for (int k = 0; k < 8; k++) c = c & 1 ? (c >> 1) ^ 0xEDB88320u : c >> 1;
-    tab[0][i] = c;
-  }
-  for (int j = 1; j < 4; j++)
-    for (uint32_t i = 0; i < 256; i++) tab[j][i] = (tab[j - 1][i] >> 8) ^ tab[0][tab[j - 1][i] & 0xff];
-  uint32_t x2n[32];
-  uint32_t p = 1u << 30;  // x^1
-  x2n[0] = p;
-  for (int k = 1; k < 32; k++) x2n[k] = p = h_mul(p, p);
-  // x^(8 * 128 * k) mod P: x^1024 = x2n[10]; powers by repeated multiplication
-  uint32_t sl[WG];
-  sl[0] = 1u << 31;  // x^0
-  for (int k = 1; k < WG; k++) sl[k] = h_mul(sl[k - 1], x2n[10]);
-  (void)hipMemcpyToSymbol(HIP_SYMBOL(c_crc4), tab, sizeof tab);
-  (void)hipMemcpyToSymbol(HIP_SYMBOL(c_slice_shift), sl, sizeof sl);
-  // CRC of n zero bytes with initial register ~0, for every ISIZE n in [0, 65536]
-  std::vector<uint32_t> ini(65537);
-  uint32_t x8 = 1u << 31;  // x^0
-  const uint32_t x8step = x2n[3];  // x^8
-  for (int n = 0; n <= 65536; n++) {
-    ini[(size_t)n] = h_mul(x8, 0xffffffffu);
-    x8 = h_mul(x8, x8step);
-  }
-  (void)hipMalloc(&g_crc_init, sizeof(uint32_t) * ini.size());
-  (void)hipMemcpy(g_crc_init, ini.data(), sizeof(uint32_t) * ini.size(), hipMemcpyHostToDevice);
-  done = true;
+const uint32_t* inflate3_tables(int device) {
+  if (device < 0 || device >= kMaxDevices) return nullptr;
+  DevTables& D = g_dev[device];
+  std::call_once(D.once, [&] {
+    static const HostTables H;
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    bool ok = hipSetDevice(device) == hipSuccess;
+    ok = ok && hipMemcpyToSymbol(HIP_SYMBOL(c_crc4), H.crc4, sizeof H.crc4) == hipSuccess;
+    ok = ok && hipMemcpyToSymbol(HIP_SYMBOL(c_slice_shift), H.slice, sizeof H.slice) == hipSuccess;
+    ok = ok && hipMalloc(&D.crc_init, sizeof(uint32_t) * H.init.size()) == hipSuccess;
+    ok = ok && hipMemcpy(D.crc_init, H.init.data(), sizeof(uint32_t) * H.init.size(),
+                         hipMemcpyHostToDevice) == hipSuccess;
+    D.ok = ok;
+    if (prev >= 0) (void)hipSetDevice(prev);
+  });
+  return D.ok ? D.crc_init : nullptr;
 }
 
 void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* blk_csize,
                      const int32_t* blk_usize, const int64_t* uoff, int64_t nblk, uint8_t* U,
-                     int32_t* status, int32_t verify_crc, uint64_t* tim, hipStream_t s) {
+                     int32_t* status, int32_t verify_crc, const uint32_t* crc_init, uint64_t* tim,
+                     hipStream_t s) {
   if (nblk <= 0) return;
   static const uint32_t ov = getenv("DQ_OV") ? (uint32_t)atoi(getenv("DQ_OV")) : OV_DEFAULT;
   static const uint32_t sflags = getenv("DQ_STORE") ? (uint32_t)atoi(getenv("DQ_STORE")) : 2;
@@ -1293,7 +1317,7 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
   }
 #define DQ_LAUNCH(TM, NBT, GT)                                                                  \
   hipLaunchKernelGGL((inflate_block_kernel<TM, NBT, GT>), dim3((unsigned)nblk), dim3(WG), 0, s, C, \
-                     blk_pos, blk_csize, blk_usize, uoff, nblk, U, status, verify_crc, g_crc_init, tim, ov, sflags)
+                     blk_pos, blk_csize, blk_usize, uoff, nblk, U, status, verify_crc, crc_init, tim, ov, sflags)
 #define DQ_CFGS(TM)                       \
   switch (cfg) {                          \
     case 1: DQ_LAUNCH(TM, 1, 4); break;   \

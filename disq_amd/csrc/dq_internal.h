@@ -71,20 +71,14 @@ void launch_exclusive_scan_i32(const int32_t* in, int64_t* out, int64_t n, int64
 void launch_exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* tmp,
                                hipStream_t s);
 
-// Kernel 2: inflate every chain block into U at uoff[b] (K2a Huffman decode to a u16 token
-// stream, event `mid`, K2b LZ77 resolve + CRC32 in LDS); status per block.
-int64_t token_bytes(int64_t uoff_total, int64_t nblk);
-void init_inflate_tables();
-void launch_inflate2(const uint8_t* C, const int64_t* blk_pos, const int32_t* blk_csize,
-                     const int32_t* blk_usize, const int64_t* uoff, int64_t nblk, uint16_t* tok,
-                     int32_t* tok_count, int32_t* counter, uint8_t* U, int32_t* status,
-                     int32_t verify_crc, int n_cu, hipEvent_t mid, hipStream_t s);
-
-// Kernel 2 (v3): fused inflate + CRC32, one workgroup per block (dq_inflate3.hip).
-void init_inflate3_tables();
+// Kernel 2: fused inflate + CRC32, one workgroup per block (dq_inflate3.hip).  The CRC tables
+// live in each device's memory: inflate3_tables(device) initialises them once per device (thread
+// safe) and returns that device's table of x^(8n) * ~0 mod P, n = 0..65536 (nullptr on failure).
+const uint32_t* inflate3_tables(int device);
 void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* blk_csize,
                      const int32_t* blk_usize, const int64_t* uoff, int64_t nblk, uint8_t* U,
-                     int32_t* status, int32_t verify_crc, uint64_t* tim, hipStream_t s);
+                     int32_t* status, int32_t verify_crc, const uint32_t* crc_init, uint64_t* tim,
+                     hipStream_t s);
 
 // Split planning (a2-a4).
 constexpr int64_t SPLIT_FROM_SBI = -2;  // SplitPlan.first_blk of a chunk taken from a .sbi
@@ -157,6 +151,15 @@ void launch_partition_ranges(const SplitPlan* plans, int64_t nsplit, const int64
                              int32_t* d_status, hipStream_t s);
 void launch_partition_digest2(const uint64_t* hash, PartRange* parts, int64_t nparts,
                               hipStream_t s);
+
+// Record export: record-index ranges -> index list; SoA rows and raw bytes gathered by index into
+// compact buffers (idx == nullptr in gather_raw: records first .. first + n - 1).
+void launch_ranges_to_idx(const int64_t* begin, const int64_t* out_off, int64_t nranges,
+                          int64_t* idx, hipStream_t s);
+void launch_gather_soa(const int64_t* idx, int64_t n, const RecSoA src, RecSoA dst, hipStream_t s);
+void launch_gather_raw(const uint8_t* U, const int64_t* rec_lin, const int32_t* block_size,
+                       const int64_t* idx, int64_t first, int64_t n, const int64_t* out_off,
+                       uint8_t* out, hipStream_t s);
 
 // Kernel 4: interval filter; keep[t] for record idx[t] (or t when idx == NULL).
 void launch_interval_filter(const uint8_t* U, const int64_t* rec_lin, const RecSoA soa,

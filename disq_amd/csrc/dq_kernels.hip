@@ -763,7 +763,7 @@ __global__ void partition_ranges_kernel(const SplitPlan* __restrict__ plans, int
   if (P.rec_lin >= 0 && P.first_blk == SPLIT_FROM_SBI) {  // .sbi chunk: both ends are pointers
     const int64_t b = lower_bound_u64(voffset, nrec, P.vstart);
     if (b >= nrec || voffset[b] != P.vstart) {
-      *d_status = 102;  // indexed offset is not a record start
+      atomicCAS(d_status, 0, 102);  // indexed offset is not a record start (a short record wins)
     } else {
       const int64_t e = lower_bound_u64(voffset, nrec, P.vend);
       r.begin = b;
@@ -772,7 +772,7 @@ __global__ void partition_ranges_kernel(const SplitPlan* __restrict__ plans, int
   } else if (P.rec_lin >= 0) {
     int64_t b = lower_bound_i64(rec_lin, nrec, P.rec_lin);
     if (b >= nrec || rec_lin[b] != P.rec_lin) {
-      *d_status = 101;  // guesser start not on the record chain (misfire)
+      atomicCAS(d_status, 0, 101);  // guesser start not on the record chain (misfire)
     } else {
       int64_t e = lower_bound_u64(voffset, nrec, P.vend);
       r.begin = b;
@@ -865,6 +865,57 @@ __global__ __launch_bounds__(256) void interval_filter_kernel(
     }
   }
   keep[t] = k;
+}
+
+// ------------------------------------------------------------------ record export (gathers)
+// idx[o_r + k] = begin_r + k for record-index ranges r (one block per range).
+__global__ __launch_bounds__(256) void ranges_to_idx_kernel(const int64_t* __restrict__ begin,
+                                                            const int64_t* __restrict__ out_off,
+                                                            int64_t nranges, int64_t* __restrict__ idx) {
+  const int64_t r = blockIdx.x;
+  if (r >= nranges) return;
+  const int64_t b = begin[r], o = out_off[r], n = out_off[r + 1] - o;
+  for (int64_t k = threadIdx.x; k < n; k += blockDim.x) idx[o + k] = b + k;
+}
+
+// dst row t = src row idx[t] for every SoA field (the batch a Spark task receives, compacted on
+// the device so only the selected records cross PCIe).
+__global__ __launch_bounds__(256) void gather_soa_kernel(const int64_t* __restrict__ idx, int64_t n,
+                                                         RecSoA src, RecSoA dst) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int64_t i = idx[t];
+  dst.voffset[t] = src.voffset[i];
+  dst.block_size[t] = src.block_size[i];
+  dst.ref_id[t] = src.ref_id[i];
+  dst.pos[t] = src.pos[i];
+  dst.l_seq[t] = src.l_seq[i];
+  dst.next_ref_id[t] = src.next_ref_id[i];
+  dst.next_pos[t] = src.next_pos[i];
+  dst.tlen[t] = src.tlen[i];
+  dst.flag[t] = src.flag[i];
+  dst.bin[t] = src.bin[i];
+  dst.n_cigar[t] = src.n_cigar[i];
+  dst.mapq[t] = src.mapq[i];
+  dst.l_read_name[t] = src.l_read_name[i];
+  dst.hash[t] = src.hash[i];
+}
+
+// The raw bytes (4 + block_size) of record idx[t] (or first + t when idx is null) to
+// out[out_off[t] ...]: one wave per record.
+__global__ __launch_bounds__(256) void gather_raw_kernel(const uint8_t* __restrict__ U,
+                                                         const int64_t* __restrict__ rec_lin,
+                                                         const int32_t* __restrict__ block_size,
+                                                         const int64_t* __restrict__ idx,
+                                                         int64_t first, int64_t n,
+                                                         const int64_t* __restrict__ out_off,
+                                                         uint8_t* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= n) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t i = idx ? idx[t] : first + t;
+  const int64_t src = rec_lin[i], len = 4 + (int64_t)block_size[i], o = out_off[t];
+  for (int64_t k = lane; k < len; k += 64) out[o + k] = U[src + k];
 }
 
 }  // namespace
@@ -1011,6 +1062,27 @@ void launch_sbi_sample(const uint64_t* voffset, int64_t nrec, int64_t g, uint64_
   if (n <= 0) return;
   hipLaunchKernelGGL(sbi_sample_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, voffset,
                      nrec, g, out);
+}
+
+void launch_ranges_to_idx(const int64_t* begin, const int64_t* out_off, int64_t nranges,
+                          int64_t* idx, hipStream_t s) {
+  if (nranges <= 0) return;
+  hipLaunchKernelGGL(ranges_to_idx_kernel, dim3((unsigned)nranges), dim3(256), 0, s, begin, out_off,
+                     nranges, idx);
+}
+
+void launch_gather_soa(const int64_t* idx, int64_t n, const RecSoA src, RecSoA dst, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(gather_soa_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, idx, n,
+                     src, dst);
+}
+
+void launch_gather_raw(const uint8_t* U, const int64_t* rec_lin, const int32_t* block_size,
+                       const int64_t* idx, int64_t first, int64_t n, const int64_t* out_off,
+                       uint8_t* out, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(gather_raw_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, U, rec_lin,
+                     block_size, idx, first, n, out_off, out);
 }
 
 }  // namespace dq

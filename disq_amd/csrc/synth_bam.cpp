@@ -251,6 +251,7 @@ struct Gen {
   int64_t n_unplaced = 0;
   int64_t per_chunk = 0;
   int64_t n_chunks = 0;
+  double spacing = 5.0;         // short-read genome offset step
 };
 
 void build_header(Gen& g) {
@@ -355,9 +356,12 @@ void gen_records(const Gen& g, int64_t r0, int64_t r1, std::vector<uint8_t>& u,
       if (recs) recs->push_back(rr);
       continue;
     }
-    int64_t spacing = o.shape == DQ_SYNTH_LONGREAD ? 30000 : 5;
+    // genome offset floor(i * s) + jitter < floor(s): non-decreasing in i; s = 5 bp for short
+    // reads, or less when the records would run past the genome (30x-WGS-sized files)
+    const double s = o.shape == DQ_SYNTH_LONGREAD ? 30000.0 : g.spacing;
+    const int64_t js = std::max<int64_t>(1, (int64_t)s);
     int32_t ref, pos;
-    locate(g.dict, i * spacing + (int64_t)r.u32((uint32_t)spacing), &ref, &pos);
+    locate(g.dict, (int64_t)((double)i * s) + (int64_t)r.u32((uint32_t)js), &ref, &pos);
     int nm_edits = 0;
     if (o.shape == DQ_SYNTH_LONGREAD) {
       int left = L;
@@ -563,23 +567,36 @@ int dq_synth_bam(const dq_synth_opts* opts, dq_synth_result* res) {
     g.dict = grch38_dict();
     g.total_records = opts->n_records;
     g.n_unplaced = (int64_t)(opts->unplaced_fraction * (double)opts->n_records);
+    int64_t usable = 0;
+    for (auto& r : g.dict) usable += r.len - 200000;
+    const int64_t mapped = std::max<int64_t>(1, g.total_records - g.n_unplaced);
+    g.spacing = std::min(5.0, (double)usable / (double)mapped);
   }
   build_header(g);
   g.per_chunk = opts->records_per_chunk > 0 ? opts->records_per_chunk : 20000;
   if (g.o.shape == DQ_SYNTH_LONGREAD && opts->records_per_chunk <= 0) g.per_chunk = 2000;
   g.n_chunks = std::max<int64_t>(1, (g.total_records + g.per_chunk - 1) / g.per_chunk);
-  std::vector<Chunk> chunks((size_t)g.n_chunks);
+  res->n_chunks = g.n_chunks;
+  int64_t klo = 0, khi = g.n_chunks;
+  if (opts->chunk_hi > 0) {
+    if (index || opts->chunk_lo < 0 || opts->chunk_lo >= opts->chunk_hi || opts->chunk_hi > g.n_chunks)
+      return -3;
+    klo = opts->chunk_lo;
+    khi = opts->chunk_hi;
+  }
+  const bool with_eof = khi == g.n_chunks;
+  std::vector<Chunk> chunks((size_t)(khi - klo));
   std::atomic<int64_t> next{0}, finished{0};
   const bool progress = getenv("DQ_SYNTH_PROGRESS") != nullptr;
   const int64_t step = std::max<int64_t>(1, g.n_chunks / 20);
   auto work = [&]() {
     for (;;) {
       int64_t k = next++;
-      if (k >= g.n_chunks) break;
-      make_chunk(g, k, chunks[(size_t)k], index);
+      if (k >= khi - klo) break;
+      make_chunk(g, klo + k, chunks[(size_t)k], index);
       int64_t f = ++finished;
       if (progress && f % step == 0) {
-        fprintf(stderr, "[synth] %lld/%lld chunks\n", (long long)f, (long long)g.n_chunks);
+        fprintf(stderr, "[synth] %lld/%lld chunks\n", (long long)f, (long long)(khi - klo));
         fflush(stderr);
       }
     }
@@ -588,9 +605,9 @@ int dq_synth_bam(const dq_synth_opts* opts, dq_synth_result* res) {
   for (int t = 0; t < g.o.nthreads; t++) th.emplace_back(work);
   for (auto& t : th) t.join();
   // concatenate
-  int64_t total = 28;
+  int64_t total = with_eof ? 28 : 0;
   for (auto& c : chunks) total += (int64_t)c.comp.size();
-  uint8_t* bam = (uint8_t*)malloc((size_t)total);
+  uint8_t* bam = (uint8_t*)malloc((size_t)std::max<int64_t>(1, total));
   if (!bam) return -5;
   int64_t off = 0;
   std::vector<int64_t> chunk_addr;
@@ -612,10 +629,12 @@ int dq_synth_bam(const dq_synth_opts* opts, dq_synth_result* res) {
   }
   static const uint8_t eof[28] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 0x42, 0x43,
                                   2,    0,    0x1b, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  memcpy(bam + off, eof, 28);
+  if (with_eof) {
+    memcpy(bam + off, eof, 28);
+    res->n_blocks += 1;
+  }
   res->bam = bam;
   res->bam_len = total;
-  res->n_blocks += 1;
   if (index) {
     std::vector<Rec> recs;
     std::vector<uint64_t> vs;

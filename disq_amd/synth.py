@@ -24,6 +24,8 @@ class _Opts(C.Structure):
         ("sbi_granularity", C.c_int64),
         ("records_per_chunk", C.c_int64),
         ("unplaced_fraction", C.c_double),
+        ("chunk_lo", C.c_int64),
+        ("chunk_hi", C.c_int64),
     ]
 
 
@@ -38,6 +40,7 @@ class _Res(C.Structure):
         ("n_records", C.c_int64),
         ("n_blocks", C.c_int64),
         ("record_bytes", C.c_int64),
+        ("n_chunks", C.c_int64),
     ]
 
 
@@ -51,6 +54,14 @@ def _L():
         _lib.dq_synth_bam.argtypes = [C.POINTER(_Opts), C.POINTER(_Res)]
         _lib.dq_synth_free.argtypes = [C.POINTER(_Res)]
     return _lib
+
+
+def chunk_count(n_records: int, shape: int = WGS, records_per_chunk: int = 0) -> int:
+    """Chunks of the logical file generate(n_records, ...) describes (synth_bam.cpp)."""
+    if shape == ANYSAM:
+        n_records = 2 * n_records + 2 if n_records > 0 else 0
+    per = records_per_chunk if records_per_chunk > 0 else (2000 if shape == LONGREAD else 20000)
+    return max(1, (n_records + per - 1) // per)
 
 
 @dataclass
@@ -76,14 +87,18 @@ class SynthBam:
 
 def generate(n_records: int, seed: int = 1, shape: int = WGS, level: int = 5, nthreads: int = 0,
              bai: bool = False, sbi_granularity: int = 0, records_per_chunk: int = 0,
-             unplaced_fraction: float = 0.005, as_buffer: bool = False):
+             unplaced_fraction: float = 0.005, as_buffer: bool = False,
+             chunks: tuple | None = None):
     """Generate a coordinate-sorted synthetic BAM.
 
     shape=ANYSAM follows T/AnySamTestUtil.java:37-105 with n_records = numPairs.
     as_buffer=True returns (ctypes address, length, free-callback) without copying (bench path).
+    chunks=(lo, hi) generates only chunks [lo, hi) of the logical file: the file's bytes starting
+    at the total length of chunks [0, lo) (see n_chunks / chunk_count()).
     """
+    lo, hi = chunks if chunks is not None else (0, 0)
     o = _Opts(n_records, seed, shape, level, nthreads or min(16, os.cpu_count() or 1), int(bai),
-              sbi_granularity, records_per_chunk, unplaced_fraction)
+              sbi_granularity, records_per_chunk, unplaced_fraction, lo, hi)
     r = _Res()
     rc = _L().dq_synth_bam(C.byref(o), C.byref(r))
     if rc != 0:

@@ -133,6 +133,9 @@ typedef struct dq_stats {
   double ms_crc;            /* CRC32 verification kernel */
   int64_t deflate_bytes;    /* compressed DEFLATE payload bytes (sum of BSIZE + 1 - 26) */
   int64_t n_filtered;       /* records kernel 4 kept (dq_run_resident with intervals), else -1 */
+  int64_t h2d_bytes;        /* compressed bytes the last open/decode copied host -> device */
+  int64_t owned_bytes;      /* decompressed bytes of the blocks starting inside the splits (the
+                               whole stream for a whole file; the shards of a file sum to it) */
 } dq_stats;
 
 int dq_ctx_create(dq_ctx** out, const dq_opts* opts);
@@ -155,6 +158,14 @@ int dq_open_path(dq_ctx* ctx, const char* path);
  * fails with DQ_EFORMAT "shard halo too small" (retry with more bytes). */
 int dq_open_shard(dq_ctx* ctx, const uint8_t* bytes, int64_t len, int64_t base, int64_t file_len,
                   int64_t p0, int64_t p1, const uint8_t* header, int64_t header_len);
+
+/* The same with the shard's bytes already in device memory (multi-GPU: a rank's own byte range
+ * stays resident in HBM and the halo arrives from the next rank over RCCL/xGMI).  dev_bytes is a
+ * caller-owned device pointer on this context's device with at least len + 4096 readable bytes,
+ * the last 4096 zero; it must stay valid and unchanged until the next open. */
+int dq_open_shard_device(dq_ctx* ctx, const void* dev_bytes, int64_t len, int64_t base,
+                         int64_t file_len, int64_t p0, int64_t p1, const uint8_t* header,
+                         int64_t header_len);
 
 /* The decompressed BAM header (AbstractSamSource.getFileHeader, D/impl/formats/sam/
  * AbstractSamSource.java:32-49) from the first `len` bytes of a file: enough BGZF blocks to hold
@@ -190,6 +201,16 @@ int dq_plan(dq_ctx* ctx, dq_chunk** chunks, int64_t* n);
 /* getIterator(span): the records of one chunk (start pointer < vend), in file order. */
 int dq_decode(dq_ctx* ctx, uint64_t vstart, uint64_t vend, int32_t with_raw, dq_batch** out);
 
+/* BamSource.getIterator(SamReader, SAMFileSpan) as a Spark task runs it (BamSource.java:172-175),
+ * with no resident file: reads from `path` only the compressed bytes of the chunk's blocks
+ * [vstart >> 16, first block past vend >> 16] plus what the last record needs (the window grows
+ * until that record is whole), inflates them and walks the records from the exact start pointer
+ * while start < vend.  The file's header is read once per context and path.  Afterwards the
+ * context holds no open file (dq_plan / dq_read need an open again).  stats.h2d_bytes
+ * (dq_get_stats) reports the compressed bytes copied to the device. */
+int dq_decode_chunk(dq_ctx* ctx, const char* path, uint64_t vstart, uint64_t vend, int32_t with_raw,
+                    dq_batch** out);
+
 /* createIndexIterator(intervals, contained=false) over one chunk, plus the unplaced-unmapped
  * tail when the chunk contains the .bai's start of the last linear bin. */
 int dq_decode_filtered(dq_ctx* ctx, uint64_t vstart, uint64_t vend, const dq_traversal* tr,
@@ -204,6 +225,14 @@ int dq_read(dq_ctx* ctx, const dq_traversal* tr, int32_t with_raw, dq_batch** ou
  * (overlap, contained=false; AbstractBinarySamSource.java:86-134) and stats.ms_filter /
  * stats.n_filtered report it; the kept-record list stays in HBM. */
 int dq_run_resident(dq_ctx* ctx, const dq_traversal* tr, dq_stats* stats);
+
+/* Stats of the last pipeline run (the ones dq_run_resident returns). */
+int dq_get_stats(dq_ctx* ctx, dq_stats* stats);
+
+/* Per-partition record counts and digests of the last pipeline run, in partition order (the
+ * shard's partitions p0..p1-1 for a shard): *n = number of partitions; up to cap entries written.
+ * The whole-file digest folds them. */
+int dq_partition_digests(dq_ctx* ctx, int64_t* counts, uint64_t* digests, int64_t cap, int64_t* n);
 
 /* Device pointer of the resident decompressed stream (for tests), and its length. */
 int dq_debug_inflated(dq_ctx* ctx, uint8_t* host_out, int64_t cap, int64_t* len);

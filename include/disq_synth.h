@@ -23,6 +23,14 @@ typedef struct dq_synth_opts {
   int64_t sbi_granularity;    /* 0 = no .sbi */
   int64_t records_per_chunk;  /* 0 = default */
   double unplaced_fraction;   /* trailing unplaced-unmapped records (WGS/LONGREAD) */
+  /* Byte range of one logical file (multi-GPU benchmark: each rank generates only its shard).
+   * The file is the concatenation of ceil(n_records / records_per_chunk) independently seeded
+   * chunks, each ending on a BGZF block boundary (chunk 0 starts with the header), then the EOF
+   * block.  chunk_hi > 0 generates chunks [chunk_lo, chunk_hi) only (plus the EOF block when
+   * chunk_hi is the last chunk); their bytes are the file's bytes at the offset equal to the
+   * total length of chunks [0, chunk_lo).  No .bai/.sbi in that mode. */
+  int64_t chunk_lo;
+  int64_t chunk_hi;
 } dq_synth_opts;
 
 typedef struct dq_synth_result {
@@ -35,6 +43,7 @@ typedef struct dq_synth_result {
   int64_t n_records;
   int64_t n_blocks;      /* including the EOF block */
   int64_t record_bytes;  /* decompressed bytes of records (excludes the header) */
+  int64_t n_chunks;      /* chunks of the whole logical file */
 } dq_synth_result;
 
 int dq_synth_bam(const dq_synth_opts* opts, dq_synth_result* res);

@@ -761,6 +761,126 @@ int dqo_bai_info(const uint8_t* b, int64_t len, int32_t* n_ref, int64_t* solb, i
   return 0;
 }
 
+/* .bai span of a list of optimized intervals, clipped to one partition chunk:
+ *   BAMFileReader.getFileSpan (H/BAMFileReader2.java:1004-1019) -> per interval htsjdk 2.16.0
+ *   CachingBAMFileIndex.getSpanOverlapping (bins from GenomicIndexUtil.regionToBins, their
+ *   chunks, Chunk.optimizeChunkList with LinearIndex.getMinimumOffset(start)), then
+ *   BAMFileSpan.merge (optimizeChunkList(all, 0)); then removeContentsBefore / removeContentsAfter
+ *   of the partition chunk (D/impl/formats/sam/AbstractBinarySamSource.java:105-107).
+ * htsjdk is not vendored (pom.xml:13), so this restates its published algorithm. */
+typedef struct { uint64_t b, e; } dchunk;
+static int dchunk_cmp(const void* x, const void* y) {
+  const dchunk* a = (const dchunk*)x;
+  const dchunk* c = (const dchunk*)y;
+  if (a->b != c->b) return a->b < c->b ? -1 : 1;
+  if (a->e != c->e) return a->e < c->e ? -1 : 1;
+  return 0;
+}
+/* Chunk.overlaps / isAdjacentTo (block-address adjacency) */
+static int dchunk_touch(const dchunk* l, const dchunk* r) {
+  if (l->b == r->b && l->e == r->e) return 1;
+  const dchunk* lo = dchunk_cmp(l, r) < 0 ? l : r;
+  const dchunk* hi = lo == l ? r : l;
+  if (lo->e > hi->b) return 1; /* overlap */
+  return (l->e >> 16) == (r->b >> 16) || (l->b >> 16) == (r->e >> 16);
+}
+/* Chunk.optimizeChunkList: sort, drop chunks ending at or before min_off, coalesce. */
+static int64_t optimize_chunks(dchunk* c, int64_t n, uint64_t min_off) {
+  qsort(c, (size_t)n, sizeof(dchunk), dchunk_cmp);
+  int64_t m = 0;
+  for (int64_t i = 0; i < n; i++) {
+    if (c[i].e <= min_off) continue;
+    if (m == 0 || !dchunk_touch(&c[m - 1], &c[i])) {
+      c[m++] = c[i];
+    } else if (c[i].e > c[m - 1].e) {
+      c[m - 1].e = c[i].e;
+    }
+  }
+  return m;
+}
+
+int64_t dqo_bai_span(const uint8_t* b, int64_t len, const int32_t* ref, const int32_t* start,
+                     const int32_t* end, int64_t n_iv, uint64_t vstart, uint64_t vend,
+                     uint64_t* out_beg, uint64_t* out_end, int64_t cap) {
+  if (len < 8 || memcmp(b, "BAI\1", 4) != 0) return DQO_EFORMAT;
+  const int32_t nr = rd32(b + 4);
+  /* offsets of each reference's section */
+  int64_t* refp = (int64_t*)malloc(sizeof(int64_t) * (size_t)(nr + 1));
+  int64_t p = 8;
+  for (int32_t i = 0; i < nr; i++) {
+    refp[i] = p;
+    if (p + 4 > len) { free(refp); return DQO_EFORMAT; }
+    const int32_t nbin = rd32(b + p);
+    p += 4;
+    for (int32_t j = 0; j < nbin; j++) {
+      if (p + 8 > len) { free(refp); return DQO_EFORMAT; }
+      p += 8 + 16 * (int64_t)rd32(b + p + 4);
+    }
+    if (p + 4 > len) { free(refp); return DQO_EFORMAT; }
+    p += 4 + 8 * (int64_t)rd32(b + p);
+  }
+  int64_t cap_all = 1024, n_all = 0;
+  dchunk* all = (dchunk*)malloc(sizeof(dchunk) * (size_t)cap_all);
+  for (int64_t k = 0; k < n_iv; k++) {
+    const int32_t r = ref[k];
+    if (r < 0 || r >= nr) continue;
+    /* GenomicIndexUtil.regionToBins(startPos, endPos) */
+    const int32_t maxp = 0x1FFFFFFF;
+    const int32_t s0 = start[k] <= 0 ? 0 : (start[k] - 1) & maxp;
+    const int32_t e0 = end[k] <= 0 ? maxp : (end[k] - 1) & maxp;
+    if (s0 > e0) continue;
+    int64_t q = refp[r];
+    const int32_t nbin = rd32(b + q);
+    q += 4;
+    int64_t cap_c = 64, n_c = 0;
+    dchunk* cl = (dchunk*)malloc(sizeof(dchunk) * (size_t)cap_c);
+    for (int32_t j = 0; j < nbin; j++) {
+      const uint32_t bin = (uint32_t)rd32(b + q);
+      const int32_t nch = rd32(b + q + 4);
+      const int64_t cq = q + 8;
+      q = cq + 16 * (int64_t)nch;
+      if (bin == 37450) continue; /* pseudo-bin (metadata) */
+      int in = bin == 0;
+      if (!in && bin >= 1 && bin <= 8) in = bin >= 1 + (uint32_t)(s0 >> 26) && bin <= 1 + (uint32_t)(e0 >> 26);
+      if (!in && bin >= 9 && bin <= 72) in = bin >= 9 + (uint32_t)(s0 >> 23) && bin <= 9 + (uint32_t)(e0 >> 23);
+      if (!in && bin >= 73 && bin <= 584) in = bin >= 73 + (uint32_t)(s0 >> 20) && bin <= 73 + (uint32_t)(e0 >> 20);
+      if (!in && bin >= 585 && bin <= 4680) in = bin >= 585 + (uint32_t)(s0 >> 17) && bin <= 585 + (uint32_t)(e0 >> 17);
+      if (!in && bin >= 4681) in = bin >= 4681 + (uint32_t)(s0 >> 14) && bin <= 4681 + (uint32_t)(e0 >> 14);
+      if (!in) continue;
+      for (int32_t c = 0; c < nch; c++) {
+        if (n_c == cap_c) { cap_c *= 2; cl = (dchunk*)realloc(cl, sizeof(dchunk) * (size_t)cap_c); }
+        cl[n_c].b = rd64(b + cq + 16 * (int64_t)c);
+        cl[n_c].e = rd64(b + cq + 16 * (int64_t)c + 8);
+        n_c++;
+      }
+    }
+    /* LinearIndex.getMinimumOffset(startPos) */
+    const int32_t nint = rd32(b + q);
+    const int32_t lb = s0 >> 14;
+    const uint64_t min_off = lb < nint ? rd64(b + q + 4 + 8 * (int64_t)lb) : 0;
+    n_c = optimize_chunks(cl, n_c, min_off);
+    for (int64_t c = 0; c < n_c; c++) {
+      if (n_all == cap_all) { cap_all *= 2; all = (dchunk*)realloc(all, sizeof(dchunk) * (size_t)cap_all); }
+      all[n_all++] = cl[c];
+    }
+    free(cl);
+  }
+  free(refp);
+  n_all = optimize_chunks(all, n_all, 0); /* BAMFileSpan.merge */
+  int64_t m = 0;
+  for (int64_t i = 0; i < n_all; i++) {
+    dchunk c = all[i];
+    if (c.e <= vstart) continue;          /* removeContentsBefore */
+    if (c.b < vstart) c.b = vstart;
+    if (c.b >= vend) continue;            /* removeContentsAfter */
+    if (c.e > vend) c.e = vend;
+    if (m < cap) { out_beg[m] = c.b; out_end[m] = c.e; }
+    m++;
+  }
+  free(all);
+  return m;
+}
+
 /* QueryInterval compareTo / overlaps / abuts and optimizeIntervals (htsjdk 2.16.0), called from
  * D/impl/formats/BoundedTraversalUtil.java:26.  end <= 0 means "to the end of the contig". */
 typedef struct { int32_t ref, start, end; } qiv;

@@ -103,6 +103,12 @@ int64_t dqo_read_all(dqo_file* f, dqo_rec* out, int64_t cap);
 int dqo_bai_info(const uint8_t* bai, int64_t len, int32_t* n_ref, int64_t* start_of_last_linear_bin,
                  int64_t* no_coordinate_count);
 
+/* .bai span of optimized intervals (getFileSpan) clipped to a partition chunk [vstart, vend)
+ * (AbstractBinarySamSource.java:105-107).  Returns the chunk count (up to cap written), or <0. */
+int64_t dqo_bai_span(const uint8_t* bai, int64_t len, const int32_t* ref, const int32_t* start,
+                     const int32_t* end, int64_t n_iv, uint64_t vstart, uint64_t vend,
+                     uint64_t* out_beg, uint64_t* out_end, int64_t cap);
+
 /* Interval preparation: QueryInterval.optimizeIntervals (htsjdk 2.16, via
  * BoundedTraversalUtil.java:10-27).  In-place on (ref, start, end) arrays; returns new count. */
 int64_t dqo_optimize_intervals(int32_t* ref, int32_t* start, int32_t* end, int64_t n);

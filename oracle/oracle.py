@@ -90,6 +90,9 @@ def lib():
         L.dqo_read_all.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
         L.dqo_bai_info.argtypes = [C.c_void_p, C.c_int64, P(C.c_int32), P(C.c_int64),
                                    P(C.c_int64)]
+        L.dqo_bai_span.restype = C.c_int64
+        L.dqo_bai_span.argtypes = [C.c_void_p, C.c_int64] + [P(C.c_int32)] * 3 + [
+            C.c_int64, C.c_uint64, C.c_uint64, P(C.c_uint64), P(C.c_uint64), C.c_int64]
         L.dqo_optimize_intervals.restype = C.c_int64
         L.dqo_optimize_intervals.argtypes = [P(C.c_int32)] * 3 + [C.c_int64]
         L.dqo_record_overlaps.argtypes = [C.c_void_p] + [P(C.c_int32)] * 3 + [C.c_int64]
@@ -252,11 +255,14 @@ class OracleBam:
         return out
 
     def read_partitions(self, split_size=0, nio=False, local_block_size=HADOOP_LOCAL_BLOCK_SIZE,
-                        traversal=None, bai=None):
+                        traversal=None, bai=None, spans=False):
         """Records per partition, as Disq's RDD would hold them.
 
         traversal: None, or (intervals, traverse_unplaced_unmapped) where intervals is None or
         a list of (ref_index, start, end) (1-based closed, already converted from contig names).
+        spans=True reads only the .bai span of the intervals clipped to each partition chunk
+        (AbstractBinarySamSource.java:102-112, as Disq does); False reads the whole chunk.  With a
+        complete index both select the same records.
         """
         if traversal is not None:
             ivs, unplaced = traversal
@@ -276,6 +282,9 @@ class OracleBam:
             if traversal is None:
                 parts.append(recs)
                 continue
+            if ivs and spans:
+                recs = np.concatenate([self.read_chunk(a, b) for a, b in bai_span(bai, q, *ch)]
+                                      or [recs[:0]])
             if ivs:
                 keep = np.array([overlaps(r, q) for r in recs], bool)
                 sel = recs[keep] if len(recs) else recs
@@ -359,6 +368,24 @@ def bai_info(bai_bytes):
     if rc != 0:
         raise OracleError("bad .bai")
     return solb.value, ncc.value
+
+
+def bai_span(bai_bytes, q, vstart, vend):
+    """getFileSpan(optimized intervals q) clipped to the partition chunk [vstart, vend):
+    [(begin, end)] virtual-offset chunks in file order (dqo_bai_span)."""
+    b = np.frombuffer(bai_bytes, np.uint8)
+    r = np.array([i[0] for i in q], np.int32)
+    s = np.array([i[1] for i in q], np.int32)
+    e = np.array([i[2] for i in q], np.int32)
+    args = (b.ctypes.data, len(b), _p(r, C.c_int32), _p(s, C.c_int32), _p(e, C.c_int32), len(q),
+            vstart, vend)
+    n = lib().dqo_bai_span(*args, None, None, 0)
+    if n < 0:
+        raise OracleError("bad .bai")
+    ob = np.zeros(max(1, n), np.uint64)
+    oe = np.zeros(max(1, n), np.uint64)
+    lib().dqo_bai_span(*args, _p(ob, C.c_uint64), _p(oe, C.c_uint64), n)
+    return list(zip(ob[:n].tolist(), oe[:n].tolist()))
 
 
 def optimize_intervals(ivs):

@@ -43,9 +43,27 @@ def test_unknown_format_rejected(tmp_path):
         HtsjdkReadsRddStorage.makeDefault().read(str(p))
 
 
-def test_structs_match_header_layout():
-    # dq_opts 32 bytes, dq_chunk 40, dq_traversal 40, dq_stats 120
-    assert ctypes.sizeof(_lib.DqOpts) == 32
-    assert ctypes.sizeof(_lib.DqChunk) == 40
-    assert ctypes.sizeof(_lib.DqTraversal) == 40
-    assert ctypes.sizeof(_lib.DqStats) == 120
+def test_structs_match_header_layout(tmp_path):
+    """ctypes mirrors of the C structs have the header's sizes and field offsets (gcc on the
+    header itself)."""
+    import subprocess
+    structs = {"dq_opts": _lib.DqOpts, "dq_chunk": _lib.DqChunk, "dq_batch": _lib.DqBatch,
+               "dq_traversal": _lib.DqTraversal, "dq_header_info": _lib.DqHeaderInfo,
+               "dq_stats": _lib.DqStats}
+    src = ["#include <stdio.h>", "#include <stddef.h>", '#include "disq_gpu.h"', "int main(void){"]
+    for name, cls in structs.items():
+        src.append(f'printf("{name} %zu\\n", sizeof({name}));')
+        for f, _ in cls._fields_:
+            src.append(f'printf("{name}.{f} %zu\\n", offsetof({name}, {f}));')
+    src.append("return 0;}")
+    c = tmp_path / "layout.c"
+    c.write_text("\n".join(src))
+    exe = tmp_path / "layout"
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+    subprocess.run(["gcc", "-I", inc, "-o", str(exe), str(c)], check=True)
+    got = dict(line.split() for line in subprocess.run([str(exe)], check=True, capture_output=True,
+                                                       text=True).stdout.splitlines())
+    for name, cls in structs.items():
+        assert int(got[name]) == ctypes.sizeof(cls), name
+        for f, _ in cls._fields_:
+            assert int(got[f"{name}.{f}"]) == getattr(cls, f).offset, (name, f)

@@ -151,15 +151,104 @@ def test_sharded_read_gloo(world, split, stitch, need, halo):
         assert max(r[4] for r in res) >= need   # the window grew to what the decoder demanded
 
 
-def test_halo_from_heads_spans_short_shards():
-    full = bytes(range(256)) * 40
-    shards = [P.Shard(0, 0, 1, 0, 1000), P.Shard(1, 0, 0, 0, 0), P.Shard(2, 1, 2, 1000, 1100),
-              P.Shard(3, 2, 3, 1100, 1500), P.Shard(4, 3, 4, 1500, len(full))]
-    halo = 600
-    heads = [full[s.lo:min(s.hi, s.lo + halo)] if not s.empty else b"" for s in shards]
-    assert P._halo_from_heads(heads, shards, 0, halo) == full[1000:1600]
-    assert P._halo_from_heads(heads, shards, 2, halo) == full[1100:1700]
-    assert P._halo_from_heads(heads, shards, 4, halo) == b""
+def test_even_offsets_plan_matches_first_byte_rule():
+    """shard_plan with even resident ranges = partition p to rank floor(start * world / len)."""
+    for n, split, world in [(597482, 40000, 3), (10 * 2 ** 30, 0, 8), (597482, 14146, 5)]:
+        sp = P.path_splits(n, split)
+        plan = P.shard_plan(n, world, split_size=split)
+        for s in plan:
+            for p in range(s.p0, s.p1):
+                assert min(world - 1, sp[p][0] * world // n) == s.rank
+
+
+def test_halo_transfers_cover_exactly_the_missing_bytes():
+    n, split = 10 * 2 ** 20, 1 << 20
+    offsets = [0, 3_000_000, 3_100_000, 3_150_000, 9_000_000, n]  # short middle ranges
+    plan = P.shard_plan(n, 5, offsets, split_size=split)
+    for halo in (4096, 300_000, 8 << 20):
+        tr = P.halo_transfers(plan, offsets, n, halo)
+        for r, s in enumerate(plan):
+            got = sorted((a, b) for q, d, a, b in tr if d == r)
+            if s.empty:
+                assert not got
+                continue
+            want_lo, want_hi = offsets[r + 1], min(n, s.hi + halo)
+            # contiguous pieces tiling [O_{r+1}, hi + halo), each from the rank that holds it
+            pos = want_lo
+            for a, b in got:
+                assert a == pos
+                pos = b
+            assert pos == max(want_lo, want_hi) or want_hi <= want_lo
+        for q, d, a, b in tr:
+            assert offsets[q] <= a < b <= offsets[q + 1] and q > d
+
+
+def _exchange_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        full = bytes((i * 7 + 3) % 251 for i in range(200_000))
+        n = len(full)
+        offsets = [0, 50_000, 52_000, 140_000, n]
+        plan = P.shard_plan(n, world, offsets, split_size=30_000)
+        own = torch.frombuffer(bytearray(full[offsets[rank]:offsets[rank + 1]]), dtype=torch.uint8)
+        got = P.exchange(own, offsets, plan, rank, 10_000, n)
+        s = plan[rank]
+        want = b"" if s.empty else full[offsets[rank + 1]:min(n, s.hi + 10_000)]
+        q.put((rank, bytes(got.numpy()) == want, len(want)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exchange_point_to_point_gloo():
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, _ in res), res
+    assert sum(n for _, _, n in res) > 0
+
+
+def _header_fail_worker(rank, world, port, q):
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        def bad(prefix):
+            raise ValueError("not a BAM")
+        try:
+            P.sharded_read(_bam1(), split_size=40000, header_reader=bad,
+                           decoder=_oracle_decoder(_bam1(), 40000))
+            q.put((rank, "no error"))
+        except Exception as e:  # noqa: BLE001
+            q.put((rank, f"{type(e).__name__}: {e}"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_header_failure_raises_on_every_rank():
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_header_fail_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+    assert res[0][1].startswith("ValueError")
+    assert all("not a BAM" in m for _, m in res), res
 
 
 # ---------------------------------------------------------------------------- GPU
@@ -274,3 +363,88 @@ def test_sharded_read_exchange_gpu(tmp_path, kind, split, halo):
         assert digest == st.digest and n == st.n_records
     if kind == "longread":
         assert max(r[3] for r in res) > halo   # the straddling long read forced a larger window
+
+
+def _check_shards_oracle(data, split, world, halo, device_bytes=False):
+    """Every shard decoded alone equals the oracle's partitions (Disq's RDD), field by field."""
+    import torch
+    from disq_amd import _lib
+    ob = O.OracleBam(data)
+    oplan = ob.plan(split)
+    parts = ob.read_partitions(split)
+    pidx = [i for i, (_, _, ch) in enumerate(oplan) if ch is not None]
+    want = dict(zip(pidx, parts))
+    with _lib.Context() as hc:
+        header = hc.header_from_prefix(data[:1 << 20])
+    dec = P.gpu_shard_decoder({"split_size": split}, device=0)
+    if device_bytes:  # the shard's bytes already in HBM (dq_open_shard_device)
+        host_dec = dec
+
+        def dec(d, base, file_len, shard, hdr, with_raw):  # noqa: F811
+            t = torch.zeros(len(d) + 4096, dtype=torch.uint8, device="cuda:0")
+            t[:len(d)] = torch.frombuffer(bytearray(d), dtype=torch.uint8).to("cuda:0")
+            torch.cuda.synchronize()
+            return host_dec((t.data_ptr(), len(d)), base, file_len, shard, hdr, with_raw)
+    digests = []
+    for s in P.shard_plan(len(data), world, split_size=split):
+        r = P.read_shard(lambda a, b: data[a:b], len(data), s, header, dec, halo=halo,
+                         with_raw=False)
+        digests += r.digests
+        for k, p in enumerate(r.part_index):
+            lo, hi = int(r.batch["part_offset"][k]), int(r.batch["part_offset"][k + 1])
+            assert hi - lo == len(want[p]), (s.rank, p)
+            for f in FIELDS:
+                assert np.array_equal(r.batch[f][lo:hi], want[p][f]), (s.rank, p, f)
+        assert sorted(r.part_index) == [p for p in pidx if s.p0 <= p < s.p1]
+    assert P.fold_digest(digests) == P.fold_digest(
+        [O.stream_digest(want[p]["hash"]) if p in want else 0 for p in range(len(oplan))])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [4, 8])
+def test_wgs_shards_equal_oracle(world):
+    """configs[2] shape (30x-WGS-like pairs with an unplaced-unmapped tail), byte-range sharded:
+    each shard's records equal the oracle's partitions."""
+    from disq_amd import synth
+    r = synth.generate(200000, seed=17, nthreads=8, unplaced_fraction=0.005)
+    _check_shards_oracle(r.bam, 1 << 20, world, halo=64 * 1024, device_bytes=(world == 8))
+
+
+def _nccl_worker(path, split, q):
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0,
+                            world_size=1)
+    try:
+        data = open(path, "rb").read()
+        n = len(data)
+        offsets = [0, n]
+        plan = P.shard_plan(n, 1, offsets, split_size=split)
+        from disq_amd import _lib
+        with _lib.Context() as c:
+            header = c.header_from_prefix(data[:1 << 20])
+        dec = P.gpu_shard_decoder({"split_size": split}, device=0)
+        r = P.read_shard_exchange(data, offsets, n, plan, 0, header, dec, halo=4096,
+                                  device=0)
+        q.put((P.fold_digest(r.digests), sum(r.counts)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_exchange_path_on_nccl_world1(tmp_path):
+    """The RCCL (nccl) branch at world size 1: resident shard in HBM, in-place device decode
+    (dq_open_shard_device), status all_reduce over RCCL."""
+    data = _bam1()
+    path = tmp_path / "in.bam"
+    path.write_bytes(data)
+    _, st = _gpu_whole(data, 40000)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_worker, args=(str(path), 40000, q))
+    p.start()
+    digest, n = q.get(timeout=100)
+    p.join(60)
+    assert p.exitcode == 0
+    assert digest == st.digest and n == st.n_records
