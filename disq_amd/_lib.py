@@ -18,7 +18,8 @@ DQ_OK, DQ_EIO, DQ_EFORMAT, DQ_EINVAL, DQ_EDEVICE, DQ_ENOMEM = 0, -1, -2, -3, -4,
 
 class DqOpts(C.Structure):
     _fields_ = [("device", C.c_int32), ("split_size", C.c_int32), ("use_nio", C.c_int32),
-                ("verify_crc", C.c_int32), ("stringency", C.c_int32), ("reserved", C.c_int32),
+                ("verify_crc", C.c_int32), ("stringency", C.c_int32),
+                ("full_traversal", C.c_int32),
                 ("hadoop_block_size", C.c_int64)]
 
 
@@ -69,7 +70,8 @@ class DqStats(C.Structure):
                 ("ms_records", C.c_double), ("ms_filter", C.c_double), ("ms_plan", C.c_double),
                 ("digest", C.c_uint64), ("ms_crc", C.c_double), ("deflate_bytes", C.c_int64),
                 ("n_filtered", C.c_int64), ("h2d_bytes", C.c_int64),
-                ("owned_bytes", C.c_int64)]
+                ("owned_bytes", C.c_int64), ("blocks_inflated", C.c_int64),
+                ("ms_span", C.c_double)]
 
 
 # Every symbol include/disq_gpu.h declares.
@@ -174,10 +176,10 @@ class Context:
     """One dq_ctx (own HIP stream) with a resident BAM."""
 
     def __init__(self, split_size=0, use_nio=False, verify_crc=False, device=0,
-                 hadoop_block_size=0, stringency=0):
+                 hadoop_block_size=0, stringency=0, full_traversal=False):
         self._h = C.c_void_p()
-        o = DqOpts(device, split_size, int(use_nio), int(verify_crc), stringency, 0,
-                   hadoop_block_size)
+        o = DqOpts(device, split_size, int(use_nio), int(verify_crc), stringency,
+                   int(full_traversal), hadoop_block_size)
         rc = lib().dq_ctx_create(C.byref(self._h), C.byref(o))
         if rc != DQ_OK:
             msg = lib().dq_last_error(self._h).decode() if self._h else ""

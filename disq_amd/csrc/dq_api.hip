@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/disq_gpu.h"
@@ -50,6 +51,21 @@ struct DevBuf {
 
 struct Interval {
   int32_t ref, start, end;
+};
+
+// A .bai (SAMv1 section 5.2) as htsjdk's index reads it: per reference its bins' chunks (the
+// 37450 pseudo-bin left out) and its 16 kbp linear index.
+struct VChunk {
+  uint64_t b, e;
+};
+struct BaiRef {
+  std::vector<uint32_t> bin;
+  std::vector<std::vector<VChunk>> chunks;  // per bin, in file order
+  std::vector<uint64_t> linear;
+};
+struct Bai {
+  std::vector<BaiRef> refs;
+  int64_t solb = -1, ncc = -1;
 };
 
 }  // namespace
@@ -116,6 +132,15 @@ struct dq_ctx {
   // index
   bool have_bai = false;
   int64_t solb = -1, ncc = -1;
+  Bai bai;
+  // partition plans of the open file (file coordinates) from its last full run: a sparse
+  // interval run (run_span) reuses them instead of guessing again
+  std::vector<SplitPlan> plan_cache;
+  bool plan_cached = false;
+  // sparse (.bai span) runs
+  DevBuf sel, wins, span_c, span_r, span_idx, span_kept, span_keep32, span_off;
+  int64_t span_extra_blocks = 4;  // blocks inflated past a window's last chunk (grows x4)
+  bool span_parts_valid = false;  // parts_h holds a span run's per-partition kept counts
   // filter scratch
   DevBuf iv_ref, iv_start, iv_end, iv_begin, idx, keep;
   int64_t iota_n = -1;  // idx holds 0..iota_n-1 (dq_run_resident's interval filter)
@@ -273,32 +298,118 @@ int parse_header(dq_ctx* ctx) {
 
 // htsjdk AbstractBAMFileIndex.getStartOfLastLinearBin / getNoCoordinateCount (2.16.0; read at
 // D/impl/formats/sam/AbstractBinarySamSource.java:93-94).
-int parse_bai(const uint8_t* b, int64_t len, int64_t* solb, int64_t* ncc) {
+int parse_bai(const uint8_t* b, int64_t len, Bai& out) {
   int64_t p = 8;
   if (len < 8 || memcmp(b, "BAI\1", 4) != 0) return DQ_EFORMAT;
-  int32_t nr = rd32(b + 4);
+  const int32_t nr = rd32(b + 4);
+  if (nr < 0) return DQ_EFORMAT;
+  Bai x;
+  x.refs.resize((size_t)nr);
   int64_t last = -1;
   for (int32_t i = 0; i < nr; i++) {
+    BaiRef& R = x.refs[(size_t)i];
     if (p + 4 > len) return DQ_EFORMAT;
-    int32_t nbin = rd32(b + p);
+    const int32_t nbin = rd32(b + p);
     p += 4;
     for (int32_t j = 0; j < nbin; j++) {
       if (p + 8 > len) return DQ_EFORMAT;
-      int32_t nch = rd32(b + p + 4);
-      p += 8 + 16 * (int64_t)nch;
+      const uint32_t bin = (uint32_t)rd32(b + p);
+      const int32_t nch = rd32(b + p + 4);
+      p += 8;
+      if (nch < 0 || p + 16 * (int64_t)nch > len) return DQ_EFORMAT;
+      if (bin != 37450) {  // the pseudo-bin holds metadata, not chunks
+        R.bin.push_back(bin);
+        std::vector<VChunk> c((size_t)nch);
+        for (int32_t k = 0; k < nch; k++) c[(size_t)k] = {rd64(b + p + 16 * k), rd64(b + p + 16 * k + 8)};
+        R.chunks.push_back(std::move(c));
+      }
+      p += 16 * (int64_t)nch;
     }
     if (p + 4 > len) return DQ_EFORMAT;
-    int32_t nint = rd32(b + p);
+    const int32_t nint = rd32(b + p);
     p += 4;
-    if (nint > 0) {
-      if (p + 8 * (int64_t)nint > len) return DQ_EFORMAT;
-      last = (int64_t)rd64(b + p + 8 * ((int64_t)nint - 1));
-      p += 8 * (int64_t)nint;
-    }
+    if (nint < 0 || p + 8 * (int64_t)nint > len) return DQ_EFORMAT;
+    R.linear.resize((size_t)nint);
+    for (int32_t k = 0; k < nint; k++) R.linear[(size_t)k] = rd64(b + p + 8 * k);
+    if (nint > 0) last = (int64_t)R.linear.back();
+    p += 8 * (int64_t)nint;
   }
-  *solb = last;
-  *ncc = p + 8 <= len ? (int64_t)rd64(b + p) : -1;
+  // htsjdk AbstractBAMFileIndex.getStartOfLastLinearBin / getNoCoordinateCount (2.16.0; read at
+  // D/impl/formats/sam/AbstractBinarySamSource.java:93-94)
+  x.solb = last;
+  x.ncc = p + 8 <= len ? (int64_t)rd64(b + p) : -1;
+  out = std::move(x);
   return 0;
+}
+
+// Chunk.optimizeChunkList (htsjdk 2.16.0): sort; drop chunks ending at or before min_off (linear
+// index); coalesce chunks that overlap or share a BGZF block (Chunk.overlaps / isAdjacentTo).
+void optimize_chunks(std::vector<VChunk>& c, uint64_t min_off) {
+  std::sort(c.begin(), c.end(), [](const VChunk& x, const VChunk& y) {
+    return x.b != y.b ? x.b < y.b : x.e < y.e;
+  });
+  std::vector<VChunk> out;
+  for (const VChunk& k : c) {
+    if (k.e <= min_off) continue;
+    if (!out.empty()) {
+      VChunk& l = out.back();
+      const bool touch = (l.b == k.b && l.e == k.e) || l.e > k.b || (l.e >> 16) == (k.b >> 16) ||
+                         (l.b >> 16) == (k.e >> 16);
+      if (touch) {
+        if (k.e > l.e) l.e = k.e;
+        continue;
+      }
+    }
+    out.push_back(k);
+  }
+  c.swap(out);
+}
+
+// BAMFileReader.getFileSpan (H/BAMFileReader2.java:1004-1019): per optimized interval
+// getSpanOverlapping (bins from GenomicIndexUtil.regionToBins, their chunks, optimized against
+// LinearIndex.getMinimumOffset(start)), then BAMFileSpan.merge.
+std::vector<VChunk> file_span(const Bai& bai, const std::vector<Interval>& q) {
+  std::vector<VChunk> all;
+  for (const Interval& iv : q) {
+    if (iv.ref < 0 || iv.ref >= (int32_t)bai.refs.size()) continue;
+    const BaiRef& R = bai.refs[(size_t)iv.ref];
+    const int32_t maxp = 0x1FFFFFFF;
+    const int32_t s0 = iv.start <= 0 ? 0 : (iv.start - 1) & maxp;
+    const int32_t e0 = iv.end <= 0 ? maxp : (iv.end - 1) & maxp;
+    if (s0 > e0) continue;
+    auto in_bins = [&](uint32_t bin) {
+      if (bin == 0) return true;
+      const int lvl_first[5] = {1, 9, 73, 585, 4681}, lvl_last[5] = {8, 72, 584, 4680, 37449},
+                shift[5] = {26, 23, 20, 17, 14};
+      for (int l = 0; l < 5; l++)
+        if ((int)bin >= lvl_first[l] && (int)bin <= lvl_last[l])
+          return bin >= (uint32_t)(lvl_first[l] + (s0 >> shift[l])) &&
+                 bin <= (uint32_t)(lvl_first[l] + (e0 >> shift[l]));
+      return false;
+    };
+    std::vector<VChunk> c;
+    for (size_t j = 0; j < R.bin.size(); j++)
+      if (in_bins(R.bin[j])) c.insert(c.end(), R.chunks[j].begin(), R.chunks[j].end());
+    const size_t lb = (size_t)(s0 >> 14);
+    optimize_chunks(c, lb < R.linear.size() ? R.linear[lb] : 0);
+    all.insert(all.end(), c.begin(), c.end());
+  }
+  optimize_chunks(all, 0);
+  return all;
+}
+
+// BAMFileSpan.removeContentsBefore / removeContentsAfter of one partition chunk
+// (D/impl/formats/sam/AbstractBinarySamSource.java:106-107).
+std::vector<VChunk> clip_span(const std::vector<VChunk>& span, uint64_t vs, uint64_t ve) {
+  std::vector<VChunk> out;
+  for (VChunk c : span) {
+    if (c.e <= vs) continue;
+    if (c.b < vs) c.b = vs;
+    if (c.b >= ve) continue;
+    if (c.e > ve) c.e = ve;
+    out.push_back(c);
+  }
+  return out;
 }
 
 // QueryInterval.optimizeIntervals (htsjdk 2.16.0, BoundedTraversalUtil.java:26): sort, then
@@ -355,6 +466,7 @@ float ev_ms(hipEvent_t a, hipEvent_t b) {
 static int run_pipeline(dq_ctx* ctx) {
   if (!ctx->have_file) RET(DQ_EINVAL, "no file open");
   if (ctx->have_pipeline) return 0;
+  ctx->span_parts_valid = false;
   hipStream_t s = ctx->s;
   const int64_t L = ctx->flen;
   int rc;
@@ -711,7 +823,12 @@ static int run_pipeline(dq_ctx* ctx) {
   S.ms_records = ev_ms(ctx->ev[3], ctx->ev[4]);
   S.ms_total = ev_ms(ctx->ev[0], ctx->ev[4]);
   S.h2d_bytes = ctx->h2d_bytes;
+  S.blocks_inflated = nblk;
   ctx->have_pipeline = true;
+  if (!ctx->chunk_mode && !ctx->index_only) {
+    ctx->plan_cache = ctx->plans_h;
+    ctx->plan_cached = true;
+  }
   ctx->voff_h.clear();
   return 0;
 }
@@ -722,6 +839,57 @@ static int fetch_index(dq_ctx* ctx) {
   ctx->voff_h.resize((size_t)ctx->nrec);
   if (ctx->nrec)
     HIPCHK(hipMemcpy(ctx->voff_h.data(), ctx->f_voff.p, 8 * (size_t)ctx->nrec, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+// Two pinned staging buffers (file reads in, record batches out).
+constexpr size_t PIN_PIECE = 32u << 20;
+static int ensure_pinned(dq_ctx* ctx) {
+  if (ctx->pin_cap >= PIN_PIECE) return 0;
+  for (int k = 0; k < 2; k++) {
+    if (ctx->pin[k]) (void)hipHostFree(ctx->pin[k]);
+    ctx->pin[k] = nullptr;
+    HIPCHK(hipHostMalloc((void**)&ctx->pin[k], PIN_PIECE, hipHostMallocDefault));
+    if (!ctx->pin_ev[k]) HIPCHK(hipEventCreateWithFlags(&ctx->pin_ev[k], hipEventDisableTiming));
+  }
+  ctx->pin_cap = PIN_PIECE;
+  return 0;
+}
+
+// Device -> pageable host copy of n bytes: pieces land in the two pinned buffers in turn while
+// host threads move the previous piece out (a plain hipMemcpy into pageable memory stages through
+// one runtime buffer on one thread).
+static int d2h_large(dq_ctx* ctx, void* dst, const void* src, size_t n) {
+  if (n < (8u << 20)) {
+    HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, ctx->s));
+    HIPCHK(hipStreamSynchronize(ctx->s));
+    return 0;
+  }
+  int rc;
+  if ((rc = ensure_pinned(ctx))) return rc;
+  const size_t np = (n + PIN_PIECE - 1) / PIN_PIECE;
+  auto issue = [&](size_t i) -> hipError_t {
+    const size_t off = i * PIN_PIECE, len = std::min(PIN_PIECE, n - off);
+    hipError_t e = hipMemcpyAsync(ctx->pin[i & 1], (const uint8_t*)src + off, len,
+                                  hipMemcpyDeviceToHost, ctx->s);
+    if (e == hipSuccess) e = hipEventRecord(ctx->pin_ev[i & 1], ctx->s);
+    return e;
+  };
+  HIPCHK(issue(0));
+  for (size_t i = 0; i < np; i++) {
+    HIPCHK(hipEventSynchronize(ctx->pin_ev[i & 1]));
+    if (i + 1 < np) HIPCHK(issue(i + 1));  // the other buffer is free: its piece was moved out
+    const size_t off = i * PIN_PIECE, len = std::min(PIN_PIECE, n - off);
+    constexpr int T = 4;
+    std::thread th[T];
+    const size_t part = (len + T - 1) / T;
+    for (int t = 0; t < T; t++)
+      th[t] = std::thread([&, t] {
+        const size_t a = std::min(len, (size_t)t * part), b = std::min(len, a + part);
+        if (b > a) memcpy((uint8_t*)dst + off + a, ctx->pin[i & 1] + a, b - a);
+      });
+    for (auto& x : th) x.join();
+  }
   return 0;
 }
 
@@ -836,24 +1004,16 @@ static int make_batch(dq_ctx* ctx, const std::vector<std::pair<int64_t, int64_t>
   }
   if (n > 0) {
     auto d2h = [&](const void* dbase, size_t esz, void* dst) {
-      return hipMemcpyAsync(dst, (const char*)dbase + (size_t)first * esz, (size_t)n * esz,
-                            hipMemcpyDeviceToHost, s);
+      return d2h_large(ctx, dst, (const char*)dbase + (size_t)first * esz, (size_t)n * esz);
     };
-    XCHK(d2h(rows.voffset, 8, b->voffset));
-    XCHK(d2h(rows.block_size, 4, b->block_size));
-    XCHK(d2h(rows.ref_id, 4, b->ref_id));
-    XCHK(d2h(rows.pos, 4, b->pos));
-    XCHK(d2h(rows.l_seq, 4, b->l_seq));
-    XCHK(d2h(rows.next_ref_id, 4, b->next_ref_id));
-    XCHK(d2h(rows.next_pos, 4, b->next_pos));
-    XCHK(d2h(rows.tlen, 4, b->tlen));
-    XCHK(d2h(rows.flag, 2, b->flag));
-    XCHK(d2h(rows.bin, 2, b->bin));
-    XCHK(d2h(rows.n_cigar, 2, b->n_cigar));
-    XCHK(d2h(rows.mapq, 1, b->mapq));
-    XCHK(d2h(rows.l_read_name, 1, b->l_read_name));
-    XCHK(d2h(rows.hash, 8, b->hash));
-    XCHK(hipStreamSynchronize(s));
+    if ((rc = d2h(rows.voffset, 8, b->voffset)) || (rc = d2h(rows.block_size, 4, b->block_size)) ||
+        (rc = d2h(rows.ref_id, 4, b->ref_id)) || (rc = d2h(rows.pos, 4, b->pos)) ||
+        (rc = d2h(rows.l_seq, 4, b->l_seq)) || (rc = d2h(rows.next_ref_id, 4, b->next_ref_id)) ||
+        (rc = d2h(rows.next_pos, 4, b->next_pos)) || (rc = d2h(rows.tlen, 4, b->tlen)) ||
+        (rc = d2h(rows.flag, 2, b->flag)) || (rc = d2h(rows.bin, 2, b->bin)) ||
+        (rc = d2h(rows.n_cigar, 2, b->n_cigar)) || (rc = d2h(rows.mapq, 1, b->mapq)) ||
+        (rc = d2h(rows.l_read_name, 1, b->l_read_name)) || (rc = d2h(rows.hash, 8, b->hash)))
+      return fail(rc);
   }
   if (ctx->base)
     for (int64_t i = 0; i < n; i++) b->voffset[i] += (uint64_t)ctx->base << 16;
@@ -869,7 +1029,7 @@ static int make_batch(dq_ctx* ctx, const std::vector<std::pair<int64_t, int64_t>
     if (direct) {  // consecutive chain records are contiguous in U
       int64_t lo = 0;
       XCHK(hipMemcpy(&lo, ctx->rec_lin.as<int64_t>() + first, 8, hipMemcpyDeviceToHost));
-      XCHK(hipMemcpy(b->raw, ctx->U.as<uint8_t>() + lo, (size_t)raw_len, hipMemcpyDeviceToHost));
+      if ((rc = d2h_large(ctx, b->raw, ctx->U.as<uint8_t>() + lo, (size_t)raw_len))) return fail(rc);
     } else {
       if ((rc = ensure_all(ctx, ctx->x_off, 8 * (size_t)n)) ||
           (rc = ensure_all(ctx, ctx->x_raw, (size_t)raw_len)))
@@ -877,8 +1037,7 @@ static int make_batch(dq_ctx* ctx, const std::vector<std::pair<int64_t, int64_t>
       XCHK(hipMemcpyAsync(ctx->x_off.p, b->raw_offset, 8 * (size_t)n, hipMemcpyHostToDevice, s));
       launch_gather_raw(ctx->U.as<uint8_t>(), ctx->rec_lin.as<int64_t>(), ctx->f_bs.as<int32_t>(),
                         d_idx, 0, n, ctx->x_off.as<int64_t>(), ctx->x_raw.as<uint8_t>(), s);
-      XCHK(hipMemcpyAsync(b->raw, ctx->x_raw.p, (size_t)raw_len, hipMemcpyDeviceToHost, s));
-      XCHK(hipStreamSynchronize(s));
+      if ((rc = d2h_large(ctx, b->raw, ctx->x_raw.p, (size_t)raw_len))) return fail(rc);
     }
   }
 #undef XCHK
@@ -996,8 +1155,282 @@ static int filtered_indices(dq_ctx* ctx, uint64_t vstart, uint64_t vend, int64_t
   return 0;
 }
 
+// ------------------------------------------------------------------ .bai span runs
+// The interval traversal of every partition as Disq runs it (AbstractBinarySamSource.java:86-112):
+// the .bai span of the optimized intervals (getFileSpan), clipped to each partition chunk, is all
+// that is read.  Only the BGZF blocks of those spans are inflated (plus a few after each span to
+// finish its last record), in the whole-file U layout; records are walked from every span start
+// (windowed chains), selected per span chunk (BAMFileIndexIterator over the chunk list) and
+// filtered by kernel 4.  The partition plans come from the last full run of the open file.
+// Results: per-partition kept counts and digests (dq_partition_digests), stats.
+static int run_span(dq_ctx* ctx, const dq_traversal* tr, dq_stats* out) {
+  hipStream_t s = ctx->s;
+  int rc;
+  if (!ctx->plan_cached || !ctx->have_bai) RET(DQ_EINVAL, "span run needs a planned file and a .bai");
+  const int64_t nblk = ctx->nblk;
+  const uint64_t vb = (uint64_t)ctx->base << 16;  // shard coordinates <-> file coordinates
+  // 1. the span of the optimized intervals, clipped to every partition chunk (shard coordinates)
+  std::vector<Interval> iv;
+  for (int64_t i = 0; i < tr->n; i++) {
+    if (tr->ref[i] < 0 || tr->ref[i] >= ctx->n_ref) RET(DQ_EINVAL, "Invalid reference index");
+    iv.push_back({tr->ref[i], tr->start[i], tr->end[i]});
+  }
+  const std::vector<Interval> q = optimize(iv);
+  const std::vector<VChunk> span = file_span(ctx->bai, q);
+  const std::vector<SplitPlan>& plans = ctx->plan_cache;
+  const int64_t nsplit = (int64_t)plans.size();
+  std::vector<uint64_t> cb, ce;            // span chunks, partition order
+  std::vector<int64_t> part_first((size_t)nsplit + 1, 0);
+  for (int64_t i = 0; i < nsplit; i++) {
+    part_first[(size_t)i] = (int64_t)cb.size();
+    const SplitPlan& P = plans[(size_t)i];
+    if (P.rec_lin < 0) continue;
+    for (const VChunk& c : clip_span(span, P.vstart + vb, P.vend + vb)) {
+      if (c.b < vb) continue;
+      cb.push_back(c.b - vb);
+      ce.push_back(c.e - vb);
+    }
+  }
+  part_first[(size_t)nsplit] = (int64_t)cb.size();
+  const int64_t nchunk = (int64_t)cb.size();
+  // block table of the open file (from its full run)
+  std::vector<int64_t> bp((size_t)nblk), uo((size_t)nblk + 1);
+  if (nblk) {
+    HIPCHK(hipMemcpyAsync(bp.data(), ctx->blk_pos.p, 8 * (size_t)nblk, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(uo.data(), ctx->uoff.p, 8 * (size_t)(nblk + 1), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+  }
+  const bool is_eof = !ctx->shard || ctx->base + ctx->flen >= ctx->file_len;
+  // 2. windows over the union of the chunks: [block of the start, block after the end's block +
+  //    extra), neighbours closer than GAP blocks merged
+  struct W { int64_t j0, jc, j1; uint64_t v0; };
+  constexpr int64_t GAP = 16;
+  int64_t extra = ctx->span_extra_blocks;
+  std::vector<uint64_t> ub(cb), ue(ce);
+  {
+    std::vector<size_t> ord(cb.size());
+    for (size_t k = 0; k < ord.size(); k++) ord[k] = k;
+    std::sort(ord.begin(), ord.end(), [&](size_t x, size_t y) { return cb[x] < cb[y]; });
+    for (size_t k = 0; k < ord.size(); k++) {
+      ub[k] = cb[ord[k]];
+      ue[k] = ce[ord[k]];
+    }
+  }
+  for (;;) {
+    std::vector<W> win;
+    for (size_t k = 0; k < ub.size(); k++) {
+      const int64_t a = (int64_t)(ub[k] >> 16), e = (int64_t)(ue[k] >> 16);
+      const int64_t j0 = std::lower_bound(bp.begin(), bp.end(), a) - bp.begin();
+      if (j0 >= nblk || bp[(size_t)j0] != a) RET(DQ_EFORMAT, ".bai chunk does not start at a BGZF block");
+      const int64_t jc = std::upper_bound(bp.begin(), bp.end(), e) - bp.begin();
+      const int64_t j1 = std::min(nblk, jc + extra);
+      if (!win.empty() && j0 <= win.back().j1 + GAP) {
+        W& w = win.back();
+        w.jc = std::max(w.jc, jc);
+        w.j1 = std::max(w.j1, j1);
+      } else {
+        win.push_back({j0, jc, j1, ub[k]});
+      }
+    }
+    // 3. sparse inflate of the windows' blocks
+    std::vector<int32_t> sel;
+    for (const W& w : win)
+      for (int64_t j = std::max<int64_t>(w.j0, sel.empty() ? 0 : sel.back() + 1); j < w.j1; j++)
+        sel.push_back((int32_t)j);
+    const int64_t nsel = (int64_t)sel.size();
+    HIPCHK(hipEventRecord(ctx->ev[5], s));
+    if (nsel) {
+      if ((rc = ensure_all(ctx, ctx->sel, 4 * (size_t)nsel))) return rc;
+      HIPCHK(hipMemcpyAsync(ctx->sel.p, sel.data(), 4 * (size_t)nsel, hipMemcpyHostToDevice, s));
+      HIPCHK(hipMemsetAsync(ctx->status.p, 0, sizeof(int32_t) * (size_t)(nblk + 1), s));
+      const uint32_t* crc_init = inflate3_tables(ctx->o.device);
+      if (!crc_init) RET(DQ_EDEVICE, "CRC32 table initialisation failed on this device");
+      launch_inflate3(ctx->cbuf(), ctx->blk_pos.as<int64_t>(), ctx->blk_cs.as<int32_t>(),
+                      ctx->blk_us.as<int32_t>(), ctx->uoff.as<int64_t>(), nblk, ctx->U.as<uint8_t>(),
+                      ctx->status.as<int32_t>(), ctx->o.verify_crc, crc_init, nullptr, s,
+                      ctx->sel.as<int32_t>(), nsel);
+    }
+    HIPCHK(hipEventRecord(ctx->ev[6], s));
+    {
+      std::vector<int32_t> st((size_t)nblk);
+      if (nblk) HIPCHK(hipMemcpyAsync(st.data(), ctx->status.p, 4 * (size_t)nblk, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      for (int32_t j : sel)
+        if (st[(size_t)j] != ST_OK) {
+          char msg[256];
+          snprintf(msg, sizeof msg, "%s in BGZF block at %lld", status_name(st[(size_t)j]),
+                   (long long)(bp[(size_t)j] + ctx->base));
+          RET(DQ_EFORMAT, msg);
+        }
+    }
+    // 4. windowed record chains
+    const int64_t SEG = 64 * 1024;
+    std::vector<Win> wv;
+    int64_t nseg = 0;
+    for (const W& w : win) {
+      Win x;
+      x.u_start = uo[(size_t)w.j0] + (int64_t)(w.v0 & 0xffff);
+      x.u_chain_end = uo[(size_t)w.jc];
+      x.u_limit = uo[(size_t)w.j1];
+      x.at_eof = (w.j1 == nblk && is_eof) ? 1 : 0;
+      x.pad = 0;
+      x.seg0 = nseg;
+      if (x.u_chain_end <= x.u_start) x.u_chain_end = x.u_start + 1;
+      nseg += (x.u_chain_end - x.u_start + SEG - 1) / SEG;
+      wv.push_back(x);
+    }
+    const int64_t nwin = (int64_t)wv.size();
+    int64_t nrec = 0;
+    int32_t* d_broken = ctx->scal.as<int32_t>() + 1;
+    int32_t* d_stat = ctx->scal.as<int32_t>() + 2;
+    if (nseg > 0) {
+      if ((rc = ensure_all(ctx, ctx->wins, sizeof(Win) * (size_t)nwin)) ||
+          (rc = ensure_all(ctx, ctx->segs, sizeof(Seg) * (size_t)(nseg + 1))) ||
+          (rc = ensure_all(ctx, ctx->segcnt, sizeof(int64_t) * (size_t)(nseg + 1))) ||
+          (rc = ensure_all(ctx, ctx->segbase, sizeof(int64_t) * (size_t)(nseg + 1))))
+        return rc;
+      HIPCHK(hipMemcpyAsync(ctx->wins.p, wv.data(), sizeof(Win) * (size_t)nwin, hipMemcpyHostToDevice, s));
+      HIPCHK(hipMemsetAsync(ctx->scal.p, 0, 64, s));
+      launch_wseg(ctx->U.as<uint8_t>(), ctx->d_ref_len.as<int32_t>(), ctx->n_ref, ctx->wins.as<Win>(),
+                  nwin, ctx->segs.as<Seg>(), nseg, SEG, d_broken, s);
+      int32_t br = 0;
+      HIPCHK(hipMemcpyAsync(&br, d_broken, 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      int32_t st = 0;
+      if (br) {
+        launch_wseg_fix(ctx->U.as<uint8_t>(), ctx->segs.as<Seg>(), ctx->wins.as<Win>(), nwin, nseg,
+                        SEG, d_stat, s);
+        HIPCHK(hipMemcpyAsync(&st, d_stat, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+      }
+      if (st == 4) {  // a window's last record runs past its blocks: more blocks, again
+        if (extra >= nblk) RET(DQ_EFORMAT, "truncated record chain");
+        extra *= 4;
+        ctx->span_extra_blocks = extra;
+        continue;
+      }
+      if (st) RET(DQ_EFORMAT, st == ST_BAD_CODE ? "Invalid record length" : "truncated record chain");
+      launch_seg_counts(ctx->segs.as<Seg>(), nseg, ctx->segcnt.as<int64_t>(), s);
+      launch_exclusive_scan_i64(ctx->segcnt.as<int64_t>(), ctx->segbase.as<int64_t>(), nseg,
+                                ctx->tmp.as<int64_t>(), s);
+      if ((rc = get_i64(ctx, ctx->segbase.as<int64_t>() + nseg, &nrec))) return rc;
+    }
+    const size_t nr = (size_t)std::max<int64_t>(1, nrec);
+    if ((rc = ensure_all(ctx, ctx->rec_lin, 8 * nr))) return rc;
+    DevBuf* b8[] = {&ctx->f_voff, &ctx->f_hash};
+    DevBuf* b4[] = {&ctx->f_bs, &ctx->f_ref, &ctx->f_pos, &ctx->f_lseq, &ctx->f_nref, &ctx->f_npos,
+                    &ctx->f_tlen};
+    DevBuf* b2[] = {&ctx->f_flag, &ctx->f_bin, &ctx->f_ncig};
+    DevBuf* b1[] = {&ctx->f_mapq, &ctx->f_lrn};
+    for (auto* b : b8) if ((rc = ensure_all(ctx, *b, 8 * nr))) return rc;
+    for (auto* b : b4) if ((rc = ensure_all(ctx, *b, 4 * nr))) return rc;
+    for (auto* b : b2) if ((rc = ensure_all(ctx, *b, 2 * nr))) return rc;
+    for (auto* b : b1) if ((rc = ensure_all(ctx, *b, nr))) return rc;
+    ctx->have_pipeline = false;  // the record arrays now hold the span records
+    ctx->voff_h.clear();
+    if (nrec > 0) {
+      launch_seg_emit2(ctx->U.as<uint8_t>(), ctx->ulen, ctx->segs.as<Seg>(),
+                       ctx->segbase.as<int64_t>(), nseg, ctx->rec_lin.as<int64_t>(), s);
+      HIPCHK(hipMemsetAsync(d_stat, 0, 4, s));
+      launch_decode_records(ctx->U.as<uint8_t>(), ctx->ulen, ctx->rec_lin.as<int64_t>(), nrec,
+                            ctx->blk_pos.as<int64_t>(), ctx->uoff.as<int64_t>(), nblk,
+                            ctx->pages.as<int32_t>(), ctx->soa(), d_stat, s);
+    }
+    // 5. records of every span chunk, kernel 4, per-partition digests of the kept records
+    int64_t nidx = 0;
+    const size_t ncs = (size_t)std::max<int64_t>(1, nchunk);
+    if ((rc = ensure_all(ctx, ctx->span_c, 16 * ncs)) ||
+        (rc = ensure_all(ctx, ctx->span_r, 8 * (3 * ncs + 2))))
+      return rc;
+    uint64_t* d_cb = ctx->span_c.as<uint64_t>();
+    uint64_t* d_ce = d_cb + ncs;
+    int64_t* d_first = ctx->span_r.as<int64_t>();
+    int64_t* d_cnt = d_first + ncs;
+    int64_t* d_off = d_cnt + ncs;  // nchunk + 1
+    if (nchunk) {
+      HIPCHK(hipMemcpyAsync(d_cb, cb.data(), 8 * (size_t)nchunk, hipMemcpyHostToDevice, s));
+      HIPCHK(hipMemcpyAsync(d_ce, ce.data(), 8 * (size_t)nchunk, hipMemcpyHostToDevice, s));
+      launch_span_ranges(ctx->f_voff.as<uint64_t>(), nrec, d_cb, d_ce, nchunk, d_first, d_cnt, s);
+      launch_exclusive_scan_i64(d_cnt, d_off, nchunk, ctx->tmp.as<int64_t>(), s);
+      if ((rc = get_i64(ctx, d_off + nchunk, &nidx))) return rc;
+    }
+    const size_t ni = (size_t)std::max<int64_t>(1, nidx);
+    if ((rc = ensure_all(ctx, ctx->span_idx, 8 * ni)) || (rc = ensure_all(ctx, ctx->keep, ni)) ||
+        (rc = ensure_all(ctx, ctx->span_keep32, 4 * ni)) ||
+        (rc = ensure_all(ctx, ctx->span_off, 8 * (ni + 1))) ||
+        (rc = ensure_all(ctx, ctx->span_kept, 8 * ni)))
+      return rc;
+    int64_t nkept = 0;
+    if (nidx > 0) {
+      launch_ranges_to_idx(d_first, d_off, nchunk, ctx->span_idx.as<int64_t>(), s);
+      if ((rc = upload_intervals(ctx, tr))) return rc;
+      launch_interval_filter(ctx->U.as<uint8_t>(), ctx->rec_lin.as<int64_t>(), ctx->soa(),
+                             ctx->span_idx.as<int64_t>(), nidx, ctx->iv_ref.as<int32_t>(),
+                             ctx->iv_start.as<int32_t>(), ctx->iv_end.as<int32_t>(),
+                             ctx->iv_begin.as<int32_t>(), ctx->n_ref, ctx->keep.as<uint8_t>(), s);
+      launch_keep_to_i32(ctx->keep.as<uint8_t>(), nidx, ctx->span_keep32.as<int32_t>(), s);
+      launch_exclusive_scan_i32(ctx->span_keep32.as<int32_t>(), ctx->span_off.as<int64_t>(), nidx,
+                                ctx->tmp.as<int64_t>(), s);
+      launch_compact_kept(ctx->span_idx.as<int64_t>(), ctx->keep.as<uint8_t>(),
+                          ctx->span_off.as<int64_t>(), nidx, ctx->span_kept.as<int64_t>(), s);
+      if ((rc = get_i64(ctx, ctx->span_off.as<int64_t>() + nidx, &nkept))) return rc;
+    }
+    // partition p: span chunks [part_first[p], part_first[p+1]) -> idx [off[.], off[.]) -> kept
+    std::vector<int64_t> cpos((size_t)nsplit + 1), ipos((size_t)nsplit + 1, 0), kpos((size_t)nsplit + 1, 0);
+    if (nchunk) {
+      std::vector<int64_t> offh((size_t)nchunk + 1);
+      HIPCHK(hipMemcpy(offh.data(), d_off, 8 * (size_t)(nchunk + 1), hipMemcpyDeviceToHost));
+      for (int64_t p = 0; p <= nsplit; p++) ipos[(size_t)p] = offh[(size_t)part_first[(size_t)p]];
+    }
+    if (nidx > 0) {
+      DevBuf pos;
+      HIPCHK(pos.ensure(16 * (size_t)(nsplit + 1)));
+      HIPCHK(hipMemcpyAsync(pos.p, ipos.data(), 8 * (size_t)(nsplit + 1), hipMemcpyHostToDevice, s));
+      launch_gather_i64(ctx->span_off.as<int64_t>(), pos.as<int64_t>(), nsplit + 1,
+                        pos.as<int64_t>() + nsplit + 1, s);
+      HIPCHK(hipMemcpyAsync(kpos.data(), pos.as<int64_t>() + nsplit + 1, 8 * (size_t)(nsplit + 1),
+                            hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+    }
+    std::vector<PartRange> parts((size_t)nsplit);
+    for (int64_t p = 0; p < nsplit; p++) parts[(size_t)p] = {kpos[(size_t)p], kpos[(size_t)p + 1], 0};
+    if ((rc = ensure_all(ctx, ctx->parts, sizeof(PartRange) * (size_t)(nsplit + 1)))) return rc;
+    if (nsplit) {
+      HIPCHK(hipMemcpyAsync(ctx->parts.p, parts.data(), sizeof(PartRange) * (size_t)nsplit,
+                            hipMemcpyHostToDevice, s));
+      if (nkept > 0)
+        launch_partition_digest_idx(ctx->f_hash.as<uint64_t>(), ctx->span_kept.as<int64_t>(),
+                                    ctx->parts.as<PartRange>(), nsplit, s);
+      HIPCHK(hipEventRecord(ctx->ev[7], s));
+      HIPCHK(hipMemcpyAsync(parts.data(), ctx->parts.p, sizeof(PartRange) * (size_t)nsplit,
+                            hipMemcpyDeviceToHost, s));
+    } else {
+      HIPCHK(hipEventRecord(ctx->ev[7], s));
+    }
+    int32_t st2 = 0;
+    HIPCHK(hipMemcpyAsync(&st2, d_stat, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (st2 && nrec > 0) RET(DQ_EFORMAT, "truncated BAM record");
+    ctx->parts_h = parts;
+    dq_stats S = ctx->stats;
+    S.n_records = nidx;
+    S.n_filtered = nkept;
+    S.blocks_inflated = nsel;
+    S.ms_inflate = ev_ms(ctx->ev[5], ctx->ev[6]);
+    S.ms_span = ev_ms(ctx->ev[5], ctx->ev[7]);
+    uint64_t dg = 0;
+    for (int64_t i = 0; i < nsplit; i++)
+      dg += dq_mix64(parts[(size_t)i].digest ^ ((uint64_t)(i + 1) * DQ_K_WORD));
+    S.digest = dg;
+    ctx->span_parts_valid = true;
+    *out = S;
+    return 0;
+  }
+}
+
 // ------------------------------------------------------------------ opening inputs
 static void reset_open(dq_ctx* ctx, int64_t len) {
+  ctx->plan_cached = false;
   ctx->flen = len;
   ctx->have_file = true;
   ctx->have_pipeline = false;
@@ -1014,29 +1447,37 @@ static void reset_open(dq_ctx* ctx, int64_t len) {
 // staging buffers in turn, each copied asynchronously while the next piece is read from the page
 // cache (the role of Disq's 2 x 4 MB NIO prefetcher, SeekableByteChannelPrefetcher.java:45).
 static int upload_file_range(dq_ctx* ctx, int fd, int64_t off, int64_t len) {
-  constexpr size_t PIECE = 32u << 20;
+  constexpr size_t PIECE = PIN_PIECE;
   int rc;
   if ((rc = ensure_all(ctx, ctx->C, (size_t)len + 4096))) return rc;
-  if (ctx->pin_cap < PIECE) {
-    for (int k = 0; k < 2; k++) {
-      if (ctx->pin[k]) (void)hipHostFree(ctx->pin[k]);
-      ctx->pin[k] = nullptr;
-      HIPCHK(hipHostMalloc((void**)&ctx->pin[k], PIECE, hipHostMallocDefault));
-      if (!ctx->pin_ev[k]) HIPCHK(hipEventCreateWithFlags(&ctx->pin_ev[k], hipEventDisableTiming));
-    }
-    ctx->pin_cap = PIECE;
-  }
+  if ((rc = ensure_pinned(ctx))) return rc;
   bool used[2] = {false, false};
   int k = 0;
   for (int64_t done = 0; done < len; k ^= 1) {
     const size_t n = (size_t)std::min<int64_t>((int64_t)PIECE, len - done);
     if (used[k]) HIPCHK(hipEventSynchronize(ctx->pin_ev[k]));  // its previous copy is done
-    size_t got = 0;
-    while (got < n) {
-      const ssize_t r = pread(fd, ctx->pin[k] + got, n - got, (off_t)(off + done + (int64_t)got));
-      if (r <= 0) RET(DQ_EIO, "short read");
-      got += (size_t)r;
-    }
+    // four readers per piece (one thread copies out of the page cache at a fraction of PCIe)
+    constexpr int T = 4;
+    bool ok[T];
+    std::thread th[T];
+    const size_t part = (n + T - 1) / T;
+    for (int t = 0; t < T; t++)
+      th[t] = std::thread([&, t] {
+        const size_t a = std::min(n, (size_t)t * part), b = std::min(n, a + part);
+        size_t got = a;
+        ok[t] = true;
+        while (got < b) {
+          const ssize_t r = pread(fd, ctx->pin[k] + got, b - got, (off_t)(off + done + (int64_t)got));
+          if (r <= 0) {
+            ok[t] = false;
+            return;
+          }
+          got += (size_t)r;
+        }
+      });
+    for (auto& x : th) x.join();
+    for (int t = 0; t < T; t++)
+      if (!ok[t]) RET(DQ_EIO, "short read");
     HIPCHK(hipMemcpyAsync(ctx->C.as<uint8_t>() + done, ctx->pin[k], n, hipMemcpyHostToDevice, ctx->s));
     HIPCHK(hipEventRecord(ctx->pin_ev[k], ctx->s));
     used[k] = true;
@@ -1252,7 +1693,8 @@ int dq_get_stats(dq_ctx* ctx, dq_stats* stats) {
 int dq_partition_digests(dq_ctx* ctx, int64_t* counts, uint64_t* digests, int64_t cap,
                          int64_t* n) {
   if (!ctx || !n) return DQ_EINVAL;
-  if (!ctx->have_pipeline) RET(DQ_EINVAL, "no pipeline run (call dq_run_resident first)");
+  if (!ctx->have_pipeline && !ctx->span_parts_valid)
+    RET(DQ_EINVAL, "no pipeline run (call dq_run_resident first)");
   *n = (int64_t)ctx->parts_h.size();
   for (int64_t i = 0; i < std::min(cap, *n); i++) {
     const PartRange& r = ctx->parts_h[(size_t)i];
@@ -1288,10 +1730,11 @@ int dq_set_index(dq_ctx* ctx, const uint8_t* bai, int64_t len) {
     ctx->have_bai = false;
     return 0;
   }
-  int64_t solb, ncc;
-  if (parse_bai(bai, len, &solb, &ncc)) RET(DQ_EFORMAT, "invalid .bai");
-  ctx->solb = solb;
-  ctx->ncc = ncc;
+  Bai x;
+  if (parse_bai(bai, len, x)) RET(DQ_EFORMAT, "invalid .bai");
+  ctx->solb = x.solb;
+  ctx->ncc = x.ncc;
+  ctx->bai = std::move(x);
   ctx->have_bai = true;
   return 0;
 }
@@ -1485,8 +1928,22 @@ int dq_run_resident(dq_ctx* ctx, const dq_traversal* tr, dq_stats* stats) {
   ON_DEVICE(ctx);
   if (tr && !tr->has_intervals && !tr->traverse_unplaced_unmapped)
     RET(DQ_EINVAL, "Traversing mapped reads only is not supported.");
+  int rc;
+  if (tr && tr->has_intervals && tr->n > 0 && !tr->traverse_unplaced_unmapped && ctx->have_bai &&
+      !ctx->o.full_traversal && !ctx->chunk_mode) {
+    // .bai span run: only the spans' blocks are inflated; the partition plans come from a full
+    // run of the open file (made once here if there is none yet)
+    if (!ctx->plan_cached) {
+      ctx->have_pipeline = false;
+      if ((rc = run_pipeline(ctx))) return rc;
+    }
+    dq_stats S{};
+    if ((rc = run_span(ctx, tr, &S))) return rc;
+    if (stats) *stats = S;
+    return 0;
+  }
   ctx->have_pipeline = false;
-  int rc = run_pipeline(ctx);
+  rc = run_pipeline(ctx);
   if (rc) return rc;
   dq_stats S = ctx->stats;
   S.n_filtered = -1;

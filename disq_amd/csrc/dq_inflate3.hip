@@ -637,7 +637,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     const int32_t* __restrict__ blk_csize, const int32_t* __restrict__ blk_usize,
     const int64_t* __restrict__ uoff, int64_t nblk, uint8_t* __restrict__ U,
     int32_t* __restrict__ status, int32_t verify_crc, const uint32_t* __restrict__ crc_init,
-    uint64_t* __restrict__ tim, uint32_t OV, uint32_t sflags) {
+    uint64_t* __restrict__ tim, uint32_t OV, uint32_t sflags, const int32_t* __restrict__ sel) {
   __shared__ LdsI L;
   // DQ_TIMING: thread 0 accumulates s_memtime cycles per phase (tim != nullptr only then)
   uint64_t tacc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -651,8 +651,9 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     }                                                     \
   } while (0)
 #define TCOUNT(i) do { if (TIMING && threadIdx.x == 0) tacc[i] += 1; } while (0)
-  const int64_t b = blockIdx.x;
-  if (b >= nblk) return;
+  if ((int64_t)blockIdx.x >= nblk) return;
+  // sel: the blocks to inflate (sparse runs: only the blocks an interval traversal needs)
+  const int64_t b = sel ? (int64_t)sel[blockIdx.x] : (int64_t)blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int64_t cpos = blk_pos[b];
   const int32_t csize = blk_csize[b];
@@ -1226,7 +1227,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   }
   TST(7);
   if (TIMING && t == 0)
-    for (int i = 0; i < 16; i++) tim[b * 16 + i] = tacc[i];
+    for (int i = 0; i < 16; i++) tim[(int64_t)blockIdx.x * 16 + i] = tacc[i];
 }
 
 uint32_t h_mul(uint32_t a, uint32_t b) {
@@ -1305,8 +1306,10 @@ const uint32_t* inflate3_tables(int device) {
 void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* blk_csize,
                      const int32_t* blk_usize, const int64_t* uoff, int64_t nblk, uint8_t* U,
                      int32_t* status, int32_t verify_crc, const uint32_t* crc_init, uint64_t* tim,
-                     hipStream_t s) {
+                     hipStream_t s, const int32_t* sel, int64_t nsel) {
   if (nblk <= 0) return;
+  const int64_t ngrid = sel ? nsel : nblk;
+  if (ngrid <= 0) return;
   static const uint32_t ov = getenv("DQ_OV") ? (uint32_t)atoi(getenv("DQ_OV")) : OV_DEFAULT;
   static const uint32_t sflags = getenv("DQ_STORE") ? (uint32_t)atoi(getenv("DQ_STORE")) : 2;
   static int cfg = -1;
@@ -1316,8 +1319,9 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
     cfg = g != 4 ? 0 : nb == 1 ? 1 : nb == 4 ? 3 : 2;
   }
 #define DQ_LAUNCH(TM, NBT, GT)                                                                  \
-  hipLaunchKernelGGL((inflate_block_kernel<TM, NBT, GT>), dim3((unsigned)nblk), dim3(WG), 0, s, C, \
-                     blk_pos, blk_csize, blk_usize, uoff, nblk, U, status, verify_crc, crc_init, tim, ov, sflags)
+  hipLaunchKernelGGL((inflate_block_kernel<TM, NBT, GT>), dim3((unsigned)ngrid), dim3(WG), 0, s, C, \
+                     blk_pos, blk_csize, blk_usize, uoff, ngrid, U, status, verify_crc, crc_init, tim, ov, \
+                     sflags, sel)
 #define DQ_CFGS(TM)                       \
   switch (cfg) {                          \
     case 1: DQ_LAUNCH(TM, 1, 4); break;   \

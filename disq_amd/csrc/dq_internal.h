@@ -78,7 +78,7 @@ const uint32_t* inflate3_tables(int device);
 void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* blk_csize,
                      const int32_t* blk_usize, const int64_t* uoff, int64_t nblk, uint8_t* U,
                      int32_t* status, int32_t verify_crc, const uint32_t* crc_init, uint64_t* tim,
-                     hipStream_t s);
+                     hipStream_t s, const int32_t* sel = nullptr, int64_t nsel = 0);
 
 // Split planning (a2-a4).
 constexpr int64_t SPLIT_FROM_SBI = -2;  // SplitPlan.first_blk of a chunk taken from a .sbi
@@ -119,6 +119,22 @@ void launch_seg_counts(const Seg* segs, int64_t nseg, int64_t* counts, hipStream
 void launch_seg_emit2(const uint8_t* U, int64_t ulen, const Seg* segs, const int64_t* base,
                       int64_t nseg, int64_t* rec_lin, hipStream_t s);
 
+// Sparse (windowed) record chains: every window is a run of inflated U bytes (whole-file layout)
+// with an exact first record start; segments [seg0, next window's seg0) belong to it.
+struct Win {
+  int64_t u_start;      // exact first record start
+  int64_t u_chain_end;  // record starts wanted: < u_chain_end
+  int64_t u_limit;      // end of the inflated bytes (reads past it: status 4, needs more)
+  int64_t seg0;         // first segment of the window
+  int32_t at_eof;       // the window runs to the end of the file
+  int32_t pad;
+};
+void launch_wseg(const uint8_t* U, const int32_t* ref_len, int32_t n_ref, const Win* wins,
+                 int64_t nwin, Seg* segs, int64_t nseg, int64_t seg_bytes, int32_t* d_broken,
+                 hipStream_t s);
+void launch_wseg_fix(const uint8_t* U, Seg* segs, const Win* wins, int64_t nwin, int64_t nseg,
+                     int64_t seg_bytes, int32_t* d_status, hipStream_t s);
+
 struct RecSoA {
   uint64_t* voffset;
   int32_t* block_size;
@@ -151,6 +167,8 @@ void launch_partition_ranges(const SplitPlan* plans, int64_t nsplit, const int64
                              int32_t* d_status, hipStream_t s);
 void launch_partition_digest2(const uint64_t* hash, PartRange* parts, int64_t nparts,
                               hipStream_t s);
+void launch_partition_digest_idx(const uint64_t* hash, const int64_t* kept, PartRange* parts,
+                                 int64_t nparts, hipStream_t s);
 
 // Record export: record-index ranges -> index list; SoA rows and raw bytes gathered by index into
 // compact buffers (idx == nullptr in gather_raw: records first .. first + n - 1).
@@ -160,6 +178,17 @@ void launch_gather_soa(const int64_t* idx, int64_t n, const RecSoA src, RecSoA d
 void launch_gather_raw(const uint8_t* U, const int64_t* rec_lin, const int32_t* block_size,
                        const int64_t* idx, int64_t first, int64_t n, const int64_t* out_off,
                        uint8_t* out, hipStream_t s);
+
+// Interval traversal over .bai span chunks (partition order): record range of every chunk, keep
+// flags -> compact kept index list, per-partition digests over an index list.
+void launch_span_ranges(const uint64_t* voffset, int64_t nrec, const uint64_t* cbeg,
+                        const uint64_t* cend, int64_t nchunk, int64_t* first, int64_t* count,
+                        hipStream_t s);
+void launch_keep_to_i32(const uint8_t* keep, int64_t n, int32_t* out, hipStream_t s);
+void launch_gather_i64(const int64_t* src, const int64_t* pos, int64_t n, int64_t* dst,
+                       hipStream_t s);
+void launch_compact_kept(const int64_t* idx, const uint8_t* keep, const int64_t* off, int64_t n,
+                         int64_t* kept, hipStream_t s);
 
 // Kernel 4: interval filter; keep[t] for record idx[t] (or t when idx == NULL).
 void launch_interval_filter(const uint8_t* U, const int64_t* rec_lin, const RecSoA soa,

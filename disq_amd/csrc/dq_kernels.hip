@@ -489,6 +489,31 @@ __device__ int walk(const uint8_t* U, int64_t ulen, int u_is_eof, int64_t start,
   return 0;
 }
 
+// walk() for a window of a sparse run: a record must also END inside the inflated bytes (the
+// bytes after a window are not inflated); 4 = the window needs more blocks.
+__device__ int walk_win(const uint8_t* U, int64_t ulen, int u_is_eof, int64_t start,
+                        int64_t seg_end, int64_t* exit, int64_t* count) {
+  int64_t p = start, n = 0;
+  while (p < seg_end) {
+    if (p + 4 > ulen) {
+      if (u_is_eof) {
+        *exit = END_CHAIN;
+        *count = n;
+        return 0;
+      }
+      return 4;
+    }
+    const int32_t bs = ld32(U, p);
+    if (bs < 32) return ST_BAD_CODE;
+    if (p + 4 + (int64_t)bs > ulen) return u_is_eof ? ST_SHORT : 4;
+    n++;
+    p += 4 + (int64_t)bs;
+  }
+  *exit = p;
+  *count = n;
+  return 0;
+}
+
 // One wave per segment (grid-stride: a few thousand resident waves instead of one dispatch per
 // segment): the first guesser hit at or after the segment start, 64 positions per step.
 __global__ __launch_bounds__(64) void seg_spec_kernel(const uint8_t* __restrict__ U, int64_t ulen,
@@ -867,6 +892,202 @@ __global__ __launch_bounds__(256) void interval_filter_kernel(
   keep[t] = k;
 }
 
+// ------------------------------------------------------------------ windowed record chains
+// Sparse runs (an interval traversal's .bai spans, AbstractBinarySamSource.java:102-112) inflate
+// only some blocks, in the whole-file U layout: each window is a run of inflated bytes whose first
+// record start is exact (a span chunk start).  The segmented chain of Kernel 3 runs inside every
+// window at once; a window's reads stop at its inflated end (status 4: needs more blocks).
+__device__ inline int64_t win_of(const Win* __restrict__ w, int64_t nwin, int64_t s) {
+  int64_t lo = 0, hi = nwin - 1;  // last window with seg0 <= s
+  while (lo < hi) {
+    const int64_t mid = (lo + hi + 1) >> 1;
+    if (w[mid].seg0 <= s) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(64) void wseg_spec_kernel(const uint8_t* __restrict__ U,
+                                                       const int32_t* __restrict__ ref_len,
+                                                       int32_t n_ref, const Win* __restrict__ wins,
+                                                       int64_t nwin, Seg* __restrict__ segs,
+                                                       int64_t nseg, int64_t seg_bytes) {
+  for (int64_t s = blockIdx.x; s < nseg; s += gridDim.x) {
+    const Win w = wins[win_of(wins, nwin, s)];
+    const int64_t k = s - w.seg0;
+    const int64_t sb = w.u_start + k * seg_bytes;
+    const int64_t se = min(w.u_chain_end, sb + seg_bytes);
+    int64_t best = INT64_MAX;
+    if (k == 0) {
+      best = w.u_start;
+    } else {
+      for (int64_t b = sb; b < se; b += 64) {
+        const int64_t v = b + threadIdx.x;
+        const bool hit =
+            v < se && check_record_start(U, w.u_limit, w.at_eof, ref_len, n_ref, v) == 1;
+        const uint64_t m = __ballot(hit);
+        if (m) {
+          best = b + __builtin_ctzll(m);
+          break;
+        }
+      }
+    }
+    if (threadIdx.x == 0) {
+      Seg g;
+      g.exact = k == 0;
+      g.status = 0;
+      g.start = best == INT64_MAX ? -1 : best;
+      g.exit = -1;
+      g.count = 0;
+      segs[s] = g;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void wseg_walk_kernel(const uint8_t* __restrict__ U,
+                                                        const Win* __restrict__ wins, int64_t nwin,
+                                                        Seg* __restrict__ segs, int64_t nseg,
+                                                        int64_t seg_bytes) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nseg) return;
+  Seg g = segs[s];
+  if (g.start < 0) return;
+  const Win w = wins[win_of(wins, nwin, s)];
+  const int64_t se = min(w.u_chain_end, w.u_start + (s - w.seg0 + 1) * seg_bytes);
+  int64_t ex = -1, cnt = 0;
+  const int r = walk_win(U, w.u_limit, w.at_eof, g.start, se, &ex, &cnt);
+  g.status = r;
+  if (r == 0) {
+    g.exit = ex;
+    g.count = cnt;
+  }
+  segs[s] = g;
+}
+
+__global__ void wseg_link_kernel(const Seg* __restrict__ segs, const Win* __restrict__ wins,
+                                 int64_t nwin, int64_t nseg, int64_t seg_bytes,
+                                 int32_t* d_broken) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nseg) return;
+  const Seg g = segs[s];
+  if (g.status != 0) {
+    *d_broken = 1;
+    return;
+  }
+  const Win w = wins[win_of(wins, nwin, s)];
+  if (s == w.seg0) return;
+  int64_t t = s - 1;
+  while (t > w.seg0 && segs[t].start < 0) t--;
+  const int64_t in = segs[t].exit;
+  const int64_t se = min(w.u_chain_end, w.u_start + (s - w.seg0 + 1) * seg_bytes);
+  const bool ok = g.start < 0 ? (in == END_CHAIN || in >= se) : (in == g.start);
+  if (!ok) *d_broken = 1;
+}
+
+// Serial link check + repair, one lane per window (as seg_fix_kernel, inside each window).
+__global__ void wseg_fix_kernel(const uint8_t* __restrict__ U, Seg* __restrict__ segs,
+                                const Win* __restrict__ wins, int64_t nwin, int64_t nseg,
+                                int64_t seg_bytes, int32_t* d_status) {
+  const int64_t wi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (wi >= nwin) return;
+  const Win w = wins[wi];
+  const int64_t s1 = wi + 1 < nwin ? wins[wi + 1].seg0 : nseg;
+  if (s1 <= w.seg0) return;
+  if (segs[w.seg0].status) {
+    atomicMax(d_status, segs[w.seg0].status);
+    return;
+  }
+  int64_t in = segs[w.seg0].exit;
+  for (int64_t s = w.seg0 + 1; s < s1; s++) {
+    Seg& g = segs[s];
+    const int64_t sb = w.u_start + (s - w.seg0) * seg_bytes;
+    const int64_t se = min(w.u_chain_end, sb + seg_bytes);
+    if (in == END_CHAIN || in >= se) {
+      g.start = in;
+      g.exit = in;
+      g.count = 0;
+      g.exact = 1;
+      g.status = 0;
+      continue;
+    }
+    if (g.start != in || g.status != 0) {
+      int64_t ex = -1, cnt = 0;
+      const int r = walk_win(U, w.u_limit, w.at_eof, in, se, &ex, &cnt);
+      g.start = in;
+      g.status = r;
+      g.exit = ex;
+      g.count = cnt;
+      if (r) {
+        atomicMax(d_status, r);
+        return;
+      }
+    }
+    g.exact = 1;
+    in = g.exit;
+  }
+}
+
+// Records of the span chunks, in partition order: chunk j selects the records whose start pointer
+// is in [beg_j, end_j) (BAMFileIndexIterator over the chunk list, H/BAMFileReader2.java:1082-1095).
+__global__ __launch_bounds__(256) void span_ranges_kernel(const uint64_t* __restrict__ voffset,
+                                                          int64_t nrec,
+                                                          const uint64_t* __restrict__ cbeg,
+                                                          const uint64_t* __restrict__ cend,
+                                                          int64_t nchunk, int64_t* __restrict__ first,
+                                                          int64_t* __restrict__ count) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nchunk) return;
+  const int64_t a = lower_bound_u64(voffset, nrec, cbeg[j]);
+  const int64_t b = lower_bound_u64(voffset, nrec, cend[j]);
+  first[j] = a;
+  count[j] = b > a ? b - a : 0;
+}
+
+// kept[off[i]] = idx[i] for every kept record (off = exclusive scan of keep).
+__global__ __launch_bounds__(256) void compact_kept_kernel(const int64_t* __restrict__ idx,
+                                                           const uint8_t* __restrict__ keep,
+                                                           const int64_t* __restrict__ off, int64_t n,
+                                                           int64_t* __restrict__ kept) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && keep[i]) kept[off[i]] = idx[i];
+}
+
+__global__ __launch_bounds__(256) void keep_to_i32_kernel(const uint8_t* __restrict__ keep, int64_t n,
+                                                          int32_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = keep[i];
+}
+
+// Partition digests over an index list: partition p = kept[begin_p, end_p) (same definition as
+// partition_digest_kernel: sum of mix64(hash + (k + 1) * K_LEN) in order).
+__global__ __launch_bounds__(256) void partition_digest_idx_kernel(const uint64_t* __restrict__ hash,
+                                                                   const int64_t* __restrict__ kept,
+                                                                   PartRange* __restrict__ parts,
+                                                                   int64_t nparts) {
+  __shared__ uint64_t red[256];
+  const int64_t i = blockIdx.x;
+  if (i >= nparts) return;
+  const PartRange r = parts[i];
+  uint64_t acc = 0;
+  for (int64_t k = r.begin + (int64_t)blockIdx.y * 256 + threadIdx.x; k < r.end; k += 256 * 64)
+    acc += dq_mix64(hash[kept[k]] + (uint64_t)(k - r.begin + 1) * DQ_K_LEN);
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && red[0])
+    atomicAdd(reinterpret_cast<unsigned long long*>(&parts[i].digest), (unsigned long long)red[0]);
+}
+
+__global__ __launch_bounds__(256) void gather_i64_kernel(const int64_t* __restrict__ src,
+                                                         const int64_t* __restrict__ pos, int64_t n,
+                                                         int64_t* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[pos[i]];
+}
+
 // ------------------------------------------------------------------ record export (gathers)
 // idx[o_r + k] = begin_r + k for record-index ranges r (one block per range).
 __global__ __launch_bounds__(256) void ranges_to_idx_kernel(const int64_t* __restrict__ begin,
@@ -1083,6 +1304,60 @@ void launch_gather_raw(const uint8_t* U, const int64_t* rec_lin, const int32_t* 
   if (n <= 0) return;
   hipLaunchKernelGGL(gather_raw_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, U, rec_lin,
                      block_size, idx, first, n, out_off, out);
+}
+
+void launch_wseg(const uint8_t* U, const int32_t* ref_len, int32_t n_ref, const Win* wins,
+                 int64_t nwin, Seg* segs, int64_t nseg, int64_t seg_bytes, int32_t* d_broken,
+                 hipStream_t s) {
+  if (nseg <= 0) return;
+  hipLaunchKernelGGL(wseg_spec_kernel, dim3((unsigned)std::min<int64_t>(nseg, 16384)), dim3(64), 0, s,
+                     U, ref_len, n_ref, wins, nwin, segs, nseg, seg_bytes);
+  hipLaunchKernelGGL(wseg_walk_kernel, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, U, wins,
+                     nwin, segs, nseg, seg_bytes);
+  hipLaunchKernelGGL(wseg_link_kernel, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, segs,
+                     wins, nwin, nseg, seg_bytes, d_broken);
+}
+
+void launch_wseg_fix(const uint8_t* U, Seg* segs, const Win* wins, int64_t nwin, int64_t nseg,
+                     int64_t seg_bytes, int32_t* d_status, hipStream_t s) {
+  if (nwin <= 0) return;
+  hipLaunchKernelGGL(wseg_fix_kernel, dim3((unsigned)((nwin + 63) / 64)), dim3(64), 0, s, U, segs,
+                     wins, nwin, nseg, seg_bytes, d_status);
+}
+
+void launch_span_ranges(const uint64_t* voffset, int64_t nrec, const uint64_t* cbeg,
+                        const uint64_t* cend, int64_t nchunk, int64_t* first, int64_t* count,
+                        hipStream_t s) {
+  if (nchunk <= 0) return;
+  hipLaunchKernelGGL(span_ranges_kernel, dim3((unsigned)((nchunk + 255) / 256)), dim3(256), 0, s,
+                     voffset, nrec, cbeg, cend, nchunk, first, count);
+}
+
+void launch_keep_to_i32(const uint8_t* keep, int64_t n, int32_t* out, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(keep_to_i32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, keep, n,
+                     out);
+}
+
+void launch_compact_kept(const int64_t* idx, const uint8_t* keep, const int64_t* off, int64_t n,
+                         int64_t* kept, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(compact_kept_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, idx,
+                     keep, off, n, kept);
+}
+
+void launch_partition_digest_idx(const uint64_t* hash, const int64_t* kept, PartRange* parts,
+                                 int64_t nparts, hipStream_t s) {
+  if (nparts <= 0) return;
+  hipLaunchKernelGGL(partition_digest_idx_kernel, dim3((unsigned)nparts, 64), dim3(256), 0, s, hash,
+                     kept, parts, nparts);
+}
+
+void launch_gather_i64(const int64_t* src, const int64_t* pos, int64_t n, int64_t* dst,
+                       hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(gather_i64_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, pos,
+                     n, dst);
 }
 
 }  // namespace dq

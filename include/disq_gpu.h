@@ -55,7 +55,8 @@ typedef struct dq_opts {
   int32_t use_nio;           /* useNio(boolean): NIO ceil(len/splitSize) splits */
   int32_t verify_crc;        /* check each BGZF block's CRC32 (stricter than htsjdk default) */
   int32_t stringency;        /* validationStringency (recorded) */
-  int32_t reserved;
+  int32_t full_traversal;    /* 1: interval runs inflate and filter the whole file; 0 (default):
+                                only the .bai spans of the intervals (dq_run_resident) */
   int64_t hadoop_block_size; /* fs.local.block.size; 0 = 32 MiB */
 } dq_opts;
 
@@ -136,6 +137,9 @@ typedef struct dq_stats {
   int64_t h2d_bytes;        /* compressed bytes the last open/decode copied host -> device */
   int64_t owned_bytes;      /* decompressed bytes of the blocks starting inside the splits (the
                                whole stream for a whole file; the shards of a file sum to it) */
+  int64_t blocks_inflated;  /* BGZF blocks the last run inflated (fewer than n_blocks in a
+                               .bai span run) */
+  double ms_span;           /* .bai span run: device time of the sparse inflate + chains + filter */
 } dq_stats;
 
 int dq_ctx_create(dq_ctx** out, const dq_opts* opts);
@@ -221,9 +225,14 @@ int dq_read(dq_ctx* ctx, const dq_traversal* tr, int32_t with_raw, dq_batch** ou
 
 /* Run the whole device pipeline on the resident file without copying records back (records
  * stay in HBM); fills stats.  This is the benchmark entry point.  With intervals in tr (needs
- * dq_set_index, as createIndexIterator does), kernel 4 also filters every record against them
- * (overlap, contained=false; AbstractBinarySamSource.java:86-134) and stats.ms_filter /
- * stats.n_filtered report it; the kept-record list stays in HBM. */
+ * dq_set_index, as createIndexIterator does; AbstractBinarySamSource.java:86-112), the traversal
+ * of every partition as Disq runs it: the .bai span of the optimized intervals clipped to each
+ * partition chunk is the only part of the file inflated (the partition plans come from a full run
+ * of the open file, made first if there is none); records of the spans are filtered by kernel 4
+ * (overlap, contained=false).  stats.n_records = records in the spans, stats.n_filtered = kept,
+ * stats.blocks_inflated, stats.ms_span; dq_partition_digests gives the kept count and digest per
+ * partition.  With opts.full_traversal, or traverse_unplaced_unmapped, every record of the file is
+ * filtered instead (stats.ms_filter; the unplaced tail is not included). */
 int dq_run_resident(dq_ctx* ctx, const dq_traversal* tr, dq_stats* stats);
 
 /* Stats of the last pipeline run (the ones dq_run_resident returns). */

@@ -121,11 +121,12 @@ def test_interval_traversal(anysam, ivs, unplaced, expected, split):
     ([("chr21", 20000, 22999), ("chr21", 5000, 9999), ("chr21", 9000, 9500)], 16),
 ])
 def test_resident_interval_filter(anysam, ivs, expected):
-    """dq_run_resident with intervals: kernel 4 over the whole resident stream keeps exactly the
-    records the per-partition createIndexIterator path returns (one partition, no unplaced)."""
+    """dq_run_resident with intervals, both ways: the .bai span run (default) and kernel 4 over
+    the whole resident stream (full_traversal) keep exactly the records the per-partition
+    createIndexIterator path returns (one partition, no unplaced)."""
     ob = O.OracleBam(anysam.bam)
     conv = [(ob.ref_index(c), s, e) for c, s, e in ivs]
-    with _lib.Context(split_size=0, verify_crc=True) as c:
+    with _lib.Context(split_size=0, verify_crc=True, full_traversal=True) as c:
         c.open_bytes(anysam.bam)
         c.set_index(anysam.bai)
         st = c.run_resident((conv, False))
@@ -133,6 +134,14 @@ def test_resident_interval_filter(anysam, ivs, expected):
         assert st.ms_filter > 0
         assert c.run_resident().n_filtered == -1
         assert c.run_resident((conv, False)).n_filtered == expected
+        assert len(c.read(traversal=(conv, False))["voffset"]) == expected
+        assert c.run_resident((conv, False)).n_filtered == expected
+    with _lib.Context(split_size=0, verify_crc=True) as c:
+        c.open_bytes(anysam.bam)
+        c.set_index(anysam.bai)
+        st = c.run_resident((conv, False))
+        assert st.n_filtered == expected
+        assert 0 < st.blocks_inflated <= st.n_blocks
         assert len(c.read(traversal=(conv, False))["voffset"]) == expected
         assert c.run_resident((conv, False)).n_filtered == expected
 

@@ -1,0 +1,48 @@
+"""CPU checks of the .bai span restatement (oracle.bai_span, htsjdk 2.16.0 getFileSpan +
+removeContentsBefore/After as Disq calls them, AbstractBinarySamSource.java:102-107): reading only
+the clipped spans selects exactly the records that reading every partition chunk whole selects.
+htsjdk is not vendored, so the span algorithm's parity with htsjdk itself is unpinned; these
+tests pin that the spans lose no overlapping record on files whose .bai the generator wrote."""
+import numpy as np
+import pytest
+
+from disq_amd import synth
+from oracle import oracle as O
+
+
+@pytest.mark.parametrize("ivs", [[(20, 5000, 9999), (20, 20000, 22999)], [(20, 1, 1000135)],
+                                 [(20, 1, 0)], [(3, 5, 10)], [(20, 500000, 500000)]])
+@pytest.mark.parametrize("split", [40000, 3000])
+def test_anysam_spans_equal_whole_chunks(ivs, split):
+    a = synth.generate(1000, shape=synth.ANYSAM, bai=True)
+    ob = O.OracleBam(a.bam)
+    x = ob.read_partitions(split, traversal=(ivs, False), bai=a.bai)
+    y = ob.read_partitions(split, traversal=(ivs, False), bai=a.bai, spans=True)
+    assert len(x) == len(y)
+    assert all(np.array_equal(p["hash"], q["hash"]) for p, q in zip(x, y))
+
+
+def test_wgs_spans_equal_whole_chunks():
+    w = synth.generate(20000, seed=4, bai=True, unplaced_fraction=0.01, nthreads=4)
+    ob = O.OracleBam(w.bam)
+    rng = np.random.default_rng(1)
+    ivs = [(0, int(s), int(s + rng.integers(10, 800))) for s in rng.integers(1, 99000, size=60)]
+    x = ob.read_partitions(1 << 20, traversal=(ivs, False), bai=w.bai)
+    y = ob.read_partitions(1 << 20, traversal=(ivs, False), bai=w.bai, spans=True)
+    assert sum(len(p) for p in x) > 0
+    assert all(np.array_equal(p["hash"], q["hash"]) for p, q in zip(x, y))
+
+
+def test_span_is_clipped_to_the_chunk():
+    a = synth.generate(1000, shape=synth.ANYSAM, bai=True)
+    ob = O.OracleBam(a.bam)
+    q = O.optimize_intervals([(20, 1, 0)])
+    full = O.bai_span(a.bai, q, 0, (1 << 64) - 1)
+    assert full and all(b < e for b, e in full)
+    (s, e, ch), = [p for p in ob.plan(0)]
+    vs, ve = ch
+    mid = (full[0][0] + full[-1][1]) // 2
+    left = O.bai_span(a.bai, q, vs, mid)
+    right = O.bai_span(a.bai, q, mid, ve)
+    assert all(vs <= b and e <= mid for b, e in left)
+    assert all(mid <= b and e <= ve for b, e in right)
