@@ -80,7 +80,8 @@ EXPORTS = ("dq_ctx_create", "dq_ctx_destroy", "dq_last_error", "dq_version", "dq
            "dq_decode_filtered", "dq_read", "dq_run_resident", "dq_debug_inflated",
            "dq_batch_free", "dq_free", "dq_open_shard", "dq_header_from_prefix",
            "dq_set_splitting_index", "dq_write_sbi", "dq_open_shard_device", "dq_decode_chunk",
-           "dq_get_stats", "dq_partition_digests")
+           "dq_get_stats", "dq_partition_digests", "dq_open_shard_path",
+           "dq_decode_chunk_filtered")
 
 _lib = None
 _lock = threading.Lock()
@@ -114,8 +115,12 @@ def lib():
                                     vp, C.c_int64]
         L.dq_open_shard_device.argtypes = [vp, vp, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
                                            C.c_int64, vp, C.c_int64]
+        L.dq_open_shard_path.argtypes = [vp, C.c_char_p, C.c_int64, C.c_int64, C.c_int64,
+                                         C.c_int64, vp, C.c_int64]
         L.dq_decode_chunk.argtypes = [vp, C.c_char_p, C.c_uint64, C.c_uint64, C.c_int32,
                                       P(P(DqBatch))]
+        L.dq_decode_chunk_filtered.argtypes = [vp, C.c_char_p, C.c_uint64, C.c_uint64,
+                                               P(DqTraversal), C.c_int32, P(P(DqBatch))]
         L.dq_get_stats.argtypes = [vp, P(DqStats)]
         L.dq_partition_digests.argtypes = [vp, P(C.c_int64), P(C.c_uint64), C.c_int64,
                                            P(C.c_int64)]
@@ -153,22 +158,41 @@ FIELDS = (("voffset", np.uint64), ("block_size", np.int32), ("ref_id", np.int32)
           ("hash", np.uint64), ("raw_offset", np.int64))
 
 
+class _BatchOwner:
+    """Frees a dq_batch once no numpy view of its arrays is left."""
+
+    def __init__(self, bp):
+        self.bp = bp
+
+    def __del__(self):
+        try:
+            lib().dq_batch_free(self.bp)
+        except Exception:
+            pass
+
+
+_CT = {np.uint64: C.c_uint64, np.int64: C.c_int64, np.int32: C.c_int32, np.uint16: C.c_uint16,
+       np.uint8: C.c_uint8}
+
+
 def batch_to_numpy(bp):
-    """Copy a dq_batch into numpy arrays and free it."""
+    """The arrays of a dq_batch as numpy views of the library's memory (no copy: a batch of a
+    whole file is tens of GB); the batch is freed when the last view is gone."""
     b = bp.contents
+    owner = _BatchOwner(bp)
+
+    def view(ptr, n, dt):
+        if not n or not ptr:
+            return np.zeros(0, dt)
+        ct = (_CT[dt] * n).from_address(C.cast(ptr, C.c_void_p).value)
+        ct._owner = owner
+        return np.ctypeslib.as_array(ct)
     n = b.n_records
-    out = {}
-    for name, dt in FIELDS:
-        ptr = getattr(b, name)
-        out[name] = np.ctypeslib.as_array(ptr, shape=(n,)).astype(dt, copy=True) if n else \
-            np.zeros(0, dt)
-    out["raw"] = (np.ctypeslib.as_array(b.raw, shape=(b.raw_len,)).copy()
-                  if (b.raw and b.raw_len) else None)
+    out = {name: view(getattr(b, name), n, dt) for name, dt in FIELDS}
+    out["raw"] = view(b.raw, b.raw_len, np.uint8) if (b.raw and b.raw_len) else None
     npart = b.n_partitions
-    out["part_offset"] = np.ctypeslib.as_array(b.part_offset, shape=(npart + 1,)).copy()
-    out["part_digest"] = (np.ctypeslib.as_array(b.part_digest, shape=(npart,)).copy()
-                          if npart else np.zeros(0, np.uint64))
-    lib().dq_batch_free(bp)
+    out["part_offset"] = view(b.part_offset, npart + 1, np.int64)
+    out["part_digest"] = view(b.part_digest, npart, np.uint64) if npart else np.zeros(0, np.uint64)
     return out
 
 
@@ -225,11 +249,23 @@ class Context:
         check(self._h, lib().dq_open_shard_device(self._h, dev_ptr, length, base, file_len, p0,
                                                   p1, self._hdr.ctypes.data, len(self._hdr)))
 
-    def decode_chunk(self, path, vstart, vend, with_raw=True):
-        """BamSource.getIterator for one task: only the chunk's bytes are read (dq_decode_chunk)."""
+    def open_shard_path(self, path, base, length, p0, p1, header):
+        """Shard bytes [base, base + length) read from `path` by the library (dq_open_shard_path)."""
+        self._hdr = np.frombuffer(header, np.uint8).copy()
+        check(self._h, lib().dq_open_shard_path(self._h, os.fsencode(path), base, length, p0, p1,
+                                                self._hdr.ctypes.data, len(self._hdr)))
+
+    def decode_chunk(self, path, vstart, vend, with_raw=True, traversal=None):
+        """BamSource.getIterator (or createIndexIterator with a traversal) for one task: only the
+        chunk's bytes -- or its .bai span -- are read (dq_decode_chunk[_filtered])."""
         bp = C.POINTER(DqBatch)()
-        check(self._h, lib().dq_decode_chunk(self._h, os.fsencode(path), vstart, vend,
-                                             int(with_raw), C.byref(bp)))
+        if traversal is None:
+            check(self._h, lib().dq_decode_chunk(self._h, os.fsencode(path), vstart, vend,
+                                                 int(with_raw), C.byref(bp)))
+        else:
+            t, keep = self._traversal(traversal)
+            check(self._h, lib().dq_decode_chunk_filtered(self._h, os.fsencode(path), vstart, vend,
+                                                          C.byref(t), int(with_raw), C.byref(bp)))
         return batch_to_numpy(bp)
 
     def stats(self):

@@ -843,7 +843,7 @@ static int fetch_index(dq_ctx* ctx) {
 }
 
 // Two pinned staging buffers (file reads in, record batches out).
-constexpr size_t PIN_PIECE = 32u << 20;
+constexpr size_t PIN_PIECE = 64u << 20;
 static int ensure_pinned(dq_ctx* ctx) {
   if (ctx->pin_cap >= PIN_PIECE) return 0;
   for (int k = 0; k < 2; k++) {
@@ -880,7 +880,7 @@ static int d2h_large(dq_ctx* ctx, void* dst, const void* src, size_t n) {
     HIPCHK(hipEventSynchronize(ctx->pin_ev[i & 1]));
     if (i + 1 < np) HIPCHK(issue(i + 1));  // the other buffer is free: its piece was moved out
     const size_t off = i * PIN_PIECE, len = std::min(PIN_PIECE, n - off);
-    constexpr int T = 4;
+    constexpr int T = 8;
     std::thread th[T];
     const size_t part = (len + T - 1) / T;
     for (int t = 0; t < T; t++)
@@ -1456,8 +1456,8 @@ static int upload_file_range(dq_ctx* ctx, int fd, int64_t off, int64_t len) {
   for (int64_t done = 0; done < len; k ^= 1) {
     const size_t n = (size_t)std::min<int64_t>((int64_t)PIECE, len - done);
     if (used[k]) HIPCHK(hipEventSynchronize(ctx->pin_ev[k]));  // its previous copy is done
-    // four readers per piece (one thread copies out of the page cache at a fraction of PCIe)
-    constexpr int T = 4;
+    // eight readers per piece (one thread copies out of the page cache at a fraction of PCIe)
+    constexpr int T = 8;
     bool ok[T];
     std::thread th[T];
     const size_t part = (n + T - 1) / T;
@@ -1528,6 +1528,117 @@ static int load_header(dq_ctx* ctx, int fd, int64_t flen) {
     if (n >= flen) return rc;
     n = std::min<int64_t>(flen, n * 8);
   }
+}
+
+// The header of `path` into ctx->hdr, read once per context and path.
+static int chunk_header(dq_ctx* ctx, const char* path, int fd, int64_t flen) {
+  if (ctx->chunk_hdr_path == path) return 0;
+  ctx->chunk_hdr_path.clear();
+  int rc = load_header(ctx, fd, flen);
+  if (rc) return rc;
+  ctx->chunk_hdr_path = path;
+  return 0;
+}
+
+// One Chunk [vstart, vend) of an open file decoded from its own bytes (dq_decode_chunk): the
+// chunk's blocks, then enough to finish its last record (grown x4 while it runs past).  On
+// success *any says whether records were read; ctx->parts_h[0] is their range.
+static int chunk_run(dq_ctx* ctx, int fd, int64_t flen, uint64_t vstart, uint64_t vend, bool* any) {
+  *any = false;
+  const int64_t c0 = (int64_t)(vstart >> 16);
+  if (vend <= vstart || c0 >= flen) return 0;
+  int64_t extra = 256 << 10, h2d = ctx->h2d_bytes;
+  int rc;
+  for (;;) {
+    const int64_t c1 = std::min<int64_t>(flen, std::min<int64_t>(flen, (int64_t)(vend >> 16)) + extra);
+    if ((rc = upload_file_range(ctx, fd, c0, c1 - c0))) return rc;
+    h2d += c1 - c0;
+    ctx->shard = true;
+    ctx->base = c0;
+    ctx->file_len = flen;
+    ctx->p0 = 0;
+    ctx->p1 = 1;
+    ctx->chunk_mode = true;
+    ctx->chunk_vs = vstart - ((uint64_t)c0 << 16);
+    ctx->chunk_ve = vend - ((uint64_t)c0 << 16);
+    ctx->h2d_bytes = h2d;
+    rc = run_pipeline(ctx);
+    if (rc == DQ_EFORMAT && ctx->err.find("halo too small") != std::string::npos && c1 < flen) {
+      extra *= 4;
+      continue;
+    }
+    break;
+  }
+  ctx->chunk_mode = false;
+  ctx->stats.h2d_bytes = h2d;
+  if (rc) {
+    ctx->have_file = false;
+    return rc;
+  }
+  *any = true;
+  return 0;
+}
+
+// One batch holding the records of `parts` in order (a single partition).
+static int concat_batches(dq_ctx* ctx, const std::vector<dq_batch*>& parts, dq_batch** out) {
+  int64_t n = 0, raw = 0;
+  bool with_raw = true;
+  for (const dq_batch* b : parts) {
+    n += b->n_records;
+    raw += b->raw_len;
+    with_raw = with_raw && (b->raw != nullptr || b->n_records == 0);
+  }
+  dq_batch* o = (dq_batch*)calloc(1, sizeof(dq_batch));
+  if (!o) RET(DQ_ENOMEM, "out of host memory");
+  const size_t m = (size_t)std::max<int64_t>(1, n);
+  o->n_records = n;
+  o->voffset = (uint64_t*)malloc(8 * m);
+  o->block_size = (int32_t*)malloc(4 * m);
+  o->ref_id = (int32_t*)malloc(4 * m);
+  o->pos = (int32_t*)malloc(4 * m);
+  o->l_seq = (int32_t*)malloc(4 * m);
+  o->next_ref_id = (int32_t*)malloc(4 * m);
+  o->next_pos = (int32_t*)malloc(4 * m);
+  o->tlen = (int32_t*)malloc(4 * m);
+  o->flag = (uint16_t*)malloc(2 * m);
+  o->bin = (uint16_t*)malloc(2 * m);
+  o->n_cigar = (uint16_t*)malloc(2 * m);
+  o->mapq = (uint8_t*)malloc(m);
+  o->l_read_name = (uint8_t*)malloc(m);
+  o->hash = (uint64_t*)malloc(8 * m);
+  o->raw_offset = (int64_t*)malloc(8 * m);
+  o->raw = with_raw ? (uint8_t*)malloc((size_t)std::max<int64_t>(1, raw)) : nullptr;
+  o->raw_len = raw;
+  o->n_partitions = 1;
+  o->part_offset = (int64_t*)malloc(16);
+  o->part_digest = (uint64_t*)calloc(2, sizeof(uint64_t));
+  if (!o->voffset || !o->block_size || !o->ref_id || !o->pos || !o->l_seq || !o->next_ref_id ||
+      !o->next_pos || !o->tlen || !o->flag || !o->bin || !o->n_cigar || !o->mapq ||
+      !o->l_read_name || !o->hash || !o->raw_offset || (with_raw && !o->raw) || !o->part_offset ||
+      !o->part_digest) {
+    dq_batch_free(o);
+    RET(DQ_ENOMEM, "out of host memory");
+  }
+  int64_t k = 0, r = 0;
+  for (const dq_batch* b : parts) {
+    const size_t c = (size_t)b->n_records;
+#define CP(f, sz) memcpy(o->f + k, b->f, (sz) * c)
+    CP(voffset, 8); CP(block_size, 4); CP(ref_id, 4); CP(pos, 4); CP(l_seq, 4); CP(next_ref_id, 4);
+    CP(next_pos, 4); CP(tlen, 4); CP(flag, 2); CP(bin, 2); CP(n_cigar, 2); CP(mapq, 1);
+    CP(l_read_name, 1); CP(hash, 8);
+#undef CP
+    for (size_t i = 0; i < c; i++) o->raw_offset[k + (int64_t)i] = b->raw_offset[i] + r;
+    if (with_raw && b->raw_len) memcpy(o->raw + r, b->raw, (size_t)b->raw_len);
+    k += (int64_t)c;
+    r += b->raw_len;
+  }
+  o->part_offset[0] = 0;
+  o->part_offset[1] = n;
+  uint64_t d = 0;
+  for (int64_t i = 0; i < n; i++) d += dq_mix64(o->hash[i] + (uint64_t)(i + 1) * DQ_K_LEN);
+  o->part_digest[0] = d;
+  *out = o;
+  return 0;
 }
 
 // ------------------------------------------------------------------ C ABI
@@ -1635,6 +1746,26 @@ int dq_open_path(dq_ctx* ctx, const char* path) {
   return upload_file_range(ctx, f.fd, 0, len);
 }
 
+int dq_open_shard_path(dq_ctx* ctx, const char* path, int64_t base, int64_t len, int64_t p0,
+                       int64_t p1, const uint8_t* header, int64_t header_len) {
+  if (!ctx || !path || base < 0 || len <= 0 || p0 < 0 || p1 <= p0 || !header || header_len <= 0)
+    return DQ_EINVAL;
+  ON_DEVICE(ctx);
+  Fd f;
+  int64_t flen = 0;
+  int rc = open_fd(ctx, path, f, &flen);
+  if (rc) return rc;
+  if (base + len > flen) RET(DQ_EINVAL, "shard range past the end of the file");
+  if ((rc = upload_file_range(ctx, f.fd, base, len))) return rc;
+  ctx->shard = true;
+  ctx->base = base;
+  ctx->file_len = flen;
+  ctx->p0 = p0;
+  ctx->p1 = p1;
+  ctx->hdr.assign(header, header + header_len);
+  return 0;
+}
+
 int dq_decode_chunk(dq_ctx* ctx, const char* path, uint64_t vstart, uint64_t vend, int32_t with_raw,
                     dq_batch** out) {
   if (!ctx || !path || !out) return DQ_EINVAL;
@@ -1643,45 +1774,123 @@ int dq_decode_chunk(dq_ctx* ctx, const char* path, uint64_t vstart, uint64_t ven
   int64_t flen = 0;
   int rc = open_fd(ctx, path, f, &flen);
   if (rc) return rc;
-  if (ctx->chunk_hdr_path != path) {
-    ctx->chunk_hdr_path.clear();
-    if ((rc = load_header(ctx, f.fd, flen))) return rc;
-    ctx->chunk_hdr_path = path;
-  }
-  const int64_t c0 = (int64_t)(vstart >> 16);
-  if (vend <= vstart || c0 >= flen) return make_batch(ctx, {}, nullptr, with_raw, {0, 0}, out);
-  // the chunk's blocks, then enough to finish its last record: grown x4 while it runs past
-  int64_t extra = 256 << 10, h2d = 0;
-  for (;;) {
-    const int64_t c1 = std::min<int64_t>(flen, (int64_t)(vend >> 16) + extra);
-    if ((rc = upload_file_range(ctx, f.fd, c0, c1 - c0))) return rc;
-    h2d += c1 - c0;
-    ctx->shard = true;
-    ctx->base = c0;
-    ctx->file_len = flen;
-    ctx->p0 = 0;
-    ctx->p1 = 1;
-    ctx->chunk_mode = true;
-    ctx->chunk_vs = vstart - ((uint64_t)c0 << 16);
-    ctx->chunk_ve = vend - ((uint64_t)c0 << 16);
-    ctx->h2d_bytes = h2d;
-    rc = run_pipeline(ctx);
-    if (rc == DQ_EFORMAT && ctx->err.find("halo too small") != std::string::npos && c1 < flen) {
-      extra *= 4;
-      continue;
-    }
-    break;
-  }
-  ctx->chunk_mode = false;
-  if (rc) {
-    ctx->have_file = false;
-    return rc;
-  }
+  if ((rc = chunk_header(ctx, path, f.fd, flen))) return rc;
+  ctx->h2d_bytes = 0;
+  bool any = false;
+  if ((rc = chunk_run(ctx, f.fd, flen, vstart, vend, &any))) return rc;
+  if (!any) return make_batch(ctx, {}, nullptr, with_raw, {0, 0}, out);
   const PartRange r = ctx->parts_h[0];
   rc = make_batch(ctx, {{r.begin, r.end}}, nullptr, with_raw, {0, r.end - r.begin}, out);
   ctx->have_file = false;  // the window is not a file the other calls can use
   ctx->have_pipeline = false;
   return rc;
+}
+
+int dq_decode_chunk_filtered(dq_ctx* ctx, const char* path, uint64_t vstart, uint64_t vend,
+                             const dq_traversal* tr, int32_t with_raw, dq_batch** out) {
+  if (!ctx || !path || !out || !tr) return DQ_EINVAL;
+  ON_DEVICE(ctx);
+  if (!tr->has_intervals && !tr->traverse_unplaced_unmapped)
+    RET(DQ_EINVAL, "Traversing mapped reads only is not supported.");
+  if (!ctx->have_bai) RET(DQ_EINVAL, "Intervals set but no index file found");
+  Fd f;
+  int64_t flen = 0;
+  int rc = open_fd(ctx, path, f, &flen);
+  if (rc) return rc;
+  if ((rc = chunk_header(ctx, path, f.fd, flen))) return rc;
+  ctx->h2d_bytes = 0;
+  std::vector<dq_batch*> parts;
+  auto cleanup = [&](int code) {
+    for (dq_batch* b : parts) dq_batch_free(b);
+    ctx->have_file = false;
+    ctx->have_pipeline = false;
+    return code;
+  };
+  if (tr->has_intervals && tr->n > 0) {
+    // the .bai span of the optimized intervals clipped to this chunk (AbstractBinarySamSource
+    // .java:102-107); nearby span chunks are read as one window
+    std::vector<Interval> iv;
+    for (int64_t i = 0; i < tr->n; i++) {
+      if (tr->ref[i] < 0 || tr->ref[i] >= ctx->n_ref) return cleanup(DQ_EINVAL);
+      iv.push_back({tr->ref[i], tr->start[i], tr->end[i]});
+    }
+    const std::vector<VChunk> span = clip_span(file_span(ctx->bai, optimize(iv)), vstart, vend);
+    constexpr int64_t GAP = 1 << 20;  // compressed bytes between chunks read through
+    for (size_t i = 0; i < span.size();) {
+      size_t j = i + 1;
+      while (j < span.size() && (int64_t)(span[j].b >> 16) <= (int64_t)(span[j - 1].e >> 16) + GAP) j++;
+      bool any = false;
+      if ((rc = chunk_run(ctx, f.fd, flen, span[i].b, span[j - 1].e, &any))) return cleanup(rc);
+      if (any) {
+        // records of the window inside one of its span chunks (BAMFileIndexIterator over the
+        // chunk list), then kernel 4 (BAMQueryMultipleIntervalsIteratorFilter, contained=false)
+        const PartRange r = ctx->parts_h[0];
+        std::vector<uint64_t> v((size_t)(r.end - r.begin));
+        if (!v.empty())
+          HIPCHK(hipMemcpy(v.data(), ctx->f_voff.as<uint64_t>() + r.begin, 8 * v.size(),
+                           hipMemcpyDeviceToHost));
+        const uint64_t vb = (uint64_t)ctx->base << 16;
+        std::vector<int64_t> idx;
+        size_t c = i;
+        for (size_t k = 0; k < v.size(); k++) {
+          const uint64_t x = v[k] + vb;
+          while (c < j && span[c].e <= x) c++;
+          if (c < j && span[c].b <= x) idx.push_back(r.begin + (int64_t)k);
+        }
+        std::vector<int64_t> kept;
+        if (!idx.empty()) {
+          const int64_t n = (int64_t)idx.size();
+          if ((rc = upload_intervals(ctx, tr)) || (rc = ensure_all(ctx, ctx->idx, 8 * (size_t)n)) ||
+              (rc = ensure_all(ctx, ctx->keep, (size_t)n)))
+            return cleanup(rc);
+          HIPCHK(hipMemcpy(ctx->idx.p, idx.data(), 8 * (size_t)n, hipMemcpyHostToDevice));
+          ctx->iota_n = -1;
+          launch_interval_filter(ctx->U.as<uint8_t>(), ctx->rec_lin.as<int64_t>(), ctx->soa(),
+                                 ctx->idx.as<int64_t>(), n, ctx->iv_ref.as<int32_t>(),
+                                 ctx->iv_start.as<int32_t>(), ctx->iv_end.as<int32_t>(),
+                                 ctx->iv_begin.as<int32_t>(), ctx->n_ref, ctx->keep.as<uint8_t>(),
+                                 ctx->s);
+          std::vector<uint8_t> keep((size_t)n);
+          HIPCHK(hipMemcpyAsync(keep.data(), ctx->keep.p, (size_t)n, hipMemcpyDeviceToHost, ctx->s));
+          HIPCHK(hipStreamSynchronize(ctx->s));
+          for (int64_t k = 0; k < n; k++)
+            if (keep[(size_t)k]) kept.push_back(idx[(size_t)k]);
+        }
+        dq_batch* b = nullptr;
+        if ((rc = make_batch(ctx, {}, &kept, with_raw, {0, (int64_t)kept.size()}, &b))) return cleanup(rc);
+        parts.push_back(b);
+      }
+      i = j;
+    }
+  }
+  // the unplaced-unmapped tail (AbstractBinarySamSource.java:116-129; queryUnmapped,
+  // H/BAMFileReader2.java:715-738): from the .bai's start of the last linear bin to EOF, the
+  // records from the first one with refID -1 on
+  if (tr->traverse_unplaced_unmapped && ctx->solb != -1 && ctx->ncc >= 1 &&
+      vstart <= (uint64_t)ctx->solb && (uint64_t)ctx->solb < vend) {
+    bool any = false;
+    if ((rc = chunk_run(ctx, f.fd, flen, (uint64_t)ctx->solb, ((uint64_t)flen << 16) | 0xffff, &any)))
+      return cleanup(rc);
+    if (any) {
+      const PartRange r = ctx->parts_h[0];
+      std::vector<int32_t> refs((size_t)(r.end - r.begin));
+      if (!refs.empty())
+        HIPCHK(hipMemcpy(refs.data(), ctx->f_ref.as<int32_t>() + r.begin, 4 * refs.size(),
+                         hipMemcpyDeviceToHost));
+      size_t k = 0;
+      while (k < refs.size() && refs[k] != -1) k++;
+      dq_batch* b = nullptr;
+      if ((rc = make_batch(ctx, {{r.begin + (int64_t)k, r.end}}, nullptr, with_raw,
+                           {0, r.end - r.begin - (int64_t)k}, &b)))
+        return cleanup(rc);
+      parts.push_back(b);
+    }
+  }
+  dq_batch* all = nullptr;
+  if ((rc = concat_batches(ctx, parts, &all))) return cleanup(rc);
+  cleanup(0);
+  *out = all;
+  return 0;
 }
 
 int dq_get_stats(dq_ctx* ctx, dq_stats* stats) {

@@ -110,17 +110,18 @@ enum { M_ERR = 0, M_BFINAL, M_BTYPE, M_POS, M_A, M_LAST, M_MORE, M_MORE1, M_STLE
 
 __device__ __attribute__((always_inline)) inline void set_err(LdsI& L, int32_t code) { atomicCAS(&L.misc[M_ERR], 0, code); }
 
-// Bit reader: a 64-bit LSB-first buffer refilled 32 bits at a time from a 4-word staging
-// queue q0, with the following 4 words already in flight in q1.  A refill never touches a word
-// loaded less than a queue length (~14 symbols) earlier, so its s_waitcnt rarely stalls (moving a
-// just-loaded word between registers would force an immediate vmcnt(0) wait on every refill).
+// Bit reader: a 64-bit LSB-first buffer refilled 32 bits at a time from `st`, the 16-byte group
+// of input words that holds the next word.  Every refill call reloads the group of the (new) next
+// word unconditionally (one global_load_dwordx4, almost always an L1/L2 hit on the same line):
+// the load then always lands in the loop-carried registers -- a conditional reload made the
+// compiler load into temporaries and copy them back, waiting for the load at once -- and is first
+// waited for at the next call, half a symbol later.  W is 16-byte aligned.
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 struct BitR {
   uint64_t bb;
   uint32_t bc;
   uint32_t wp;    // word index of the next word to enter bb (br_pos = 32 * wp - bc)
-  uint32_t qn;    // words of q0 consumed
-  uint32_t q0[4];
-  uint32_t q1[4];
+  u32x4v st;      // words [wp & ~3, +4)
 };
 
 #define DQ_AI __device__ __attribute__((always_inline)) inline
@@ -138,28 +139,16 @@ DQ_AI void br_init(BitR& r, const uint32_t* __restrict__ W, uint32_t bitpos) {
   r.bb = ((hi << 32) | lo) >> sh;
   r.bc = 64 - sh;
   r.wp = wi + 2;
-  r.qn = 0;
-#pragma unroll
-  for (int k = 0; k < 4; k++) r.q0[k] = W[wi + 2 + k];
-#pragma unroll
-  for (int k = 0; k < 4; k++) r.q1[k] = W[wi + 6 + k];
+  r.st = reinterpret_cast<const u32x4v*>(W)[r.wp >> 2];
 }
 DQ_AI void br_refill(BitR& r, const uint32_t* __restrict__ W) {
-  if (r.bc <= 32) {
-    r.bb |= (uint64_t)r.q0[0] << r.bc;
-    r.bc += 32;
-    r.wp++;
-    r.q0[0] = r.q0[1];
-    r.q0[1] = r.q0[2];
-    r.q0[2] = r.q0[3];
-    if (++r.qn == 4) {
-#pragma unroll
-      for (int k = 0; k < 4; k++) r.q0[k] = r.q1[k];
-#pragma unroll
-      for (int k = 0; k < 4; k++) r.q1[k] = W[r.wp + 4 + k];
-      r.qn = 0;
-    }
-  }
+  const bool need = r.bc <= 32;
+  const uint32_t q = r.wp & 3;
+  const uint32_t w = q == 0 ? r.st.x : q == 1 ? r.st.y : q == 2 ? r.st.z : r.st.w;
+  r.bb |= need ? (uint64_t)w << r.bc : 0ull;
+  r.bc += need ? 32u : 0u;
+  r.wp += need ? 1u : 0u;
+  r.st = reinterpret_cast<const u32x4v*>(W)[r.wp >> 2];
 }
 DQ_AI uint32_t br_pos(const BitR& r) { return r.wp * 32 - r.bc; }
 DQ_AI uint32_t br_take(BitR& r, uint32_t n) {
@@ -664,9 +653,9 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   // (pointer arithmetic on C keeps the global address space: an integer round trip would turn
   // every load into a FLAT load, which the compiler must wait for with vmcnt(0) lgkmcnt(0))
   const uint8_t* dp = C + cpos + 18;
-  const int mis = (int)(reinterpret_cast<uintptr_t>(dp) & 3);
+  const int mis = (int)(reinterpret_cast<uintptr_t>(dp) & 15);
   const uint32_t* W =
-      reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(dp - mis, 4));
+      reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(dp - mis, 16));
   const uint32_t a0 = 8u * (uint32_t)mis;
   const int32_t dbytes = csize - 26;
   const uint32_t endbits = a0 + 8u * (uint32_t)max(dbytes, 0);

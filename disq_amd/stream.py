@@ -17,20 +17,21 @@ from __future__ import annotations
 import math
 import threading
 import time
-from typing import Callable, Optional
+from typing import Optional
 
 import numpy as np
 
 from . import parallel as P
 
 
-def stream_read(read_bytes: Callable[[int, int], bytes], file_len: int, header: bytes,
+def stream_read(read_bytes, file_len: int, header: bytes,
                 window: int = 8 << 30, depth: int = 2, split_size: int = 0,
                 use_nio: bool = False, hadoop_block_size: int = 0, device: int = 0,
                 verify_crc: bool = True, halo: int = 4 << 20, on_window=None) -> dict:
     """Decode the whole file in windows of ~`window` compressed bytes on one GPU.
 
-    read_bytes(a, b) returns the file's bytes [a, b) (page cache, host memory or a generator).
+    read_bytes(a, b) returns the file's bytes [a, b) (page cache, host memory or a generator), or
+    read_bytes is a path: the library reads each window itself (dq_open_shard_path).
     on_window(k, ctx, shard), if given, runs on the window's context after its pipeline (e.g. to
     export records with ctx.read()).  Returns the per-partition counts and digests, the whole-file
     digest, record and decompressed byte totals, and timings."""
@@ -61,9 +62,12 @@ def stream_read(read_bytes: Callable[[int, int], bytes], file_len: int, header: 
                     h = halo
                     while True:
                         end = min(file_len, s.hi + h)
-                        data = read_bytes(s.lo, end)
                         try:
-                            c.open_shard(data, s.lo, file_len, s.p0, s.p1, header)
+                            if isinstance(read_bytes, str):
+                                c.open_shard_path(read_bytes, s.lo, end - s.lo, s.p0, s.p1, header)
+                            else:
+                                c.open_shard(read_bytes(s.lo, end), s.lo, file_len, s.p0, s.p1,
+                                             header)
                             st = c.run_resident()
                             break
                         except _lib.DqError as e:
@@ -104,13 +108,12 @@ def stream_read_path(path: str, header: Optional[bytes] = None, **kw) -> dict:
     import os
     file_len = os.path.getsize(path)
 
-    def read_bytes(a, b):
-        with open(path, "rb") as f:
-            f.seek(a)
-            return f.read(b - a)
     if header is None:
         from . import _lib
+
+        def prefix(n):
+            with open(path, "rb") as f:
+                return f.read(n)
         with _lib.Context(device=kw.get("device", 0)) as c:
-            header = P.broadcast_header(c.header_from_prefix, lambda n: read_bytes(0, n), file_len,
-                                        0, 1)
-    return stream_read(read_bytes, file_len, header, **kw)
+            header = P.broadcast_header(c.header_from_prefix, prefix, file_len, 0, 1)
+    return stream_read(path, file_len, header, **kw)

@@ -171,6 +171,12 @@ int dq_open_shard_device(dq_ctx* ctx, const void* dev_bytes, int64_t len, int64_
                          int64_t file_len, int64_t p0, int64_t p1, const uint8_t* header,
                          int64_t header_len);
 
+/* The same, reading the shard's bytes [base, base + len) from `path` itself (pinned staging,
+ * parallel reads from the page cache overlapped with the copies to the device): the streaming
+ * (out-of-core) reader's windows and multi-GPU ranks that read a shared file. */
+int dq_open_shard_path(dq_ctx* ctx, const char* path, int64_t base, int64_t len, int64_t p0,
+                       int64_t p1, const uint8_t* header, int64_t header_len);
+
 /* The decompressed BAM header (AbstractSamSource.getFileHeader, D/impl/formats/sam/
  * AbstractSamSource.java:32-49) from the first `len` bytes of a file: enough BGZF blocks to hold
  * it (the last one may be cut).  Writes up to cap bytes to out; *out_len = header length.  Used
@@ -214,6 +220,16 @@ int dq_decode(dq_ctx* ctx, uint64_t vstart, uint64_t vend, int32_t with_raw, dq_
  * (dq_get_stats) reports the compressed bytes copied to the device. */
 int dq_decode_chunk(dq_ctx* ctx, const char* path, uint64_t vstart, uint64_t vend, int32_t with_raw,
                     dq_batch** out);
+
+/* createIndexIterator(intervals, contained=false) + the unplaced-unmapped tail for one task
+ * (AbstractBinarySamSource.java:86-134) with no resident file: the .bai span of the optimized
+ * intervals (dq_set_index first) clipped to the chunk is the only part of `path` read -- span
+ * chunks closer than 1 MiB are read as one window, each decoded from its exact start pointer --
+ * then kernel 4 keeps the overlapping records; if the chunk holds the .bai's start of the last
+ * linear bin and traverse_unplaced_unmapped is set, the records with refID -1 from there to EOF
+ * follow (queryUnmapped).  One partition in the batch. */
+int dq_decode_chunk_filtered(dq_ctx* ctx, const char* path, uint64_t vstart, uint64_t vend,
+                             const dq_traversal* tr, int32_t with_raw, dq_batch** out);
 
 /* createIndexIterator(intervals, contained=false) over one chunk, plus the unplaced-unmapped
  * tail when the chunk contains the .bai's start of the last linear bin. */

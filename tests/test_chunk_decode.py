@@ -99,3 +99,52 @@ def test_context_used_from_another_thread(golden):
     t.join(120)
     c.close()
     assert np.array_equal(out["b"]["hash"], ob.read_chunk(*ch)["hash"])
+
+
+def check_filtered(path, bai, split, ivs, unplaced):
+    data = open(path, "rb").read()
+    ob = O.OracleBam(data)
+    parts = iter(ob.read_partitions(split, traversal=(ivs, unplaced), bai=bai))
+    n = 0
+    with _lib.Context(split_size=split, verify_crc=True) as c:
+        c.set_index(bai)
+        for s, e, ch in ob.plan(split):
+            if ch is None:
+                continue
+            b = c.decode_chunk(path, *ch, traversal=(ivs, unplaced))
+            ref = next(parts)
+            assert len(b["voffset"]) == len(ref), (s, e)
+            for f in FIELDS:
+                assert np.array_equal(b[f], ref[f]), (s, f)
+            n += len(ref)
+    return n
+
+
+@pytest.mark.parametrize("split", [40000, 8000, 3000])
+@pytest.mark.parametrize("ivs,unplaced,expected", [
+    ([(20, 5000, 9999), (20, 20000, 22999)], False, 16),
+    ([(20, 5000, 9999), (20, 20000, 22999)], True, 18),
+    ([(20, 1, 1000135)], False, 2000),
+    (None, True, 2),
+    ([], True, 2),
+])
+def test_anysam_filtered_chunks(tmp_path, split, ivs, unplaced, expected):
+    a = synth.generate(1000, shape=synth.ANYSAM, bai=True)
+    p = str(tmp_path / "a.bam")
+    a.write(p)
+    assert check_filtered(p, a.bai, split, ivs, unplaced) == expected
+
+
+def test_wgs_filtered_chunks(tmp_path):
+    """Many intervals on a WGS-like file: each task reads only its chunk's .bai span."""
+    w = synth.generate(60000, seed=41, bai=True, nthreads=8, unplaced_fraction=0.01)
+    p = str(tmp_path / "w.bam")
+    w.write(p)
+    rng = np.random.default_rng(4)
+    ivs = [(0, int(s), int(s + rng.integers(10, 600))) for s in rng.integers(1, 290000, size=200)]
+    for unplaced in (False, True):
+        assert check_filtered(p, w.bai, 1 << 20, ivs, unplaced) > 0
+    with _lib.Context(split_size=1 << 20) as c:
+        c.set_index(w.bai)
+        c.decode_chunk(p, *O.OracleBam(w.bam).plan(1 << 20)[0][2], traversal=(ivs[:3], False))
+        assert c.stats().h2d_bytes < len(w.bam) // 2

@@ -36,3 +36,14 @@ def test_stream_long_reads_grow_halo():
     out = stream.stream_read(lambda a, b: data[a:b], len(data), header, window=1 << 20, depth=2,
                              split_size=256 << 10, halo=4096)
     assert out["digest"] == st.digest and out["n_records"] == st.n_records
+
+
+def test_stream_from_path(tmp_path):
+    r = synth.generate(60000, seed=37, nthreads=8)
+    p = str(tmp_path / "s.bam")
+    r.write(p)
+    with _lib.Context(split_size=1 << 20, verify_crc=True) as c:
+        c.open_path(p)
+        st = c.run_resident()
+    out = stream.stream_read_path(p, window=2 << 20, depth=2, split_size=1 << 20, halo=32 << 10)
+    assert out["digest"] == st.digest and out["n_records"] == 60000

@@ -67,12 +67,8 @@ def main():
                          "open_h2d_s": round(t1 - t0, 3), "device_ms": round(st.ms_total, 2),
                          "kernel_gbs": round(st.decompressed_bytes / st.ms_total / 1e6, 2)}
             log(f"[stream] whole file: {whole}")
-        fd = os.open(path, os.O_RDONLY)
-
-        def read_bytes(a, b):
-            return os.pread(fd, b - a, a)
         window = int(args.window_gb * 1e9)
-        s = stream.stream_read(read_bytes, flen, header, window=window, depth=args.depth)
+        s = stream.stream_read(path, flen, header, window=window, depth=args.depth)
         log(f"[stream] streaming: {s['seconds']:.2f} s, {s['windows']} windows")
         exported = {"records": 0, "raw_bytes": 0}
 
@@ -80,9 +76,8 @@ def main():
             b = c.read(with_raw=True)
             exported["records"] += len(b["voffset"])
             exported["raw_bytes"] += 0 if b["raw"] is None else len(b["raw"])
-        e = stream.stream_read(read_bytes, flen, header, window=window, depth=args.depth,
+        e = stream.stream_read(path, flen, header, window=window, depth=args.depth,
                                on_window=export)
-        os.close(fd)
         out.update({
             "window_gb": args.window_gb, "depth": args.depth, "windows": s["windows"],
             "whole_file": whole,
@@ -90,7 +85,7 @@ def main():
                           "seconds": round(s["seconds"], 3),
                           "decompressed_gbs": round(s["owned_bytes"] / s["seconds"] / 1e9, 3),
                           "compressed_read_gb": round(s["compressed_read"] / 1e9, 3),
-                          "path": "page cache -> H2D (pageable) -> pipeline; records stay in HBM"},
+                          "path": "page cache -> pinned staging (dq_open_shard_path) -> pipeline; records stay in HBM"},
             "end_to_end": {"digest": f"{e['digest']:016x}", "seconds": round(e["seconds"], 3),
                            "decompressed_gbs": round(e["owned_bytes"] / e["seconds"] / 1e9, 3),
                            "reads_per_s": round(e["n_records"] / e["seconds"], 1),
