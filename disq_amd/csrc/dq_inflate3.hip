@@ -126,6 +126,17 @@ struct BitR {
 
 #define DQ_AI __device__ __attribute__((always_inline)) inline
 
+// The thread index behind an empty volatile asm: values derived from it cannot be hoisted out of
+// the deflate-block loop.  Hoisted per-thread constants (bit-reversed indices, LDS addresses,
+// lane masks) lived across the whole loop and were spilled to scratch once per workgroup --
+// 48 B/thread, ~24 KiB of HBM writes per BGZF block -- while recomputing them costs a few VALU
+// ops per deflate block.
+DQ_AI int tid_fresh() {
+  int t = (int)threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 DQ_AI void st_nt(uint4* d, uint4 v) {  // streaming store (nt): U is not re-read by this kernel
   u32x4 x = {v.x, v.y, v.z, v.w};
@@ -446,7 +457,7 @@ DQ_AI int canon_from_counts(LdsI& L, HuffCanon& h, int32_t* q0p, int32_t* qnp) {
 // Build both decode tables from L.u.d.x.h.lens (all threads; barriers inside).
 // Litlen symbols are handled by threads 0..319 (waves 0-4), distance symbols by wave 5.
 DQ_AI void build_tables(LdsI& L, int nlen, int ndist) {
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int t = tid_fresh(), lane = t & 63, wv = t >> 6;
   for (int i = t; i < T_END; i += WG) L.u.d.T[i] = 0;
   const bool isl = t < 320, isd = t >= 320 && t < 352;
   const int sym = isl ? t : t - 320;
@@ -541,7 +552,7 @@ DQ_AI uint32_t read_lengths(const uint32_t* __restrict__ W, LdsI& L, uint32_t P,
   // words cover the longest possible header (17 + 57 + 320 * 14 bits)
   const uint32_t* hb = reinterpret_cast<const uint32_t*>(L.u.d.T);
   auto word = [&](uint32_t i) -> uint32_t { return hb[min(i - hbase, (uint32_t)HB_WORDS - 1)]; };
-  const int lane = threadIdx.x & 63;
+  const int lane = tid_fresh() & 63;
   const int total = nlen + ndist;
   int have = 0, prev = -1;
   for (int iter = 0; iter < 400 && have < total; iter++) {
@@ -670,6 +681,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   __syncthreads();
   int32_t produced = 0;
   while (L.misc[M_ERR] == 0 && produced < isize) {
+    const int t = tid_fresh(), lane = t & 63, wv = t >> 6;
     // ---- 1. block header
     if (t == 0) {
       const uint32_t pos = (uint32_t)L.misc[M_POS];
