@@ -81,7 +81,7 @@ EXPORTS = ("dq_ctx_create", "dq_ctx_destroy", "dq_last_error", "dq_version", "dq
            "dq_batch_free", "dq_free", "dq_open_shard", "dq_header_from_prefix",
            "dq_set_splitting_index", "dq_write_sbi", "dq_open_shard_device", "dq_decode_chunk",
            "dq_get_stats", "dq_partition_digests", "dq_open_shard_path",
-           "dq_decode_chunk_filtered")
+           "dq_decode_chunk_filtered", "dq_debug_guess_all")
 
 _lib = None
 _lock = threading.Lock()
@@ -133,6 +133,7 @@ def lib():
         L.dq_read.argtypes = [vp, P(DqTraversal), C.c_int32, P(P(DqBatch))]
         L.dq_run_resident.argtypes = [vp, P(DqTraversal), P(DqStats)]
         L.dq_debug_inflated.argtypes = [vp, vp, C.c_int64, P(C.c_int64)]
+        L.dq_debug_guess_all.argtypes = [vp, vp, C.c_int64, P(C.c_int64)]
         L.dq_batch_free.argtypes = [P(DqBatch)]
         L.dq_free.argtypes = [vp]
         _lib = L
@@ -386,4 +387,13 @@ class Context:
         check(self._h, lib().dq_debug_inflated(self._h, None, 0, C.byref(n)))
         out = np.zeros(max(1, n.value), np.uint8)
         check(self._h, lib().dq_debug_inflated(self._h, out.ctypes.data, n.value, C.byref(n)))
+        return out[: n.value]
+
+    def guess_all(self):
+        """Virtual offsets where the GPU record guesser fires, over every decompressed position
+        of the resident file (dq_debug_guess_all)."""
+        n = C.c_int64()
+        check(self._h, lib().dq_debug_guess_all(self._h, None, 0, C.byref(n)))
+        out = np.zeros(max(1, n.value), np.uint64)
+        check(self._h, lib().dq_debug_guess_all(self._h, out.ctypes.data, n.value, C.byref(n)))
         return out[: n.value]

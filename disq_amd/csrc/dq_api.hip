@@ -693,9 +693,13 @@ static int run_pipeline(dq_ctx* ctx) {
     if (P.status == 100 && ctx->shard && !is_eof)
       RET(DQ_EFORMAT, "shard halo too small: the record guesser needs bytes past the shard");
     if (P.status != 0) {
-      char msg[160];
-      snprintf(msg, sizeof msg, "split planning failed (code %d) for split [%lld, %lld)", P.status,
-               (long long)P.split_start, (long long)P.split_end);
+      char msg[224];
+      snprintf(msg, sizeof msg, "split planning failed for split [%lld, %lld): %s (code %d)",
+               (long long)P.split_start, (long long)P.split_end,
+               P.status == ST_BAD_HEADER ? "the guessed BGZF block is a member header inside block "
+                                           "payload that carries data"
+                                         : status_name(P.status),
+               P.status);
       RET(DQ_EFORMAT, msg);
     }
     if (P.rec_lin >= 0 && start_lin < 0) start_lin = P.rec_lin;
@@ -2196,6 +2200,37 @@ int dq_debug_inflated(dq_ctx* ctx, uint8_t* host_out, int64_t cap, int64_t* len)
   if (len) *len = ctx->ulen;
   if (host_out && cap > 0)
     HIPCHK(hipMemcpy(host_out, ctx->U.p, (size_t)std::min(cap, ctx->ulen), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int dq_debug_guess_all(dq_ctx* ctx, uint64_t* voffs, int64_t cap, int64_t* n) {
+  if (!ctx || !n) return DQ_EINVAL;
+  ON_DEVICE(ctx);
+  if (ctx->shard || ctx->chunk_mode) RET(DQ_EINVAL, "dq_debug_guess_all checks a whole resident file");
+  int rc = run_pipeline(ctx);
+  if (rc) return rc;
+  const int64_t ulen = ctx->ulen;
+  DevBuf d;
+  HIPCHK(d.ensure((size_t)std::max<int64_t>(ulen, 1)));
+  launch_guess_all(ctx->U.as<uint8_t>(), ulen, 1, ctx->d_ref_len.as<int32_t>(), ctx->n_ref,
+                   d.as<uint8_t>(), ctx->s);
+  HIPCHK(hipGetLastError());
+  std::vector<uint8_t> f((size_t)ulen);
+  std::vector<int64_t> uo((size_t)ctx->nblk + 1), bp((size_t)ctx->nblk);
+  HIPCHK(hipMemcpyAsync(f.data(), d.p, (size_t)ulen, hipMemcpyDeviceToHost, ctx->s));
+  HIPCHK(hipMemcpyAsync(uo.data(), ctx->uoff.p, 8 * uo.size(), hipMemcpyDeviceToHost, ctx->s));
+  HIPCHK(hipMemcpyAsync(bp.data(), ctx->blk_pos.p, 8 * bp.size(), hipMemcpyDeviceToHost, ctx->s));
+  HIPCHK(hipStreamSynchronize(ctx->s));
+  int64_t k = 0;
+  size_t j = 0;
+  for (int64_t x = 0; x < ulen; x++) {
+    if (f[(size_t)x] == 4) RET(DQ_EFORMAT, "guesser needed data past the end of a whole file");
+    if (f[(size_t)x] != 1) continue;
+    while (j + 1 < bp.size() && uo[j + 1] <= x) j++;
+    if (k < cap && voffs) voffs[k] = ((uint64_t)bp[j] << 16) | (uint64_t)(x - uo[j]);
+    k++;
+  }
+  *n = k;
   return 0;
 }
 

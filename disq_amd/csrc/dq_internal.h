@@ -94,6 +94,8 @@ struct SplitPlan {
 void launch_plan_blocks(const Cand* cand, const int64_t* d_ncand, const int64_t* blk_pos,
                         const int32_t* blk_usize, const int64_t* uoff, const int64_t* d_nblk,
                         SplitPlan* plans, int64_t nsplit, hipStream_t s);
+void launch_guess_all(const uint8_t* U, int64_t ulen, int32_t u_is_eof, const int32_t* ref_len,
+                      int32_t n_ref, uint8_t* flag, hipStream_t s);
 void launch_first_record(const uint8_t* U, int64_t ulen, int32_t u_is_eof, const int32_t* ref_len,
                          int32_t n_ref, const int64_t* blk_pos, const int64_t* uoff,
                          const int64_t* d_nblk, SplitPlan* plans, int64_t nsplit, hipStream_t s);

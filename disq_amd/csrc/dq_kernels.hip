@@ -385,24 +385,39 @@ __global__ void plan_blocks_kernel(const Cand* __restrict__ cand, const int64_t*
   P.status = 0;
   const int64_t s = P.split_start, e = P.split_end;
   int64_t p = s;
-  int64_t found = -1;
-  for (;;) {
-    int64_t k = lower_bound_cand(cand, nc, p);
-    if (k >= nc) break;             // scan runs off the data -> null
-    const Cand c = cand[k];
-    if (c.pos != p && c.pos >= e) break;  // :91 end check (skipped for the first position)
-    if (c.valid == 1) {
-      found = c.pos;
-      break;
+  int64_t found = -1, j = -1;
+  // BgzfBlockSource's lazy iterator (BgzfBlockSource.java:63-84): guess from `start`, then from
+  // the guessed block's end, while start <= split end.  A guess off the BGZF chain is a member
+  // header inside payload (stored blocks keep payload bytes verbatim): an empty one (uSize 0)
+  // gives getFirstReadInPartition no positions to test, so the iterator just moves on past it;
+  // one with data would be inflated by the reference (which then fails on the bytes after it,
+  // or reads garbage) -- not reproduced: reported as ST_BAD_HEADER.
+  for (int hops = 0; found < 0; hops++) {
+    if (p > e || hops > 4096) return;
+    int64_t g = -1;
+    for (;;) {
+      int64_t k = lower_bound_cand(cand, nc, p);
+      if (k >= nc) break;             // scan runs off the data -> null
+      const Cand c = cand[k];
+      if (c.pos != p && c.pos >= e) break;  // :91 end check (skipped for the first position)
+      if (c.valid == 1) {
+        g = k;
+        break;
+      }
+      if (c.valid == 2) break;        // IOException -> null
+      p = c.pos + 4;                  // :144, tested without an end check
     }
-    if (c.valid == 2) break;        // IOException -> null
-    p = c.pos + 4;                  // :144, tested without an end check
-  }
-  if (found < 0) return;
-  int64_t j = lower_bound_i64(blk_pos, nb, found);
-  if (j >= nb || blk_pos[j] != found) {
-    P.status = ST_BAD_HEADER;  // guessed block is not on the BGZF chain
-    return;
+    if (g < 0) return;
+    const Cand c = cand[g];
+    j = lower_bound_i64(blk_pos, nb, c.pos);
+    if (j < nb && blk_pos[j] == c.pos) {
+      found = c.pos;
+    } else if (c.usize == 0 && c.csize > 0) {
+      p = c.pos + c.csize;            // an empty member inside payload: skipped
+    } else {
+      P.status = ST_BAD_HEADER;       // a member with data inside payload
+      return;
+    }
   }
   // BgzfBlockSource: blocks while start <= split end
   int64_t jl = j;
@@ -1194,6 +1209,22 @@ void launch_plan_blocks(const Cand* cand, const int64_t* d_ncand, const int64_t*
   if (nsplit <= 0) return;
   hipLaunchKernelGGL(plan_blocks_kernel, dim3((unsigned)((nsplit + 63) / 64)), dim3(64), 0, s,
                      cand, d_ncand, blk_pos, blk_usize, uoff, d_nblk, plans, nsplit);
+}
+
+// Guesser at every position of the resident stream (BamRecordGuesserChecker's exhaustive check,
+// D/impl/formats/bam/BamRecordGuesserChecker.java:104-120): flag[x] = checkRecordStart(x).
+__global__ void guess_all_kernel(const uint8_t* U, int64_t ulen, int32_t u_is_eof,
+                                 const int32_t* ref_len, int32_t n_ref, uint8_t* flag) {
+  const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= ulen) return;
+  flag[x] = (uint8_t)check_record_start(U, ulen, u_is_eof, ref_len, n_ref, x);
+}
+
+void launch_guess_all(const uint8_t* U, int64_t ulen, int32_t u_is_eof, const int32_t* ref_len,
+                      int32_t n_ref, uint8_t* flag, hipStream_t s) {
+  if (ulen <= 0) return;
+  hipLaunchKernelGGL(guess_all_kernel, dim3((unsigned)((ulen + 255) / 256)), dim3(256), 0, s, U,
+                     ulen, u_is_eof, ref_len, n_ref, flag);
 }
 
 void launch_first_record(const uint8_t* U, int64_t ulen, int32_t u_is_eof, const int32_t* ref_len,

@@ -262,6 +262,12 @@ int dq_partition_digests(dq_ctx* ctx, int64_t* counts, uint64_t* digests, int64_
 /* Device pointer of the resident decompressed stream (for tests), and its length. */
 int dq_debug_inflated(dq_ctx* ctx, uint8_t* host_out, int64_t cap, int64_t* len);
 
+/* Test hook: the GPU record guesser (BamRecordGuesser.checkRecordStart) evaluated at EVERY
+ * decompressed position of a whole resident file, as BamRecordGuesserChecker does with a
+ * granularity-1 index (D/impl/formats/bam/BamRecordGuesserChecker.java:104-120).  Writes the
+ * virtual offsets where it fires, ascending, up to cap; *n = how many there are. */
+int dq_debug_guess_all(dq_ctx* ctx, uint64_t* voffs, int64_t cap, int64_t* n);
+
 void dq_batch_free(dq_batch* b);
 void dq_free(void* p);
 

@@ -1,0 +1,146 @@
+"""Adversarial fixtures for split planning.
+
+1. A BGZF member header inside record payload at a split start.  Stored (level-0) blocks keep the
+   payload bytes verbatim in the file, so BgzfBlockGuesser.guessNextBGZFPos
+   (D/impl/formats/bgzf/BgzfBlockGuesser.java:76-149) sees them:
+   - "eof": a complete empty member (the 28-byte EOF block) -- the guesser accepts it, the split's
+     block iterator (BgzfBlockSource.java:63-84) yields it with uSize 0, then continues from
+     its end (fake position + 28) to the next real block;
+   - "broken": the magic with a bad 'BC' subfield -- the guesser rejects it and scans on from
+     the magic + 4 (:138-144).
+   In both cases getFirstReadInPartition (BamSource.java:110-153) ends on the same record start
+   as without the fake bytes.
+   - "data": a member with data (ISIZE > 0) -- the reference would inflate the fake member and
+     run the record guesser over its bytes; the GPU planner does not reproduce that and must
+     fail loudly instead of planning a different chunk.
+2. A record longer than MAX_READ_SIZE (10,000,000 positions, BamSource.java:44,132-135): a split
+   that starts inside it scans 10 M positions without a record start and gets no chunk (an empty
+   partition), while later splits inside the record find the next record.
+"""
+import numpy as np
+import pytest
+
+from disq_amd import synth
+from oracle import oracle as O
+
+import bamutil as B
+
+BROKEN = bytes.fromhex("1f8b08040000000000ff0600424402001b00")  # 'BD' instead of 'BC'
+
+
+def fake_header_bam(kind, clean=False):
+    """Level-0 BAM with `payload` in the qualities of record 400 (clean=True: zero bytes)."""
+    r = synth.generate(800, seed=21, level=0, nthreads=4)
+    u = bytearray(B.inflate_all(r.bam))
+    off, ln = B.record_spans(u)[400]
+    q = off + B.qual_offset(bytes(u[off:off + ln]))
+    if kind == "eof":
+        payload = B.EOF_BLOCK
+    elif kind == "broken":
+        payload = BROKEN
+    else:
+        payload = B.bgzf_member(b"hello, world", 6)
+    u[q + 10:q + 10 + len(payload)] = bytes(len(payload)) if clean else payload
+    bam = B.bgzf(bytes(u), level=0)
+    if clean:
+        return bam
+    fake = bam.find(payload)
+    assert 0 < fake < len(bam) - 28
+    return bam, fake, payload
+
+
+@pytest.mark.parametrize("kind", ["eof", "broken"])
+def test_oracle_fake_header_at_split_start(kind):
+    bam, fake, payload = fake_header_bam(kind)
+    split = fake - 7  # split 1 starts 7 bytes before the fake member
+    ob = O.OracleBam(bam)
+    g = ob.guess_next_bgzf(split, 2 * split)
+    if kind == "eof":
+        assert g == (fake, 28, 0)  # the guesser takes the embedded member
+    else:
+        assert g[0] > fake  # rejected: the next real block
+    parts = ob.read_partitions(split)
+    allr = ob.read_all()
+    got = np.concatenate([p["voffset"] for p in parts])
+    assert np.array_equal(got, allr["voffset"])
+    # the same chunks as the file without the fake bytes; split 1 starts in the first real block
+    # after the fake member
+    plan = ob.plan(split)
+    assert plan == O.OracleBam(fake_header_bam(kind, clean=True)).plan(split)
+    nxt = ob.guess_next_bgzf(fake + 4, 1 << 40)[0]
+    assert plan[1][2][0] >> 16 == nxt
+
+
+def giant_bam():
+    r = synth.generate(300, seed=22, nthreads=4)
+    u = B.inflate_all(r.bam)
+    off, _ = B.record_spans(u)[250]
+    giant = B.make_record(0, 1_000_000, b"giant", 7_000_000)
+    assert len(giant) > 10_000_000
+    u2 = u[:off] + giant + u[off:]
+    return B.bgzf(u2, level=5), off, len(giant)
+
+
+def test_oracle_max_read_size_empty_partition():
+    """Split 1 starts two blocks into the giant record and its blocks reach past the record's
+    end: the first 10 M positions hold no record start, so the split gets no chunk, and the
+    records that start later in it are in no partition (BamSource.java:132-135 -- a reference
+    quirk the GPU path reproduces)."""
+    bam, off, glen = giant_bam()
+    ob = O.OracleBam(bam)
+    blocks = ob.split_blocks(0, len(bam))
+    uo = np.cumsum([0] + [b[2] for b in blocks])
+    j = int(np.searchsorted(uo, off, side="right")) - 1  # block holding the giant's first byte
+    split = blocks[j + 2][0]
+    assert off < uo[j + 2] < off + glen - 10_000_000
+    r2 = int(np.searchsorted(uo, off + glen, side="right")) - 1  # block of the next record
+    assert blocks[r2][0] < 2 * split  # ... which split 1 reaches
+    plan = ob.plan(split)
+    assert plan[1][2] is None
+    allr = ob.read_all()
+    assert (allr["block_size"] + 4 == glen).sum() == 1
+    parts = ob.read_partitions(split)
+    n_lost = len(allr) - sum(len(p) for p in parts)
+    # the records after split 0's chunk end and before split 2's first record are in no partition
+    v = allr["voffset"]
+    lo = (split << 16) | 0xffff
+    hi = plan[2][2][0] if len(plan) > 2 else 1 << 63
+    assert n_lost == int(((v > lo) & (v < hi)).sum()) > 0
+
+
+# ---- the GPU path on the same fixtures (bit-exact against the oracle)
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["eof", "broken"])
+def test_gpu_fake_header_at_split_start(kind):
+    from test_gpu_parity import assert_parity
+    bam, fake, _ = fake_header_bam(kind)
+    for split in (fake - 7, fake, fake - 40000):
+        assert_parity(bam, split)
+
+
+@pytest.mark.gpu
+def test_gpu_fake_member_with_data_fails_like_the_reference():
+    """The reference fails on the bytes after a data-carrying fake member (htsjdk 'Invalid GZIP
+    header' escapes getFirstReadInPartition); the GPU planner refuses the split loudly."""
+    from disq_amd import _lib
+    bam, fake, _ = fake_header_bam("data")
+    with pytest.raises(O.OracleError):
+        O.OracleBam(bam).plan(fake - 7)
+    with _lib.Context(split_size=fake - 7) as c:
+        with pytest.raises(_lib.DqError, match="BGZF"):
+            c.open_bytes(bam)
+            c.plan()
+
+
+@pytest.mark.gpu
+def test_gpu_max_read_size_empty_partition():
+    from test_gpu_parity import assert_parity
+    bam, off, glen = giant_bam()
+    ob = O.OracleBam(bam)
+    blocks = ob.split_blocks(0, len(bam))
+    uo = np.cumsum([0] + [b[2] for b in blocks])
+    j = int(np.searchsorted(uo, off, side="right")) - 1
+    split = blocks[j + 2][0]
+    b = assert_parity(bam, split)
+    assert int(b["part_offset"][2] - b["part_offset"][1]) == 0
