@@ -52,6 +52,19 @@ class DqBatch(C.Structure):
                 ("part_digest", C.POINTER(C.c_uint64))]
 
 
+class DqTextBatch(C.Structure):
+    _fields_ = [("n_lines", C.c_int64),
+                ("line_offset", C.POINTER(C.c_int64)),
+                ("line_len", C.POINTER(C.c_int32)),
+                ("hash", C.POINTER(C.c_uint64)),
+                ("data_offset", C.POINTER(C.c_int64)),
+                ("data", C.POINTER(C.c_uint8)),
+                ("n_bytes", C.c_int64),
+                ("n_partitions", C.c_int64),
+                ("part_offset", C.POINTER(C.c_int64)),
+                ("part_digest", C.POINTER(C.c_uint64))]
+
+
 class DqTraversal(C.Structure):
     _fields_ = [("ref", C.POINTER(C.c_int32)), ("start", C.POINTER(C.c_int32)),
                 ("end", C.POINTER(C.c_int32)), ("n", C.c_int64), ("has_intervals", C.c_int32),
@@ -81,7 +94,8 @@ EXPORTS = ("dq_ctx_create", "dq_ctx_destroy", "dq_last_error", "dq_version", "dq
            "dq_batch_free", "dq_free", "dq_open_shard", "dq_header_from_prefix",
            "dq_set_splitting_index", "dq_write_sbi", "dq_open_shard_device", "dq_decode_chunk",
            "dq_get_stats", "dq_partition_digests", "dq_open_shard_path",
-           "dq_decode_chunk_filtered", "dq_debug_guess_all")
+           "dq_decode_chunk_filtered", "dq_debug_guess_all", "dq_text_open_memory",
+           "dq_text_open_path", "dq_text_run", "dq_text_read", "dq_text_batch_free")
 
 _lib = None
 _lock = threading.Lock()
@@ -135,6 +149,11 @@ def lib():
         L.dq_debug_inflated.argtypes = [vp, vp, C.c_int64, P(C.c_int64)]
         L.dq_debug_guess_all.argtypes = [vp, vp, C.c_int64, P(C.c_int64)]
         L.dq_batch_free.argtypes = [P(DqBatch)]
+        L.dq_text_open_memory.argtypes = [vp, vp, C.c_int64]
+        L.dq_text_open_path.argtypes = [vp, C.c_char_p]
+        L.dq_text_run.argtypes = [vp, C.c_int32, P(DqStats)]
+        L.dq_text_read.argtypes = [vp, C.c_int32, P(P(DqTextBatch))]
+        L.dq_text_batch_free.argtypes = [P(DqTextBatch)]
         L.dq_free.argtypes = [vp]
         _lib = L
         return L
@@ -300,6 +319,42 @@ class Context:
 
     def open_path(self, path):
         check(self._h, lib().dq_open_path(self._h, path.encode()))
+
+    # ---- BGZF text (VCF) path
+    def text_open_bytes(self, data):
+        buf = np.frombuffer(data, np.uint8)
+        check(self._h, lib().dq_text_open_memory(self._h, buf.ctypes.data, len(buf)))
+
+    def text_open_path(self, path):
+        check(self._h, lib().dq_text_open_path(self._h, path.encode()))
+
+    def text_run(self, drop_header_lines=True):
+        st = DqStats()
+        check(self._h, lib().dq_text_run(self._h, int(drop_header_lines), C.byref(st)))
+        return st
+
+    def text_read(self, drop_header_lines=True):
+        """The lines of every split, in partition order: dict of numpy arrays (line_offset,
+        line_len, hash, data_offset, data, part_offset, part_digest)."""
+        bp = C.POINTER(DqTextBatch)()
+        check(self._h, lib().dq_text_read(self._h, int(drop_header_lines), C.byref(bp)))
+        try:
+            b = bp.contents
+            n, npart = b.n_lines, b.n_partitions
+
+            def arr(ptr, k, dt):
+                if not k or not ptr:
+                    return np.zeros(0, dt)
+                return np.ctypeslib.as_array(ptr, shape=(k,)).astype(dt, copy=True)
+            return {"line_offset": arr(b.line_offset, n, np.int64),
+                    "line_len": arr(b.line_len, n, np.int32),
+                    "hash": arr(b.hash, n, np.uint64),
+                    "data_offset": arr(b.data_offset, n + 1, np.int64),
+                    "data": arr(b.data, b.n_bytes, np.uint8),
+                    "part_offset": arr(b.part_offset, npart + 1, np.int64),
+                    "part_digest": arr(b.part_digest, npart, np.uint64)}
+        finally:
+            lib().dq_text_batch_free(bp)
 
     def set_index(self, bai_bytes):
         if bai_bytes is None:

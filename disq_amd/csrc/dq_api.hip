@@ -84,6 +84,14 @@ struct dq_ctx {
   int64_t p0 = 0, p1 = 0;    // Disq partitions owned by the shard
   std::vector<uint8_t> hdr;  // shard: the decompressed BAM header, supplied by the caller
   bool header_only = false;  // dq_header_from_prefix: stop after the header
+  // BGZF text (VCF) path: the pipeline stops after inflate; lines instead of records
+  bool text_mode = false;
+  bool have_text = false;
+  int32_t text_drop = -1;
+  int64_t t_nterm = 0, t_total = 0, t_nkept = 0;
+  DevBuf t_tcount, t_toff, t_term, t_crf, t_plans, t_rng, t_idx, t_vs, t_vl, t_hash, t_keep,
+      t_keep32, t_koff, t_kept;
+  std::vector<TextPlan> tplans_h;
   const uint8_t* cext = nullptr;  // dq_open_shard_device: caller-owned device bytes instead of C
   // dq_decode_chunk: the window holds one Chunk [chunk_vs, chunk_ve) (shard coordinates); its
   // records are walked from the exact start pointer, no split planning or guessing
@@ -98,6 +106,7 @@ struct dq_ctx {
   const uint8_t* cbuf() const { return cext ? cext : C.as<uint8_t>(); }
   // kernel 1
   DevBuf slots, counts, offs, cand, flags, voff, scal, tmp;
+  DevBuf scan_over, scan_map, scan_big;  // second scan pass (dense BGZF regions)
   int64_t ncand = 0;
   // chain + inflate
   DevBuf blk_pos, blk_cs, blk_us, uoff, status, U;
@@ -485,23 +494,39 @@ static int run_pipeline(dq_ctx* ctx) {
   int32_t* d_stat = d_overflow + 2;
   int64_t* d_nblk = reinterpret_cast<int64_t*>(ctx->scal.as<char>() + 64);
   HIPCHK(hipMemsetAsync(ctx->scal.p, 0, 4096, s));
+  if ((rc = ensure_all(ctx, ctx->scan_over, sizeof(int32_t) * (size_t)(1 + SCAN_OVER_MAX)))) return rc;
+  HIPCHK(hipMemsetAsync(ctx->scan_over.p, 0, sizeof(int32_t), s));
   launch_bgzf_scan(ctx->cbuf(), L, L, ctx->slots.as<Cand>(), 0, ctx->counts.as<int32_t>(),
-                   nch, nullptr, d_overflow, s);
+                   nch, nullptr, ctx->scan_over.as<int32_t>(), s);
+  int32_t n_over = 0;
+  HIPCHK(hipMemcpyAsync(&n_over, ctx->scan_over.p, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (n_over > SCAN_OVER_MAX) RET(DQ_EFORMAT, "too many dense BGZF regions");
+  if (n_over > 0) {  // chunks with more than SCAN_CAP magic positions: second pass
+    if ((rc = ensure_all(ctx, ctx->scan_map, sizeof(int32_t) * (size_t)nch))) return rc;
+    if ((rc = ensure_all(ctx, ctx->scan_big, sizeof(Cand) * (size_t)n_over * SCAN_CAP_BIG))) return rc;
+    HIPCHK(hipMemsetAsync(ctx->scan_map.p, 0xff, sizeof(int32_t) * (size_t)nch, s));
+    launch_bgzf_scan_listed(ctx->cbuf(), L, L, ctx->scan_big.as<Cand>(), n_over,
+                            ctx->counts.as<int32_t>(), ctx->scan_over.as<int32_t>(),
+                            ctx->scan_map.as<int32_t>(), s);
+    int32_t bad = 0;
+    HIPCHK(hipMemcpyAsync(&bad, ctx->scan_over.p, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (bad < 0) RET(DQ_EFORMAT, "more than 640 BGZF magic positions in a 16 KiB window");
+  }
   launch_exclusive_scan_i32(ctx->counts.as<int32_t>(), ctx->offs.as<int64_t>(), nch,
                             ctx->tmp.as<int64_t>(), s);
-  dbg(s, "scan", nch);
+  dbg(s, "scan", nch, n_over);
   int64_t ncand = 0;
   if ((rc = get_i64(ctx, ctx->offs.as<int64_t>() + nch, &ncand))) return rc;
-  int32_t overflow = 0;
-  HIPCHK(hipMemcpy(&overflow, d_overflow, 4, hipMemcpyDeviceToHost));
-  if (overflow) RET(DQ_EFORMAT, "more than 32 BGZF headers in a 16 KiB window is not supported");
   ctx->ncand = ncand;
   const int64_t capc = std::max<int64_t>(1, ncand);
   if ((rc = ensure_all(ctx, ctx->cand, sizeof(Cand) * (size_t)capc))) return rc;
   if ((rc = ensure_all(ctx, ctx->flags, sizeof(int32_t) * (size_t)capc))) return rc;
   if ((rc = ensure_all(ctx, ctx->voff, sizeof(int64_t) * (size_t)(capc + 1)))) return rc;
   launch_gather_slots(ctx->slots.as<Cand>(), ctx->counts.as<int32_t>(), ctx->offs.as<int64_t>(), nch,
-                      ctx->cand.as<Cand>(), capc, s);
+                      ctx->cand.as<Cand>(), capc, n_over > 0 ? ctx->scan_map.as<int32_t>() : nullptr,
+                      ctx->scan_big.as<Cand>(), s);
   // ncand on device for the kernels that need it
   int64_t* d_ncand = d_nblk + 1;
   HIPCHK(hipMemcpyAsync(d_ncand, &ncand, sizeof(int64_t), hipMemcpyHostToDevice, s));
@@ -608,6 +633,13 @@ static int run_pipeline(dq_ctx* ctx) {
                  (long long)pos);
         RET(DQ_EFORMAT, msg);
       }
+  }
+  if (ctx->text_mode) {  // BGZF text: lines are planned by text_run
+    ctx->stats = dq_stats{};
+    ctx->stats.ms_scan = ev_ms(ctx->ev[0], ctx->ev[1]);
+    ctx->stats.ms_inflate = ev_ms(ctx->ev[5], ctx->ev[6]);
+    ctx->have_pipeline = true;
+    return 0;
   }
   // ---- header (n_ref, reference lengths for the guesser)
   if ((rc = parse_header(ctx))) return rc;
@@ -834,6 +866,158 @@ static int run_pipeline(dq_ctx* ctx) {
     ctx->plan_cached = true;
   }
   ctx->voff_h.clear();
+  return 0;
+}
+
+// ------------------------------------------------------------------ BGZF text (VCF) path
+// TextInputFormat + LineRecordReader over Disq's splittable BGZF codec, per split (dq_text.hip
+// holds the characterisation, oracle/disq_oracle.c the literal restatement): terminators of the
+// resident stream, each split's line range, the values (drop '#' lines as VcfSource does), their
+// hashes and per-partition digests; everything stays in HBM.
+static int text_run(dq_ctx* ctx, int32_t drop_hash) {
+  if (!ctx->text_mode) RET(DQ_EINVAL, "not a text context (dq_text_open_*)");
+  int rc = run_pipeline(ctx);
+  if (rc) return rc;
+  if (ctx->have_text && ctx->text_drop == drop_hash) return 0;
+  hipStream_t s = ctx->s;
+  const int64_t nblk = ctx->nblk, ulen = ctx->ulen, L = ctx->flen;
+  int32_t* d_stat = ctx->scal.as<int32_t>() + 2;
+  int64_t* d_ncand = reinterpret_cast<int64_t*>(ctx->scal.as<char>() + 64) + 1;
+  HIPCHK(hipEventRecord(ctx->ev[2], s));
+  {  // an empty block inside the stream would end a split's stream there: not reproduced
+    std::vector<int32_t> us((size_t)nblk);
+    if (nblk) HIPCHK(hipMemcpyAsync(us.data(), ctx->blk_us.p, 4 * (size_t)nblk, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (int64_t b = 0; b + 1 < nblk; b++)
+      if (us[(size_t)b] == 0) RET(DQ_EFORMAT, "empty BGZF block inside a text stream is not supported");
+  }
+  // terminators
+  const int64_t nt = text_tiles(ulen);
+  if ((rc = ensure_all(ctx, ctx->t_tcount, 4 * (size_t)std::max<int64_t>(1, nt)))) return rc;
+  if ((rc = ensure_all(ctx, ctx->t_toff, 8 * (size_t)(nt + 1)))) return rc;
+  if ((rc = ensure_all(ctx, ctx->tmp, sizeof(int64_t) * (size_t)(4 * (nt / 1024 + 1) + 4096)))) return rc;
+  launch_text_terms(ctx->U.as<uint8_t>(), ulen, ctx->t_tcount.as<int32_t>(), nullptr, nullptr, false, s);
+  if (nt > 0)
+    launch_exclusive_scan_i32(ctx->t_tcount.as<int32_t>(), ctx->t_toff.as<int64_t>(), nt,
+                              ctx->tmp.as<int64_t>(), s);
+  int64_t nterm = 0;
+  if (nt > 0 && (rc = get_i64(ctx, ctx->t_toff.as<int64_t>() + nt, &nterm))) return rc;
+  if ((rc = ensure_all(ctx, ctx->t_term, 8 * (size_t)(nterm + 1)))) return rc;
+  launch_text_terms(ctx->U.as<uint8_t>(), ulen, nullptr, ctx->t_toff.as<int64_t>(),
+                    ctx->t_term.as<int64_t>(), true, s);
+  ctx->t_nterm = nterm;
+  if ((rc = ensure_all(ctx, ctx->t_crf, 8 * (size_t)std::max<int64_t>(1, nblk)))) return rc;
+  launch_text_cr_fills(ctx->U.as<uint8_t>(), ctx->uoff.as<int64_t>(), ctx->blk_us.as<int32_t>(), nblk,
+                       ctx->t_crf.as<int64_t>(), s);
+  // split plans (FileInputFormat splits: the same arithmetic as the BAM path, a1)
+  std::vector<std::pair<int64_t, int64_t>> splits;
+  if (path_splits(ctx->o, L, splits)) RET(DQ_EINVAL, "splitSize must be > 0 with useNio");
+  const int64_t nsplit = (int64_t)splits.size();
+  ctx->tplans_h.assign((size_t)nsplit, TextPlan{});
+  for (int64_t i = 0; i < nsplit; i++) {
+    ctx->tplans_h[(size_t)i].split_start = splits[(size_t)i].first;
+    ctx->tplans_h[(size_t)i].split_end = splits[(size_t)i].second;
+  }
+  if ((rc = ensure_all(ctx, ctx->t_plans, sizeof(TextPlan) * (size_t)(nsplit + 1)))) return rc;
+  HIPCHK(hipMemcpyAsync(ctx->t_plans.p, ctx->tplans_h.data(), sizeof(TextPlan) * (size_t)nsplit,
+                        hipMemcpyHostToDevice, s));
+  launch_text_plan(ctx->cand.as<Cand>(), d_ncand, ctx->blk_pos.as<int64_t>(), ctx->blk_us.as<int32_t>(),
+                   ctx->uoff.as<int64_t>(), nblk, L, ctx->U.as<uint8_t>(), ulen,
+                   ctx->t_term.as<int64_t>(), nterm, ctx->t_crf.as<int64_t>(),
+                   ctx->t_plans.as<TextPlan>(), nsplit, s);
+  HIPCHK(hipMemcpyAsync(ctx->tplans_h.data(), ctx->t_plans.p, sizeof(TextPlan) * (size_t)nsplit,
+                        hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(hipEventRecord(ctx->ev[3], s));
+  int32_t bom = 0;
+  std::vector<int64_t> rng(2 * (size_t)nsplit + 1);  // begin[nsplit] | out_off[nsplit + 1]
+  int64_t total = 0;
+  for (int64_t i = 0; i < nsplit; i++) {
+    const TextPlan& P = ctx->tplans_h[(size_t)i];
+    if (P.status) {
+      char msg[224];
+      snprintf(msg, sizeof msg, "text split [%lld, %lld): %s", (long long)P.split_start,
+               (long long)P.split_end,
+               P.status == ST_TEXT_START
+                   ? "no BGZF block starts in the split or at its end (the reference fails reading it)"
+                   : "the guessed BGZF block is not on the block chain");
+      RET(DQ_EFORMAT, msg);
+    }
+    if (P.k0 == 0 && P.bom) bom = 1;
+    rng[(size_t)i] = P.k0;
+    rng[(size_t)nsplit + (size_t)i] = total;
+    total += P.k1 - P.k0;
+  }
+  rng[2 * (size_t)nsplit] = total;
+  ctx->t_total = total;
+  const size_t nt1 = (size_t)std::max<int64_t>(1, total);
+  if ((rc = ensure_all(ctx, ctx->t_rng, 8 * rng.size()))) return rc;
+  if ((rc = ensure_all(ctx, ctx->t_idx, 8 * nt1))) return rc;
+  if ((rc = ensure_all(ctx, ctx->t_vs, 8 * nt1))) return rc;
+  if ((rc = ensure_all(ctx, ctx->t_vl, 4 * nt1))) return rc;
+  if ((rc = ensure_all(ctx, ctx->t_hash, 8 * nt1))) return rc;
+  if ((rc = ensure_all(ctx, ctx->t_keep, nt1))) return rc;
+  if ((rc = ensure_all(ctx, ctx->t_keep32, 4 * nt1))) return rc;
+  if ((rc = ensure_all(ctx, ctx->t_koff, 8 * (nt1 + 1)))) return rc;
+  if ((rc = ensure_all(ctx, ctx->t_kept, 8 * nt1))) return rc;
+  if ((rc = ensure_all(ctx, ctx->tmp, sizeof(int64_t) * (size_t)(4 * ((int64_t)nt1 / 1024 + 1) + 4096))))
+    return rc;
+  HIPCHK(hipMemcpyAsync(ctx->t_rng.p, rng.data(), 8 * rng.size(), hipMemcpyHostToDevice, s));
+  const int64_t* d_begin = ctx->t_rng.as<int64_t>();
+  const int64_t* d_outoff = d_begin + nsplit;
+  launch_ranges_to_idx(d_begin, d_outoff, nsplit, ctx->t_idx.as<int64_t>(), s);
+  launch_text_values(ctx->U.as<uint8_t>(), ulen, ctx->t_term.as<int64_t>(), nterm,
+                     ctx->t_idx.as<int64_t>(), total, bom, drop_hash, ctx->t_vs.as<int64_t>(),
+                     ctx->t_vl.as<int32_t>(), ctx->t_hash.as<uint64_t>(), ctx->t_keep.as<uint8_t>(), s);
+  launch_keep_to_i32(ctx->t_keep.as<uint8_t>(), total, ctx->t_keep32.as<int32_t>(), s);
+  if (total > 0)
+    launch_exclusive_scan_i32(ctx->t_keep32.as<int32_t>(), ctx->t_koff.as<int64_t>(), total,
+                              ctx->tmp.as<int64_t>(), s);
+  int64_t nkept = 0;
+  if (total > 0 && (rc = get_i64(ctx, ctx->t_koff.as<int64_t>() + total, &nkept))) return rc;
+  launch_compact_kept(nullptr, ctx->t_keep.as<uint8_t>(), ctx->t_koff.as<int64_t>(), total,
+                      ctx->t_kept.as<int64_t>(), s);
+  ctx->t_nkept = nkept;
+  if ((rc = ensure_all(ctx, ctx->parts, sizeof(PartRange) * (size_t)(nsplit + 1)))) return rc;
+  if (total > 0) {
+    launch_text_parts(d_outoff, ctx->t_koff.as<int64_t>(), nsplit, ctx->parts.as<PartRange>(), s);
+  } else {
+    HIPCHK(hipMemsetAsync(ctx->parts.p, 0, sizeof(PartRange) * (size_t)nsplit, s));
+  }
+  launch_partition_digest_idx(ctx->t_hash.as<uint64_t>(), ctx->t_kept.as<int64_t>(),
+                              ctx->parts.as<PartRange>(), nsplit, s);
+  HIPCHK(hipEventRecord(ctx->ev[4], s));
+  ctx->parts_h.assign((size_t)nsplit, PartRange{});
+  HIPCHK(hipMemcpyAsync(ctx->parts_h.data(), ctx->parts.p, sizeof(PartRange) * (size_t)nsplit,
+                        hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  (void)d_stat;
+  dq_stats& S = ctx->stats;
+  S.compressed_bytes = L;
+  S.decompressed_bytes = ulen;
+  S.n_blocks = nblk;
+  S.n_partitions = nsplit;
+  S.n_records = nkept;
+  S.n_filtered = total - nkept;  // '#' lines dropped
+  uint64_t dg = 0;
+  for (int64_t i = 0; i < nsplit; i++)
+    dg += dq_mix64(ctx->parts_h[(size_t)i].digest ^ ((uint64_t)(i + 1) * DQ_K_WORD));
+  S.digest = dg;
+  S.ms_plan = ev_ms(ctx->ev[2], ctx->ev[3]);
+  S.ms_records = ev_ms(ctx->ev[3], ctx->ev[4]);
+  S.ms_total = ev_ms(ctx->ev[0], ctx->ev[4]);
+  S.h2d_bytes = ctx->h2d_bytes;
+  S.blocks_inflated = nblk;
+  {
+    std::vector<int32_t> cs((size_t)nblk);
+    if (nblk) HIPCHK(hipMemcpy(cs.data(), ctx->blk_cs.p, 4 * (size_t)nblk, hipMemcpyDeviceToHost));
+    int64_t db = 0;
+    for (int32_t c : cs) db += c - 26;
+    S.deflate_bytes = db;
+    S.owned_bytes = ulen;
+  }
+  ctx->have_text = true;
+  ctx->text_drop = drop_hash;
   return 0;
 }
 
@@ -1445,6 +1629,8 @@ static void reset_open(dq_ctx* ctx, int64_t len) {
   ctx->p1 = 0;
   ctx->cext = nullptr;
   ctx->chunk_mode = false;
+  ctx->text_mode = false;
+  ctx->have_text = false;
 }
 
 // Bytes [off, off + len) of an open file into C (plus the 4 KiB zero pad): read() into two pinned
@@ -2232,6 +2418,102 @@ int dq_debug_guess_all(dq_ctx* ctx, uint64_t* voffs, int64_t cap, int64_t* n) {
   }
   *n = k;
   return 0;
+}
+
+int dq_text_open_memory(dq_ctx* ctx, const uint8_t* bytes, int64_t len) {
+  int rc = dq_open_memory(ctx, bytes, len);
+  if (rc == 0) ctx->text_mode = true;
+  return rc;
+}
+
+int dq_text_open_path(dq_ctx* ctx, const char* path) {
+  int rc = dq_open_path(ctx, path);
+  if (rc == 0) ctx->text_mode = true;
+  return rc;
+}
+
+int dq_text_run(dq_ctx* ctx, int32_t drop_header_lines, dq_stats* stats) {
+  if (!ctx) return DQ_EINVAL;
+  ON_DEVICE(ctx);
+  // a re-run times the whole pipeline again
+  ctx->have_pipeline = false;
+  ctx->have_text = false;
+  int rc = text_run(ctx, drop_header_lines ? 1 : 0);
+  if (rc) return rc;
+  if (stats) *stats = ctx->stats;
+  return 0;
+}
+
+int dq_text_read(dq_ctx* ctx, int32_t drop_header_lines, dq_text_batch** out) {
+  if (!ctx || !out) return DQ_EINVAL;
+  ON_DEVICE(ctx);
+  *out = nullptr;
+  int rc = text_run(ctx, drop_header_lines ? 1 : 0);
+  if (rc) return rc;
+  hipStream_t s = ctx->s;
+  const int64_t n = ctx->t_nkept, nsplit = (int64_t)ctx->tplans_h.size();
+  const size_t n1 = (size_t)std::max<int64_t>(1, n);
+  DevBuf o_start, o_len, o_hash, o_off, o_data, tmp;
+  HIPCHK(o_start.ensure(8 * n1));
+  HIPCHK(o_len.ensure(4 * n1));
+  HIPCHK(o_hash.ensure(8 * n1));
+  HIPCHK(o_off.ensure(8 * (n1 + 1)));
+  HIPCHK(tmp.ensure(sizeof(int64_t) * (size_t)(4 * ((int64_t)n1 / 1024 + 1) + 4096)));
+  launch_text_export(ctx->t_kept.as<int64_t>(), n, ctx->t_vs.as<int64_t>(), ctx->t_vl.as<int32_t>(),
+                     ctx->t_hash.as<uint64_t>(), o_start.as<int64_t>(), o_len.as<int32_t>(),
+                     o_hash.as<uint64_t>(), s);
+  if (n > 0) launch_exclusive_scan_i32(o_len.as<int32_t>(), o_off.as<int64_t>(), n, tmp.as<int64_t>(), s);
+  int64_t nbytes = 0;
+  if (n > 0 && (rc = get_i64(ctx, o_off.as<int64_t>() + n, &nbytes))) return rc;
+  HIPCHK(o_data.ensure((size_t)std::max<int64_t>(1, nbytes)));
+  launch_text_gather(ctx->U.as<uint8_t>(), ctx->t_vs.as<int64_t>(), ctx->t_vl.as<int32_t>(),
+                     ctx->t_kept.as<int64_t>(), o_off.as<int64_t>(), n, o_data.as<uint8_t>(), s);
+  dq_text_batch* b = (dq_text_batch*)calloc(1, sizeof(dq_text_batch));
+  if (!b) return DQ_ENOMEM;
+  b->n_lines = n;
+  b->n_partitions = nsplit;
+  b->line_offset = (int64_t*)malloc(8 * n1);
+  b->line_len = (int32_t*)malloc(4 * n1);
+  b->hash = (uint64_t*)malloc(8 * n1);
+  b->data_offset = (int64_t*)malloc(8 * (n1 + 1));
+  b->data = (uint8_t*)malloc((size_t)std::max<int64_t>(1, nbytes));
+  b->part_offset = (int64_t*)malloc(8 * (size_t)(nsplit + 1));
+  b->part_digest = (uint64_t*)malloc(8 * (size_t)std::max<int64_t>(1, nsplit));
+  if (!b->line_offset || !b->line_len || !b->hash || !b->data_offset || !b->data || !b->part_offset ||
+      !b->part_digest) {
+    dq_text_batch_free(b);
+    return DQ_ENOMEM;
+  }
+  if (n > 0) {
+    HIPCHK(hipMemcpyAsync(b->line_offset, o_start.p, 8 * (size_t)n, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(b->line_len, o_len.p, 4 * (size_t)n, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(b->hash, o_hash.p, 8 * (size_t)n, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(b->data_offset, o_off.p, 8 * (size_t)(n + 1), hipMemcpyDeviceToHost, s));
+  } else {
+    b->data_offset[0] = 0;
+  }
+  if (nbytes > 0) HIPCHK(hipMemcpyAsync(b->data, o_data.p, (size_t)nbytes, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  b->n_bytes = nbytes;
+  for (int64_t i = 0; i < nsplit; i++) {
+    b->part_offset[i] = ctx->parts_h[(size_t)i].begin;
+    b->part_digest[i] = ctx->parts_h[(size_t)i].digest;
+  }
+  b->part_offset[nsplit] = n;
+  *out = b;
+  return 0;
+}
+
+void dq_text_batch_free(dq_text_batch* b) {
+  if (!b) return;
+  free(b->line_offset);
+  free(b->line_len);
+  free(b->hash);
+  free(b->data_offset);
+  free(b->data);
+  free(b->part_offset);
+  free(b->part_digest);
+  free(b);
 }
 
 void dq_batch_free(dq_batch* b) {

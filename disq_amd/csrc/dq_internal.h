@@ -17,6 +17,7 @@ enum : int32_t {
   ST_CRC = 9,             // CRC32 mismatch (verify_crc)
   ST_ISIZE = 10,          // ISIZE > 65536
   ST_HANG = 11,           // internal: batch loop made no progress
+  ST_TEXT_START = 12,     // text split: no block start in the split and none at its end
 };
 
 // ------------------------------------------------------------------ hashing
@@ -44,15 +45,22 @@ struct Cand {          // a BgzfBlockGuesser-visible magic position
 };
 
 constexpr int SCAN_CHUNK = 16384;  // bytes of C per scan workgroup
-constexpr int SCAN_CAP = 32;       // candidate slots per chunk (overflow -> serial chain)
+constexpr int SCAN_CAP = 32;       // candidate slots per chunk in the first scan pass
+constexpr int SCAN_CAP_BIG = 640;  // slots of a re-scanned chunk (BGZF members are >= 28 bytes)
+constexpr int SCAN_OVER_MAX = 1 << 22;  // chunks the second pass can take
 
 // Kernel 1: BGZF candidate scan of C[0, n) (file offsets; L = readable bytes).  Writes each
 // chunk's candidates sorted into slots[chunk * SCAN_CAP ...] and its count.
 void launch_bgzf_scan(const uint8_t* C, int64_t n, int64_t L, Cand* slots, int64_t cap,
                       int32_t* chunk_counts, int64_t n_chunks, int64_t* d_count,
-                      int32_t* d_overflow, hipStream_t s);
+                      int32_t* over_list, hipStream_t s);
+// Second pass over the chunks listed in over_list[1..over_list[0]] (more than SCAN_CAP hits).
+void launch_bgzf_scan_listed(const uint8_t* C, int64_t n, int64_t L, Cand* big, int64_t n_over,
+                             int32_t* chunk_counts, int32_t* over_list, int32_t* over_map,
+                             hipStream_t s);
 void launch_gather_slots(const Cand* slots, const int32_t* counts, const int64_t* offs,
-                         int64_t nchunks, Cand* out, int64_t cap, hipStream_t s);
+                         int64_t nchunks, Cand* out, int64_t cap, const int32_t* over_map,
+                         const Cand* big, hipStream_t s);
 void launch_valid_flags(const Cand* cand, const int64_t* ncand, int64_t cap, int32_t* flags,
                         hipStream_t s);
 // Chain check: valid candidates must be htsjdk blocks linked by pos + BSIZE + 1.
@@ -198,5 +206,35 @@ void launch_interval_filter(const uint8_t* U, const int64_t* rec_lin, const RecS
                             const int32_t* iv_start, const int32_t* iv_end,
                             const int32_t* ref_iv_begin, int32_t n_ref, uint8_t* keep,
                             hipStream_t s);
+
+// ------------------------------------------------------------------ BGZF text (VCF) path
+struct TextPlan {
+  int64_t split_start, split_end;
+  int64_t k0, k1;   // the split's lines: indices [k0, k1)
+  int64_t b0;       // the split stream's first block (-1 none)
+  int32_t status;
+  int32_t bom;      // line k0 == 0 starts with a UTF-8 BOM that LineRecordReader strips
+};
+int64_t text_tiles(int64_t ulen);
+void launch_text_terms(const uint8_t* U, int64_t ulen, int32_t* tile_count, const int64_t* tile_off,
+                       int64_t* term_pos, bool emit, hipStream_t s);
+void launch_text_cr_fills(const uint8_t* U, const int64_t* uoff, const int32_t* blk_us, int64_t nblk,
+                          int64_t* last_cr_fill, hipStream_t s);
+void launch_text_plan(const Cand* cand, const int64_t* ncand, const int64_t* blk_pos,
+                      const int32_t* blk_us, const int64_t* uoff, int64_t nblk, int64_t flen,
+                      const uint8_t* U, int64_t ulen, const int64_t* term, int64_t nterm,
+                      const int64_t* last_cr_fill, TextPlan* plans, int64_t nsplit, hipStream_t s);
+void launch_text_values(const uint8_t* U, int64_t ulen, const int64_t* term, int64_t nterm,
+                        const int64_t* idx, int64_t n, int32_t bom, int32_t drop_hash,
+                        int64_t* vstart, int32_t* vlen, uint64_t* hash, uint8_t* keep,
+                        hipStream_t s);
+void launch_text_parts(const int64_t* out_off, const int64_t* koff, int64_t nsplit, PartRange* parts,
+                       hipStream_t s);
+void launch_text_export(const int64_t* kept, int64_t n, const int64_t* vstart, const int32_t* vlen,
+                        const uint64_t* hash, int64_t* o_start, int32_t* o_len, uint64_t* o_hash,
+                        hipStream_t s);
+void launch_text_gather(const uint8_t* U, const int64_t* vstart, const int32_t* vlen,
+                        const int64_t* kept, const int64_t* out_off, int64_t n, uint8_t* out,
+                        hipStream_t s);
 
 }  // namespace dq

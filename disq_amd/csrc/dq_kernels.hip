@@ -57,16 +57,22 @@ __device__ int guesser_at(const uint8_t* C, int64_t q, int64_t L, int32_t* cs, i
   return 0;
 }
 
-// One workgroup of 256 lanes per 64 KiB chunk; each lane tests 16 positions per step with one
+// One workgroup of 256 lanes per 16 KiB chunk; each lane tests 16 positions per step with one
 // 16-byte coalesced load (+4 look-ahead bytes).  Hits are rare and collected in LDS, then
-// written sorted into the chunk's fixed slot range.
+// written sorted into the chunk's fixed slot range of CAP entries.  Pass 1 (LISTED = false)
+// covers every chunk with CAP = SCAN_CAP and lists the chunks with more hits (highly
+// compressible data: BGZF blocks of ~100 bytes); pass 2 (LISTED = true) re-scans only those,
+// with CAP = SCAN_CAP_BIG slots each (over_map[chunk] = their index).
+template <int CAP, bool LISTED>
 __global__ __launch_bounds__(256) void bgzf_scan_kernel(const uint8_t* __restrict__ C, int64_t n,
                                                         int64_t L, Cand* __restrict__ slots,
                                                         int32_t* __restrict__ counts,
-                                                        int32_t* __restrict__ overflow) {
-  __shared__ Cand hits[SCAN_CAP];
+                                                        int32_t* __restrict__ over_list,
+                                                        int32_t* __restrict__ over_map) {
+  __shared__ Cand hits[CAP];
   __shared__ int32_t nh;
-  const int64_t base = (int64_t)blockIdx.x * SCAN_CHUNK;
+  const int64_t chunk = LISTED ? (int64_t)over_list[1 + blockIdx.x] : (int64_t)blockIdx.x;
+  const int64_t base = chunk * SCAN_CHUNK;
   if (threadIdx.x == 0) nh = 0;
   __syncthreads();
   for (int it = 0; it < SCAN_CHUNK / 4096; it++) {
@@ -86,7 +92,7 @@ __global__ __launch_bounds__(256) void bgzf_scan_kernel(const uint8_t* __restric
           int32_t cs = 0, us = 0;
           int r = guesser_at(C, q, L, &cs, &us);
           int slot = atomicAdd(&nh, 1);
-          if (slot < SCAN_CAP) {
+          if (slot < CAP) {
             Cand c;
             c.pos = q;
             c.csize = cs;
@@ -101,32 +107,44 @@ __global__ __launch_bounds__(256) void bgzf_scan_kernel(const uint8_t* __restric
   }
   __syncthreads();
   int32_t m = nh;
-  if (m > SCAN_CAP) {
+  if (m > CAP) {
     if (threadIdx.x == 0) {
-      *overflow = 1;
-      counts[blockIdx.x] = 0;
+      counts[chunk] = 0;
+      if (LISTED) {
+        over_list[0] = -1;  // more than SCAN_CAP_BIG magic positions in 16 KiB: unsupported
+      } else {
+        const int32_t k = atomicAdd(&over_list[0], 1);
+        if (k < SCAN_OVER_MAX) over_list[1 + k] = (int32_t)chunk;
+      }
     }
     return;
   }
   // rank sort by position
+  const int64_t slot0 = LISTED ? (int64_t)blockIdx.x * CAP : chunk * CAP;
   for (int i = threadIdx.x; i < m; i += 256) {
     Cand c = hits[i];
     int rank = 0;
     for (int j = 0; j < m; j++) rank += hits[j].pos < c.pos;
-    slots[(int64_t)blockIdx.x * SCAN_CAP + rank] = c;
+    slots[slot0 + rank] = c;
   }
-  if (threadIdx.x == 0) counts[blockIdx.x] = m;
+  if (threadIdx.x == 0) {
+    counts[chunk] = m;
+    if (LISTED) over_map[chunk] = (int32_t)blockIdx.x;
+  }
 }
 
 __global__ void gather_slots_kernel(const Cand* __restrict__ slots, const int32_t* __restrict__ counts,
                                     const int64_t* __restrict__ offs, int64_t nchunks,
-                                    Cand* __restrict__ out, int64_t cap) {
+                                    Cand* __restrict__ out, int64_t cap,
+                                    const int32_t* __restrict__ over_map, const Cand* __restrict__ big) {
   int64_t ch = blockIdx.x;
   if (ch >= nchunks) return;
   int32_t m = counts[ch];
   int64_t o = offs[ch];
+  const int32_t ov = over_map ? over_map[ch] : -1;
+  const Cand* src = ov >= 0 ? big + (int64_t)ov * SCAN_CAP_BIG : slots + ch * SCAN_CAP;
   for (int i = threadIdx.x; i < m; i += blockDim.x)
-    if (o + i < cap) out[o + i] = slots[ch * SCAN_CAP + i];
+    if (o + i < cap) out[o + i] = src[i];
 }
 
 // ------------------------------------------------------------------ scans
@@ -1064,7 +1082,7 @@ __global__ __launch_bounds__(256) void compact_kept_kernel(const int64_t* __rest
                                                            const int64_t* __restrict__ off, int64_t n,
                                                            int64_t* __restrict__ kept) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n && keep[i]) kept[off[i]] = idx[i];
+  if (i < n && keep[i]) kept[off[i]] = idx ? idx[i] : i;
 }
 
 __global__ __launch_bounds__(256) void keep_to_i32_kernel(const uint8_t* __restrict__ keep, int64_t n,
@@ -1159,17 +1177,27 @@ __global__ __launch_bounds__(256) void gather_raw_kernel(const uint8_t* __restri
 // ------------------------------------------------------------------ launchers
 void launch_bgzf_scan(const uint8_t* C, int64_t n, int64_t L, Cand* slots_out, int64_t cap,
                       int32_t* chunk_counts, int64_t n_chunks, int64_t* d_count,
-                      int32_t* d_overflow, hipStream_t s) {
+                      int32_t* over_list, hipStream_t s) {
   (void)cap;
   (void)d_count;
-  hipLaunchKernelGGL(bgzf_scan_kernel, dim3((unsigned)n_chunks), dim3(256), 0, s, C, n, L,
-                     slots_out, chunk_counts, d_overflow);
+  if (n_chunks <= 0) return;
+  hipLaunchKernelGGL((bgzf_scan_kernel<SCAN_CAP, false>), dim3((unsigned)n_chunks), dim3(256), 0, s,
+                     C, n, L, slots_out, chunk_counts, over_list, nullptr);
+}
+
+void launch_bgzf_scan_listed(const uint8_t* C, int64_t n, int64_t L, Cand* big, int64_t n_over,
+                             int32_t* chunk_counts, int32_t* over_list, int32_t* over_map,
+                             hipStream_t s) {
+  if (n_over <= 0) return;
+  hipLaunchKernelGGL((bgzf_scan_kernel<SCAN_CAP_BIG, true>), dim3((unsigned)n_over), dim3(256), 0,
+                     s, C, n, L, big, chunk_counts, over_list, over_map);
 }
 
 void launch_gather_slots(const Cand* slots, const int32_t* counts, const int64_t* offs,
-                         int64_t nchunks, Cand* out, int64_t cap, hipStream_t s) {
+                         int64_t nchunks, Cand* out, int64_t cap, const int32_t* over_map,
+                         const Cand* big, hipStream_t s) {
   hipLaunchKernelGGL(gather_slots_kernel, dim3((unsigned)nchunks), dim3(64), 0, s, slots, counts,
-                     offs, nchunks, out, cap);
+                     offs, nchunks, out, cap, over_map, big);
 }
 
 void launch_exclusive_scan_i32(const int32_t* in, int64_t* out, int64_t n, int64_t* tmp,

@@ -268,6 +268,36 @@ int dq_debug_inflated(dq_ctx* ctx, uint8_t* host_out, int64_t cap, int64_t* len)
  * virtual offsets where it fires, ascending, up to cap; *n = how many there are. */
 int dq_debug_guess_all(dq_ctx* ctx, uint64_t* voffs, int64_t cap, int64_t* n);
 
+/* ---- BGZF text (VCF) path ----------------------------------
+ * Replaces, for a BGZF-compressed text file, Hadoop's TextInputFormat record reader running over
+ * Disq's splittable codecs: BGZFCodec / BGZFEnhancedGzipCodec.createInputStream
+ * (D/impl/formats/bgzf/BGZFCodec.java:57-68, BGZFEnhancedGzipCodec.java:41-74) and
+ * BGZFSplitCompressionInputStream (BGZFSplitCompressionInputStream.java:14-106) under Hadoop 2.7
+ * LineRecordReader, as VcfSource.getVariants uses them (D/impl/formats/vcf/VcfSource.java:88-113).
+ * A partition is one FileInputFormat split (same arithmetic as the BAM path); its lines are the
+ * values LineRecordReader returns, terminators excluded; drop_header_lines drops the values
+ * starting with '#' (VcfSource.java:108).  Parsing a line into a VariantContext is the caller's. */
+typedef struct dq_text_batch {
+  int64_t n_lines;
+  int64_t* line_offset;   /* value offset in the file's decompressed stream */
+  int32_t* line_len;      /* value length in bytes */
+  uint64_t* hash;         /* hash of the value bytes (same function as the record hash) */
+  int64_t* data_offset;   /* value k = data[data_offset[k], data_offset[k] + line_len[k]) */
+  uint8_t* data;
+  int64_t n_bytes;
+  int64_t n_partitions;
+  int64_t* part_offset;   /* lines of partition p: [part_offset[p], part_offset[p + 1]) */
+  uint64_t* part_digest;  /* ordered digest of the partition's line hashes */
+} dq_text_batch;
+
+int dq_text_open_memory(dq_ctx* ctx, const uint8_t* bytes, int64_t len);
+int dq_text_open_path(dq_ctx* ctx, const char* path);
+/* Scan, inflate, line planning and digests; the lines stay in HBM.  stats: n_records = lines
+ * kept, n_filtered = '#' lines dropped, digest = whole-file digest of the partition digests. */
+int dq_text_run(dq_ctx* ctx, int32_t drop_header_lines, dq_stats* stats);
+int dq_text_read(dq_ctx* ctx, int32_t drop_header_lines, dq_text_batch** out);
+void dq_text_batch_free(dq_text_batch* b);
+
 void dq_batch_free(dq_batch* b);
 void dq_free(void* p);
 

@@ -1037,3 +1037,256 @@ int dqo_run_partitions(const uint8_t* data, int64_t len, const int64_t* starts,
   pthread_mutex_destroy(&j.mu);
   return j.err ? DQO_EFORMAT : 0;
 }
+
+/* ================================================================== BGZF text (VCF) path
+ * TextInputFormat over a BGZF file with Disq's splittable codecs: per split, the lines Hadoop's
+ * LineRecordReader returns.  Restated, as a literal simulation:
+ *   D/impl/formats/bgzf/BGZFCodec.java:57-68 (and BGZFEnhancedGzipCodec.java:41-74 for BGZF
+ *     data): adjustedStart = guessNextBGZFPos(start, end).pos, or end when there is none;
+ *   D/impl/formats/bgzf/BGZFSplitCompressionInputStream.java:14-106: reads within one block;
+ *     at a block end it reports END_OF_BLOCK, then returns ONE byte of the next block and
+ *     advertises getPos = adjustedStart + (block address relative to adjustedStart) + 1;
+ *   htsjdk 2.16.0 BlockCompressedInputStream (stream mode; not vendored): available(),
+ *     endOfBlock(), getPosition() with the end-of-block pointer normalisation;
+ *   Hadoop 2.7 (not vendored): LineRecordReader.initialize/nextKeyValue/skipUtfByteOrderMark,
+ *     CompressedSplitLineReader.fillBuffer/readLine/needAdditionalRecordAfterSplit,
+ *     LineReader.readDefaultLine (CR, LF and CRLF terminators) with io.file.buffer.size = 4096;
+ *   D/impl/formats/vcf/VcfSource.java:103-113: lines starting with '#' are dropped. */
+#define TX_BUF 4096
+typedef struct {
+  rdr r;              /* block loader (inflate_block) */
+  int64_t start_pos;  /* adjustedStart: stream address 0 */
+  int have;           /* mCurrentBlock != null */
+  int64_t addr;       /* absolute address of the current block */
+  int32_t csize, len, off;
+  const uint8_t* data;
+  int64_t processed;  /* processedPosition (relative) */
+  int64_t cpos;       /* compressedStreamPosition */
+  int advertise;
+  int64_t u_base;     /* absolute decompressed offset of the current block's first byte */
+  const int64_t* chain_pos; const int64_t* chain_u; int64_t nchain;
+  int err;
+} tstream;
+
+static int64_t tx_u_of(tstream* t, int64_t addr) {
+  int64_t lo = 0, hi = t->nchain;
+  while (lo < hi) {
+    int64_t m = (lo + hi) / 2;
+    if (t->chain_pos[m] < addr) lo = m + 1; else hi = m;
+  }
+  if (lo < t->nchain && t->chain_pos[lo] == addr) return t->chain_u[lo];
+  return -1;
+}
+
+/* BlockCompressedInputStream.readBlock: the next block at the stream position */
+static int tx_read_block(tstream* t) {
+  int64_t a = t->have ? t->addr + t->csize : t->start_pos;
+  blkbuf* b;
+  int e = rdr_load(&t->r, a, &b);
+  if (e) { t->err = e == R_FORMAT ? DQO_EFORMAT : DQO_EIO; return -1; }
+  t->have = 1;
+  t->r.cur = b;  /* keep it cached while other blocks load */
+  t->addr = a;
+  t->csize = b->csize;
+  t->len = b->len;
+  t->off = 0;
+  t->data = b->data;
+  if (b->len > 0) {
+    t->u_base = tx_u_of(t, a);
+    if (t->u_base < 0) { set_err(t->r.f, "text block off the BGZF chain"); t->err = DQO_EFORMAT; return -1; }
+  }
+  return 0;
+}
+static int tx_available(tstream* t) {
+  if (!t->have || t->off == t->len)
+    if (tx_read_block(t)) return -1;
+  return t->len - t->off;
+}
+static int tx_end_of_block(const tstream* t) { return t->have && t->off == t->len; }
+static int64_t tx_position_block(const tstream* t) { /* getPosition() >> 16, relative */
+  if (!t->have) return 0;
+  if (t->off > 0 && t->off == t->len) return t->addr + t->csize - t->start_pos;
+  return t->addr - t->start_pos;
+}
+/* readWithinBlock: n > 0 bytes, -1 end of stream, -2 end of block; *u0 = offset of byte 0 */
+static int tx_read_within(tstream* t, uint8_t* dst, int n, int64_t* u0) {
+  if (tx_end_of_block(t)) {
+    int av = tx_available(t);
+    if (av < 0) return -3;
+    t->processed = tx_position_block(t);
+    return av == 0 ? -1 : -2;
+  }
+  int av = tx_available(t);
+  if (av < 0) return -3;
+  int k = av < n ? av : n;
+  if (k == 0) return 0;  /* an empty first block: read(b, off, 0) == 0, EOF to LineReader */
+  memcpy(dst, t->data + t->off, (size_t)k);
+  *u0 = t->u_base + t->off;
+  t->off += k;
+  return k;
+}
+/* BGZFSplitCompressionInputStream.read(b, 0, n) */
+static int tx_read(tstream* t, uint8_t* dst, int n, int64_t* u0) {
+  int res = tx_read_within(t, dst, n, u0);
+  if (res == -3) return -3;
+  if (res == -2) t->advertise = 1;
+  if (t->advertise) {
+    res = tx_read_within(t, dst, 1, u0);
+    if (res == -3) return -3;
+    t->cpos = t->start_pos + t->processed + 1;
+    t->advertise = 0;
+  }
+  return res;
+}
+
+typedef struct {
+  tstream* s;
+  uint8_t buf[TX_BUF];
+  int64_t bu0;        /* absolute decompressed offset of buf[0] */
+  int blen, bpos;
+  int need_additional, finished;
+  int64_t end;        /* getAdjustedEnd */
+} lreader;
+
+static int lr_fill(lreader* L, int in_delim) {
+  int64_t u0 = 0;
+  int n = tx_read(L->s, L->buf, TX_BUF, &u0);
+  if (n == -3) return -3;
+  if (n > 0) L->bu0 = u0;
+  if (in_delim && n > 0) L->need_additional = L->buf[0] != '\n';
+  return n;
+}
+
+typedef struct {
+  int64_t start;      /* absolute decompressed offset of the line's first byte (-1: none) */
+  int64_t len;        /* value length (terminator excluded) */
+  uint8_t head[3];    /* the value's first bytes */
+  int nhead;
+} tline;
+
+/* LineReader.readDefaultLine (maxLineLength, maxBytesToConsume = Integer.MAX_VALUE): returns the
+ * bytes consumed; the value is the line's first `len` bytes. */
+static int64_t lr_read_line(lreader* L, tline* o) {
+  int64_t consumed = 0;
+  int nl_len = 0, prev_cr = 0;
+  o->start = -1;
+  o->len = 0;
+  o->nhead = 0;
+  do {
+    int startp = L->bpos;
+    if (L->bpos >= L->blen) {
+      startp = L->bpos = 0;
+      if (prev_cr) ++consumed;
+      L->blen = lr_fill(L, prev_cr);
+      if (L->blen == -3) return -3;
+      if (L->blen <= 0) break;
+    }
+    if (o->start < 0) o->start = L->bu0 + startp;
+    for (; L->bpos < L->blen; ++L->bpos) {
+      if (L->buf[L->bpos] == '\n') { nl_len = prev_cr ? 2 : 1; ++L->bpos; break; }
+      if (prev_cr) { nl_len = 1; break; }
+      prev_cr = L->buf[L->bpos] == '\r';
+    }
+    int rl = L->bpos - startp;
+    if (prev_cr && nl_len == 0) --rl;
+    consumed += rl;
+    int app = rl - nl_len;
+    for (int i = 0; i < app && o->nhead < 3; i++) o->head[o->nhead++] = L->buf[startp + i];
+    if (app > 0) o->len += app;
+  } while (nl_len == 0);
+  return consumed;
+}
+/* CompressedSplitLineReader.readLine */
+static int64_t csl_read_line(lreader* L, tline* o) {
+  if (L->finished) { o->start = -1; o->len = 0; o->nhead = 0; return 0; }
+  if (L->s->cpos > L->end) L->finished = 1;
+  return lr_read_line(L, o);
+}
+
+/* Block chain of a whole BGZF file: positions and decompressed offsets (test helper). */
+static int64_t tx_chain(dqo_file* f, int64_t** pos, int64_t** uo) {
+  int64_t cap = f->len / 26 + 2, n = 0, u = 0, a = 0;
+  *pos = (int64_t*)malloc(sizeof(int64_t) * (size_t)cap);
+  *uo = (int64_t*)malloc(sizeof(int64_t) * (size_t)cap);
+  if (!*pos || !*uo) return DQO_ENOMEM;
+  while (a + 18 <= f->len && n < cap) {
+    const uint8_t* h = f->data + a;
+    if (h[0] != 0x1f || h[1] != 0x8b) break;
+    int32_t cs = rd16(h + 16) + 1;
+    if (cs < 26 || a + cs > f->len) break;
+    (*pos)[n] = a;
+    (*uo)[n] = u;
+    u += rd32(h + cs - 4);
+    n++;
+    a += cs;
+  }
+  return n;
+}
+
+/* The lines of split [start, end): value offsets (absolute in the decompressed stream) and
+ * lengths, in order; drop_hash drops values starting with '#' (VcfSource.java:108).  Returns the
+ * count (entries written up to cap) or a negative DQO_ error. */
+int64_t dqo_text_split_lines(dqo_file* f, int64_t start, int64_t end, int drop_hash,
+                             int64_t* vstart, int64_t* vlen, int64_t cap) {
+  int64_t *cp = NULL, *cu = NULL;
+  int64_t nchain = tx_chain(f, &cp, &cu);
+  tstream* t = (tstream*)calloc(1, sizeof(tstream));
+  lreader* L = (lreader*)calloc(1, sizeof(lreader));
+  int64_t n = 0;
+  if (nchain < 0) { n = nchain; goto out; }
+  if (!t || !L || rdr_init(&t->r, f)) { n = DQO_ENOMEM; goto out; }
+  t->chain_pos = cp; t->chain_u = cu; t->nchain = nchain;
+  {
+    /* BGZFCodec.createInputStream */
+    int64_t gp = 0; int32_t gc = 0, gu = 0;
+    const int64_t adj = dqo_guess_next_bgzf(f, start, end, &gp, &gc, &gu) ? gp : end;
+    t->start_pos = adj;
+    t->cpos = adj;  /* updatePos(false), processedPosition 0 */
+    L->s = t;
+    L->end = end;
+    tline ln;
+    int64_t pos = adj;
+    /* LineRecordReader.initialize: start = adjustedStart; unless 0, the first line is dropped */
+    if (adj != 0) {
+      int64_t k = csl_read_line(L, &ln);
+      if (k < 0) { n = t->err ? t->err : DQO_EFORMAT; goto out; }
+      pos += k;
+    }
+    /* one nextKeyValue call per iteration */
+    for (;;) {
+      if (!(t->cpos <= end || (!L->finished && L->need_additional))) break;
+      int64_t k = csl_read_line(L, &ln);
+      if (k < 0) { n = t->err ? t->err : DQO_EFORMAT; goto out; }
+      int64_t vs = ln.start, vl = ln.len;
+      const uint8_t* hd = ln.head;
+      int nh = ln.nhead;
+      if (pos == 0 && vl >= 3 && hd[0] == 0xEF && hd[1] == 0xBB && hd[2] == 0xBF) {
+        vs += 3;  /* skipUtfByteOrderMark */
+        vl -= 3;
+        k -= 3;
+        hd += 3;
+        nh = 0;
+      }
+      pos += k;
+      if (k == 0) break;
+      if (drop_hash && vl > 0) {
+        uint8_t c0;
+        if (nh > 0) c0 = hd[0];
+        else { /* after a BOM: the value's first byte */
+          int64_t lo = 0, hi = nchain;
+          while (lo + 1 < hi) { int64_t m = (lo + hi) / 2; if (cu[m] <= vs) lo = m; else hi = m; }
+          blkbuf* b;
+          if (rdr_load(&t->r, cp[lo], &b)) { n = DQO_EFORMAT; goto out; }
+          c0 = b->data[vs - cu[lo]];
+        }
+        if (c0 == '#') continue;
+      }
+      if (vstart && n < cap) { vstart[n] = vs; vlen[n] = vl; }
+      n++;
+    }
+  }
+out:
+  if (t) rdr_free(&t->r);
+  free(t); free(L); free(cp); free(cu);
+  return n;
+}

@@ -124,6 +124,12 @@ uint64_t dqo_stream_digest(const uint64_t* hashes, int64_t n, uint64_t start_ind
 /* Inflate every BGZF block of the file in order from offset 0 (real headers, htsjdk
  * BlockCompressedInputStream semantics).  Returns decompressed length, or <0.  If out==NULL,
  * returns the required length. */
+/* BGZF text (VCF) path: the lines Hadoop's LineRecordReader returns for split [start, end) of a
+ * BGZF text file read through Disq's BGZFCodec (value offsets in the decompressed stream and
+ * value lengths); drop_hash drops lines starting with '#' (VcfSource.getVariants). */
+int64_t dqo_text_split_lines(dqo_file* f, int64_t start, int64_t end, int drop_hash,
+                             int64_t* vstart, int64_t* vlen, int64_t cap);
+
 int64_t dqo_inflate_file(dqo_file* f, uint8_t* out, int64_t cap);
 
 /* CPU baseline: Disq's per-partition work (a4 + a6..a8 + hash) for a list of splits on

@@ -96,6 +96,9 @@ def lib():
         L.dqo_optimize_intervals.restype = C.c_int64
         L.dqo_optimize_intervals.argtypes = [P(C.c_int32)] * 3 + [C.c_int64]
         L.dqo_record_overlaps.argtypes = [C.c_void_p] + [P(C.c_int32)] * 3 + [C.c_int64]
+        L.dqo_text_split_lines.restype = C.c_int64
+        L.dqo_text_split_lines.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_int, C.c_void_p,
+                                           C.c_void_p, C.c_int64]
         L.dqo_record_hash.restype = C.c_uint64
         L.dqo_record_hash.argtypes = [C.c_void_p, C.c_int64]
         L.dqo_stream_digest.restype = C.c_uint64
@@ -322,6 +325,58 @@ class OracleBam:
                             local_block_size=HADOOP_LOCAL_BLOCK_SIZE):
         return [self.read_chunk(*ch) for _, _, ch in
                 self.plan_sbi(sbi_bytes, split_size, nio, local_block_size) if ch is not None]
+
+
+class OracleText:
+    """A BGZF-compressed text file (VCF) read as Disq's VcfSource reads it: Hadoop TextInputFormat
+    with Disq's splittable BGZF codec (BGZFCodec.java:57-68, BGZFSplitCompressionInputStream.java),
+    LineRecordReader per split, lines starting with '#' dropped (VcfSource.java:103-113)."""
+
+    def __init__(self, data: bytes):
+        self._buf = np.frombuffer(data, np.uint8).copy()
+        self.len = len(self._buf)
+        self._h = lib().dqo_open_mem(self._buf.ctypes.data, self.len, 1)
+        self._u = None
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().dqo_close(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+    def inflated(self):
+        if self._u is None:
+            n = lib().dqo_inflate_file(self._h, None, 0)
+            if n < 0:
+                raise OracleError(f"oracle error {n}: {lib().dqo_last_error(self._h).decode()}")
+            out = np.zeros(n, np.uint8)
+            lib().dqo_inflate_file(self._h, out.ctypes.data, n)
+            self._u = out
+        return self._u
+
+    def split_lines(self, start, end, drop_hash=True):
+        """(value offsets in the decompressed stream, value lengths) of split [start, end)."""
+        n = lib().dqo_text_split_lines(self._h, start, end, int(drop_hash), None, None, 0)
+        if n < 0:
+            raise OracleError(f"oracle error {n}: {lib().dqo_last_error(self._h).decode()}")
+        vs = np.zeros(max(n, 1), np.int64)
+        vl = np.zeros(max(n, 1), np.int64)
+        m = lib().dqo_text_split_lines(self._h, start, end, int(drop_hash), vs.ctypes.data,
+                                       vl.ctypes.data, n)
+        assert m == n
+        return vs[:n], vl[:n]
+
+    def read_partitions(self, split_size=0, drop_hash=True, nio=False,
+                        local_block_size=HADOOP_LOCAL_BLOCK_SIZE):
+        return [self.split_lines(s, e, drop_hash)
+                for s, e in path_splits(self.len, split_size, nio, local_block_size)]
+
+    def lines(self, part):
+        u = self.inflated()
+        vs, vl = part
+        return [bytes(u[a:a + b]) for a, b in zip(vs.tolist(), vl.tolist())]
 
 
 def sbi_offsets(sbi_bytes):
