@@ -95,7 +95,8 @@ EXPORTS = ("dq_ctx_create", "dq_ctx_destroy", "dq_last_error", "dq_version", "dq
            "dq_set_splitting_index", "dq_write_sbi", "dq_open_shard_device", "dq_decode_chunk",
            "dq_get_stats", "dq_partition_digests", "dq_open_shard_path",
            "dq_decode_chunk_filtered", "dq_debug_guess_all", "dq_text_open_memory",
-           "dq_text_open_path", "dq_text_run", "dq_text_read", "dq_text_batch_free")
+           "dq_text_open_path", "dq_text_run", "dq_text_read", "dq_text_batch_free",
+           "dq_bgzf_compress", "dq_bgzf_compress_resident", "dq_bgzf_fetch")
 
 _lib = None
 _lock = threading.Lock()
@@ -154,6 +155,9 @@ def lib():
         L.dq_text_run.argtypes = [vp, C.c_int32, P(DqStats)]
         L.dq_text_read.argtypes = [vp, C.c_int32, P(P(DqTextBatch))]
         L.dq_text_batch_free.argtypes = [P(DqTextBatch)]
+        L.dq_bgzf_compress.argtypes = [vp, vp, C.c_int64, P(C.c_void_p), P(C.c_int64)]
+        L.dq_bgzf_compress_resident.argtypes = [vp, P(C.c_int64), P(C.c_double)]
+        L.dq_bgzf_fetch.argtypes = [vp, vp, C.c_int64]
         L.dq_free.argtypes = [vp]
         _lib = L
         return L
@@ -319,6 +323,29 @@ class Context:
 
     def open_path(self, path):
         check(self._h, lib().dq_open_path(self._h, path.encode()))
+
+    # ---- BGZF compression (write path)
+    def bgzf_compress(self, data) -> bytes:
+        """BGZF blocks of `data` (65280 bytes each, no EOF terminator), compressed on the GPU."""
+        buf = np.frombuffer(data, np.uint8)
+        out, n = C.c_void_p(), C.c_int64()
+        check(self._h, lib().dq_bgzf_compress(self._h, buf.ctypes.data if len(buf) else None,
+                                              len(buf), C.byref(out), C.byref(n)))
+        try:
+            return C.string_at(out, n.value) if n.value else b""
+        finally:
+            lib().dq_free(out)
+
+    def bgzf_compress_resident(self):
+        """Compress the open file's resident decompressed stream; (compressed length, device ms)."""
+        n, ms = C.c_int64(), C.c_double()
+        check(self._h, lib().dq_bgzf_compress_resident(self._h, C.byref(n), C.byref(ms)))
+        return n.value, ms.value
+
+    def bgzf_fetch(self, n) -> np.ndarray:
+        out = np.zeros(max(1, n), np.uint8)
+        check(self._h, lib().dq_bgzf_fetch(self._h, out.ctypes.data, n))
+        return out[:n]
 
     # ---- BGZF text (VCF) path
     def text_open_bytes(self, data):

@@ -92,6 +92,9 @@ struct dq_ctx {
   DevBuf t_tcount, t_toff, t_term, t_crf, t_plans, t_rng, t_idx, t_vs, t_vl, t_hash, t_keep,
       t_keep32, t_koff, t_kept;
   std::vector<TextPlan> tplans_h;
+  // BGZF deflate (write path)
+  DevBuf z_in, z_stage, z_link, z_slots, z_size, z_off, z_out;
+  int64_t z_len = 0;
   const uint8_t* cext = nullptr;  // dq_open_shard_device: caller-owned device bytes instead of C
   // dq_decode_chunk: the window holds one Chunk [chunk_vs, chunk_ve) (shard coordinates); its
   // records are walked from the exact start pointer, no split planning or guessing
@@ -609,7 +612,7 @@ static int run_pipeline(dq_ctx* ctx) {
       for (int64_t i = 0; i < nblk; i++)
         for (int k = 0; k < 16; k++) acc[k] += (double)h[16 * (size_t)i + k];
       static const char* nm[16] = {"header", "tables", "spec", "rounds", "scan", "emit",
-                                   "resolve+store", "crc", "hdr_read_lengths", "unmerged_spec_err_eob", "redo_rounds", "unmerged_other",
+                                   "resolve+store", "crc", "hdr_read_lengths", "resolve_chain_cycles", "redo_rounds", "resolve_max_hops_sum",
                                    "unmerged_spec_exit", "merge_j_sum", "redo_merged", "res_batches"};
       fprintf(stderr, "[dq] inflate3 phase cycles per BGZF block (thread 0, s_memtime):");
       for (int k = 0; k < 16; k++)
@@ -1018,6 +1021,47 @@ static int text_run(dq_ctx* ctx, int32_t drop_hash) {
   }
   ctx->have_text = true;
   ctx->text_drop = drop_hash;
+  return 0;
+}
+
+// ------------------------------------------------------------------ BGZF deflate (write path)
+// htsjdk BlockCompressedOutputStream over a byte stream in HBM: blocks of 65280 bytes compressed
+// in batches (the per-lane bit staging is 80 KiB per block), packed into ctx->z_out.
+static int bgzf_compress_dev(dq_ctx* ctx, const uint8_t* d_src, int64_t len, double* ms) {
+  if (!deflate_tables(ctx->o.device)) RET(DQ_EDEVICE, "deflate table initialisation failed");
+  hipStream_t s = ctx->s;
+  const int64_t nblk = bgzf_block_count(len);
+  const int64_t batch = std::min<int64_t>(std::max<int64_t>(nblk, 1), 8192);
+  int rc;
+  if ((rc = ensure_all(ctx, ctx->z_stage, bgzf_stage_bytes(batch)))) return rc;
+  if ((rc = ensure_all(ctx, ctx->z_link, (size_t)batch * 65536 * 2))) return rc;
+  if ((rc = ensure_all(ctx, ctx->z_slots, (size_t)batch * 65536))) return rc;
+  if ((rc = ensure_all(ctx, ctx->z_size, 4 * (size_t)batch))) return rc;
+  if ((rc = ensure_all(ctx, ctx->z_off, 8 * (size_t)batch))) return rc;
+  if ((rc = ensure_all(ctx, ctx->z_out, (size_t)std::max<int64_t>(nblk, 1) * 65536))) return rc;
+  HIPCHK(hipEventRecord(ctx->ev[0], s));
+  std::vector<int32_t> sz((size_t)batch);
+  std::vector<int64_t> off((size_t)batch);
+  int64_t total = 0;
+  for (int64_t b0 = 0; b0 < nblk; b0 += batch) {
+    const int64_t nb = std::min(batch, nblk - b0);
+    launch_bgzf_deflate(d_src, len, b0, nb, ctx->z_stage.as<uint32_t>(), ctx->z_link.as<uint16_t>(),
+                        ctx->z_slots.as<uint8_t>(), ctx->z_size.as<int32_t>(), s);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(sz.data(), ctx->z_size.p, 4 * (size_t)nb, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (int64_t i = 0; i < nb; i++) {
+      off[(size_t)i] = total;
+      total += sz[(size_t)i];
+    }
+    HIPCHK(hipMemcpyAsync(ctx->z_off.p, off.data(), 8 * (size_t)nb, hipMemcpyHostToDevice, s));
+    launch_bgzf_pack(ctx->z_slots.as<uint8_t>(), ctx->z_size.as<int32_t>(), ctx->z_off.as<int64_t>(), nb,
+                     ctx->z_out.as<uint8_t>(), s);
+  }
+  HIPCHK(hipEventRecord(ctx->ev[1], s));
+  HIPCHK(hipStreamSynchronize(s));
+  ctx->z_len = total;
+  if (ms) *ms = ev_ms(ctx->ev[0], ctx->ev[1]);
   return 0;
 }
 
@@ -2514,6 +2558,44 @@ void dq_text_batch_free(dq_text_batch* b) {
   free(b->part_offset);
   free(b->part_digest);
   free(b);
+}
+
+int dq_bgzf_compress(dq_ctx* ctx, const uint8_t* data, int64_t len, uint8_t** out, int64_t* out_len) {
+  if (!ctx || !out || !out_len || len < 0 || (!data && len > 0)) return DQ_EINVAL;
+  ON_DEVICE(ctx);
+  *out = nullptr;
+  *out_len = 0;
+  int rc;
+  if ((rc = ensure_all(ctx, ctx->z_in, (size_t)len + 64))) return rc;
+  if (len) HIPCHK(hipMemcpy(ctx->z_in.p, data, (size_t)len, hipMemcpyHostToDevice));
+  double ms = 0;
+  if ((rc = bgzf_compress_dev(ctx, ctx->z_in.as<uint8_t>(), len, &ms))) return rc;
+  uint8_t* b = (uint8_t*)malloc((size_t)std::max<int64_t>(1, ctx->z_len));
+  if (!b) return DQ_ENOMEM;
+  if (ctx->z_len) HIPCHK(hipMemcpy(b, ctx->z_out.p, (size_t)ctx->z_len, hipMemcpyDeviceToHost));
+  *out = b;
+  *out_len = ctx->z_len;
+  return 0;
+}
+
+int dq_bgzf_compress_resident(dq_ctx* ctx, int64_t* out_len, double* ms) {
+  if (!ctx) return DQ_EINVAL;
+  ON_DEVICE(ctx);
+  int rc = ctx->text_mode ? text_run(ctx, ctx->text_drop < 0 ? 1 : ctx->text_drop) : run_pipeline(ctx);
+  if (rc) return rc;
+  double t = 0;
+  if ((rc = bgzf_compress_dev(ctx, ctx->U.as<uint8_t>(), ctx->ulen, &t))) return rc;
+  if (out_len) *out_len = ctx->z_len;
+  if (ms) *ms = t;
+  return 0;
+}
+
+int dq_bgzf_fetch(dq_ctx* ctx, uint8_t* host_out, int64_t cap) {
+  if (!ctx || (!host_out && cap > 0)) return DQ_EINVAL;
+  ON_DEVICE(ctx);
+  if (cap < ctx->z_len) RET(DQ_EINVAL, "buffer smaller than the compressed stream");
+  if (ctx->z_len) HIPCHK(hipMemcpy(host_out, ctx->z_out.p, (size_t)ctx->z_len, hipMemcpyDeviceToHost));
+  return 0;
 }
 
 void dq_batch_free(dq_batch* b) {

@@ -1168,17 +1168,15 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       lines_done = lines_to;
     }
     if (TIMING && t == 0) {
-      (void)wgm;
-      (void)tb0; (void)tb1;
+      tacc[9] += tb1 - tb0;  // (a) chains of thread 0's wave
+      tacc[11] += (uint64_t)wgm;  // max hops over the workgroup
       tacc[15] += 1;
     }
   }
   if (TIMING && t == 0) {
     tacc[14] = (uint64_t)L.misc[23];
     tacc[13] = (uint64_t)L.misc[24];
-    tacc[9] = (uint64_t)L.misc[25];
     tacc[12] = (uint64_t)L.misc[26];
-    tacc[11] = (uint64_t)L.misc[27];
   }
   if (sflags & 1) {  // the whole block at the end
     const int32_t lines_to = isize >= head ? (isize - head) / 16 : 0;
@@ -1317,7 +1315,7 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
   if (cfg < 0) {  // DQ_CFG="nb,g" (tuning experiments); default 4,1
     int nb = 4, g = 1;
     if (const char* e = getenv("DQ_CFG")) sscanf(e, "%d,%d", &nb, &g);
-    cfg = g != 4 ? 0 : nb == 1 ? 1 : nb == 4 ? 3 : 2;
+    cfg = g != 4 ? (nb == 2 ? 4 : nb == 8 ? 5 : 0) : nb == 1 ? 1 : nb == 4 ? 3 : 2;
   }
 #define DQ_LAUNCH(TM, NBT, GT)                                                                  \
   hipLaunchKernelGGL((inflate_block_kernel<TM, NBT, GT>), dim3((unsigned)ngrid), dim3(WG), 0, s, C, \
@@ -1328,6 +1326,8 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
     case 1: DQ_LAUNCH(TM, 1, 4); break;   \
     case 2: DQ_LAUNCH(TM, 2, 4); break;   \
     case 3: DQ_LAUNCH(TM, 4, 4); break;   \
+    case 4: DQ_LAUNCH(TM, 2, 1); break;   \
+    case 5: DQ_LAUNCH(TM, 8, 1); break;   \
     default: DQ_LAUNCH(TM, 4, 1); break;  \
   }
   if (tim) {

@@ -237,4 +237,15 @@ void launch_text_gather(const uint8_t* U, const int64_t* vstart, const int32_t* 
                         const int64_t* kept, const int64_t* out_off, int64_t n, uint8_t* out,
                         hipStream_t s);
 
+// ------------------------------------------------------------------ BGZF deflate (write path)
+int64_t bgzf_block_count(int64_t n);
+size_t bgzf_stage_bytes(int64_t nblk);
+bool deflate_tables(int device);
+// Blocks [blk0, blk0 + nblk) of src[0, n_in) (65280 bytes each) into fixed 64 KiB slots.
+void launch_bgzf_deflate(const uint8_t* src, int64_t n_in, int64_t blk0, int64_t nblk,
+                         uint32_t* stage, uint16_t* link, uint8_t* out_slots, int32_t* out_size,
+                         hipStream_t s);
+void launch_bgzf_pack(const uint8_t* slots, const int32_t* size, const int64_t* off, int64_t nblk,
+                      uint8_t* out, hipStream_t s);
+
 }  // namespace dq

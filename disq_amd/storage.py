@@ -62,6 +62,7 @@ class HtsjdkReadsTraversalParameters:
 class SAMFileHeader:
     text: str
     sequences: List[tuple]  # (name, length)
+    raw: bytes = b""        # the BAM header as stored (BAMFileWriter.writeHeader's bytes)
 
     def getSequenceDictionary(self):
         return self.sequences
@@ -134,7 +135,7 @@ def _parse_header(raw: bytes) -> SAMFileHeader:
         length = struct.unpack_from("<i", raw, p + 4 + ln)[0]
         seqs.append((name, length))
         p += 8 + ln
-    return SAMFileHeader(text, seqs)
+    return SAMFileHeader(text, seqs, bytes(raw[:p]))
 
 
 def _is_hidden(name):  # HiddenFileFilter (D/impl/file/HiddenFileFilter.java)
@@ -252,6 +253,32 @@ class HtsjdkReadsRddStorage:
                         fields["raw_offset"] = fields["raw_offset"] - r0
                     parts.append(ReadsPartition(fields, raw, int(b["part_digest"][p]), f))
         return HtsjdkReadsRdd(header, ReadsRDD(parts))
+
+    def write(self, rdd: HtsjdkReadsRdd, path: str, tempPartsDirectory: Optional[str] = None):
+        """BamSink.save (D/impl/formats/bam/BamSink.java:32-69) with GPU BGZF compression: each
+        partition's records as a headerless BGZF part (HeaderlessBamOutputFormat, no terminator),
+        the header as its own BGZF blocks (BAMFileWriter.writeHeader), the 28-byte EOF block, then
+        the parts merged in partition order (Merger.mergeParts) into `path`."""
+        header = rdd.getHeader()
+        if not header.raw:
+            raise ValueError("header has no BAM encoding")
+        eof = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+        with _lib.Context(device=self._device) as ctx:
+            pieces = [ctx.bgzf_compress(header.raw)]
+            for p in rdd.getReads().partitions:
+                raw = b"" if p.raw is None else p.raw.tobytes()
+                pieces.append(ctx.bgzf_compress(raw))
+        pieces.append(eof)
+        if tempPartsDirectory:
+            os.makedirs(tempPartsDirectory, exist_ok=True)
+            names = ["header"] + [f"part-r-{i:05d}" for i in range(len(pieces) - 2)] + ["terminator"]
+            for n, d in zip(names, pieces):
+                with open(os.path.join(tempPartsDirectory, n), "wb") as fh:
+                    fh.write(d)
+        with open(path, "wb") as fh:
+            for d in pieces:
+                fh.write(d)
+        return path
 
     @staticmethod
     def _find_index(path):

@@ -298,6 +298,22 @@ int dq_text_run(dq_ctx* ctx, int32_t drop_header_lines, dq_stats* stats);
 int dq_text_read(dq_ctx* ctx, int32_t drop_header_lines, dq_text_batch** out);
 void dq_text_batch_free(dq_text_batch* b);
 
+/* ---- BGZF compression: the write path -----------------------
+ * Replaces htsjdk BlockCompressedOutputStream under HeaderlessBamOutputFormat.BamRecordWriter
+ * (D/impl/formats/bam/HeaderlessBamOutputFormat.java:26-50) and BamSink's header file
+ * (BAMFileWriter.writeHeader, D/impl/formats/bam/BamSink.java:46-50): `data` is cut into blocks
+ * of 65280 bytes (htsjdk DEFAULT_UNCOMPRESSED_BLOCK_SIZE, the last one shorter), each compressed
+ * on the GPU into one BGZF member ('BC' extra field, BSIZE, CRC32, ISIZE).  No EOF terminator is
+ * written (BamSink appends BlockCompressedStreamConstants.EMPTY_GZIP_BLOCK once, after all parts).
+ * The DEFLATE bit stream is this library's own (LZ77 + fixed Huffman, or stored when that does
+ * not fit): the blocks inflate to exactly htsjdk's block contents; the compressed bytes differ
+ * from java.util.zip.Deflater's.  *out is malloc'ed (dq_free). */
+int dq_bgzf_compress(dq_ctx* ctx, const uint8_t* data, int64_t len, uint8_t** out, int64_t* out_len);
+/* The same over the resident decompressed stream of the open file (benchmark / round trip): the
+ * result stays in HBM (dq_bgzf_fetch copies it out); *ms = device time. */
+int dq_bgzf_compress_resident(dq_ctx* ctx, int64_t* out_len, double* ms);
+int dq_bgzf_fetch(dq_ctx* ctx, uint8_t* host_out, int64_t cap);
+
 void dq_batch_free(dq_batch* b);
 void dq_free(void* p);
 

@@ -1,0 +1,95 @@
+"""GPU BGZF compression, the write path: dq_bgzf_compress replaces
+htsjdk BlockCompressedOutputStream under HeaderlessBamOutputFormat / BamSink.
+
+Bar: the output is valid BGZF -- every member has the 'BC' field, BSIZE, a correct CRC32 and
+ISIZE -- cut at htsjdk's 65280-byte block boundaries, and it inflates (zlib, independent of this
+library) to exactly the input; a BAM assembled as BamSink.save does (header blocks, part blocks,
+EOF block) reads back through the oracle to the same records.  Compressed bytes are not compared
+with java.util.zip.Deflater's (a different encoder): parity is on the decompressed content."""
+import os
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+from disq_amd import _lib, synth
+from oracle import oracle as O
+import bamutil as B
+
+pytestmark = pytest.mark.gpu
+
+
+def members(bgzf):
+    out, p = [], 0
+    while p < len(bgzf):
+        h = bgzf[p:p + 18]
+        assert h[:4] == b"\x1f\x8b\x08\x04" and h[10:12] == b"\x06\x00" and h[12:14] == b"BC"
+        cs = struct.unpack_from("<H", h, 16)[0] + 1
+        body = bgzf[p + 18:p + cs - 8]
+        crc, isize = struct.unpack_from("<II", bgzf, p + cs - 8)
+        data = zlib.decompress(body, -15)
+        assert len(data) == isize and zlib.crc32(data) & 0xffffffff == crc
+        out.append(data)
+        p += cs
+    assert p == len(bgzf)
+    return out
+
+
+def check_roundtrip(c, data):
+    z = c.bgzf_compress(data)
+    blocks = members(z)
+    assert b"".join(blocks) == data
+    assert [len(x) for x in blocks] == [min(B.BLOCK_U, len(data) - i)
+                                        for i in range(0, len(data), B.BLOCK_U)]
+    return z
+
+
+def test_edge_sizes():
+    rng = np.random.default_rng(1)
+    with _lib.Context() as c:
+        assert c.bgzf_compress(b"") == b""
+        for n in (1, 2, 3, 257, 4096, B.BLOCK_U - 1, B.BLOCK_U, B.BLOCK_U + 1, 3 * B.BLOCK_U + 17):
+            check_roundtrip(c, rng.integers(0, 4, size=n, dtype=np.uint8).tobytes())
+
+
+def test_incompressible_blocks_are_stored():
+    data = np.random.default_rng(2).integers(0, 256, size=200000, dtype=np.uint8).tobytes()
+    with _lib.Context() as c:
+        z = len(check_roundtrip(c, data))
+    assert z == len(data) + 4 * 26 + 4 * 5  # every block stored
+
+
+def test_bam_stream_ratio_and_roundtrip():
+    r = synth.generate(40000, seed=5, nthreads=8)
+    u = B.inflate_all(r.bam)
+    with _lib.Context() as c:
+        z = check_roundtrip(c, u)
+    assert len(z) < 0.6 * len(u)  # LZ77 + fixed Huffman on BAM records
+
+
+def test_bamsink_assembly_reads_back(tmp_path, golden):
+    """BamSink.save: header file + headerless part files + terminator, merged in order."""
+    from disq_amd.storage import HtsjdkReadsRddStorage
+    src = os.path.join(golden, "1.bam")
+    st = HtsjdkReadsRddStorage.makeDefault().splitSize(128 * 1024)
+    rdd = st.read(src)
+    out = str(tmp_path / "out.bam")
+    st.write(rdd, out)
+    ob = O.OracleBam.from_path(out, verify_crc=True)
+    ref = O.OracleBam.from_path(src)
+    a, b = ob.read_all(), ref.read_all()
+    assert len(a) == len(b) == 4917
+    assert np.array_equal(a["hash"], b["hash"])
+    # and the GPU read path reads it back to the same records
+    back = st.read(out)
+    assert np.array_equal(back.getReads().hashes(), b["hash"])
+
+
+def test_resident_stream_roundtrip(golden):
+    with _lib.Context(verify_crc=True) as c:
+        c.open_path(os.path.join(golden, "1.bam"))
+        n, ms = c.bgzf_compress_resident()
+        z = c.bgzf_fetch(n).tobytes()
+    want = O.OracleBam.from_path(os.path.join(golden, "1.bam")).inflate_all().tobytes()
+    assert b"".join(members(z)) == want
