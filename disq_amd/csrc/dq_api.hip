@@ -1045,9 +1045,25 @@ static int bgzf_compress_dev(dq_ctx* ctx, const uint8_t* d_src, int64_t len, dou
   int64_t total = 0;
   for (int64_t b0 = 0; b0 < nblk; b0 += batch) {
     const int64_t nb = std::min(batch, nblk - b0);
+    static const bool timing = getenv("DQ_DEFLATE_TIMING") != nullptr;
+    uint64_t* tim = nullptr;
+    if (timing) HIPCHK(hipMalloc(&tim, 8 * 8 * (size_t)nb));
     launch_bgzf_deflate(d_src, len, b0, nb, ctx->z_stage.as<uint32_t>(), ctx->z_link.as<uint16_t>(),
-                        ctx->z_slots.as<uint8_t>(), ctx->z_size.as<int32_t>(), s);
+                        ctx->z_slots.as<uint8_t>(), ctx->z_size.as<int32_t>(), tim, s);
     HIPCHK(hipGetLastError());
+    if (timing) {
+      std::vector<uint64_t> h(8 * (size_t)nb);
+      HIPCHK(hipMemcpyAsync(h.data(), tim, 8 * h.size(), hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      (void)hipFree(tim);
+      double acc[8] = {0};
+      for (int64_t i = 0; i < nb; i++)
+        for (int k = 1; k < 8; k++) acc[k] += (double)(h[8 * (size_t)i + k] - h[8 * (size_t)i + k - 1]);
+      static const char* nm[8] = {"", "load", "crc+links", "parse", "huffman", "count+scan", "write", "store"};
+      fprintf(stderr, "[dq] deflate phase cycles per block:");
+      for (int k = 1; k < 8; k++) fprintf(stderr, " %s=%.0f", nm[k], acc[k] / (double)nb);
+      fprintf(stderr, "\n");
+    }
     HIPCHK(hipMemcpyAsync(sz.data(), ctx->z_size.p, 4 * (size_t)nb, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     for (int64_t i = 0; i < nb; i++) {

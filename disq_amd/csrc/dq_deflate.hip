@@ -35,7 +35,7 @@ constexpr int SHORT = 8;                 // distances 1..SHORT always tried
 constexpr int CHAIN = 6;                 // hash-chain links tried
 constexpr int HBITS = 11;                // LDS head table: 2048 entries
 constexpr int MAXM = 258;
-constexpr int SLOT_WORDS = 80;           // staged bits per lane: <= 255 * 9 + 10 bits
+constexpr int SLOT_WORDS = 256;          // staged symbols per lane: <= 255 + the end of block
 constexpr int MAX_DEFLATE = 65536 - 26;  // BSIZE limit: 18-byte header + payload + 8 trailer
 
 __constant__ uint32_t c_dcrc[256];
@@ -91,34 +91,149 @@ __device__ inline void fixed_ll(int sym, uint32_t& code, int& len) {
   else { len = 8; code = rev(0xC0 + sym - 280, 8); }
 }
 
-struct BitOut {
-  uint32_t* w;  // staging slot
-  uint64_t acc;
-  int n;        // bits in acc
-  int words;
-  __device__ void put(uint32_t v, int len) {
-    acc |= (uint64_t)v << n;
-    n += len;
-    if (n >= 32) {
-      w[words++] = (uint32_t)acc;
-      acc >>= 32;
-      n -= 32;
-    }
-  }
-  __device__ int flush() {  // total bits
-    const int bits = words * 32 + n;
-    if (n > 0) w[words] = (uint32_t)acc;
-    return bits;
-  }
-};
-
 struct alignas(16) DLds {
   uint8_t in[65536 + 16];     // the block's bytes; later the deflate image (<= 65510 bytes)
   uint32_t crc_t[256];
   uint32_t lane_bits[DWG];
   uint32_t lane_crc[DWG];
-  int32_t head[1 << HBITS];
+  uint16_t lane_nsym[DWG];
+  int32_t head[1 << HBITS];   // hash heads; then histograms, code tables and scratch (H_* below)
   int32_t misc[8];
+};
+// word offsets inside DLds::head once the hash heads are dead
+enum { H_LL = 0, H_D = 288, H_CL = 320, C_LL = 352, C_D = 640, C_CL = 672, H_TOK = 704,
+       H_SORT = 864, H_W = 1152, H_LEN = 1440, H_LEN_D = 1728, H_LEN_CL = 1760, H_SORT_D = 1792,
+       H_W_D = 1824, H_CNT = 1856, H_CNT_D = 1890, H_BL = 1924, H_END = 1956 };
+static_assert(H_END <= (1 << HBITS), "code tables fit the head table");
+constexpr uint8_t c_clord[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+// Code lengths (<= maxlen) of an alphabet of m <= 286 symbols from frequencies f, by one wave:
+// a rank sort (frequency, symbol), then on lane 0 the in-place minimum-redundancy algorithm of
+// Moffat and Katajainen and the Kraft fix-up that caps the lengths (the usual length-limiting
+// heuristic: move codes from longer to shorter levels until the code is complete).  len[] is
+// written for every symbol (0 = unused).  Fewer than two used symbols get lengths 1 (a complete
+// code, which every inflater accepts).
+__device__ void build_lengths(const int32_t* f, int m, int maxlen, int32_t* sorted, int32_t* w,
+                              int32_t* len, int32_t* cnt, int lane) {
+  int used = 0;
+  for (int s0 = 0; s0 < m; s0 += 64) {
+    const int s = s0 + lane;
+    const bool u = s < m && f[s] > 0;
+    used += __popcll(__ballot(u));
+  }
+  for (int s = lane; s < m; s += 64) {
+    len[s] = 0;
+    const int fs = f[s];
+    if (fs <= 0) continue;
+    int r = 0;
+    for (int k = 0; k < m; k++) {
+      const int fk = f[k];
+      r += fk > 0 && (fk < fs || (fk == fs && k < s));
+    }
+    sorted[r] = s;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  if (lane != 0) return;
+  if (used < 2) {
+    // one or no used symbol: symbols 0 and 1 (or the used one and another) get length 1
+    int a = used == 1 ? sorted[0] : 0;
+    int c = a == 0 ? 1 : 0;
+    len[a] = 1;
+    len[c] = 1;
+    return;
+  }
+  const int n = used;
+  for (int i = 0; i < n; i++) w[i] = f[sorted[i]];
+  // Moffat-Katajainen: w ascending -> code lengths (w[0] longest)
+  w[0] += w[1];
+  int root = 0, leaf = 2;
+  for (int next = 1; next < n - 1; next++) {
+    if (leaf >= n || w[root] < w[leaf]) { w[next] = w[root]; w[root++] = next; }
+    else w[next] = w[leaf++];
+    if (leaf >= n || (root < next && w[root] < w[leaf])) { w[next] += w[root]; w[root++] = next; }
+    else w[next] += w[leaf++];
+  }
+  w[n - 2] = 0;
+  for (int next = n - 3; next >= 0; next--) w[next] = w[w[next]] + 1;
+  int avbl = 1, usedn = 0, dpth = 0;
+  root = n - 2;
+  int next = n - 1;
+  while (avbl > 0) {
+    while (root >= 0 && w[root] == dpth) { usedn++; root--; }
+    while (avbl > usedn) { w[next--] = dpth; avbl--; }
+    avbl = 2 * usedn;
+    dpth++;
+    usedn = 0;
+  }
+  // counts per length (cnt: 33 LDS words), capped at maxlen, Kraft fix-up
+  for (int l = 0; l <= 32; l++) cnt[l] = 0;
+  for (int i = 0; i < n; i++) cnt[min(w[i], 32)]++;
+  for (int l = maxlen + 1; l <= 32; l++) { cnt[maxlen] += cnt[l]; cnt[l] = 0; }
+  uint32_t total = 0;
+  for (int l = maxlen; l > 0; l--) total += (uint32_t)cnt[l] << (maxlen - l);
+  while (total != (1u << maxlen)) {
+    cnt[maxlen]--;
+    for (int l = maxlen - 1; l > 0; l--)
+      if (cnt[l]) { cnt[l]--; cnt[l + 1] += 2; break; }
+    total--;
+  }
+  // shortest codes to the most frequent symbols
+  int j = n;
+  for (int l = 1; l <= maxlen; l++)
+    for (int c = cnt[l]; c > 0; c--) len[sorted[--j]] = l;
+}
+
+// Canonical codes (RFC 1951 3.2.2), bit-reversed for the LSB-first stream: code | len << 16.
+// bl: 32 LDS words of scratch (length counts, then next codes).
+__device__ void canon_codes(const int32_t* len, int m, uint32_t* code, int32_t* bl) {
+  for (int l = 0; l < 32; l++) bl[l] = 0;
+  for (int s = 0; s < m; s++) bl[len[s]]++;
+  bl[0] = 0;
+  uint32_t c = 0;
+  for (int l = 1; l < 16; l++) {
+    c = (c + (uint32_t)bl[l - 1]) << 1;
+    bl[16 + l] = (int32_t)c;
+  }
+  for (int s = 0; s < m; s++) {
+    const int l = len[s];
+    code[s] = l ? (rev((uint32_t)bl[16 + l]++, l) | ((uint32_t)l << 16)) : 0u;
+  }
+}
+
+// 4 bytes at an arbitrary LDS offset x from two aligned words
+__device__ inline uint32_t ld4(const uint8_t* in, int x) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(in + (x & ~3));
+  return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(x & 3));  // byte shift
+}
+
+// Staged symbol word: litlen symbol | length extra << 9 | distance symbol << 14 | distance extra << 19
+__device__ inline uint32_t sym_ll(uint32_t w) { return w & 511; }
+__device__ inline uint32_t sym_lx(uint32_t w) { return (w >> 9) & 31; }
+__device__ inline uint32_t sym_d(uint32_t w) { return (w >> 14) & 31; }
+__device__ inline uint32_t sym_dx(uint32_t w) { return w >> 19; }
+__device__ inline int lextra_bits(int s) { return (s < 265 || s == 285) ? 0 : (s - 261) >> 2; }
+__device__ inline int dextra_bits(int d) { return d < 4 ? 0 : (d - 2) >> 1; }
+__device__ inline int fixed_len_of(int s) { return s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8; }
+
+struct ImgOut {  // LSB-first bits OR-ed into the LDS image from bit position p on
+  uint32_t* img;
+  uint64_t acc;
+  int n;
+  uint32_t w;
+  __device__ ImgOut(uint32_t* im, uint32_t p) : img(im), acc(0), n((int)(p & 31)), w(p >> 5) {}
+  __device__ void put(uint32_t v, int len) {
+    acc |= (uint64_t)v << n;
+    n += len;
+    if (n >= 32) {
+      atomicOr(&img[w++], (uint32_t)acc);
+      acc >>= 32;
+      n -= 32;
+    }
+  }
+  __device__ void flush() {
+    if (n > 0) atomicOr(&img[w], (uint32_t)acc);
+  }
 };
 
 __device__ inline uint32_t hash3(const uint8_t* in, int p) {
@@ -131,8 +246,16 @@ __global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __rest
                                                            int64_t nblk, uint32_t* __restrict__ stage,
                                                            uint16_t* __restrict__ link,
                                                            uint8_t* __restrict__ out_slots,
-                                                           int32_t* __restrict__ out_size) {
+                                                           int32_t* __restrict__ out_size,
+                                                           uint64_t* __restrict__ tim) {
   __shared__ DLds L;
+  uint64_t tm[8];
+  int ti = 0;
+#define DTS()                                                            \
+  do {                                                                   \
+    if (tim && threadIdx.x == 0 && ti < 8) tm[ti++] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+  DTS();
   const int64_t b = (int64_t)blockIdx.x;  // block within this launch
   if (b >= nblk) return;
   const int t = threadIdx.x;
@@ -157,6 +280,7 @@ __global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __rest
     for (int i = h + 16 * nv + t; i < n; i += DWG) L.in[i] = s[i];
   }
   __syncthreads();
+  DTS();
   const int s0 = min(n, t * SEG), s1 = min(n, s0 + SEG);
   // ---- CRC32 of the segment (raw register, init 0)
   {
@@ -181,84 +305,198 @@ __global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __rest
   }
   __threadfence_block();
   __syncthreads();
-  // ---- greedy LZ77 over the segment, fixed Huffman into the lane's staging slot
-  BitOut bo{stage + ((int64_t)b * DWG + t) * SLOT_WORDS, 0, 0, 0};
-  if (t == 0) bo.put(3u, 3);  // BFINAL = 1, BTYPE = 01
+  // ---- greedy LZ77 over the segment: symbols into the lane's staging slot, histograms in LDS
+  int32_t* H = L.head;  // the hash heads are dead from here
+  for (int i = t; i < H_CL + 32; i += DWG) H[i] = 0;
+  __syncthreads();
+  DTS();
+  uint32_t* sw = stage + ((int64_t)b * DWG + t) * SLOT_WORDS;
+  int ns = 0;
   for (int p = s0; p < s1;) {
     int best = 0, bd = 0;
     if (p + 3 <= s1) {
-      const uint8_t c0 = L.in[p], c1 = L.in[p + 1], c2 = L.in[p + 2];
+      const uint32_t p4 = ld4(L.in, p);
       const int lim = min(MAXM, s1 - p);
       auto try_q = [&](int q) {
-        if (L.in[q] != c0 || L.in[q + 1] != c1 || L.in[q + 2] != c2) return;
-        int l = 3;
-        while (l < lim && L.in[q + l] == L.in[p + l]) l++;
+        uint32_t x = (ld4(L.in, q) ^ p4);
+        if (x & 0xffffffu) return;
+        // extend 4 bytes at a time; the first differing byte ends the match
+        int l = 0;
+        while (x == 0 && l + 4 < lim) {
+          l += 4;
+          x = ld4(L.in, q + l) ^ ld4(L.in, p + l);
+        }
+        l = x ? l + (int)(__builtin_ctz(x) >> 3) : l + 4;
+        l = min(l, lim);
         if (l > best) {
           best = l;
           bd = p - q;
         }
       };
       for (int d = 1; d <= SHORT && d <= p && best < lim; d++) try_q(p - d);
-      // links were stored by other threads of this workgroup: read past the L1 (glc)
-      const volatile uint16_t* vlk = lk;
-      int q = vlk[p];
+      // links were stored by this workgroup before the barrier (fenced); nothing read them since,
+      // so no stale L1 line can hold them
+      int q = lk[p];
       // links only go back: stop at DEFLATE's 32 KiB window
       for (int k = 0; k < CHAIN && q != 0xffff && p - q <= 32768 && best < lim; k++) {
         if (p - q > SHORT) try_q(q);
-        q = vlk[q];
+        q = lk[q];
       }
     }
     if (best >= 3) {
-      int sym, nx, xv;
+      int sym, nx, xv, ds, dnx, dxv;
       len_code(best, sym, nx, xv);
-      uint32_t code;
-      int cl;
-      fixed_ll(sym, code, cl);
-      bo.put(code, cl);
-      if (nx) bo.put((uint32_t)xv, nx);
-      int ds, dnx, dxv;
       dist_code(bd, ds, dnx, dxv);
-      bo.put(rev((uint32_t)ds, 5), 5);
-      if (dnx) bo.put((uint32_t)dxv, dnx);
+      sw[ns++] = (uint32_t)sym | ((uint32_t)xv << 9) | ((uint32_t)ds << 14) | ((uint32_t)dxv << 19);
+      atomicAdd(&H[H_LL + sym], 1);
+      atomicAdd(&H[H_D + ds], 1);
       p += best;
     } else {
-      uint32_t code;
-      int cl;
-      fixed_ll(L.in[p], code, cl);
-      bo.put(code, cl);
+      sw[ns++] = L.in[p];
+      atomicAdd(&H[H_LL + L.in[p]], 1);
       p++;
     }
   }
-  // the lane holding the block's last byte ends the deflate block (lane 0 for an empty block)
+  // the lane holding the block's last byte ends the deflate block
   const int last_lane = n > 0 ? (n - 1) / SEG : 0;
-  if (t == last_lane) bo.put(0u, 7);  // end of block (256: seven 0 bits)
-  L.lane_bits[t] = (uint32_t)bo.flush();
+  if (t == last_lane) {
+    sw[ns++] = 256;
+    atomicAdd(&H[H_LL + 256], 1);
+  }
+  L.lane_nsym[t] = (uint16_t)ns;
+  __threadfence_block();
   __syncthreads();
-  // ---- exclusive scan of lane bit counts (one wave), CRC fold
+  DTS();
+  // ---- dynamic Huffman codes: wave 0 the literal/length alphabet, wave 1 the distances
+  const int lane = t & 63, wv = t >> 6;
+  if (wv == 0) build_lengths(H + H_LL, 286, 15, H + H_SORT, H + H_W, H + H_LEN, H + H_CNT, lane);
+  if (wv == 1) build_lengths(H + H_D, 30, 15, H + H_SORT_D, H + H_W_D, H + H_LEN_D, H + H_CNT_D, lane);
+  __syncthreads();
+  if (t == 0) {
+    canon_codes(H + H_LEN, 286, reinterpret_cast<uint32_t*>(H + C_LL), H + H_BL);
+    canon_codes(H + H_LEN_D, 30, reinterpret_cast<uint32_t*>(H + C_D), H + H_BL);
+    // code-length sequence, run-length coded (16: repeat 3-6, 17: 3-10 zeros, 18: 11-138 zeros)
+    int nlit = 286, ndist = 30;
+    while (nlit > 257 && H[H_LEN + nlit - 1] == 0) nlit--;
+    while (ndist > 1 && H[H_LEN_D + ndist - 1] == 0) ndist--;
+    uint16_t* tok = reinterpret_cast<uint16_t*>(H + H_TOK);
+    int nt = 0;
+    const int N = nlit + ndist;
+    auto L_at = [&](int i) { return i < nlit ? H[H_LEN + i] : H[H_LEN_D + i - nlit]; };
+    for (int i = 0; i < N;) {
+      const int v = L_at(i);
+      int run = 1;
+      while (i + run < N && L_at(i + run) == v) run++;
+      int r = run;
+      if (v == 0) {
+        while (r >= 11) { const int k = min(r, 138); tok[nt++] = (uint16_t)(18 | ((k - 11) << 5)); r -= k; }
+        if (r >= 3) { tok[nt++] = (uint16_t)(17 | ((r - 3) << 5)); r = 0; }
+        while (r > 0) { tok[nt++] = 0; r--; }
+      } else {
+        tok[nt++] = (uint16_t)v;
+        r--;
+        while (r >= 3) { const int k = min(r, 6); tok[nt++] = (uint16_t)(16 | ((k - 3) << 5)); r -= k; }
+        while (r > 0) { tok[nt++] = (uint16_t)v; r--; }
+      }
+      i += run;
+    }
+    for (int k = 0; k < nt; k++) H[H_CL + (tok[k] & 31)]++;
+    L.misc[2] = nlit;
+    L.misc[3] = ndist;
+    L.misc[4] = nt;
+  }
+  __syncthreads();
+  if (wv == 0) build_lengths(H + H_CL, 19, 7, H + H_SORT, H + H_W, H + H_LEN_CL, H + H_CNT, lane);
+  __syncthreads();
+  if (t == 0) {
+    canon_codes(H + H_LEN_CL, 19, reinterpret_cast<uint32_t*>(H + C_CL), H + H_BL);
+    int ncl = 19;
+    while (ncl > 4 && H[H_LEN_CL + c_clord[ncl - 1]] == 0) ncl--;
+    L.misc[5] = ncl;
+    const uint16_t* tok = reinterpret_cast<const uint16_t*>(H + H_TOK);
+    uint32_t hb = 3 + 5 + 5 + 4 + 3 * (uint32_t)ncl;
+    for (int k = 0; k < L.misc[4]; k++) {
+      const int sy = tok[k] & 31;
+      hb += (uint32_t)H[H_LEN_CL + sy] + (sy == 16 ? 2 : sy == 17 ? 3 : sy == 18 ? 7 : 0);
+    }
+    L.misc[6] = (int32_t)hb;  // dynamic header bits
+  }
+  __syncthreads();
+  DTS();
+  // ---- bits per lane under the dynamic and the fixed code
+  {
+    const uint32_t* cll = reinterpret_cast<const uint32_t*>(H + C_LL);
+    const uint32_t* cd = reinterpret_cast<const uint32_t*>(H + C_D);
+    uint32_t bdyn = 0, bfix = 0;
+    for (int k = 0; k < ns; k++) {
+      const uint32_t x = sw[k];
+      const int ll = (int)sym_ll(x);
+      int extra = 0;
+      if (ll > 256) {
+        const int d = (int)sym_d(x);
+        extra = lextra_bits(ll) + dextra_bits(d);
+        bdyn += cd[d] >> 16;
+        bfix += 5;
+      }
+      bdyn += (cll[ll] >> 16) + extra;
+      bfix += fixed_len_of(ll) + extra;
+    }
+    L.lane_bits[t] = bdyn;
+    // fixed totals: the sort scratch is dead
+    reinterpret_cast<uint32_t*>(H + H_SORT)[t] = bfix;
+  }
+  __syncthreads();
+  // ---- choose dynamic or fixed; exclusive scan of the chosen lane bit counts; CRC fold
   if (t < 64) {
-    uint32_t v[4], s = 0;
+    uint32_t dsum = 0, fsum = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      v[k] = L.lane_bits[4 * t + k];
-      s += v[k];
+      dsum += L.lane_bits[4 * t + k];
+      fsum += reinterpret_cast<uint32_t*>(H + H_SORT)[4 * t + k];
     }
-    uint32_t inc = s;
+    for (int o = 32; o >= 1; o >>= 1) {
+      dsum += __shfl_xor(dsum, o, 64);
+      fsum += __shfl_xor(fsum, o, 64);
+    }
+    const bool dyn = (uint32_t)L.misc[6] + dsum < 3u + fsum;
+    uint32_t v[4], sm = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      v[k] = dyn ? L.lane_bits[4 * t + k] : reinterpret_cast<uint32_t*>(H + H_SORT)[4 * t + k];
+      sm += v[k];
+    }
+    uint32_t inc = sm;
     for (int d = 1; d < 64; d <<= 1) {
       const uint32_t y = __shfl_up(inc, d, 64);
       if (t >= d) inc += y;
     }
-    uint32_t off = inc - s;
+    const uint32_t hdr_bits = dyn ? (uint32_t)L.misc[6] : 3u;
+    uint32_t off = hdr_bits + inc - sm;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       L.lane_bits[4 * t + k] = off;  // now: bit offset of lane 4t+k
       off += v[k];
     }
-    if (t == 63) L.misc[0] = (int32_t)inc;  // total bits
+    if (t == 63) L.misc[0] = (int32_t)(hdr_bits + inc);  // total bits
+    if (t == 0) L.misc[7] = dyn ? 1 : 0;
     uint32_t c = L.lane_crc[4 * t] ^ L.lane_crc[4 * t + 1] ^ L.lane_crc[4 * t + 2] ^ L.lane_crc[4 * t + 3];
     for (int o = 32; o >= 1; o >>= 1) c ^= __shfl_xor(c, o, 64);
     if (t == 0) L.misc[1] = (int32_t)(c ^ gf2_mul(x8n((uint32_t)n), 0xffffffffu) ^ 0xffffffffu);
   }
   __syncthreads();
+  DTS();
+  const bool dyn = L.misc[7] != 0;
+  if (!dyn) {  // the fixed code into the code tables
+    uint32_t* cll = reinterpret_cast<uint32_t*>(H + C_LL);
+    uint32_t* cd = reinterpret_cast<uint32_t*>(H + C_D);
+    for (int sy = t; sy < 286; sy += DWG) {
+      uint32_t code;
+      int cl;
+      fixed_ll(sy, code, cl);
+      cll[sy] = code | ((uint32_t)cl << 16);
+    }
+    if (t < 30) cd[t] = rev((uint32_t)t, 5) | (5u << 16);
+  }
   const uint32_t total_bits = (uint32_t)L.misc[0];
   const int dbytes = (int)((total_bits + 7) / 8);
   uint8_t* o = out_slots + b * 65536;
@@ -267,25 +505,54 @@ __global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __rest
   const bool stored = dbytes > min(MAX_DEFLATE, n + 5);
   int payload;
   if (!stored) {
-    // ---- place every lane's bits into the LDS image (the input is dead now)
+    // ---- the header, then every lane's symbols, OR-ed into the LDS image (the input is dead)
     uint32_t* img = reinterpret_cast<uint32_t*>(L.in);
-    __syncthreads();
     for (int i = t; i < (int)(sizeof(L.in) / 4); i += DWG) img[i] = 0;
     __syncthreads();
-    {
-      const uint32_t off = L.lane_bits[t];
-      const uint32_t nb = (t == DWG - 1 ? total_bits : L.lane_bits[t + 1]) - off;
-      const uint32_t* sw = stage + ((int64_t)b * DWG + t) * SLOT_WORDS;
-      const uint32_t nw = (nb + 31) / 32, sh = off & 31, w0 = off >> 5;
-      for (uint32_t k = 0; k < nw; k++) {
-        uint32_t v = sw[k];
-        const uint32_t rem = nb - 32 * k;
-        if (rem < 32) v &= (1u << rem) - 1u;
-        atomicOr(&img[w0 + k], v << sh);
-        if (sh) atomicOr(&img[w0 + k + 1], v >> (32 - sh));
+    if (t == 0) {
+      ImgOut io(img, 0);
+      if (!dyn) {
+        io.put(3u, 3);  // BFINAL 1, BTYPE 01
+      } else {
+        io.put(5u, 3);  // BFINAL 1, BTYPE 10
+        io.put((uint32_t)(L.misc[2] - 257), 5);
+        io.put((uint32_t)(L.misc[3] - 1), 5);
+        const int ncl = L.misc[5];
+        io.put((uint32_t)(ncl - 4), 4);
+        for (int k = 0; k < ncl; k++) io.put((uint32_t)H[H_LEN_CL + c_clord[k]], 3);
+        const uint16_t* tok = reinterpret_cast<const uint16_t*>(H + H_TOK);
+        const uint32_t* ccl = reinterpret_cast<const uint32_t*>(H + C_CL);
+        for (int k = 0; k < L.misc[4]; k++) {
+          const int sy = tok[k] & 31, ex = tok[k] >> 5;
+          io.put(ccl[sy] & 0xffff, (int)(ccl[sy] >> 16));
+          if (sy == 16) io.put((uint32_t)ex, 2);
+          else if (sy == 17) io.put((uint32_t)ex, 3);
+          else if (sy == 18) io.put((uint32_t)ex, 7);
+        }
       }
+      io.flush();
+    }
+    {
+      const uint32_t* cll = reinterpret_cast<const uint32_t*>(H + C_LL);
+      const uint32_t* cd = reinterpret_cast<const uint32_t*>(H + C_D);
+      ImgOut io(img, L.lane_bits[t]);
+      for (int k = 0; k < ns; k++) {
+        const uint32_t x = sw[k];
+        const int ll = (int)sym_ll(x);
+        io.put(cll[ll] & 0xffff, (int)(cll[ll] >> 16));
+        if (ll > 256) {
+          const int lx = lextra_bits(ll);
+          if (lx) io.put(sym_lx(x), lx);
+          const int d = (int)sym_d(x);
+          io.put(cd[d] & 0xffff, (int)(cd[d] >> 16));
+          const int dx = dextra_bits(d);
+          if (dx) io.put(sym_dx(x), dx);
+        }
+      }
+      io.flush();
     }
     __syncthreads();
+    DTS();
     payload = dbytes;
     // stored 16 bytes at a time after the 18-byte header: o + 18 is 2 mod 16, so bytes
     for (int i = t; i < payload; i += DWG) o[18 + i] = L.in[i];
@@ -311,6 +578,10 @@ __global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __rest
     tr[4] = (uint8_t)n; tr[5] = (uint8_t)(n >> 8); tr[6] = (uint8_t)(n >> 16); tr[7] = (uint8_t)(n >> 24);
     out_size[b] = bsize + 1;
   }
+  DTS();
+  if (tim && t == 0)
+    for (int k = 0; k < 8; k++) tim[b * 8 + k] = k < ti ? tm[k] - tm[0] : 0;
+#undef DTS
 }
 
 // Packs the fixed-stride block slots into one contiguous BGZF stream: one workgroup per block.
@@ -374,10 +645,10 @@ bool deflate_tables(int device) {
 
 void launch_bgzf_deflate(const uint8_t* src, int64_t n_in, int64_t blk0, int64_t nblk,
                          uint32_t* stage, uint16_t* link, uint8_t* out_slots, int32_t* out_size,
-                         hipStream_t s) {
+                         uint64_t* tim, hipStream_t s) {
   if (nblk <= 0) return;
   hipLaunchKernelGGL(bgzf_deflate_kernel, dim3((unsigned)nblk), dim3(DWG), 0, s, src, n_in, blk0, nblk,
-                     stage, link, out_slots, out_size);
+                     stage, link, out_slots, out_size, tim);
 }
 
 void launch_bgzf_pack(const uint8_t* slots, const int32_t* size, const int64_t* off, int64_t nblk,

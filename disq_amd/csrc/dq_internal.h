@@ -244,7 +244,7 @@ bool deflate_tables(int device);
 // Blocks [blk0, blk0 + nblk) of src[0, n_in) (65280 bytes each) into fixed 64 KiB slots.
 void launch_bgzf_deflate(const uint8_t* src, int64_t n_in, int64_t blk0, int64_t nblk,
                          uint32_t* stage, uint16_t* link, uint8_t* out_slots, int32_t* out_size,
-                         hipStream_t s);
+                         uint64_t* tim, hipStream_t s);
 void launch_bgzf_pack(const uint8_t* slots, const int32_t* size, const int64_t* off, int64_t nblk,
                       uint8_t* out, hipStream_t s);
 
