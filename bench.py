@@ -341,19 +341,23 @@ def interval_bench(ctx, rs, shard, file_len, header, bai, args):
     does (AbstractBinarySamSource.java:86-112): the .bai span of the optimized intervals clipped
     to every partition chunk is the only part inflated (dq_run_resident, span run), then kernel 4.
     Compared with kernel 4 over every record of the file (full_traversal): same kept count."""
+    stage = "setup"
     try:
         from disq_amd import _lib
         from disq_amd.storage import _parse_header
         _reopen(ctx, rs, shard, file_len, header)
         ctx.set_index(bai)
         ivs = make_intervals(_parse_header(header).sequences, args.intervals)
+        stage = "first span run"
         st = ctx.run_resident((ivs, False))  # the partition plans (full run) + a first span run
+        stage = "timed span runs"
         wall, dev = [], []
         for _ in range(3):
             t0 = time.perf_counter()
             st = ctx.run_resident((ivs, False))
             wall.append(time.perf_counter() - t0)
             dev.append(st.ms_span)
+        stage = "full traversal"
         with _lib.Context(split_size=args.split_size, verify_crc=not args.no_crc,
                           full_traversal=True) as fc:
             _reopen(fc, rs, shard, file_len, header)
@@ -370,7 +374,7 @@ def interval_bench(ctx, rs, shard, file_len, header, bai, args):
                 "kept_match": fst.n_filtered == st.n_filtered,
                 "unplaced_tail": "not included (traverse_unplaced_unmapped = false)"}
     except Exception as e:  # noqa: BLE001 -- reported in the line; the headline metric stands
-        return {"error": f"{type(e).__name__}: {e}"}
+        return {"error": f"{type(e).__name__}: {e}", "stage": stage}
 
 
 def cpu_baseline(data, ctx, rs, shard, file_len, header, args, ncores):

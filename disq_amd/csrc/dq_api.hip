@@ -240,6 +240,12 @@ int ensure_all(dq_ctx* ctx, DevBuf& b, size_t bytes) {
   return 0;
 }
 
+// Scratch of launch_exclusive_scan_* over n elements (>= 2 ceil(n / 1024) + 64 entries, plus the
+// recursion): every scan sizes it for its own n.
+int ensure_scan(dq_ctx* ctx, int64_t n) {
+  return ensure_all(ctx, ctx->tmp, sizeof(int64_t) * (size_t)(4 * (n / 1024 + 1) + 4096));
+}
+
 const char* status_name(int32_t st) {
   switch (st) {
     case ST_BAD_HEADER: return "invalid BGZF/GZIP block header";
@@ -517,6 +523,7 @@ static int run_pipeline(dq_ctx* ctx) {
     HIPCHK(hipStreamSynchronize(s));
     if (bad < 0) RET(DQ_EFORMAT, "more than 640 BGZF magic positions in a 16 KiB window");
   }
+  if ((rc = ensure_scan(ctx, nch))) return rc;
   launch_exclusive_scan_i32(ctx->counts.as<int32_t>(), ctx->offs.as<int64_t>(), nch,
                             ctx->tmp.as<int64_t>(), s);
   dbg(s, "scan", nch, n_over);
@@ -534,6 +541,7 @@ static int run_pipeline(dq_ctx* ctx) {
   int64_t* d_ncand = d_nblk + 1;
   HIPCHK(hipMemcpyAsync(d_ncand, &ncand, sizeof(int64_t), hipMemcpyHostToDevice, s));
   launch_valid_flags(ctx->cand.as<Cand>(), d_ncand, capc, ctx->flags.as<int32_t>(), s);
+  if ((rc = ensure_scan(ctx, ncand))) return rc;
   launch_exclusive_scan_i32(ctx->flags.as<int32_t>(), ctx->voff.as<int64_t>(), ncand,
                             ctx->tmp.as<int64_t>(), s);
   const int64_t capb = std::max<int64_t>(1, ncand);
@@ -581,6 +589,7 @@ static int run_pipeline(dq_ctx* ctx) {
   ctx->nblk = nblk;
   if (nblk == 0 && L > 0) RET(DQ_EFORMAT, "no BGZF blocks found");
   if ((rc = ensure_all(ctx, ctx->uoff, sizeof(int64_t) * (size_t)(nblk + 1)))) return rc;
+  if ((rc = ensure_scan(ctx, nblk))) return rc;
   launch_exclusive_scan_i32(ctx->blk_us.as<int32_t>(), ctx->uoff.as<int64_t>(), nblk,
                             ctx->tmp.as<int64_t>(), s);
   int64_t ulen = 0;
@@ -775,6 +784,7 @@ static int run_pipeline(dq_ctx* ctx) {
     }
     dbg(s, "segs", nseg, br);
     launch_seg_counts(ctx->segs.as<Seg>(), nseg, ctx->segcnt.as<int64_t>(), s);
+    if ((rc = ensure_scan(ctx, nseg))) return rc;
     launch_exclusive_scan_i64(ctx->segcnt.as<int64_t>(), ctx->segbase.as<int64_t>(), nseg,
                               ctx->tmp.as<int64_t>(), s);
     if ((rc = get_i64(ctx, ctx->segbase.as<int64_t>() + nseg, &nrec))) return rc;
@@ -973,6 +983,7 @@ static int text_run(dq_ctx* ctx, int32_t drop_hash) {
                      ctx->t_idx.as<int64_t>(), total, bom, drop_hash, ctx->t_vs.as<int64_t>(),
                      ctx->t_vl.as<int32_t>(), ctx->t_hash.as<uint64_t>(), ctx->t_keep.as<uint8_t>(), s);
   launch_keep_to_i32(ctx->t_keep.as<uint8_t>(), total, ctx->t_keep32.as<int32_t>(), s);
+  if ((rc = ensure_scan(ctx, total))) return rc;
   if (total > 0)
     launch_exclusive_scan_i32(ctx->t_keep32.as<int32_t>(), ctx->t_koff.as<int64_t>(), total,
                               ctx->tmp.as<int64_t>(), s);
@@ -1559,6 +1570,7 @@ static int run_span(dq_ctx* ctx, const dq_traversal* tr, dq_stats* out) {
       }
       if (st) RET(DQ_EFORMAT, st == ST_BAD_CODE ? "Invalid record length" : "truncated record chain");
       launch_seg_counts(ctx->segs.as<Seg>(), nseg, ctx->segcnt.as<int64_t>(), s);
+      if ((rc = ensure_scan(ctx, nseg))) return rc;
       launch_exclusive_scan_i64(ctx->segcnt.as<int64_t>(), ctx->segbase.as<int64_t>(), nseg,
                                 ctx->tmp.as<int64_t>(), s);
       if ((rc = get_i64(ctx, ctx->segbase.as<int64_t>() + nseg, &nrec))) return rc;
@@ -1599,6 +1611,7 @@ static int run_span(dq_ctx* ctx, const dq_traversal* tr, dq_stats* out) {
       HIPCHK(hipMemcpyAsync(d_cb, cb.data(), 8 * (size_t)nchunk, hipMemcpyHostToDevice, s));
       HIPCHK(hipMemcpyAsync(d_ce, ce.data(), 8 * (size_t)nchunk, hipMemcpyHostToDevice, s));
       launch_span_ranges(ctx->f_voff.as<uint64_t>(), nrec, d_cb, d_ce, nchunk, d_first, d_cnt, s);
+      if ((rc = ensure_scan(ctx, nchunk))) return rc;
       launch_exclusive_scan_i64(d_cnt, d_off, nchunk, ctx->tmp.as<int64_t>(), s);
       if ((rc = get_i64(ctx, d_off + nchunk, &nidx))) return rc;
     }
@@ -1617,6 +1630,7 @@ static int run_span(dq_ctx* ctx, const dq_traversal* tr, dq_stats* out) {
                              ctx->iv_start.as<int32_t>(), ctx->iv_end.as<int32_t>(),
                              ctx->iv_begin.as<int32_t>(), ctx->n_ref, ctx->keep.as<uint8_t>(), s);
       launch_keep_to_i32(ctx->keep.as<uint8_t>(), nidx, ctx->span_keep32.as<int32_t>(), s);
+      if ((rc = ensure_scan(ctx, nidx))) return rc;
       launch_exclusive_scan_i32(ctx->span_keep32.as<int32_t>(), ctx->span_off.as<int64_t>(), nidx,
                                 ctx->tmp.as<int64_t>(), s);
       launch_compact_kept(ctx->span_idx.as<int64_t>(), ctx->keep.as<uint8_t>(),
@@ -1658,7 +1672,28 @@ static int run_span(dq_ctx* ctx, const dq_traversal* tr, dq_stats* out) {
     int32_t st2 = 0;
     HIPCHK(hipMemcpyAsync(&st2, d_stat, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    if (st2 && nrec > 0) RET(DQ_EFORMAT, "truncated BAM record");
+    if (st2 && nrec > 0) {
+      // diagnostics: the first record start that is out of order or whose block_size runs past U
+      std::vector<int64_t> rl((size_t)nrec);
+      HIPCHK(hipMemcpy(rl.data(), ctx->rec_lin.p, 8 * (size_t)nrec, hipMemcpyDeviceToHost));
+      int64_t bad = -1, wmax = 0;
+      for (const Win& x : wv) wmax = std::max(wmax, x.u_limit - x.u_start);
+      for (int64_t i = 0; i < nrec && bad < 0; i++) {
+        int32_t bs = 0;
+        if (rl[(size_t)i] < 0 || rl[(size_t)i] + 4 > ctx->ulen) { bad = i; break; }
+        if (i % 4096 == 0 || (i > 0 && rl[(size_t)i] <= rl[(size_t)i - 1])) {
+          HIPCHK(hipMemcpy(&bs, ctx->U.as<uint8_t>() + rl[(size_t)i], 4, hipMemcpyDeviceToHost));
+          if (bs < 32 || rl[(size_t)i] + 4 + bs > ctx->ulen || (i > 0 && rl[(size_t)i] <= rl[(size_t)i - 1])) bad = i;
+        }
+      }
+      char msg[320];
+      snprintf(msg, sizeof msg,
+               "truncated BAM record (span run: %lld records, %lld windows, %lld segments, largest "
+               "window %lld bytes, ulen %lld, first bad record %lld at %lld)",
+               (long long)nrec, (long long)nwin, (long long)nseg, (long long)wmax,
+               (long long)ctx->ulen, (long long)bad, bad >= 0 ? (long long)rl[(size_t)bad] : -1LL);
+      RET(DQ_EFORMAT, msg);
+    }
     ctx->parts_h = parts;
     dq_stats S = ctx->stats;
     S.n_records = nidx;
