@@ -1927,6 +1927,15 @@ static int concat_batches(dq_ctx* ctx, const std::vector<dq_batch*>& parts, dq_b
 }
 
 // ------------------------------------------------------------------ C ABI
+// queryUnmapped reads the unplaced-unmapped tail to the end of the FILE (H/BAMFileReader2.java:
+// 715-738): a shard whose bytes stop before it cannot produce that tail.
+static int check_tail_reachable(dq_ctx* ctx, const dq_traversal* tr) {
+  if (tr && tr->traverse_unplaced_unmapped && ctx->shard && !ctx->chunk_mode &&
+      ctx->base + ctx->flen < ctx->file_len)
+    RET(DQ_EINVAL, "traverseUnplacedUnmapped on a shard that does not reach the end of the file");
+  return 0;
+}
+
 extern "C" {
 
 const char* dq_version(void) { return "disq_amd 0.1 (gfx950)"; }
@@ -2373,6 +2382,7 @@ int dq_decode_filtered(dq_ctx* ctx, uint64_t vstart, uint64_t vend, const dq_tra
   ON_DEVICE(ctx);
   if (!tr->has_intervals && !tr->traverse_unplaced_unmapped)
     RET(DQ_EINVAL, "Traversing mapped reads only is not supported.");
+  if (int rc0 = check_tail_reachable(ctx, tr)) return rc0;
   int rc = run_pipeline(ctx);
   if (rc) return rc;
   int64_t b, e;
@@ -2390,6 +2400,7 @@ int dq_read(dq_ctx* ctx, const dq_traversal* tr, int32_t with_raw, dq_batch** ou
   ON_DEVICE(ctx);
   if (tr && !tr->has_intervals && !tr->traverse_unplaced_unmapped)
     RET(DQ_EINVAL, "Traversing mapped reads only is not supported.");
+  if (int rc0 = check_tail_reachable(ctx, tr)) return rc0;
   int rc = run_pipeline(ctx);
   if (rc) return rc;
   std::vector<int64_t> idx, bounds{0};
@@ -2422,6 +2433,7 @@ int dq_run_resident(dq_ctx* ctx, const dq_traversal* tr, dq_stats* stats) {
   ON_DEVICE(ctx);
   if (tr && !tr->has_intervals && !tr->traverse_unplaced_unmapped)
     RET(DQ_EINVAL, "Traversing mapped reads only is not supported.");
+  if (int rc0 = check_tail_reachable(ctx, tr)) return rc0;
   int rc;
   if (tr && tr->has_intervals && tr->n > 0 && !tr->traverse_unplaced_unmapped && ctx->have_bai &&
       !ctx->o.full_traversal && !ctx->chunk_mode) {

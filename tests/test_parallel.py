@@ -448,3 +448,23 @@ def test_exchange_path_on_nccl_world1(tmp_path):
     p.join(60)
     assert p.exitcode == 0
     assert digest == st.digest and n == st.n_records
+
+
+@pytest.mark.gpu
+def test_unplaced_tail_needs_the_file_end(golden):
+    """queryUnmapped reads to the end of the file: a shard that stops earlier refuses
+    traverseUnplacedUnmapped instead of returning a cut tail; the last shard may run it."""
+    from disq_amd import _lib
+    data = open(os.path.join(golden, "1.bam"), "rb").read()
+    with _lib.Context(split_size=40000) as c:
+        hdr = c.header_from_prefix(data[:1 << 20])
+    plan = [s for s in P.shard_plan(len(data), 2, split_size=40000) if not s.empty]
+    first, last = plan[0], plan[-1]
+    with _lib.Context(split_size=40000) as c:
+        c.open_shard(data[first.lo:min(len(data), first.hi + 65536)], first.lo, len(data),
+                     first.p0, first.p1, hdr)
+        with pytest.raises(_lib.DqError, match="end of the file"):
+            c.read(traversal=(None, True))
+    with _lib.Context(split_size=40000) as c:
+        c.open_shard(data[last.lo:], last.lo, len(data), last.p0, last.p1, hdr)
+        c.read(traversal=(None, True))
