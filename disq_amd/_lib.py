@@ -96,7 +96,8 @@ EXPORTS = ("dq_ctx_create", "dq_ctx_destroy", "dq_last_error", "dq_version", "dq
            "dq_get_stats", "dq_partition_digests", "dq_open_shard_path",
            "dq_decode_chunk_filtered", "dq_debug_guess_all", "dq_text_open_memory",
            "dq_text_open_path", "dq_text_run", "dq_text_read", "dq_text_batch_free",
-           "dq_bgzf_compress", "dq_bgzf_compress_resident", "dq_bgzf_fetch")
+           "dq_bgzf_compress", "dq_bgzf_compress_resident", "dq_bgzf_fetch",
+           "dq_text_set_index", "dq_text_set_intervals")
 
 _lib = None
 _lock = threading.Lock()
@@ -155,6 +156,9 @@ def lib():
         L.dq_text_run.argtypes = [vp, C.c_int32, P(DqStats)]
         L.dq_text_read.argtypes = [vp, C.c_int32, P(P(DqTextBatch))]
         L.dq_text_batch_free.argtypes = [P(DqTextBatch)]
+        L.dq_text_set_index.argtypes = [vp, vp, C.c_int64]
+        L.dq_text_set_intervals.argtypes = [vp, P(C.c_char_p), P(C.c_int32), P(C.c_int32),
+                                            C.c_int64]
         L.dq_bgzf_compress.argtypes = [vp, vp, C.c_int64, P(C.c_void_p), P(C.c_int64)]
         L.dq_bgzf_compress_resident.argtypes = [vp, P(C.c_int64), P(C.c_double)]
         L.dq_bgzf_fetch.argtypes = [vp, vp, C.c_int64]
@@ -354,6 +358,33 @@ class Context:
 
     def text_open_path(self, path):
         check(self._h, lib().dq_text_open_path(self._h, path.encode()))
+
+    def text_set_index(self, tbi_bytes):
+        """The tabix index of the open text file (the .tbi as on disk, gzip-decompressed here, as
+        htsjdk's IndexFactory does when it loads it); None clears it."""
+        if tbi_bytes is None:
+            check(self._h, lib().dq_text_set_index(self._h, None, 0))
+            return
+        import gzip
+        d = bytes(tbi_bytes)
+        if d[:2] == b"\x1f\x8b":
+            d = gzip.decompress(d)
+        self._tbi = np.frombuffer(d, np.uint8).copy()
+        check(self._h, lib().dq_text_set_index(self._h, self._tbi.ctypes.data, len(self._tbi)))
+
+    def text_set_intervals(self, intervals):
+        """[(contig, start, end)] 1-based closed, or None for no interval filter."""
+        if intervals is None:
+            check(self._h, lib().dq_text_set_intervals(self._h, None, None, None, -1))
+            return
+        n = len(intervals)
+        names = (C.c_char_p * max(1, n))(*[c.encode() for c, _, _ in intervals])
+        st = np.array([a for _, a, _ in intervals], np.int32)
+        en = np.array([b for _, _, b in intervals], np.int32)
+        self._tiv = (names, st, en)  # alive for the call
+        check(self._h, lib().dq_text_set_intervals(
+            self._h, names, st.ctypes.data_as(C.POINTER(C.c_int32)),
+            en.ctypes.data_as(C.POINTER(C.c_int32)), n))
 
     def text_run(self, drop_header_lines=True):
         st = DqStats()

@@ -92,6 +92,15 @@ struct dq_ctx {
   DevBuf t_tcount, t_toff, t_term, t_crf, t_plans, t_rng, t_idx, t_vs, t_vl, t_hash, t_keep,
       t_keep32, t_koff, t_kept;
   std::vector<TextPlan> tplans_h;
+  // VCF interval traversal (VcfSource.getVariants with intervals): tabix model + intervals
+  bool have_tbi = false;
+  Bai tbi;
+  std::vector<std::string> tbi_names;
+  bool text_iv = false;
+  std::vector<std::string> tiv_contig;           // distinct contigs of the intervals
+  std::vector<int32_t> tiv_cid, tiv_start, tiv_end;  // per interval (contig id into tiv_contig)
+  DevBuf t_ivnames, t_ivnoff, t_ivbeg, t_ivstart, t_ivend, t_ivmaxend;
+  int64_t t_pruned = 0;                          // splits the index filter removed
   // BGZF deflate (write path)
   DevBuf z_in, z_stage, z_link, z_slots, z_size, z_off, z_out;
   int64_t z_len = 0;
@@ -316,11 +325,18 @@ int parse_header(dq_ctx* ctx) {
 
 // htsjdk AbstractBAMFileIndex.getStartOfLastLinearBin / getNoCoordinateCount (2.16.0; read at
 // D/impl/formats/sam/AbstractBinarySamSource.java:93-94).
+// The per-reference bin / chunk / linear-index records shared by .bai and tabix (.tbi) files
+// (SAMv1 section 5.2; tabix format), from offset p.
+int parse_bai_body(const uint8_t* b, int64_t len, int64_t p, int32_t nr, Bai& out);
+
 int parse_bai(const uint8_t* b, int64_t len, Bai& out) {
-  int64_t p = 8;
   if (len < 8 || memcmp(b, "BAI\1", 4) != 0) return DQ_EFORMAT;
   const int32_t nr = rd32(b + 4);
   if (nr < 0) return DQ_EFORMAT;
+  return parse_bai_body(b, len, 8, nr, out);
+}
+
+int parse_bai_body(const uint8_t* b, int64_t len, int64_t p, int32_t nr, Bai& out) {
   Bai x;
   x.refs.resize((size_t)nr);
   int64_t last = -1;
@@ -358,6 +374,29 @@ int parse_bai(const uint8_t* b, int64_t len, Bai& out) {
   x.ncc = p + 8 <= len ? (int64_t)rd64(b + p) : -1;
   out = std::move(x);
   return 0;
+}
+
+// Tabix index (htsjdk TabixIndex, read by VcfSource through IndexFactory.loadIndex,
+// D/impl/formats/vcf/VcfSource.java:155-158): the decompressed bytes -- magic "TBI\1", n_ref,
+// format, col_seq, col_beg, col_end, meta, skip, l_nm, the NUL-separated sequence names, then the
+// BAI-layout per-reference records.
+int parse_tbi(const uint8_t* b, int64_t len, Bai& out, std::vector<std::string>& names) {
+  if (len < 36 || memcmp(b, "TBI\1", 4) != 0) return DQ_EFORMAT;
+  const int32_t nr = rd32(b + 4), l_nm = rd32(b + 32);
+  if (nr < 0 || l_nm < 0 || 36 + (int64_t)l_nm > len) return DQ_EFORMAT;
+  names.clear();
+  std::string cur;
+  for (int32_t i = 0; i < l_nm; i++) {
+    const char c = (char)b[36 + i];
+    if (c == 0) {
+      names.push_back(cur);
+      cur.clear();
+    } else {
+      cur.push_back(c);
+    }
+  }
+  if ((int32_t)names.size() != nr) return DQ_EFORMAT;
+  return parse_bai_body(b, len, 36 + l_nm, nr, out);
 }
 
 // Chunk.optimizeChunkList (htsjdk 2.16.0): sort; drop chunks ending at or before min_off (linear
@@ -925,6 +964,40 @@ static int text_run(dq_ctx* ctx, int32_t drop_hash) {
   // split plans (FileInputFormat splits: the same arithmetic as the BAM path, a1)
   std::vector<std::pair<int64_t, int64_t>> splits;
   if (path_splits(ctx->o, L, splits)) RET(DQ_EINVAL, "splitSize must be > 0 with useNio");
+  ctx->t_pruned = 0;
+  if (ctx->text_iv) {
+    // TribbleIndexIntervalFilteringTextInputFormat.getSplits (D/impl/formats/tribble/
+    // TribbleIndexIntervalFilteringTextInputFormat.java:32-62): the index blocks of every interval
+    // (TabixIndex.getBlocks -> the bins' chunks, optimized against the linear index), and only the
+    // splits whose [start << 16, end << 16] overlaps one of them (its `overlaps`, :64-68).
+    if (!ctx->have_tbi) RET(DQ_EINVAL, "Intervals set but no index file found");
+    std::vector<VChunk> blocks;
+    for (size_t i = 0; i < ctx->tiv_start.size(); i++) {
+      const std::string& cn = ctx->tiv_contig[(size_t)ctx->tiv_cid[i]];
+      const auto it = std::find(ctx->tbi_names.begin(), ctx->tbi_names.end(), cn);
+      if (it == ctx->tbi_names.end()) continue;
+      const int32_t tid = (int32_t)(it - ctx->tbi_names.begin());
+      const std::vector<VChunk> c = file_span(ctx->tbi, {Interval{tid, ctx->tiv_start[i], ctx->tiv_end[i]}});
+      blocks.insert(blocks.end(), c.begin(), c.end());
+    }
+    auto ov = [](uint64_t a, uint64_t b, uint64_t a2, uint64_t b2) {
+      return (a2 >= a && a2 <= b) || (b2 >= a && b2 <= b) || (a >= a2 && b <= b2);
+    };
+    std::vector<std::pair<int64_t, int64_t>> kept;
+    for (const auto& sp : splits) {
+      const uint64_t vs = (uint64_t)sp.first << 16, ve = (uint64_t)sp.second << 16;
+      bool any = false;
+      for (const VChunk& c : blocks)
+        if (ov(vs, ve, c.b, c.e)) {
+          any = true;
+          break;
+        }
+      if (any) kept.push_back(sp);
+    }
+    ctx->t_pruned = (int64_t)(splits.size() - kept.size());
+    splits.swap(kept);
+    drop_hash = 1;  // the VCF codec never sees header lines (VcfSource.java:108)
+  }
   const int64_t nsplit = (int64_t)splits.size();
   ctx->tplans_h.assign((size_t)nsplit, TextPlan{});
   for (int64_t i = 0; i < nsplit; i++) {
@@ -982,6 +1055,12 @@ static int text_run(dq_ctx* ctx, int32_t drop_hash) {
   launch_text_values(ctx->U.as<uint8_t>(), ulen, ctx->t_term.as<int64_t>(), nterm,
                      ctx->t_idx.as<int64_t>(), total, bom, drop_hash, ctx->t_vs.as<int64_t>(),
                      ctx->t_vl.as<int32_t>(), ctx->t_hash.as<uint64_t>(), ctx->t_keep.as<uint8_t>(), s);
+  if (ctx->text_iv)
+    launch_vcf_overlap(ctx->U.as<uint8_t>(), ctx->t_vs.as<int64_t>(), ctx->t_vl.as<int32_t>(), total,
+                       ctx->t_ivnames.as<uint8_t>(), ctx->t_ivnoff.as<int32_t>(),
+                       (int32_t)ctx->tiv_contig.size(), ctx->t_ivbeg.as<int32_t>(),
+                       ctx->t_ivstart.as<int32_t>(), ctx->t_ivmaxend.as<int32_t>(),
+                       ctx->t_keep.as<uint8_t>(), s);
   launch_keep_to_i32(ctx->t_keep.as<uint8_t>(), total, ctx->t_keep32.as<int32_t>(), s);
   if ((rc = ensure_scan(ctx, total))) return rc;
   if (total > 0)
@@ -2524,6 +2603,86 @@ int dq_debug_guess_all(dq_ctx* ctx, uint64_t* voffs, int64_t cap, int64_t* n) {
     k++;
   }
   *n = k;
+  return 0;
+}
+
+int dq_text_set_index(dq_ctx* ctx, const uint8_t* tbi, int64_t len) {
+  if (!ctx) return DQ_EINVAL;
+  ctx->have_text = false;
+  if (!tbi) {
+    ctx->have_tbi = false;
+    return 0;
+  }
+  Bai x;
+  std::vector<std::string> names;
+  if (parse_tbi(tbi, len, x, names)) RET(DQ_EFORMAT, "invalid tabix index (expects the decompressed .tbi bytes)");
+  ctx->tbi = std::move(x);
+  ctx->tbi_names = std::move(names);
+  ctx->have_tbi = true;
+  return 0;
+}
+
+int dq_text_set_intervals(dq_ctx* ctx, const char* const* contig, const int32_t* start,
+                          const int32_t* end, int64_t n) {
+  if (!ctx) return DQ_EINVAL;
+  ON_DEVICE(ctx);
+  ctx->have_text = false;
+  ctx->tiv_contig.clear();
+  ctx->tiv_cid.clear();
+  ctx->tiv_start.clear();
+  ctx->tiv_end.clear();
+  if (!contig || n < 0) {
+    ctx->text_iv = false;
+    return 0;
+  }
+  if (n > 0 && (!start || !end)) return DQ_EINVAL;
+  for (int64_t i = 0; i < n; i++) {
+    if (!contig[i]) RET(DQ_EINVAL, "interval may not be null");
+    const std::string c(contig[i]);
+    auto it = std::find(ctx->tiv_contig.begin(), ctx->tiv_contig.end(), c);
+    int32_t id = (int32_t)(it - ctx->tiv_contig.begin());
+    if (it == ctx->tiv_contig.end()) ctx->tiv_contig.push_back(c);
+    ctx->tiv_cid.push_back(id);
+    ctx->tiv_start.push_back(start[i]);
+    ctx->tiv_end.push_back(end[i]);
+  }
+  // device form: intervals grouped by contig, sorted by start, with running maximum ends
+  const int32_t nc = (int32_t)ctx->tiv_contig.size();
+  std::vector<int32_t> beg((size_t)nc + 1, 0), st, en, mx, noff((size_t)nc + 1, 0);
+  std::string names;
+  for (int32_t c = 0; c < nc; c++) {
+    std::vector<std::pair<int32_t, int32_t>> v;
+    for (size_t i = 0; i < ctx->tiv_cid.size(); i++)
+      if (ctx->tiv_cid[i] == c) v.push_back({ctx->tiv_start[i], ctx->tiv_end[i]});
+    std::sort(v.begin(), v.end());
+    int32_t m = INT32_MIN;
+    for (const auto& x : v) {
+      st.push_back(x.first);
+      en.push_back(x.second);
+      m = std::max(m, x.second);
+      mx.push_back(m);
+    }
+    beg[(size_t)c + 1] = (int32_t)st.size();
+    names += ctx->tiv_contig[(size_t)c];
+    noff[(size_t)c + 1] = (int32_t)names.size();
+  }
+  int rc;
+  const size_t ni = std::max<size_t>(1, st.size());
+  if ((rc = ensure_all(ctx, ctx->t_ivnames, std::max<size_t>(1, names.size()))) ||
+      (rc = ensure_all(ctx, ctx->t_ivnoff, 4 * noff.size())) ||
+      (rc = ensure_all(ctx, ctx->t_ivbeg, 4 * beg.size())) ||
+      (rc = ensure_all(ctx, ctx->t_ivstart, 4 * ni)) || (rc = ensure_all(ctx, ctx->t_ivend, 4 * ni)) ||
+      (rc = ensure_all(ctx, ctx->t_ivmaxend, 4 * ni)))
+    return rc;
+  if (!names.empty()) HIPCHK(hipMemcpy(ctx->t_ivnames.p, names.data(), names.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(ctx->t_ivnoff.p, noff.data(), 4 * noff.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(ctx->t_ivbeg.p, beg.data(), 4 * beg.size(), hipMemcpyHostToDevice));
+  if (!st.empty()) {
+    HIPCHK(hipMemcpy(ctx->t_ivstart.p, st.data(), 4 * st.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(ctx->t_ivend.p, en.data(), 4 * en.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(ctx->t_ivmaxend.p, mx.data(), 4 * mx.size(), hipMemcpyHostToDevice));
+  }
+  ctx->text_iv = true;
   return 0;
 }
 

@@ -233,6 +233,10 @@ void launch_text_parts(const int64_t* out_off, const int64_t* koff, int64_t nspl
 void launch_text_export(const int64_t* kept, int64_t n, const int64_t* vstart, const int32_t* vlen,
                         const uint64_t* hash, int64_t* o_start, int32_t* o_len, uint64_t* o_hash,
                         hipStream_t s);
+void launch_vcf_overlap(const uint8_t* U, const int64_t* vstart, const int32_t* vlen, int64_t n,
+                        const uint8_t* names, const int32_t* noff, int32_t nnames,
+                        const int32_t* ivbeg, const int32_t* ivstart, const int32_t* ivmaxend,
+                        uint8_t* keep, hipStream_t s);
 void launch_text_gather(const uint8_t* U, const int64_t* vstart, const int32_t* vlen,
                         const int64_t* kept, const int64_t* out_off, int64_t n, uint8_t* out,
                         hipStream_t s);

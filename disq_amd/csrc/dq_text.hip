@@ -323,7 +323,89 @@ __global__ void text_export_kernel(const int64_t* __restrict__ kept, int64_t n,
   o_hash[i] = hash[t];
 }
 
+// VcfSource's OverlapDetector filter (D/impl/formats/vcf/VcfSource.java:108-111) on the raw line:
+// VariantContext contig = CHROM, start = POS, end = POS + len(REF) - 1, or the INFO END value when
+// present (htsjdk AbstractVCFCodec); kept when some interval of that contig overlaps
+// [start, end] (1-based, closed).  Intervals per contig are sorted by start with a running
+// maximum of their ends, so one binary search answers overlapsAny.
+__device__ inline int64_t vcf_field_end(const uint8_t* U, int64_t x, int64_t z) {
+  while (x < z && U[x] != '\t') x++;
+  return x;
+}
+__device__ inline int64_t vcf_int(const uint8_t* U, int64_t x, int64_t z, bool* ok) {
+  int64_t v = 0;
+  bool any = false, neg = false;
+  if (x < z && (U[x] == '-' || U[x] == '+')) neg = U[x++] == '-';
+  while (x < z && U[x] >= '0' && U[x] <= '9') {
+    v = v * 10 + (U[x++] - '0');
+    any = true;
+  }
+  *ok = any;
+  return neg ? -v : v;
+}
+
+__global__ void vcf_overlap_kernel(const uint8_t* __restrict__ U, const int64_t* __restrict__ vstart,
+                                   const int32_t* __restrict__ vlen, int64_t n,
+                                   const uint8_t* __restrict__ names, const int32_t* __restrict__ noff,
+                                   int32_t nnames, const int32_t* __restrict__ ivbeg,
+                                   const int32_t* __restrict__ ivstart,
+                                   const int32_t* __restrict__ ivmaxend, uint8_t* __restrict__ keep) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n || !keep[t]) return;
+  const int64_t a = vstart[t], z = a + vlen[t];
+  const int64_t c1 = vcf_field_end(U, a, z);
+  const int64_t clen = c1 - a;
+  int cid = -1;
+  for (int i = 0; i < nnames && cid < 0; i++) {
+    if (noff[i + 1] - noff[i] != clen) continue;
+    bool eq = true;
+    for (int64_t k = 0; k < clen && eq; k++) eq = U[a + k] == names[noff[i] + k];
+    if (eq) cid = i;
+  }
+  uint8_t k = 0;
+  if (cid >= 0 && c1 < z) {
+    bool ok = false;
+    const int64_t pos = vcf_int(U, c1 + 1, z, &ok);
+    const int64_t f2 = vcf_field_end(U, c1 + 1, z);           // end of POS
+    const int64_t f3 = vcf_field_end(U, f2 + 1, z);           // end of ID
+    const int64_t f4 = vcf_field_end(U, f3 + 1, z);           // end of REF
+    int64_t end = pos + (f4 - (f3 + 1)) - 1;
+    const int64_t f5 = vcf_field_end(U, f4 + 1, z);           // ALT
+    const int64_t f6 = vcf_field_end(U, f5 + 1, z);           // QUAL
+    const int64_t f7 = vcf_field_end(U, f6 + 1, z);           // FILTER
+    const int64_t f8 = vcf_field_end(U, f7 + 1, z);           // INFO
+    for (int64_t x = f7 + 1; x + 4 <= f8; x++) {              // END= at the start of a key
+      if ((x == f7 + 1 || U[x - 1] == ';') && U[x] == 'E' && U[x + 1] == 'N' && U[x + 2] == 'D' &&
+          U[x + 3] == '=') {
+        bool ok2 = false;
+        const int64_t e = vcf_int(U, x + 4, f8, &ok2);
+        if (ok2) end = e;
+        break;
+      }
+    }
+    if (ok) {
+      int lo = ivbeg[cid], hi = ivbeg[cid + 1];  // last interval with start <= end
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((int64_t)ivstart[mid] <= end) lo = mid + 1;
+        else hi = mid;
+      }
+      if (lo > ivbeg[cid] && (int64_t)ivmaxend[lo - 1] >= pos) k = 1;
+    }
+  }
+  keep[t] = k;
+}
+
 }  // namespace
+
+void launch_vcf_overlap(const uint8_t* U, const int64_t* vstart, const int32_t* vlen, int64_t n,
+                        const uint8_t* names, const int32_t* noff, int32_t nnames,
+                        const int32_t* ivbeg, const int32_t* ivstart, const int32_t* ivmaxend,
+                        uint8_t* keep, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(vcf_overlap_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, U,
+                     vstart, vlen, n, names, noff, nnames, ivbeg, ivstart, ivmaxend, keep);
+}
 
 void launch_text_parts(const int64_t* out_off, const int64_t* koff, int64_t nsplit, PartRange* parts,
                        hipStream_t s) {

@@ -292,6 +292,84 @@ class HtsjdkReadsRddStorage:
         return None
 
 
+class VariantsPartition(list):
+    """The variant lines of one Spark partition (bytes, terminators excluded)."""
+
+
+class VariantsRDD:
+    def __init__(self, partitions):
+        self.partitions = partitions
+
+    def count(self):
+        return sum(len(p) for p in self.partitions)
+
+    def getNumPartitions(self):
+        return len(self.partitions)
+
+    def collect(self):
+        return [l for p in self.partitions for l in p]
+
+
+class HtsjdkVariantsRdd:
+    def __init__(self, header_lines, variants: VariantsRDD):
+        self._header = header_lines
+        self._variants = variants
+
+    def getHeader(self):
+        """The '#' lines of the file (VCFHeader source text)."""
+        return self._header
+
+    def getVariants(self):
+        """The data lines per partition, as VcfSource hands them to VCFCodec.decode."""
+        return self._variants
+
+
+class HtsjdkVariantsRddStorage:
+    """Builder + read() of Disq's variants entry point (D/HtsjdkVariantsRddStorage.java:25-83,
+    VcfSource.getVariants D/impl/formats/vcf/VcfSource.java:88-113) for BGZF-compressed VCF on the
+    GPU text path.  Lines are returned undecoded: VCFCodec record parsing stays with the caller."""
+
+    def __init__(self, device: int = 0):
+        self._split_size = 0
+        self._device = device
+
+    @staticmethod
+    def makeDefault(device: int = 0) -> "HtsjdkVariantsRddStorage":
+        return HtsjdkVariantsRddStorage(device)
+
+    def splitSize(self, splitSize: int):
+        self._split_size = int(splitSize)
+        return self
+
+    def read(self, path: str, intervals: Optional[Sequence[Interval]] = None) -> HtsjdkVariantsRdd:
+        if not (path.endswith(".gz") or path.endswith(".bgz")):
+            raise ValueError(f"{path}: the GPU text path reads BGZF-compressed VCF (.vcf.gz/.vcf.bgz)")
+        with _lib.Context(split_size=self._split_size, device=self._device) as ctx:
+            ctx.text_open_path(path)
+            if intervals is not None:
+                tbi = path + ".tbi"  # TabixUtils.STANDARD_INDEX_EXTENSION (VcfSource.java:147)
+                if not os.path.exists(tbi):
+                    raise ValueError(f"Intervals set but no index file found for {path} at {tbi}")
+                with open(tbi, "rb") as fh:
+                    ctx.text_set_index(fh.read())
+                ctx.text_set_intervals([(iv.getContig(), iv.getStart(), iv.getEnd())
+                                        for iv in intervals])
+            b = ctx.text_read(True)
+            with _lib.Context(split_size=0, device=self._device) as hc:  # the header lines
+                hc.text_open_path(path)
+                hb = hc.text_read(False)
+        d, do, ln, po = b["data"], b["data_offset"], b["line_len"], b["part_offset"]
+        parts = [VariantsPartition(bytes(d[do[k]:do[k] + ln[k]]) for k in range(po[p], po[p + 1]))
+                 for p in range(len(po) - 1)]
+        header = []
+        for k in range(len(hb["line_len"])):
+            line = bytes(hb["data"][hb["data_offset"][k]:hb["data_offset"][k] + hb["line_len"][k]])
+            if not line.startswith(b"#"):
+                break
+            header.append(line)
+        return HtsjdkVariantsRdd(header, VariantsRDD(parts))
+
+
 class BAMSBIIndexer:
     """htsjdk BAMSBIIndexer (M/htsjdk/samtools/BAMSBIIndexer.java:20-66) on the GPU read path."""
 

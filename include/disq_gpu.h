@@ -291,6 +291,17 @@ typedef struct dq_text_batch {
 } dq_text_batch;
 
 int dq_text_open_memory(dq_ctx* ctx, const uint8_t* bytes, int64_t len);
+/* VcfSource.getVariants with intervals (D/impl/formats/vcf/VcfSource.java:88-113, 144-168): the
+ * tabix index (the DECOMPRESSED bytes of the .tbi; NULL clears) and the intervals (contig names,
+ * 1-based closed starts and ends; contig == NULL or n < 0 clears, n == 0 keeps nothing).  With
+ * intervals set, dq_text_run / dq_text_read keep only the splits whose [start, end] overlaps an
+ * index block of some interval (TribbleIndexIntervalFilteringTextInputFormat.getSplits) and only
+ * the lines whose variant (CHROM, POS .. POS + len(REF) - 1 or INFO END) overlaps an interval
+ * (OverlapDetector.overlapsAny); '#' lines are always dropped then.  stats.n_partitions counts
+ * the kept splits. */
+int dq_text_set_index(dq_ctx* ctx, const uint8_t* tbi, int64_t len);
+int dq_text_set_intervals(dq_ctx* ctx, const char* const* contig, const int32_t* start,
+                          const int32_t* end, int64_t n);
 int dq_text_open_path(dq_ctx* ctx, const char* path);
 /* Scan, inflate, line planning and digests; the lines stay in HBM.  stats: n_records = lines
  * kept, n_filtered = '#' lines dropped, digest = whole-file digest of the partition digests. */

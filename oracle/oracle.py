@@ -378,6 +378,75 @@ class OracleText:
         vs, vl = part
         return [bytes(u[a:a + b]) for a, b in zip(vs.tolist(), vl.tolist())]
 
+    def read_partitions_intervals(self, split_size, intervals, tbi_bytes, nio=False,
+                                  local_block_size=HADOOP_LOCAL_BLOCK_SIZE):
+        """VcfSource.getVariants with intervals (D/impl/formats/vcf/VcfSource.java:88-113,
+        144-168): TribbleIndexIntervalFilteringTextInputFormat keeps the splits overlapping an
+        index block of some interval (TribbleIndexIntervalFilteringTextInputFormat.java:32-68;
+        TabixIndex.getBlocks restated as the bins' chunks optimized against the linear index, the
+        same rule as the .bai, via dqo_bai_span on the tabix records); each kept split's lines,
+        '#' dropped, filtered by OverlapDetector.overlapsAny on (CHROM, POS, end) with end =
+        POS + len(REF) - 1 or INFO END.  intervals: [(contig, start, end)] 1-based closed.
+        Returns [(split index, (offsets, lengths))] for the kept splits."""
+        names, fake_bai = tabix_as_bai(tbi_bytes)
+        blocks = []
+        for c, a, b in intervals:
+            if c not in names:
+                continue
+            blocks += bai_span(fake_bai, [(names.index(c), a, b)], 0, (1 << 64) - 1)
+
+        def ov(a, b, a2, b2):  # TribbleIndexIntervalFilteringTextInputFormat.overlaps
+            return (a <= a2 <= b) or (a <= b2 <= b) or (a >= a2 and b <= b2)
+        u = self.inflated()
+        out = []
+        for k, (s, e) in enumerate(path_splits(self.len, split_size, nio, local_block_size)):
+            if not any(ov(s << 16, e << 16, cb, ce) for cb, ce in blocks):
+                continue
+            vs, vl = self.split_lines(s, e, True)
+            keep = [i for i, (a, n) in enumerate(zip(vs.tolist(), vl.tolist()))
+                    if vcf_overlaps(bytes(u[a:a + n]), intervals)]
+            out.append((k, (vs[keep], vl[keep])))
+        return out
+
+
+def tabix_as_bai(tbi_bytes):
+    """(sequence names, the same per-reference index records as .bai bytes) of a tabix index
+    (gzip-compressed or not)."""
+    import gzip
+    import struct
+    d = bytes(tbi_bytes)
+    if d[:2] == b"\x1f\x8b":
+        d = gzip.decompress(d)
+    if d[:4] != b"TBI\x01":
+        raise OracleError("not a tabix index")
+    n_ref = struct.unpack_from("<i", d, 4)[0]
+    l_nm = struct.unpack_from("<i", d, 32)[0]
+    names = [x.decode() for x in d[36:36 + l_nm].split(b"\x00")[:n_ref]]
+    return names, b"BAI\x01" + struct.pack("<i", n_ref) + d[36 + l_nm:]
+
+
+def vcf_overlaps(line, intervals):
+    """OverlapDetector.overlapsAny(VCFCodec.decode(line)) for a data line: contig CHROM, start
+    POS, end POS + len(REF) - 1 or the INFO END value (htsjdk AbstractVCFCodec)."""
+    f = line.split(b"\t")
+    if len(f) < 4:
+        return False
+    try:
+        pos = int(f[1])
+    except ValueError:
+        return False
+    end = pos + len(f[3]) - 1
+    if len(f) >= 8:
+        for kv in f[7].split(b";"):
+            if kv.startswith(b"END="):
+                try:
+                    end = int(kv[4:])
+                except ValueError:
+                    pass
+                break
+    c = f[0].decode(errors="replace")
+    return any(c == ic and pos <= ie and end >= ist for ic, ist, ie in intervals)
+
 
 def sbi_offsets(sbi_bytes):
     """SBIIndex.readIndex (M/htsjdk/samtools/SBIIndex.java:123-144): the virtual offsets."""

@@ -91,3 +91,74 @@ def test_split_without_block_start_fails(golden):
         c.text_open_bytes(d)
         with pytest.raises(_lib.DqError, match="no BGZF block starts"):
             c.text_run()
+
+
+def assert_interval_parity(data, split, intervals, tbi):
+    ot = O.OracleText(data)
+    want = ot.read_partitions_intervals(split, intervals, tbi)
+    with _lib.Context(split_size=split, verify_crc=True) as c:
+        c.text_open_bytes(data)
+        c.text_set_index(tbi)
+        c.text_set_intervals(intervals)
+        st = c.text_run()
+        b = c.text_read()
+    po = b["part_offset"]
+    assert len(po) - 1 == len(want) == st.n_partitions
+    for i, (_, (vs, vl)) in enumerate(want):
+        lo, hi = int(po[i]), int(po[i + 1])
+        assert np.array_equal(b["line_offset"][lo:hi], vs), i
+        assert np.array_equal(b["line_len"][lo:hi], vl), i
+    return b, want
+
+
+@pytest.mark.parametrize("intervals,nparts", [
+    ([("chr1", 2700000, 2800000)], 1),   # T/HtsjdkVariantsRddTest.java:127: one partition
+    ([("chr1", 1, 100000)], None),
+    ([("chr1", 2700000, 2800000), ("chr1", 4000000, 4100000), ("chr1", 4050000, 4060000)], None),
+    ([("chr2", 1, 1000000)], 0),          # a contig the index does not know: no split
+    ([("chr1", 1, 300000000)], 4),
+])
+def test_hiseq_vcf_intervals(golden, intervals, nparts):
+    d = open(os.path.join(golden, "HiSeq.10000.vcf.bgz"), "rb").read()
+    tbi = open(os.path.join(golden, "HiSeq.10000.vcf.bgz.tbi"), "rb").read()
+    b, want = assert_interval_parity(d, 128 * 1024, intervals, tbi)
+    if nparts is not None:
+        assert len(want) == nparts
+    txt = gzip.decompress(d)
+    exp = [l for l in T.split_lines(txt) if not l.startswith(b"#") and O.vcf_overlaps(l, intervals)]
+    assert len(b["line_len"]) == len(exp)
+
+
+def test_synthetic_vcf_intervals_with_info_end():
+    text = T.make_vcf(6000, seed=4)
+    data = T.bgzf_text(text, block_u=8000)
+    tbi = T.whole_file_tabix(["chr1", "chr2", "chrX"], len(data))
+    rng = np.random.default_rng(9)
+    ivs = [(("chr1", "chr2", "chrX", "chr7")[int(rng.integers(0, 4))], int(a), int(a) + int(rng.integers(0, 3000)))
+           for a in rng.integers(1, 400000, size=40)]
+    for split in (0, 30000):
+        b, want = assert_interval_parity(data, split, ivs, tbi)
+        assert sum(len(p[0]) for _, p in want) > 0
+
+
+def test_intervals_need_an_index(golden):
+    d = open(os.path.join(golden, "HiSeq.10000.vcf.bgz"), "rb").read()
+    with _lib.Context(split_size=128 * 1024) as c:
+        c.text_open_bytes(d)
+        c.text_set_intervals([("chr1", 1, 10)])
+        with pytest.raises(_lib.DqError, match="no index"):
+            c.text_run()
+
+
+def test_variants_storage_mirror(golden, tmp_path):
+    """HtsjdkVariantsRddStorage.read as T/HtsjdkVariantsRddTest.java:124-149 uses it."""
+    import shutil
+    from disq_amd.storage import HtsjdkVariantsRddStorage, Interval
+    p = str(tmp_path / "HiSeq.10000.vcf.bgz")
+    shutil.copy(os.path.join(golden, "HiSeq.10000.vcf.bgz"), p)
+    st = HtsjdkVariantsRddStorage.makeDefault().splitSize(128 * 1024)
+    v = st.read(p).getVariants()
+    assert v.getNumPartitions() == 4 and v.count() == 9965
+    shutil.copy(os.path.join(golden, "HiSeq.10000.vcf.bgz.tbi"), p + ".tbi")
+    v = st.read(p, [Interval("chr1", 2700000, 2800000)]).getVariants()
+    assert v.getNumPartitions() == 1 and v.count() == 243

@@ -82,3 +82,28 @@ def test_synthetic_every_line_once(newline, bom):
                     continue
                 dedup.append((o, l))
         assert [l for _, l in dedup] == want, (newline, bom, split)
+
+
+def test_hiseq_interval_keeps_one_partition(golden):
+    """T/HtsjdkVariantsRddTest.java:124-149: splitSize 128 KiB, interval chr1:2700000-2800000 ->
+    exactly 1 partition (the tabix index filter), holding every overlapping variant."""
+    d = open(os.path.join(golden, "HiSeq.10000.vcf.bgz"), "rb").read()
+    tbi = open(os.path.join(golden, "HiSeq.10000.vcf.bgz.tbi"), "rb").read()
+    iv = [("chr1", 2700000, 2800000)]
+    ot = O.OracleText(d)
+    parts = ot.read_partitions_intervals(128 * 1024, iv, tbi)
+    assert len(parts) == 1
+    want = [l for l in variant_lines(gzip.decompress(d)) if O.vcf_overlaps(l, iv)]
+    assert ot.lines(parts[0][1]) == want
+    assert len(want) == 243
+
+
+def test_vcf_overlap_uses_info_end():
+    text = T.make_vcf(600, seed=2)
+    lines = [l for l in T.split_lines(text) if not l.startswith(b"#")]
+    f = lines[0].split(b"\t")
+    assert f[7].startswith(b"SVTYPE=DEL;END=")
+    pos, end = int(f[1]), int(f[7].split(b";")[1][4:])
+    assert O.vcf_overlaps(lines[0], [("chr1", end, end)])
+    assert not O.vcf_overlaps(lines[0], [("chr1", end + 1, end + 10)])
+    assert not O.vcf_overlaps(lines[0], [("chr2", pos, end)])

@@ -54,3 +54,35 @@ def split_lines(text):
     if a < n:
         out.append(text[a:])
     return out
+
+
+def make_vcf(n, seed=0, contigs=("chr1", "chr2", "chrX"), end_every=7):
+    """A sorted VCF-like text: CHROM POS ID REF ALT QUAL FILTER INFO, some records with an INFO END
+    (symbolic alleles) and multi-base REFs, a '#' header."""
+    rng = np.random.default_rng(seed)
+    out = [b"##fileformat=VCFv4.2", b"#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO"]
+    per = n // len(contigs)
+    for c in contigs:
+        pos = 1
+        for i in range(per):
+            pos += int(rng.integers(1, 400))
+            ref = b"ACGT"[int(rng.integers(0, 4)):][:1] * int(rng.integers(1, 6))
+            info = b"DP=%d" % int(rng.integers(1, 99))
+            alt = b"T"
+            if end_every and i % end_every == 0:
+                info = b"SVTYPE=DEL;END=%d;DP=3" % (pos + int(rng.integers(50, 5000)))
+                alt = b"<DEL>"
+            out.append(b"\t".join([c.encode(), b"%d" % pos, b".", ref, alt, b"50", b"PASS", info]))
+    return b"\n".join(out) + b"\n"
+
+
+def whole_file_tabix(contigs, bgzf_len):
+    """A decompressed tabix index whose only bin (0) holds one chunk over the whole file, for
+    every contig: index pruning keeps every split, the line filter decides."""
+    import struct
+    names = b"".join(c.encode() + b"\x00" for c in contigs)
+    d = b"TBI\x01" + struct.pack("<iiiiiiii", len(contigs), 2, 1, 2, 0, ord("#"), 0, len(names)) + names
+    for _ in contigs:
+        d += struct.pack("<i", 1) + struct.pack("<Ii", 0, 1) + struct.pack("<QQ", 0, bgzf_len << 16)
+        d += struct.pack("<i", 0)
+    return d
