@@ -110,18 +110,16 @@ enum { M_ERR = 0, M_BFINAL, M_BTYPE, M_POS, M_A, M_LAST, M_MORE, M_MORE1, M_STLE
 
 __device__ __attribute__((always_inline)) inline void set_err(LdsI& L, int32_t code) { atomicCAS(&L.misc[M_ERR], 0, code); }
 
-// Bit reader: a 64-bit LSB-first buffer refilled 32 bits at a time from `st`, the 16-byte group
-// of input words that holds the next word.  Every refill call reloads the group of the (new) next
-// word unconditionally (one global_load_dwordx4, almost always an L1/L2 hit on the same line):
-// the load then always lands in the loop-carried registers -- a conditional reload made the
-// compiler load into temporaries and copy them back, waiting for the load at once -- and is first
-// waited for at the next call, half a symbol later.  W is 16-byte aligned.
-typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+// Bit reader: a 64-bit LSB-first buffer refilled 32 bits at a time from `nw`, the next input word,
+// which every refill call reloads unconditionally (one global_load_dword, almost always an L1/L2
+// hit): the load lands in a loop-carried register and is first waited for at the next call, half
+// a symbol later.  (A 16-byte group load needs a 4-way select of the word on every refill:
+// 3 compares + 3 cndmasks + hazard nops per refill, 2 refills per symbol.)
 struct BitR {
   uint64_t bb;
   uint32_t bc;
   uint32_t wp;    // word index of the next word to enter bb (br_pos = 32 * wp - bc)
-  u32x4v st;      // words [wp & ~3, +4)
+  uint32_t nw;    // W[wp]
 };
 
 #define DQ_AI __device__ __attribute__((always_inline)) inline
@@ -150,16 +148,14 @@ DQ_AI void br_init(BitR& r, const uint32_t* __restrict__ W, uint32_t bitpos) {
   r.bb = ((hi << 32) | lo) >> sh;
   r.bc = 64 - sh;
   r.wp = wi + 2;
-  r.st = reinterpret_cast<const u32x4v*>(W)[r.wp >> 2];
+  r.nw = W[r.wp];
 }
 DQ_AI void br_refill(BitR& r, const uint32_t* __restrict__ W) {
   const bool need = r.bc <= 32;
-  const uint32_t q = r.wp & 3;
-  const uint32_t w = q == 0 ? r.st.x : q == 1 ? r.st.y : q == 2 ? r.st.z : r.st.w;
-  r.bb |= need ? (uint64_t)w << r.bc : 0ull;
+  r.bb |= need ? (uint64_t)r.nw << r.bc : 0ull;
   r.bc += need ? 32u : 0u;
   r.wp += need ? 1u : 0u;
-  r.st = reinterpret_cast<const u32x4v*>(W)[r.wp >> 2];
+  r.nw = W[r.wp];
 }
 DQ_AI uint32_t br_pos(const BitR& r) { return r.wp * 32 - r.bc; }
 DQ_AI uint32_t br_take(BitR& r, uint32_t n) {
@@ -202,11 +198,19 @@ DQ_AI uint32_t d_second(const LdsI& L, uint32_t e, uint32_t bb) {
 
 // Length / distance bases and extra bits by arithmetic (RFC 1951 3.2.5): a few ALU ops instead of
 // a dependent LDS table read on the symbol path.  k = length symbol - 257 (0..28), d = 0..29.
+// Written as selects over one formula (k in 4..27 and 28 + 1; d >= 2) so they compile to
+// cndmasks, not to divergent branches inside the symbol loop.
 DQ_AI uint32_t lbase(uint32_t k) {
-  return k < 8 ? k + 3 : k == 28 ? 258u : ((4u + ((k - 4) & 3)) << ((k - 4) >> 2)) + 3;
+  const uint32_t km = max(k, 4u) - 4u;
+  const uint32_t b = ((4u + (km & 3u)) << (km >> 2)) + 3u;
+  return (k < 4u ? k + 3u : b) - (k == 28u ? 1u : 0u);
 }
 DQ_AI uint32_t lextra(uint32_t k) { return (k < 8 || k == 28) ? 0u : (k - 4) >> 2; }
-DQ_AI uint32_t dbase(uint32_t d) { return d < 2 ? d + 1 : ((2u + (d & 1)) << ((d >> 1) - 1)) + 1; }
+DQ_AI uint32_t dbase(uint32_t d) {
+  const uint32_t dm = max(d, 2u);
+  const uint32_t b = ((2u + (dm & 1u)) << ((dm >> 1) - 1u)) + 1u;
+  return d < 2u ? d + 1u : b;
+}
 DQ_AI uint32_t dextra(uint32_t d) { return d < 4 ? 0u : (d - 2) >> 1; }
 
 // One full symbol: a literal (value in len), a match (len, dist) or EOB.  Straight-line: every

@@ -451,20 +451,33 @@ def test_exchange_path_on_nccl_world1(tmp_path):
 
 
 @pytest.mark.gpu
-def test_unplaced_tail_needs_the_file_end(golden):
+def test_unplaced_tail_needs_the_file_end():
     """queryUnmapped reads to the end of the file: a shard that stops earlier refuses
-    traverseUnplacedUnmapped instead of returning a cut tail; the last shard may run it."""
-    from disq_amd import _lib
-    data = open(os.path.join(golden, "1.bam"), "rb").read()
-    with _lib.Context(split_size=40000) as c:
+    traverseUnplacedUnmapped instead of returning a cut tail; the last shard runs it, with the
+    .bai (AbstractBinarySamSource.java:87 -- no index, no traversal) and equals the oracle."""
+    from disq_amd import _lib, synth
+    a = synth.generate(20000, seed=5, shape=synth.WGS, bai=True, unplaced_fraction=0.05)
+    data, split = a.bam, 200000
+    with _lib.Context(split_size=split) as c:
         hdr = c.header_from_prefix(data[:1 << 20])
-    plan = [s for s in P.shard_plan(len(data), 2, split_size=40000) if not s.empty]
+    plan = [s for s in P.shard_plan(len(data), 2, split_size=split) if not s.empty]
     first, last = plan[0], plan[-1]
-    with _lib.Context(split_size=40000) as c:
+    assert first.hi < len(data)
+    with _lib.Context(split_size=split) as c:
+        c.set_index(a.bai)
         c.open_shard(data[first.lo:min(len(data), first.hi + 65536)], first.lo, len(data),
                      first.p0, first.p1, hdr)
         with pytest.raises(_lib.DqError, match="end of the file"):
             c.read(traversal=(None, True))
-    with _lib.Context(split_size=40000) as c:
+    ob = O.OracleBam(data)
+    oplan = ob.plan(split)
+    parts = ob.read_partitions(split, traversal=(None, True), bai=a.bai)
+    pidx = [i for i, (_, _, ch) in enumerate(oplan) if ch is not None]
+    want = [p for i, p in zip(pidx, parts) if last.p0 <= i < last.p1]
+    want = np.concatenate(want) if want else None
+    with _lib.Context(split_size=split) as c:
+        c.set_index(a.bai)
         c.open_shard(data[last.lo:], last.lo, len(data), last.p0, last.p1, hdr)
-        c.read(traversal=(None, True))
+        b = c.read(traversal=(None, True), with_raw=False)
+    assert len(want) == 1000 and len(b["voffset"]) == len(want)  # the unplaced tail
+    assert np.array_equal(b["voffset"], want["voffset"])
