@@ -53,7 +53,8 @@ using namespace dqi;
 constexpr int WG = 512;           // threads per workgroup
 constexpr int NDEC = 512;         // speculative decode lanes (<= WG)
 constexpr uint32_t OV_DEFAULT = 96;  // speculative warm-up bits before each segment
-constexpr int OUTCAP = 65536 + 20;  // + alignment shift (<= 15) + descriptor overhang
+constexpr int OUTCAP = 65536 + 24;  // + alignment shift (<= 15) + descriptor overhang; bm 8-aligned
+constexpr int RES_NXT = 2048;        // resolve batch bytes (NB * G * WG) at most
 
 // 16-bit decode table layout: [litlen root | litlen subtables | dist root | dist subtables]
 constexpr int LR = 10, DR = 8;            // root bits
@@ -71,7 +72,7 @@ enum : int32_t { F_EXIT = 0, F_EOB = 1, F_ERR = 2, F_END = 3 };
 
 struct alignas(16) LdsI {
   uint8_t out[OUTCAP];            // output image: byte x at out[sh + x]
-  uint32_t bm[2048];              // match-start bitmap
+  alignas(8) uint32_t bm[2048];   // match-start bitmap (read as 64-bit words in resolve)
   union {
     struct {
       uint16_t T[T_END];
@@ -89,7 +90,10 @@ struct alignas(16) LdsI {
         } h;
       } x;
     } d;
-    uint16_t last_start[2048];    // resolve: last match start <= end of bitmap word (0xffff none)
+    struct {
+      uint16_t last_start[1024];  // last match start <= end of 64-bit bitmap word (0xffff none)
+      uint16_t nxt[RES_NXT];      // next pointer of each byte of the batch
+    } r;
     uint32_t crc4[4][256];
   } u;
   int32_t misc[32];
@@ -968,13 +972,14 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     return;
   }
   // ---- 6. resolve matches, chunk by chunk
-  {  // last_start: max-scan over bitmap words (4 words per thread)
-    int ls[4];
+  const uint64_t* bm64 = reinterpret_cast<const uint64_t*>(L.bm);
+  {  // last_start: max-scan over 64-bit bitmap words (2 words per thread)
+    int ls[2];
     int run = -1;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const uint32_t m = L.bm[4 * t + k];
-      if (m) run = 32 * (4 * t + k) + 31 - __builtin_clz(m);
+    for (int k = 0; k < 2; k++) {
+      const uint64_t m = bm64[2 * t + k];
+      if (m) run = 64 * (2 * t + k) + 63 - __clzll(m);
       ls[k] = run;
     }
     const int wm = wave_incl_max(run);  // wave inclusive max-scan of the thread's last value
@@ -984,9 +989,9 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     __syncthreads();
     for (int w = 0; w < wv; w++) ex = max(ex, L.wsum[w]);
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < 2; k++) {
       const int v = max(ex, ls[k]);
-      L.u.last_start[4 * t + k] = v < 0 ? (uint16_t)0xffff : (uint16_t)v;
+      L.u.r.last_start[2 * t + k] = v < 0 ? (uint16_t)0xffff : (uint16_t)v;
     }
     if (t == 0) L.misc[M_CARRY_MS] = -1;
     __syncthreads();
@@ -1000,6 +1005,8 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   constexpr int CH = G * WG;
   constexpr int BATCH = NB * CH;
   constexpr int NE = NB * G;
+  static_assert(BATCH <= RES_NXT, "the batch's next-pointers fit the resolve scratch");
+  uint16_t* nxt = L.u.r.nxt;
   for (int32_t bs = 0; bs < isize; bs += BATCH) {
     const uint64_t tb0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
     const int32_t carry_ms = L.misc[M_CARRY_MS];
@@ -1010,8 +1017,8 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     uint32_t next_desc = 0;
     if (t == WG - 1 && bs + BATCH < isize) {
       const int32_t x = bs + BATCH - 1;
-      const uint32_t m = L.bm[x >> 5];  // bit 31 of the last word: every bit is at or before x
-      const int32_t ms = m ? (x | 31) - (int32_t)__builtin_clz(m) : (int32_t)L.u.last_start[(x >> 5) - 1];
+      const uint64_t m = bm64[x >> 6];  // bit 63 of the last word: every bit is at or before x
+      const int32_t ms = m ? (x | 63) - (int32_t)__clzll(m) : (int32_t)L.u.r.last_start[(x >> 6) - 1];
       if (ms != 0xffff) {
         const uint32_t desc = ms < bs ? carry_desc : load_desc(L, sh + ms);
         if ((ms >= bs || ms == carry_ms) && ms + (int32_t)(desc >> 15) + 3 > bs + BATCH) {
@@ -1020,22 +1027,21 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
         }
       }
     }
-    // (a) sources: every byte follows its copy chain until a literal or a byte before its step.
-    //     Only the bitmap, last_start and the descriptors of this batch are read (all static
-    //     until (b) writes), so a thread's chains advance together, without barriers.
-    //     First hop per group: one bitmap word, one last_start and two descriptors (G <= 4 bytes
-    //     have at most two owners: matches are >= 3 bytes long).
+    // (a) sources.  First hop, every byte: its owner (one 64-bit bitmap word, one last_start) and
+    //     the owner's descriptor give the copy source (G <= 4 bytes have at most two owners:
+    //     matches are >= 3 bytes long).  A source before the byte's 512-byte step is final (that
+    //     step is complete when (b) reaches this one); so is a literal.
     int32_t xs[NE], fr[NE], sbk[NB];
     uint32_t pending = 0;
     {
-      uint32_t mw[NB];
+      uint64_t mw[NB];
       int32_t lsv[NB];
 #pragma unroll
       for (int k = 0; k < NB; k++) {
         const int32_t g0 = bs + k * CH + G * t;
-        const int w = min(g0 >> 5, 2047);  // bytes past isize: read anything, copy = false
-        mw[k] = L.bm[w];
-        lsv[k] = w ? (int32_t)L.u.last_start[w - 1] : 0xffff;
+        const int w = min(g0 >> 6, 1023);  // bytes past isize: read anything, copy = false
+        mw[k] = bm64[w];
+        lsv[k] = w ? (int32_t)L.u.r.last_start[w - 1] : 0xffff;
       }
       int32_t msv[NE];
       uint32_t da[NB], db[NB];
@@ -1044,8 +1050,8 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
         const int32_t g0 = bs + k * CH + G * t;
 #pragma unroll
         for (int i = 0; i < G; i++) {
-          const uint32_t mi = mw[k] & (0xffffffffu >> (31 - ((g0 + i) & 31)));
-          msv[k * G + i] = mi ? (g0 | 31) - (int32_t)__builtin_clz(mi) : lsv[k];
+          const uint64_t mi = mw[k] & (~0ull >> (63 - ((g0 + i) & 63)));
+          msv[k * G + i] = mi ? (g0 | 63) - (int32_t)__clzll(mi) : lsv[k];
         }
         da[k] = load_desc(L, sh + min(max(msv[k * G], bs), 65535));
         db[k] = G > 1 ? load_desc(L, sh + min(max(msv[k * G + G - 1], bs), 65535)) : da[k];
@@ -1072,58 +1078,34 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
           fr[e] = copy ? src : x;
           xs[e] = src;
           pending |= done ? 0u : 1u << e;
+          // next pointer: a final source (or the literal itself), else the in-step source
+          nxt[x - bs] = (uint16_t)(copy ? src : x);
         }
       }
     }
-    // further hops (chains inside a step): per byte
+    // Further hops stay inside the byte's step: nxt is the copy-source function on the batch,
+    // and a pending byte jumps along it, publishing how far it got (pointer jumping: a byte that
+    // reads an advanced pointer skips that byte's whole chain).  Every value read is a byte of
+    // the same chain, so no barrier orders the rounds; each read advances at least one hop.
+    // Ends at a literal (nxt[p] == p) or at a byte before the step.  No descriptor is read.
     int hop = 1;
-    for (; pending != 0 && hop < WG + 2; hop++) {
-      uint32_t mk[NE], lk[NE];
+    if (__syncthreads_or(pending != 0)) {
+      for (; pending != 0 && hop < WG + 2; hop++) {
+        int32_t qv[NE];
 #pragma unroll
-      for (int e = 0; e < NE; e++) {  // owner lookups: bitmap word + last start before it
-        if (!((pending >> e) & 1)) continue;
-        const int w = xs[e] >> 5;
-        mk[e] = L.bm[w] & (0xffffffffu >> (31 - (xs[e] & 31)));
-        lk[e] = L.u.last_start[max(w - 1, 0)];
-      }
-      int32_t msk[NE];
-      uint32_t dk[NE];
+        for (int e = 0; e < NE; e++)
+          qv[e] = ((pending >> e) & 1) ? (int32_t)nxt[xs[e] - bs] : 0;
 #pragma unroll
-      for (int e = 0; e < NE; e++) {
-        if (!((pending >> e) & 1)) continue;
-        msk[e] = mk[e] ? (xs[e] | 31) - (int32_t)__builtin_clz(mk[e])
-                       : (xs[e] >= 32 ? (int32_t)lk[e] : 0xffff);
-        dk[e] = load_desc(L, sh + min(max(msk[e], bs), 65535));
-      }
-#pragma unroll
-      for (int e = 0; e < NE; e++) {
-        if (!((pending >> e) & 1)) continue;
-        const int32_t x = xs[e], ms = msk[e];
-        int32_t from = -1;  // final byte position to read, or -1 to hop on
-        uint32_t desc = dk[e];
-        if (ms == 0xffff) {
-          from = x;
-        } else if (ms < bs) {
-          if (ms == carry_ms) desc = carry_desc;
-          else from = x;  // that match ended before this batch: x is a literal
-        }
-        if (from < 0) {
-          const int32_t len = (int32_t)(desc >> 15) + 3, D = (int32_t)(desc & 0x7fff) + 1;
-          if (x >= ms + len) {
-            from = x;
+        for (int e = 0; e < NE; e++) {
+          if (!((pending >> e) & 1)) continue;
+          const int32_t p = xs[e], q = qv[e];
+          if (q == p || q < sbk[e / G]) {
+            fr[e] = q;
+            pending &= ~(1u << e);
           } else {
-            const int32_t jj = x - ms;
-            const int32_t q = (int32_t)((float)jj * __builtin_amdgcn_rcpf((float)D));
-            int32_t r = jj - q * D;
-            r = r >= D ? r - D : r;
-            const int32_t src = ms - D + r;
-            if (src < sbk[e / G]) from = src;
-            else xs[e] = src;
+            xs[e] = q;
           }
-        }
-        if (from >= 0) {
-          fr[e] = from;
-          pending &= ~(1u << e);
+          nxt[(e / G) * CH + G * t + e % G] = (uint16_t)q;
         }
       }
     }
@@ -1136,6 +1118,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       }
     }
     __syncthreads();  // every chain has read its descriptors before (b) overwrites them
+    const uint64_t tb2 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
     const int wgm = TIMING ? L.misc[22] : 0;
     // (b) 512-byte steps in order: one LDS read + write per copied byte, one barrier per step
 #pragma unroll
@@ -1159,6 +1142,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
         __syncthreads();
       }
     }
+    const uint64_t tb3 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
     // (c) store the 16-byte U lines this batch completed (overlaps the next batch's chains)
     const int32_t c1 = min(isize, bs + BATCH);
     const int32_t lines_to = c1 >= head ? (c1 - head) / 16 : 0;
@@ -1174,13 +1158,11 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     if (TIMING && t == 0) {
       tacc[9] += tb1 - tb0;  // (a) chains of thread 0's wave
       tacc[11] += (uint64_t)wgm;  // max hops over the workgroup
+      tacc[12] += tb2 - tb1;  // waiting at the barrier for the slowest wave's chains
+      tacc[13] += tb3 - tb2;  // (b) the ordered steps
+      tacc[14] += __builtin_amdgcn_s_memtime() - tb3;  // (c) issuing the U stores
       tacc[15] += 1;
     }
-  }
-  if (TIMING && t == 0) {
-    tacc[14] = (uint64_t)L.misc[23];
-    tacc[13] = (uint64_t)L.misc[24];
-    tacc[12] = (uint64_t)L.misc[26];
   }
   if (sflags & 1) {  // the whole block at the end
     const int32_t lines_to = isize >= head ? (isize - head) / 16 : 0;
@@ -1197,7 +1179,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   TST(6);
   // ---- 7. CRC32: thread t hashes the 128-byte slice ending (511 - t) * 128 bytes before isize
   if (verify_crc) {
-    __syncthreads();  // last_start is dead: the CRC tables reuse it
+    __syncthreads();  // the resolve scratch is dead: the CRC tables reuse it
     for (int i = t; i < 1024; i += WG) (&L.u.crc4[0][0])[i] = (&c_crc4[0][0])[i];
     __syncthreads();
     const int32_t e = isize - (WG - 1 - t) * 128;
@@ -1316,10 +1298,10 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
   static const uint32_t ov = getenv("DQ_OV") ? (uint32_t)atoi(getenv("DQ_OV")) : OV_DEFAULT;
   static const uint32_t sflags = getenv("DQ_STORE") ? (uint32_t)atoi(getenv("DQ_STORE")) : 2;
   static int cfg = -1;
-  if (cfg < 0) {  // DQ_CFG="nb,g" (tuning experiments); default 4,1
+  if (cfg < 0) {  // DQ_CFG="nb,g" (tuning experiments: 4,1 default, 2,1 or 1,4)
     int nb = 4, g = 1;
     if (const char* e = getenv("DQ_CFG")) sscanf(e, "%d,%d", &nb, &g);
-    cfg = g != 4 ? (nb == 2 ? 4 : nb == 8 ? 5 : 0) : nb == 1 ? 1 : nb == 4 ? 3 : 2;
+    cfg = g == 4 ? 1 : nb == 2 ? 4 : 0;
   }
 #define DQ_LAUNCH(TM, NBT, GT)                                                                  \
   hipLaunchKernelGGL((inflate_block_kernel<TM, NBT, GT>), dim3((unsigned)ngrid), dim3(WG), 0, s, C, \
@@ -1328,10 +1310,7 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
 #define DQ_CFGS(TM)                       \
   switch (cfg) {                          \
     case 1: DQ_LAUNCH(TM, 1, 4); break;   \
-    case 2: DQ_LAUNCH(TM, 2, 4); break;   \
-    case 3: DQ_LAUNCH(TM, 4, 4); break;   \
     case 4: DQ_LAUNCH(TM, 2, 1); break;   \
-    case 5: DQ_LAUNCH(TM, 8, 1); break;   \
     default: DQ_LAUNCH(TM, 4, 1); break;  \
   }
   if (tim) {
