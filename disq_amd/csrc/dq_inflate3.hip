@@ -80,6 +80,7 @@ struct alignas(16) LdsI {
       uint16_t lsym[288];
       uint8_t dsym[32];
       union {
+        uint16_t pair[1 << LR];   // decode: second literal of a root index (lit << 4 | len), 0 none
         struct {
           uint8_t lens[320];      // litlen lengths [0, 288), distance lengths [288, 320)
           uint8_t clen[20];
@@ -220,18 +221,26 @@ DQ_AI uint32_t dextra(uint32_t d) { return d < 4 ? 0u : (d - 2) >> 1; }
 // One full symbol: a literal (value in len), a match (len, dist) or EOB.  Straight-line: every
 // lane does the litlen and the distance lookup (a literal lane consumes no distance bits), so a
 // wave mixing literals and matches does not execute both paths one after the other.
-DQ_AI int dsym(BitR& r, const uint32_t* __restrict__ W, const LdsI& L, uint32_t& len,
-               uint32_t& dist) {
+// Literal pairs: when the root index also holds a second whole literal (pair table) and the
+// boundary between the two lies before `lim` (the next bit position at which the caller looks at
+// symbol boundaries: segment start/exit, checkpoint, end of data), both are taken at once and
+// `lit2` is the second (else 0xffffffff) -- the boundaries the caller sees are unchanged.
+DQ_AI int dsym(BitR& r, const uint32_t* __restrict__ W, const LdsI& L, uint32_t p, uint32_t lim,
+               uint32_t& len, uint32_t& dist, uint32_t& lit2) {
   br_refill(r, W);  // >= 33 bits: a litlen code + its extra bits (<= 20)
   uint32_t bb = (uint32_t)r.bb;
-  uint32_t e = L.u.d.T[bb & ((1u << LR) - 1)];
+  const uint32_t ri = bb & ((1u << LR) - 1);
+  uint32_t e = L.u.d.T[ri];
+  const uint32_t pe = L.u.d.x.pair[ri];
   if (e & (E_LINK | E_SLOW)) e = ll_second(L, e, bb);
   const uint32_t nb = e & 15, sym = e >> 4;
   const bool is_len = sym - 257u < 29u;
   const uint32_t lk = min(sym - 257u, 28u);
   const uint32_t lx = is_len ? lextra(lk) : 0u;
   len = is_len ? lbase(lk) + ((bb >> nb) & ((1u << lx) - 1)) : sym;
-  br_take(r, nb + lx);
+  const bool two = pe != 0 && p + nb < lim;  // pe != 0: the root entry is a literal
+  lit2 = two ? pe >> 4 : 0xffffffffu;
+  br_take(r, nb + lx + (two ? (pe & 15) : 0u));
   br_refill(r, W);  // >= 33 bits: a distance code + its extra bits (<= 28)
   bb = (uint32_t)r.bb;
   uint32_t e2 = L.u.d.T[T_DROOT + (bb & ((1u << DR) - 1))];
@@ -285,14 +294,15 @@ DQ_AI int run_seg(const uint32_t* __restrict__ W, const LdsI& L, uint32_t start,
       f = p >= sE && counting ? F_EXIT : (counting ? F_END : F_DEAD);
       break;
     }
-    uint32_t len = 0, dist = 0;
-    const int k = dsym(r, W, L, len, dist);
+    uint32_t len = 0, dist = 0, lit2;
+    const uint32_t lim = min(min(thr, counting ? sE : sB), endbits);
+    const int k = dsym(r, W, L, p, lim, len, dist, lit2);
     if (k > S_MATCH) {
       *Ep = (int32_t)(k == S_EOB ? br_pos(r) : p);
       f = !counting ? F_DEAD : (k == S_EOB ? F_EOB : F_ERR);
       break;
     }
-    cnt += counting ? (k == S_MATCH ? (int32_t)len : 1) : 0;
+    cnt += counting ? (k == S_MATCH ? (int32_t)len : (lit2 != 0xffffffffu ? 2 : 1)) : 0;
   }
   *Bp = B;
   *cntp = cnt;
@@ -332,14 +342,14 @@ DQ_AI int run_redo(const uint32_t* __restrict__ W, const LdsI& L, uint32_t s0, u
       thr = j < NCK ? thr + CKI : 0xffffffffu;
       cur = j < NCK ? ck[j * ckstride] : 0xffffffffu;
     }
-    uint32_t len = 0, dist = 0;
-    const int k = dsym(r, W, L, len, dist);
+    uint32_t len = 0, dist = 0, lit2;
+    const int k = dsym(r, W, L, p, min(min(thr, sE), endbits), len, dist, lit2);
     if (k > S_MATCH) {
       *Ep = (int32_t)(k == S_EOB ? br_pos(r) : p);
       f = k == S_EOB ? F_EOB : F_ERR;
       break;
     }
-    cnt += k == S_MATCH ? (int32_t)len : 1;
+    cnt += k == S_MATCH ? (int32_t)len : (lit2 != 0xffffffffu ? 2 : 1);
   }
   *cntp = cnt;
   return f;
@@ -354,11 +364,15 @@ DQ_AI void emit_seg(const uint32_t* __restrict__ W, LdsI& L, uint32_t start, uin
   for (;;) {
     const uint32_t q = br_pos(r);
     if (q >= target || q >= endbits || p >= isize) return;
-    uint32_t len = 0, dist = 0;
-    const int k = dsym(r, W, L, len, dist);
+    uint32_t len = 0, dist = 0, lit2;
+    const int k = dsym(r, W, L, q, min(target, endbits), len, dist, lit2);
     if (k == S_LIT) {
       L.out[sh + p] = (uint8_t)len;
       p++;
+      if (lit2 != 0xffffffffu && p < isize) {
+        L.out[sh + p] = (uint8_t)lit2;
+        p++;
+      }
     } else if (k == S_MATCH) {
       if ((int32_t)dist > p) {
         set_err(L, ST_BAD_DIST);
@@ -808,8 +822,24 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     TST(0);
     // ---- 2. tables
     build_tables(L, nlen, ndist);
-    TST(1);
     if (L.misc[M_ERR]) break;
+    // pair table (the header scratch is dead): root index i whose literal leaves room for a
+    // second whole literal code in the remaining root bits -- the root entry of i >> l1 (its
+    // upper bits zero) is that literal iff its code fits them
+    for (int i = t; i < (1 << LR); i += WG) {
+      const uint32_t e1 = L.u.d.T[i];
+      const uint32_t l1 = e1 & 15;
+      uint16_t v = 0;
+      if (!(e1 & (E_LINK | E_SLOW)) && (e1 >> 4) < 256 && l1 > 0 && l1 < (uint32_t)LR) {
+        const uint32_t e2 = L.u.d.T[(uint32_t)i >> l1];
+        const uint32_t l2 = e2 & 15;
+        if (!(e2 & (E_LINK | E_SLOW)) && (e2 >> 4) < 256 && l2 > 0 && l1 + l2 <= (uint32_t)LR)
+          v = (uint16_t)e2;
+      }
+      L.u.d.x.pair[i] = v;
+    }
+    __syncthreads();
+    TST(1);
     const uint32_t a = (uint32_t)L.misc[M_A];
     if (a > endbits) {
       if (t == 0) L.misc[M_ERR] = ST_OVERREAD;
