@@ -1037,120 +1037,121 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   constexpr int NE = NB * G;
   static_assert(BATCH <= RES_NXT, "the batch's next-pointers fit the resolve scratch");
   uint16_t* nxt = L.u.r.nxt;
+  // (a) sources of batch `b0`.  First hop, every byte: its owner (one 64-bit bitmap word, one
+  //     last_start) and the owner's descriptor give the copy source (G <= 4 bytes have at most
+  //     two owners: matches are >= 3 bytes long).  A source before the byte's 512-byte step is
+  //     final (that step is complete when (b) reaches this one); so is a literal.  Every byte
+  //     publishes its source in nxt.  The match straddling the batch start is the carry (cms,
+  //     cdesc): its descriptor lies before the batch.
+  auto first_hop = [&](int32_t b0, int32_t cms, uint32_t cdesc, int32_t* fr, int32_t* xs,
+                       uint32_t& pending) {
+    pending = 0;
+    uint64_t mw[NB];
+    int32_t lsv[NB];
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+      const int32_t g0 = b0 + k * CH + G * t;
+      const int w = min(g0 >> 6, 1023);  // bytes past isize: read anything, copy = false
+      mw[k] = bm64[w];
+      lsv[k] = w ? (int32_t)L.u.r.last_start[w - 1] : 0xffff;
+    }
+    int32_t msv[NE];
+    uint32_t da[NB], db[NB];
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+      const int32_t g0 = b0 + k * CH + G * t;
+#pragma unroll
+      for (int i = 0; i < G; i++) {
+        const uint64_t mi = mw[k] & (~0ull >> (63 - ((g0 + i) & 63)));
+        msv[k * G + i] = mi ? (g0 | 63) - (int32_t)__clzll(mi) : lsv[k];
+      }
+      da[k] = load_desc(L, sh + min(max(msv[k * G], b0), 65535));
+      db[k] = G > 1 ? load_desc(L, sh + min(max(msv[k * G + G - 1], b0), 65535)) : da[k];
+    }
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+      const int32_t g0 = b0 + k * CH + G * t;
+      const int32_t sbk = b0 + k * CH + ((G * t) & ~511);
+#pragma unroll
+      for (int i = 0; i < G; i++) {
+        const int e = k * G + i;
+        const int32_t x = g0 + i, ms = msv[e];
+        const bool before = ms < b0;  // descriptors before the batch are overwritten: the carry
+        const uint32_t desc = before ? cdesc : (ms == msv[k * G + G - 1] ? db[k] : da[k]);
+        const int32_t len = (int32_t)(desc >> 15) + 3, D = (int32_t)(desc & 0x7fff) + 1;
+        const bool copy = x < isize && ms != 0xffff && (!before || ms == cms) && x < ms + len;
+        // src = ms - D + (x - ms) mod D; x - ms <= 257: a float reciprocal + one fix-up is exact
+        const int32_t jj = x - ms;
+        const int32_t q = (int32_t)((float)jj * __builtin_amdgcn_rcpf((float)D));
+        int32_t r = jj - q * D;
+        r = r >= D ? r - D : r;
+        const int32_t src = ms - D + r;
+        const bool done = !copy || src < sbk;
+        fr[e] = copy ? src : x;
+        xs[e] = src;
+        pending |= done ? 0u : 1u << e;
+        nxt[x - b0] = (uint16_t)(copy ? src : x);  // a final source (or the literal), else in-step
+      }
+    }
+  };
+  // Pointer jumping inside the byte's step: a pending byte reads nxt at its current source and
+  // publishes how far it got, so a byte that reads an advanced pointer skips that byte's chain.
+  // Every value read is a byte of the same chain, so no barrier orders the rounds and each read
+  // advances at least one hop; it ends at a literal (nxt[p] == p) or a byte before the step.
+  auto jump_round = [&](int32_t b0, int32_t* fr, int32_t* xs, uint32_t& pending) {
+    int32_t qv[NE];
+#pragma unroll
+    for (int e = 0; e < NE; e++) qv[e] = ((pending >> e) & 1) ? (int32_t)nxt[xs[e] - b0] : 0;
+#pragma unroll
+    for (int e = 0; e < NE; e++) {
+      if (!((pending >> e) & 1)) continue;
+      const int32_t p = xs[e], q = qv[e];
+      const int32_t sbk = b0 + (e / G) * CH + ((G * t) & ~511);
+      if (q == p || q < sbk) {
+        fr[e] = q;
+        pending &= ~(1u << e);
+      } else {
+        xs[e] = q;
+      }
+      nxt[(e / G) * CH + G * t + e % G] = (uint16_t)q;
+    }
+  };
+  // Software pipeline over batches: while batch k's ordered steps (b) run, batch k+1 takes its
+  // first hop (its descriptors are intact until its own steps) and one jump round after each
+  // step barrier (nxt holds batch k+1 only: batch k's sources are final in registers by then).
+  int32_t frA[NE], xsA[NE];
+  uint32_t pendA = 0;
+  int32_t cms = -1;     // carry into the current batch
+  uint32_t cdesc = 0;
+  first_hop(0, cms, cdesc, frA, xsA, pendA);
+  __syncthreads();
+  for (int hop = 0; pendA != 0 && hop < WG + 2; hop++) jump_round(0, frA, xsA, pendA);
   for (int32_t bs = 0; bs < isize; bs += BATCH) {
     const uint64_t tb0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
-    const int32_t carry_ms = L.misc[M_CARRY_MS];
-    const uint32_t carry_desc = (uint32_t)L.misc[M_CARRY_DESC];
-    // the match covering the batch's last byte continues into the next batch, whose chains can
-    // no longer read its descriptor (overwritten in (b)): keep it aside
-    int32_t next_ms = -1;
-    uint32_t next_desc = 0;
-    if (t == WG - 1 && bs + BATCH < isize) {
-      const int32_t x = bs + BATCH - 1;
+    const int32_t nbs = bs + BATCH;
+    const bool more = nbs < isize;
+    // carry into batch k+1: the match covering batch k's last byte, if it continues (all threads
+    // compute it, from batch k's descriptors, before (b) overwrites them)
+    int32_t ncms = -1;
+    uint32_t ncdesc = 0;
+    if (more) {
+      const int32_t x = nbs - 1;
       const uint64_t m = bm64[x >> 6];  // bit 63 of the last word: every bit is at or before x
       const int32_t ms = m ? (x | 63) - (int32_t)__clzll(m) : (int32_t)L.u.r.last_start[(x >> 6) - 1];
       if (ms != 0xffff) {
-        const uint32_t desc = ms < bs ? carry_desc : load_desc(L, sh + ms);
-        if ((ms >= bs || ms == carry_ms) && ms + (int32_t)(desc >> 15) + 3 > bs + BATCH) {
-          next_ms = ms;
-          next_desc = desc;
+        const uint32_t desc = ms < bs ? cdesc : load_desc(L, sh + ms);
+        if ((ms >= bs || ms == cms) && ms + (int32_t)(desc >> 15) + 3 > nbs) {
+          ncms = ms;
+          ncdesc = desc;
         }
       }
     }
-    // (a) sources.  First hop, every byte: its owner (one 64-bit bitmap word, one last_start) and
-    //     the owner's descriptor give the copy source (G <= 4 bytes have at most two owners:
-    //     matches are >= 3 bytes long).  A source before the byte's 512-byte step is final (that
-    //     step is complete when (b) reaches this one); so is a literal.
-    int32_t xs[NE], fr[NE], sbk[NB];
-    uint32_t pending = 0;
-    {
-      uint64_t mw[NB];
-      int32_t lsv[NB];
-#pragma unroll
-      for (int k = 0; k < NB; k++) {
-        const int32_t g0 = bs + k * CH + G * t;
-        const int w = min(g0 >> 6, 1023);  // bytes past isize: read anything, copy = false
-        mw[k] = bm64[w];
-        lsv[k] = w ? (int32_t)L.u.r.last_start[w - 1] : 0xffff;
-      }
-      int32_t msv[NE];
-      uint32_t da[NB], db[NB];
-#pragma unroll
-      for (int k = 0; k < NB; k++) {
-        const int32_t g0 = bs + k * CH + G * t;
-#pragma unroll
-        for (int i = 0; i < G; i++) {
-          const uint64_t mi = mw[k] & (~0ull >> (63 - ((g0 + i) & 63)));
-          msv[k * G + i] = mi ? (g0 | 63) - (int32_t)__clzll(mi) : lsv[k];
-        }
-        da[k] = load_desc(L, sh + min(max(msv[k * G], bs), 65535));
-        db[k] = G > 1 ? load_desc(L, sh + min(max(msv[k * G + G - 1], bs), 65535)) : da[k];
-      }
-#pragma unroll
-      for (int k = 0; k < NB; k++) {
-        const int32_t g0 = bs + k * CH + G * t;
-        sbk[k] = bs + k * CH + ((G * t) & ~511);
-#pragma unroll
-        for (int i = 0; i < G; i++) {
-          const int e = k * G + i;
-          const int32_t x = g0 + i, ms = msv[e];
-          const bool before = ms < bs;  // descriptors before the batch are overwritten: the carry
-          const uint32_t desc = before ? carry_desc : (ms == msv[k * G + G - 1] ? db[k] : da[k]);
-          const int32_t len = (int32_t)(desc >> 15) + 3, D = (int32_t)(desc & 0x7fff) + 1;
-          const bool copy = x < isize && ms != 0xffff && (!before || ms == carry_ms) && x < ms + len;
-          // src = ms - D + (x - ms) mod D; x - ms <= 257: a float reciprocal + one fix-up is exact
-          const int32_t jj = x - ms;
-          const int32_t q = (int32_t)((float)jj * __builtin_amdgcn_rcpf((float)D));
-          int32_t r = jj - q * D;
-          r = r >= D ? r - D : r;
-          const int32_t src = ms - D + r;
-          const bool done = !copy || src < sbk[k];
-          fr[e] = copy ? src : x;
-          xs[e] = src;
-          pending |= done ? 0u : 1u << e;
-          // next pointer: a final source (or the literal itself), else the in-step source
-          nxt[x - bs] = (uint16_t)(copy ? src : x);
-        }
-      }
-    }
-    // Further hops stay inside the byte's step: nxt is the copy-source function on the batch,
-    // and a pending byte jumps along it, publishing how far it got (pointer jumping: a byte that
-    // reads an advanced pointer skips that byte's whole chain).  Every value read is a byte of
-    // the same chain, so no barrier orders the rounds; each read advances at least one hop.
-    // Ends at a literal (nxt[p] == p) or at a byte before the step.  No descriptor is read.
-    int hop = 1;
-    if (__syncthreads_or(pending != 0)) {
-      for (; pending != 0 && hop < WG + 2; hop++) {
-        int32_t qv[NE];
-#pragma unroll
-        for (int e = 0; e < NE; e++)
-          qv[e] = ((pending >> e) & 1) ? (int32_t)nxt[xs[e] - bs] : 0;
-#pragma unroll
-        for (int e = 0; e < NE; e++) {
-          if (!((pending >> e) & 1)) continue;
-          const int32_t p = xs[e], q = qv[e];
-          if (q == p || q < sbk[e / G]) {
-            fr[e] = q;
-            pending &= ~(1u << e);
-          } else {
-            xs[e] = q;
-          }
-          nxt[(e / G) * CH + G * t + e % G] = (uint16_t)q;
-        }
-      }
-    }
+    __syncthreads();  // every wave's jumps of batch k are done: nxt is free for batch k+1
+    int32_t frB[NE], xsB[NE];
+    uint32_t pendB = 0;
+    if (more) first_hop(nbs, ncms, ncdesc, frB, xsB, pendB);
     const uint64_t tb1 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
-    if (TIMING) {
-      const int wmax = __builtin_amdgcn_readlane(wave_incl_max(hop), 63);
-      if (lane == 0) {
-        if (wv == 0) atomicAdd(&L.misc[21], wmax);
-        atomicMax(&L.misc[22], wmax);
-      }
-    }
-    __syncthreads();  // every chain has read its descriptors before (b) overwrites them
-    const uint64_t tb2 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
-    const int wgm = TIMING ? L.misc[22] : 0;
-    // (b) 512-byte steps in order: one LDS read + write per copied byte, one barrier per step
+    // (b) batch k's 512-byte steps in order: one LDS read + write per copied byte, one barrier
 #pragma unroll
     for (int k = 0; k < NB; k++) {
 #pragma unroll
@@ -1159,22 +1160,18 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
           const int32_t g0 = bs + k * CH + G * t;
           uint8_t v[G];
 #pragma unroll
-          for (int i = 0; i < G; i++) v[i] = O[min(fr[k * G + i], 65535)];
+          for (int i = 0; i < G; i++) v[i] = O[min(frA[k * G + i], 65535)];
 #pragma unroll
           for (int i = 0; i < G; i++)
-            if (g0 + i < isize && fr[k * G + i] != g0 + i) L.out[sh + g0 + i] = v[i];
-        }
-        if (TIMING && k == 0 && j == 0 && t == 0) L.misc[22] = 0;
-        if (k == NB - 1 && j == G - 1 && t == WG - 1) {  // the old carry was read before step 0
-          L.misc[M_CARRY_MS] = next_ms;
-          L.misc[M_CARRY_DESC] = (int32_t)next_desc;
+            if (g0 + i < isize && frA[k * G + i] != g0 + i) L.out[sh + g0 + i] = v[i];
         }
         __syncthreads();
+        if (pendB) jump_round(nbs, frB, xsB, pendB);
       }
     }
-    const uint64_t tb3 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
-    // (c) store the 16-byte U lines this batch completed (overlaps the next batch's chains)
-    const int32_t c1 = min(isize, bs + BATCH);
+    const uint64_t tb2 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
+    // (c) store the 16-byte U lines this batch completed
+    const int32_t c1 = min(isize, nbs);
     const int32_t lines_to = c1 >= head ? (c1 - head) / 16 : 0;
     if (!(sflags & 1)) {
       for (int32_t k = lines_done + t; k < lines_to; k += WG) {
@@ -1185,12 +1182,17 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       }
       lines_done = lines_to;
     }
+    const uint64_t tb3 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
+    for (int hop = 0; pendB != 0 && hop < WG + 2; hop++) jump_round(nbs, frB, xsB, pendB);
+#pragma unroll
+    for (int e = 0; e < NE; e++) frA[e] = frB[e];
+    cms = ncms;
+    cdesc = ncdesc;
     if (TIMING && t == 0) {
-      tacc[9] += tb1 - tb0;  // (a) chains of thread 0's wave
-      tacc[11] += (uint64_t)wgm;  // max hops over the workgroup
-      tacc[12] += tb2 - tb1;  // waiting at the barrier for the slowest wave's chains
-      tacc[13] += tb3 - tb2;  // (b) the ordered steps
-      tacc[14] += __builtin_amdgcn_s_memtime() - tb3;  // (c) issuing the U stores
+      tacc[9] += tb1 - tb0;   // carry + barrier + first hop of the next batch
+      tacc[12] += tb2 - tb1;  // (b) the ordered steps with the next batch's jump rounds
+      tacc[13] += tb3 - tb2;  // (c) issuing the U stores
+      tacc[14] += __builtin_amdgcn_s_memtime() - tb3;  // the rest of wave 0's jumps
       tacc[15] += 1;
     }
   }
