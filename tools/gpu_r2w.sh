@@ -2,7 +2,7 @@
 # Round-2 evidence after the pointer-jumping resolve: rocprof kernel trace of the default bench
 # workload, the inflate kernel's HBM traffic (FETCH/WRITE passes) and its SQ counters.
 set -eo pipefail
-out=gpurun_out/r2w
+out=gpurun_out/${1:-r2w}
 mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof -o run -- \
