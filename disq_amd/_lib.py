@@ -87,6 +87,13 @@ class DqStats(C.Structure):
                 ("ms_span", C.c_double)]
 
 
+class DqMultiResult(C.Structure):
+    _fields_ = [("n_devices", C.c_int32), ("reserved", C.c_int32), ("n_partitions", C.c_int64),
+                ("n_records", C.c_int64), ("compressed_bytes", C.c_int64),
+                ("decompressed_bytes", C.c_int64), ("digest", C.c_uint64), ("ms_wall", C.c_double),
+                ("ms_shard_wall_max", C.c_double), ("ms_device_max", C.c_double)]
+
+
 # Every symbol include/disq_gpu.h declares.
 EXPORTS = ("dq_ctx_create", "dq_ctx_destroy", "dq_last_error", "dq_version", "dq_open_memory",
            "dq_open_path", "dq_set_index", "dq_read_header", "dq_plan", "dq_decode",
@@ -97,7 +104,7 @@ EXPORTS = ("dq_ctx_create", "dq_ctx_destroy", "dq_last_error", "dq_version", "dq
            "dq_decode_chunk_filtered", "dq_debug_guess_all", "dq_text_open_memory",
            "dq_text_open_path", "dq_text_run", "dq_text_read", "dq_text_batch_free",
            "dq_bgzf_compress", "dq_bgzf_compress_resident", "dq_bgzf_fetch",
-           "dq_text_set_index", "dq_text_set_intervals")
+           "dq_text_set_index", "dq_text_set_intervals", "dq_decode_file_multi")
 
 _lib = None
 _lock = threading.Lock()
@@ -148,6 +155,7 @@ def lib():
                                          P(P(DqBatch))]
         L.dq_read.argtypes = [vp, P(DqTraversal), C.c_int32, P(P(DqBatch))]
         L.dq_run_resident.argtypes = [vp, P(DqTraversal), P(DqStats)]
+        L.dq_decode_file_multi.argtypes = [vp, C.c_char_p, P(C.c_int32), C.c_int32, P(DqMultiResult)]
         L.dq_debug_inflated.argtypes = [vp, vp, C.c_int64, P(C.c_int64)]
         L.dq_debug_guess_all.argtypes = [vp, vp, C.c_int64, P(C.c_int64)]
         L.dq_batch_free.argtypes = [P(DqBatch)]
@@ -494,6 +502,15 @@ class Context:
         check(self._h, lib().dq_run_resident(self._h, C.byref(t) if t is not None else None,
                                              C.byref(st)))
         return st
+
+    def decode_file_multi(self, path, devices):
+        """dq_decode_file_multi: the file's partitions sharded over `devices` (one context and
+        host thread each, records left in HBM); returns DqMultiResult."""
+        dv = (C.c_int32 * len(devices))(*devices)
+        r = DqMultiResult()
+        check(self._h, lib().dq_decode_file_multi(self._h, os.fsencode(path), dv, len(devices),
+                                                  C.byref(r)))
+        return r
 
     def inflated(self):
         n = C.c_int64()

@@ -13,6 +13,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -2296,6 +2297,130 @@ int dq_partition_digests(dq_ctx* ctx, int64_t* counts, uint64_t* digests, int64_
     if (counts) counts[i] = r.end - r.begin;
     if (digests) digests[i] = r.digest;
   }
+  return 0;
+}
+
+// Whole-node mode in one process (SURVEY.md section 8(b) dq_decode_file_multi): the file's Disq
+// partitions are cut into contiguous groups, one per device, by the byte range holding each split's
+// first byte (even ranges: parallel.shard_plan); every device decodes its group from the file
+// alone -- its split range plus a halo for the straddling record, grown x4 while too short -- on
+// its own context and host thread.  No data crosses between devices: each reads its halo from the
+// (page-cached) file.  The per-partition digests fold, in partition order, to the digest of a
+// single-device run of the whole file.
+int dq_decode_file_multi(dq_ctx* ctx, const char* path, const int32_t* devices, int32_t n_devices,
+                         dq_multi_result* out) {
+  if (!ctx || !path || !out || n_devices <= 0 || n_devices > 64) return DQ_EINVAL;
+  ON_DEVICE(ctx);
+  memset(out, 0, sizeof(*out));
+  const auto t0 = std::chrono::steady_clock::now();
+  int64_t flen = 0;
+  int rc;
+  {
+    Fd f;
+    if ((rc = open_fd(ctx, path, f, &flen))) return rc;
+    if ((rc = chunk_header(ctx, path, f.fd, flen))) return rc;
+  }
+  std::vector<std::pair<int64_t, int64_t>> splits;
+  if (path_splits(ctx->o, flen, splits)) RET(DQ_EINVAL, "splitSize must be > 0 with useNio");
+  const int64_t P = (int64_t)splits.size();
+  const int W = n_devices;
+  std::vector<int64_t> O((size_t)W + 1);
+  for (int r = 0; r < W; r++) O[(size_t)r] = (int64_t)(((__int128)r * flen + W - 1) / W);
+  O[(size_t)W] = flen;
+  struct Shard {
+    int64_t p0 = 0, p1 = 0, lo = 0, hi = 0;
+    int rc = 0;
+    std::string err;
+    std::vector<int64_t> counts;
+    std::vector<uint64_t> digests;
+    double ms_device = 0, ms_wall = 0;
+    int64_t owned = 0;
+  };
+  std::vector<Shard> sh((size_t)W);
+  for (int64_t p = 0; p < P; p++) {
+    const int64_t st = splits[(size_t)p].first;
+    int r = (int)(std::upper_bound(O.begin(), O.end(), st) - O.begin()) - 1;
+    r = std::min(W - 1, std::max(0, r));
+    Shard& s = sh[(size_t)r];
+    if (s.p1 == s.p0) {
+      s.p0 = p;
+      s.lo = st;
+    }
+    s.p1 = p + 1;
+    s.hi = splits[(size_t)p].second;
+  }
+  const std::vector<uint8_t> hdr = ctx->hdr;
+  const std::string pth = path;
+  auto work = [&](int r) {
+    Shard& s = sh[(size_t)r];
+    const auto w0 = std::chrono::steady_clock::now();
+    dq_opts o = ctx->o;
+    o.device = devices[r];
+    dq_ctx* c = nullptr;
+    if ((s.rc = dq_ctx_create(&c, &o))) {
+      s.err = "dq_ctx_create failed on device " + std::to_string(devices[r]);
+      return;
+    }
+    int64_t halo = 4 << 20;
+    for (;;) {
+      const int64_t end = std::min(flen, s.hi + halo);
+      dq_stats st;
+      s.rc = dq_open_shard_path(c, pth.c_str(), s.lo, end - s.lo, s.p0, s.p1, hdr.data(),
+                                (int64_t)hdr.size());
+      if (!s.rc) s.rc = dq_run_resident(c, nullptr, &st);
+      if (s.rc == DQ_EFORMAT && end < flen &&
+          std::string(dq_last_error(c)).find("halo too small") != std::string::npos) {
+        halo *= 4;
+        continue;
+      }
+      if (!s.rc) {
+        s.ms_device = st.ms_total;
+        s.owned = st.owned_bytes;
+      }
+      break;
+    }
+    if (!s.rc) {
+      const int64_t np = s.p1 - s.p0;
+      s.counts.resize((size_t)np);
+      s.digests.resize((size_t)np);
+      int64_t n = 0;
+      s.rc = dq_partition_digests(c, s.counts.data(), s.digests.data(), np, &n);
+      if (!s.rc && n != np) {
+        s.rc = DQ_EFORMAT;
+        s.err = "shard partition count mismatch";
+      }
+    }
+    if (s.rc && s.err.empty()) s.err = dq_last_error(c);
+    dq_ctx_destroy(c);
+    s.ms_wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+  };
+  std::vector<std::thread> th;
+  for (int r = 0; r < W; r++)
+    if (sh[(size_t)r].p1 > sh[(size_t)r].p0) th.emplace_back(work, r);
+  for (auto& x : th) x.join();
+  uint64_t dg = 0;
+  for (int r = 0; r < W; r++) {
+    const Shard& s = sh[(size_t)r];
+    if (s.p1 == s.p0) continue;
+    if (s.rc) {
+      ctx->err = "device " + std::to_string(devices[r]) + ": " + s.err;
+      return s.rc;
+    }
+    for (int64_t k = 0; k < s.p1 - s.p0; k++) {
+      const int64_t i = s.p0 + k;
+      out->n_records += s.counts[(size_t)k];
+      dg += dq_mix64(s.digests[(size_t)k] ^ ((uint64_t)(i + 1) * DQ_K_WORD));
+    }
+    out->ms_device_max = std::max(out->ms_device_max, s.ms_device);
+    out->ms_shard_wall_max = std::max(out->ms_shard_wall_max, s.ms_wall);
+    out->decompressed_bytes += s.owned;
+  }
+  // partitions owned by no shard (none: every split has an owner) would fold as empty
+  out->n_devices = W;
+  out->n_partitions = P;
+  out->digest = dg;
+  out->compressed_bytes = flen;
+  out->ms_wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return 0;
 }
 

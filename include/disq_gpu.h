@@ -177,6 +177,28 @@ int dq_open_shard_device(dq_ctx* ctx, const void* dev_bytes, int64_t len, int64_
 int dq_open_shard_path(dq_ctx* ctx, const char* path, int64_t base, int64_t len, int64_t p0,
                        int64_t p1, const uint8_t* header, int64_t header_len);
 
+/* Whole-node mode in one process (the benchmark entry of SURVEY.md section 8(b)): the file's
+ * partitions in contiguous groups, one per device of `devices` (by the even byte range holding
+ * each split's first byte, as disq_amd.parallel.shard_plan), each group decoded on its own
+ * context and host thread from the file alone (dq_open_shard_path with a halo grown x4 while too
+ * short + dq_run_resident; records stay in HBM and are freed).  `ctx` supplies the options and
+ * reads the header once.  digest folds every partition's digest in partition order: it equals
+ * dq_stats.digest of a one-device run of the whole file. */
+typedef struct dq_multi_result {
+  int32_t n_devices;
+  int32_t reserved;
+  int64_t n_partitions;
+  int64_t n_records;
+  int64_t compressed_bytes;    /* file length */
+  int64_t decompressed_bytes;  /* sum of the shards' owned bytes (= the file's stream) */
+  uint64_t digest;
+  double ms_wall;              /* header read + all shards (open, upload, pipeline), host clock */
+  double ms_shard_wall_max;    /* slowest shard, host clock */
+  double ms_device_max;        /* slowest shard's device pipeline (HIP events) */
+} dq_multi_result;
+int dq_decode_file_multi(dq_ctx* ctx, const char* path, const int32_t* devices, int32_t n_devices,
+                         dq_multi_result* out);
+
 /* The decompressed BAM header (AbstractSamSource.getFileHeader, D/impl/formats/sam/
  * AbstractSamSource.java:32-49) from the first `len` bytes of a file: enough BGZF blocks to hold
  * it (the last one may be cut).  Writes up to cap bytes to out; *out_len = header length.  Used

@@ -481,3 +481,26 @@ def test_unplaced_tail_needs_the_file_end():
         b = c.read(traversal=(None, True), with_raw=False)
     assert len(want) == 1000 and len(b["voffset"]) == len(want)  # the unplaced tail
     assert np.array_equal(b["voffset"], want["voffset"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ndev", [1, 3, 8])
+def test_decode_file_multi_equals_oracle(tmp_path, ndev):
+    """dq_decode_file_multi (whole-node mode in one process): the partitions sharded over
+    `ndev` contexts (all on device 0 here; one per GPU on a node) fold to the oracle's digest."""
+    from disq_amd import _lib, synth
+    r = synth.generate(200000, seed=23, nthreads=8, unplaced_fraction=0.005)
+    path = tmp_path / "wgs.bam"
+    path.write_bytes(r.bam)
+    split = 1 << 20
+    ob = O.OracleBam(r.bam)
+    oplan = ob.plan(split)
+    parts = iter(ob.read_partitions(split))
+    dig = [O.stream_digest(next(parts)["hash"]) if ch is not None else 0 for _, _, ch in oplan]
+    with _lib.Context(split_size=split) as c:
+        m = c.decode_file_multi(str(path), [0] * ndev)
+    assert m.n_devices == ndev and m.n_partitions == len(oplan)
+    assert m.n_records == sum(len(p) for p in ob.read_partitions(split))
+    assert m.digest == P.fold_digest(dig)
+    assert m.compressed_bytes == len(r.bam)
+    assert m.decompressed_bytes == len(ob.inflate_all())
