@@ -20,7 +20,10 @@ class DqOpts(C.Structure):
     _fields_ = [("device", C.c_int32), ("split_size", C.c_int32), ("use_nio", C.c_int32),
                 ("verify_crc", C.c_int32), ("stringency", C.c_int32),
                 ("full_traversal", C.c_int32),
-                ("hadoop_block_size", C.c_int64)]
+                ("hadoop_block_size", C.c_int64), ("compat", C.c_int32), ("reserved", C.c_int32)]
+
+
+COMPAT_DISQ_EXACT, COMPAT_DEDUPE = 0, 1
 
 
 class DqChunk(C.Structure):
@@ -236,10 +239,11 @@ class Context:
     """One dq_ctx (own HIP stream) with a resident BAM."""
 
     def __init__(self, split_size=0, use_nio=False, verify_crc=False, device=0,
-                 hadoop_block_size=0, stringency=0, full_traversal=False):
+                 hadoop_block_size=0, stringency=0, full_traversal=False,
+                 compat=COMPAT_DISQ_EXACT):
         self._h = C.c_void_p()
         o = DqOpts(device, split_size, int(use_nio), int(verify_crc), stringency,
-                   int(full_traversal), hadoop_block_size)
+                   int(full_traversal), hadoop_block_size, int(compat), 0)
         rc = lib().dq_ctx_create(C.byref(self._h), C.byref(o))
         if rc != DQ_OK:
             msg = lib().dq_last_error(self._h).decode() if self._h else ""

@@ -789,6 +789,14 @@ static int run_pipeline(dq_ctx* ctx) {
     }
     if (P.rec_lin >= 0 && start_lin < 0) start_lin = P.rec_lin;
   }
+  if (ctx->o.compat == DQ_COMPAT_DEDUPE && !ctx->chunk_mode) {
+    // chunk ends at splitEnd << 16: the records of a block starting at the split end belong to
+    // the next partition only
+    for (auto& P : ctx->plans_h)
+      if (P.rec_lin >= 0 && P.first_blk != SPLIT_FROM_SBI) P.vend = (uint64_t)P.split_end << 16;
+    HIPCHK(hipMemcpyAsync(ctx->plans.p, ctx->plans_h.data(), sizeof(SplitPlan) * (size_t)nsplit,
+                          hipMemcpyHostToDevice, s));
+  }
   // ---- Kernel 3: record chain, SoA decode, hashes
   int64_t nrec = 0;
   const int64_t SEG = 64 * 1024;  // record-chain segment: one wave walks it

@@ -58,7 +58,18 @@ typedef struct dq_opts {
   int32_t full_traversal;    /* 1: interval runs inflate and filter the whole file; 0 (default):
                                 only the .bai spans of the intervals (dq_run_resident) */
   int64_t hadoop_block_size; /* fs.local.block.size; 0 = 32 MiB */
+  int32_t compat;            /* DQ_COMPAT_DISQ_EXACT (default) or DQ_COMPAT_DEDUPE */
+  int32_t reserved;
 } dq_opts;
+
+/* dq_opts.compat.  DISQ_EXACT reproduces Disq's chunk ends, (splitEnd << 16) | 0xffff
+ * (BamSource.java:136-143): when a BGZF block starts exactly at a split end, the records starting
+ * in it are read by that partition and again by the next one (BgzfBlockSource includes a block at
+ * pos == splitEnd in both splits).  DEDUPE ends guessed chunks at splitEnd << 16 instead, so each
+ * record belongs to exactly one partition (the one whose split holds its start block); .sbi chunks
+ * are unaffected (they never overlap). */
+#define DQ_COMPAT_DISQ_EXACT 0
+#define DQ_COMPAT_DEDUPE 1
 
 /* One Spark partition of the BAM read plan: a PathChunk (D/impl/file/PathChunk.java). */
 typedef struct dq_chunk {

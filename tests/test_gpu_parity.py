@@ -230,3 +230,32 @@ def test_large_properties():
     ob = O.OracleBam(s.bam)
     recs = ob.read_all()
     assert np.array_equal(recs["hash"], b["hash"])
+
+
+@pytest.mark.parametrize("split", [14146, 40000, 128 * 1024])
+def test_compat_dedupe_partitions_tile_the_file(golden, split):
+    """dq_opts.compat = DEDUPE: chunk ends at splitEnd << 16, so a block starting at a split end
+    (1.bam @ 14146: Disq reads its records twice, 5123 for 4917) belongs to the next partition
+    only; the partitions concatenate to the file's record list.  DISQ_EXACT keeps the oracle's
+    (Disq's) partitions."""
+    data = open(os.path.join(golden, "1.bam"), "rb").read()
+    ob = O.OracleBam(data)
+    allrec = ob.read_all()
+    exact = ob.read_partitions(split)
+    plan = [(s, e) for s, e, ch in ob.plan(split) if ch is not None]
+    want = [p[p["voffset"] < (np.uint64(e) << np.uint64(16))] for p, (s, e) in zip(exact, plan)]
+    assert np.array_equal(np.concatenate(want)["voffset"], allrec["voffset"])
+    with _lib.Context(split_size=split, compat=_lib.COMPAT_DEDUPE) as c:
+        c.open_bytes(data)
+        b = c.read(with_raw=False)
+        chunks = c.plan()
+    po = b["part_offset"]
+    assert len(po) - 1 == len(want)
+    for i, w in enumerate(want):
+        assert np.array_equal(b["voffset"][int(po[i]):int(po[i + 1])], w["voffset"])
+    assert np.array_equal(b["voffset"], allrec["voffset"])
+    assert all(ch is None or ch[1] == (e << 16) for s, e, ch in chunks)
+    with _lib.Context(split_size=split) as c:
+        c.open_bytes(data)
+        n_exact = len(c.read(with_raw=False)["voffset"])
+    assert n_exact == sum(len(p) for p in exact) == (5123 if split == 14146 else 4917)
