@@ -238,6 +238,7 @@ def main():
     el = time.perf_counter() - t0
     ms_step = el * 1e3 / args.steps
     stats, ubytes, nrec, digest = outs[-1]
+    comp_bytes = file_len  # C of the whole job (every rank's shard)
     for i, o in enumerate(outs):
         log(f"[bench] step {i}: {o[0].ms_total:.1f} ms device (scan {o[0].ms_scan:.1f}, inflate "
             f"{o[0].ms_inflate:.1f}, plan {o[0].ms_plan:.1f}, records {o[0].ms_records:.1f})")
@@ -321,6 +322,14 @@ def main():
                 "interval_mode": interval_mode,
                 "end_to_end": e2e,
                 "parity": parity,
+                # whole-pipeline algorithmic bytes C + 2U + 60R (unfused
+                # record walk) over the step time, against the spec and the measured HBM peaks
+                "pipeline_roofline": {
+                    "bytes_alg": int(comp_bytes + 2 * ubytes + 60 * nrec),
+                    "achieved_gbs": round((comp_bytes + 2 * ubytes + 60 * nrec) / (ms_step / 1e3) / 1e9, 2),
+                    "frac_of_8000_gbs": round((comp_bytes + 2 * ubytes + 60 * nrec) / (ms_step / 1e3) / 8e12, 5),
+                    "frac_of_6290_gbs_measured": round((comp_bytes + 2 * ubytes + 60 * nrec) / (ms_step / 1e3) / 6.29e12, 5),
+                },
             },
             "roofline": {
                 "bound": "hbm",
@@ -333,6 +342,8 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
                 "traffic_src": traffic_src,
+                "pmc_src": "profiles/r2ac_inflate_pmc.txt (VALU busy 58 %, 63.9 % of wave cycles "
+                           "waiting, LDS bank conflicts 40 %)",
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_launch_ms": round(infl_avg, 3),
             },
