@@ -328,10 +328,14 @@ __device__ int check_internal(const uint8_t* U, int64_t ulen, int u_is_eof, cons
   return 0;
 }
 
-// checkRecordStart (BamRecordGuesser.java:34-52): 1 true, 0 false, 4 need more data.
+// checkRecordStart (BamRecordGuesser.java:34-52): 1 true, 0 false, 4 need more data.  NCHK
+// chained records (READS_TO_CHECK = 10, :16); the record-chain speculation (seg_spec) uses 3: its
+// guesses are verified link by link and a wrong one is repaired, so it needs a likely start, not
+// Disq's planning decision.
+template <int NCHK = 10>
 __device__ int check_record_start(const uint8_t* U, int64_t ulen, int u_is_eof,
                                   const int32_t* ref_len, int32_t n_ref, int64_t v) {
-  for (int k = 0; k < 10; k++) {
+  for (int k = 0; k < NCHK; k++) {
     int64_t nv = 0;
     int r = check_internal(U, ulen, u_is_eof, ref_len, n_ref, v, &nv);
     if (r == 1) {
@@ -564,7 +568,7 @@ __global__ __launch_bounds__(64) void seg_spec_kernel(const uint8_t* __restrict_
     } else {
       for (int64_t b = sb; b < se; b += 64) {
         const int64_t v = b + threadIdx.x;
-        const bool hit = v < se && check_record_start(U, ulen, u_is_eof, ref_len, n_ref, v) == 1;
+        const bool hit = v < se && check_record_start<3>(U, ulen, u_is_eof, ref_len, n_ref, v) == 1;
         const uint64_t m = __ballot(hit);
         if (m) {
           best = b + __builtin_ctzll(m);
@@ -957,7 +961,7 @@ __global__ __launch_bounds__(64) void wseg_spec_kernel(const uint8_t* __restrict
       for (int64_t b = sb; b < se; b += 64) {
         const int64_t v = b + threadIdx.x;
         const bool hit =
-            v < se && check_record_start(U, w.u_limit, w.at_eof, ref_len, n_ref, v) == 1;
+            v < se && check_record_start<3>(U, w.u_limit, w.at_eof, ref_len, n_ref, v) == 1;
         const uint64_t m = __ballot(hit);
         if (m) {
           best = b + __builtin_ctzll(m);
