@@ -14,8 +14,10 @@
 //                  wave scan).
 //   2. tables   -- canonical codes are assigned in parallel (per-wave ballots give each symbol
 //                  its rank among equal lengths); 10-bit litlen / 8-bit distance root tables of
-//                  16-bit entries (sym << 4 | length) plus 32 / 128-entry second-level tables for
-//                  longer codes, so every code decodes with at most two LDS reads.
+//                  16-bit entries that carry the decoded value (literal byte, length base and
+//                  extra-bit count, distance base and extra-bit count: ent_ll / ent_d) plus 32 /
+//                  128-entry second-level tables for longer codes, so every code decodes with at
+//                  most two LDS reads and no arithmetic on the symbol number.
 //   3. spec     -- the bit range is cut into NDEC segments; lane t starts decoding at the first
 //                  bit of segment t (an arbitrary bit) and records its EXIT: the first litlen-mode
 //                  symbol boundary at or past the start of segment t+1.  Huffman codes
@@ -50,6 +52,8 @@ namespace {
 
 using namespace dqi;
 
+#define DQ_HD __device__ __host__ __attribute__((always_inline)) inline
+
 constexpr int WG = 512;           // threads per workgroup
 constexpr int NDEC = 512;         // speculative decode lanes (<= WG)
 constexpr uint32_t OV_DEFAULT = 96;  // speculative warm-up bits before each segment
@@ -65,8 +69,31 @@ constexpr int T_DROOT = T_LSUB + LSLOTS * (1 << LSB);
 constexpr int T_DSUB = T_DROOT + (1 << DR);
 constexpr int T_END = T_DSUB + DSLOTS * (1 << DSB);
 constexpr int HB_WORDS = 160;             // staged dynamic-header words (aliases T)
-constexpr uint16_t E_LINK = 0x8000;  // | slot: second-level table
-constexpr uint16_t E_SLOW = 0x4000;  // no second-level table left: canonical decode
+// Root entries whose code length field (bits 0-3) is 0 are not codes: 0 = no code (incomplete
+// table), E_LINK | slot << 4 = second-level table `slot`, E_SLOW = canonical decode.
+constexpr uint16_t E_LINK = 0x0200;
+constexpr uint16_t E_SLOW = 0x0100;
+// Decoded litlen entry: code length (bits 0-3), M = length/EOB/invalid (bit 4), extra-bit count
+// (bits 5-7), value (bits 8-15): the literal byte or length base - 3.  EOB and the invalid symbols
+// 286/287 are M entries with 0 extra bits and values no length base has.
+constexpr uint32_t LL_EOB = 0xFE10, LL_BAD = 0xFD10;
+DQ_HD uint16_t ent_ll(uint32_t sym, uint32_t len) {
+  if (sym < 256) return (uint16_t)(sym << 8 | len);
+  if (sym == 256) return (uint16_t)(LL_EOB | len);
+  if (sym > 285) return (uint16_t)(LL_BAD | len);
+  const uint32_t k = sym - 257;  // RFC 1951 3.2.5
+  const uint32_t x = (k < 8 || k == 28) ? 0u : (k - 4) >> 2;
+  const uint32_t base = k < 8 ? k + 3 : k == 28 ? 258u : ((4u + (k & 3u)) << ((k - 4) >> 2)) + 3u;
+  return (uint16_t)((base - 3) << 8 | x << 5 | 16u | len);
+}
+// Decoded distance entry: code length (bits 0-3), extra-bit count (4-7), base - 1 = m << s with
+// s (8-11) and m (12-13), invalid symbol 30/31 (bit 14).
+DQ_HD uint16_t ent_d(uint32_t d, uint32_t len) {
+  if (d >= 30) return (uint16_t)(0x4000u | len);
+  const uint32_t x = d < 4 ? 0u : (d - 2) >> 1;
+  const uint32_t m = d < 2 ? d : 2u + (d & 1u), sh = d < 2 ? 0u : (d >> 1) - 1u;
+  return (uint16_t)(m << 12 | sh << 8 | x << 4 | len);
+}
 
 enum : int32_t { F_EXIT = 0, F_EOB = 1, F_ERR = 2, F_END = 3 };
 
@@ -188,41 +215,30 @@ DQ_AI uint32_t load_desc(const LdsI& L, int a) {
 // Second-level / canonical lookup for a root entry flagged E_LINK or E_SLOW.
 DQ_AI uint32_t ll_second(const LdsI& L, uint32_t e, uint32_t bb) {
   if (e & E_LINK)
-    return L.u.d.T[T_LSUB + ((e & 15) << LSB) + ((bb >> LR) & ((1u << LSB) - 1))];
+    return L.u.d.T[T_LSUB + (((e >> 4) & 15) << LSB) + ((bb >> LR) & ((1u << LSB) - 1))];
+  if (!(e & E_SLOW)) return 0u;
   int l = 0;
   const int k = canon_decode(bb, L.u.d.hl, LR + 1, &l);
-  return k < 0 ? 0u : (((uint32_t)L.u.d.lsym[k] << 4) | (uint32_t)l);
+  return k < 0 ? 0u : ent_ll(L.u.d.lsym[k], (uint32_t)l);
 }
 DQ_AI uint32_t d_second(const LdsI& L, uint32_t e, uint32_t bb) {
   if (e & E_LINK)
-    return L.u.d.T[T_DSUB + ((e & 15) << DSB) + ((bb >> DR) & ((1u << DSB) - 1))];
+    return L.u.d.T[T_DSUB + (((e >> 4) & 15) << DSB) + ((bb >> DR) & ((1u << DSB) - 1))];
+  if (!(e & E_SLOW)) return 0u;
   int l = 0;
   const int k = canon_decode(bb, L.u.d.hd, DR + 1, &l);
-  return k < 0 ? 0u : (((uint32_t)L.u.d.dsym[k] << 4) | (uint32_t)l);
+  return k < 0 ? 0u : ent_d(L.u.d.dsym[k], (uint32_t)l);
 }
 
-// Length / distance bases and extra bits by arithmetic (RFC 1951 3.2.5): a few ALU ops instead of
-// a dependent LDS table read on the symbol path.  k = length symbol - 257 (0..28), d = 0..29.
-// Written as selects over one formula (k in 4..27 and 28 + 1; d >= 2) so they compile to
-// cndmasks, not to divergent branches inside the symbol loop.
-DQ_AI uint32_t lbase(uint32_t k) {
-  const uint32_t km = max(k, 4u) - 4u;
-  const uint32_t b = ((4u + (km & 3u)) << (km >> 2)) + 3u;
-  return (k < 4u ? k + 3u : b) - (k == 28u ? 1u : 0u);
-}
-DQ_AI uint32_t lextra(uint32_t k) { return (k < 8 || k == 28) ? 0u : (k - 4) >> 2; }
-DQ_AI uint32_t dbase(uint32_t d) {
-  const uint32_t dm = max(d, 2u);
-  const uint32_t b = ((2u + (dm & 1u)) << ((dm >> 1) - 1u)) + 1u;
-  return d < 2u ? d + 1u : b;
-}
-DQ_AI uint32_t dextra(uint32_t d) { return d < 4 ? 0u : (d - 2) >> 1; }
 
-// One full symbol: a literal (value in len), a match (len, dist) or EOB.  Straight-line: every
-// lane does the litlen and the distance lookup (a literal lane consumes no distance bits), so a
-// wave mixing literals and matches does not execute both paths one after the other.
+// One full symbol: a literal (value in len), a match (len, dist) or EOB (len = the bit after it).
+// Straight-line: every lane does the litlen and the distance lookup (a literal lane consumes no
+// distance bits), so a wave mixing literals and matches does not execute both paths one after the
+// other.  The table
+// entries carry the values (ent_ll / ent_d): a length is value + 3 + its extra bits, a distance
+// m << s + 1 + its extra bits, each extra field one bit-field extract.
 // Literal pairs: when the root index also holds a second whole literal (pair table) and the
-// boundary between the two lies before `lim` (the next bit position at which the caller looks at
+// boundary between them lies before `lim` (the next bit position at which the caller looks at
 // symbol boundaries: segment start/exit, checkpoint, end of data), both are taken at once and
 // `lit2` is the second (else 0xffffffff) -- the boundaries the caller sees are unchanged.
 DQ_AI int dsym(BitR& r, const uint32_t* __restrict__ W, const LdsI& L, uint32_t p, uint32_t lim,
@@ -232,28 +248,30 @@ DQ_AI int dsym(BitR& r, const uint32_t* __restrict__ W, const LdsI& L, uint32_t 
   const uint32_t ri = bb & ((1u << LR) - 1);
   uint32_t e = L.u.d.T[ri];
   const uint32_t pe = L.u.d.x.pair[ri];
-  if (e & (E_LINK | E_SLOW)) e = ll_second(L, e, bb);
-  const uint32_t nb = e & 15, sym = e >> 4;
-  const bool is_len = sym - 257u < 29u;
-  const uint32_t lk = min(sym - 257u, 28u);
-  const uint32_t lx = is_len ? lextra(lk) : 0u;
-  len = is_len ? lbase(lk) + ((bb >> nb) & ((1u << lx) - 1)) : sym;
+  if ((e & 15) == 0) e = ll_second(L, e, bb);
+  const uint32_t nb = e & 15;
+  const uint32_t lx = __builtin_amdgcn_ubfe(e, 5, 3);
+  const bool is_m = (e & 16) != 0;
+  len = (e >> 8) + (is_m ? 3u : 0u) + __builtin_amdgcn_ubfe(bb, nb, lx);
   const bool two = pe != 0 && p + nb < lim;  // pe != 0: the root entry is a literal
-  lit2 = two ? pe >> 4 : 0xffffffffu;
+  lit2 = two ? pe >> 8 : 0xffffffffu;
   br_take(r, nb + lx + (two ? (pe & 15) : 0u));
   br_refill(r, W);  // >= 33 bits: a distance code + its extra bits (<= 28)
   bb = (uint32_t)r.bb;
   uint32_t e2 = L.u.d.T[T_DROOT + (bb & ((1u << DR) - 1))];
-  if (is_len && (e2 & (E_LINK | E_SLOW))) e2 = d_second(L, e2, bb);
-  const uint32_t nb2 = e2 & 15, ds = e2 >> 4;
-  const uint32_t dd = min(ds, 29u);
-  const uint32_t dx = dextra(dd);
-  dist = dbase(dd) + ((bb >> nb2) & ((1u << dx) - 1));
-  br_take(r, is_len ? nb2 + dx : 0u);
-  if (nb == 0 || sym > 285) return S_ERR;
-  if (sym < 256) return S_LIT;
-  if (sym == 256) return S_EOB;
-  if (nb2 == 0 || ds >= 30) return S_ERR;
+  if (is_m && (e2 & 15) == 0) e2 = d_second(L, e2, bb);
+  const uint32_t nb2 = e2 & 15, dx = __builtin_amdgcn_ubfe(e2, 4, 4);
+  dist = (__builtin_amdgcn_ubfe(e2, 12, 2) << __builtin_amdgcn_ubfe(e2, 8, 4)) + 1u +
+         __builtin_amdgcn_ubfe(bb, nb2, dx);
+  br_take(r, is_m ? nb2 + dx : 0u);
+  const uint32_t kind = e & 0xfff0u;
+  if (nb == 0 || kind == (LL_BAD & 0xfff0u)) return S_ERR;
+  if (!is_m) return S_LIT;
+  if (kind == (LL_EOB & 0xfff0u)) {  // M entry: the distance bits taken above are not the
+    len = p + nb;                      // stream's, so the bit after EOB is returned in len
+    return S_EOB;
+  }
+  if (nb2 == 0 || (e2 & 0x4000u)) return S_ERR;
   return S_MATCH;
 }
 
@@ -298,7 +316,7 @@ DQ_AI int run_seg(const uint32_t* __restrict__ W, const LdsI& L, uint32_t start,
     const uint32_t lim = min(min(thr, counting ? sE : sB), endbits);
     const int k = dsym(r, W, L, p, lim, len, dist, lit2);
     if (k > S_MATCH) {
-      *Ep = (int32_t)(k == S_EOB ? br_pos(r) : p);
+      *Ep = (int32_t)(k == S_EOB ? len : p);
       f = !counting ? F_DEAD : (k == S_EOB ? F_EOB : F_ERR);
       break;
     }
@@ -345,7 +363,7 @@ DQ_AI int run_redo(const uint32_t* __restrict__ W, const LdsI& L, uint32_t s0, u
     uint32_t len = 0, dist = 0, lit2;
     const int k = dsym(r, W, L, p, min(min(thr, sE), endbits), len, dist, lit2);
     if (k > S_MATCH) {
-      *Ep = (int32_t)(k == S_EOB ? br_pos(r) : p);
+      *Ep = (int32_t)(k == S_EOB ? len : p);
       f = k == S_EOB ? F_EOB : F_ERR;
       break;
     }
@@ -379,7 +397,11 @@ DQ_AI void emit_seg(const uint32_t* __restrict__ W, LdsI& L, uint32_t start, uin
         return;
       }
       const uint32_t desc = (dist - 1) | ((len - 3) << 15);
-      volatile uint8_t* o = L.out + sh + p;  // byte stores: a merged unaligned b16 store stalls
+      // three ds_write_b8 (a merged unaligned b16 store stalls): volatile keeps them apart, the LDS
+      // address space keeps them DS stores (a generic volatile pointer became flat stores with a
+      // full vmcnt wait after each)
+      volatile __attribute__((address_space(3))) uint8_t* o =
+          (volatile __attribute__((address_space(3))) uint8_t*)(L.out + sh + p);
       o[0] = (uint8_t)desc;
       o[1] = (uint8_t)(desc >> 8);
       o[2] = (uint8_t)(desc >> 16);
@@ -515,7 +537,7 @@ DQ_AI void build_tables(LdsI& L, int nlen, int ndist) {
     q = H.offs[len] + rank;
     if (isl) L.u.d.lsym[q] = (uint16_t)sym;
     else L.u.d.dsym[q] = (uint8_t)sym;
-    const uint16_t ent = (uint16_t)((sym << 4) | len);
+    const uint16_t ent = isl ? ent_ll((uint32_t)sym, (uint32_t)len) : ent_d((uint32_t)sym, (uint32_t)len);
     if (len <= R) {
       const uint32_t rv = bitrev(code, len);
       uint16_t* root = L.u.d.T + (isl ? 0 : T_DROOT);
@@ -546,7 +568,7 @@ DQ_AI void build_tables(LdsI& L, int nlen, int ndist) {
       if (start) {
         const int R2 = isl ? LR : DR;
         const uint32_t ridx = bitrev(pf, R2) + (isl ? 0 : T_DROOT);
-        L.u.d.T[ridx] = slot < cap ? (uint16_t)(E_LINK | slot) : E_SLOW;
+        L.u.d.T[ridx] = slot < cap ? (uint16_t)(E_LINK | slot << 4) : E_SLOW;
       }
     }
   }
@@ -559,7 +581,7 @@ DQ_AI void build_tables(LdsI& L, int nlen, int ndist) {
       const int m = len - R;
       const uint32_t tail = bitrev(code & ((1u << m) - 1), m);
       uint16_t* sub = L.u.d.T + (isl ? T_LSUB : T_DSUB) + (slot << sb);
-      const uint16_t ent = (uint16_t)((sym << 4) | len);
+      const uint16_t ent = isl ? ent_ll((uint32_t)sym, (uint32_t)len) : ent_d((uint32_t)sym, (uint32_t)len);
       for (uint32_t k = 0; k < (1u << (sb - m)); k++) sub[tail | (k << m)] = ent;
     }
   }
@@ -830,10 +852,10 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       const uint32_t e1 = L.u.d.T[i];
       const uint32_t l1 = e1 & 15;
       uint16_t v = 0;
-      if (!(e1 & (E_LINK | E_SLOW)) && (e1 >> 4) < 256 && l1 > 0 && l1 < (uint32_t)LR) {
+      if (l1 > 0 && !(e1 & 16) && l1 < (uint32_t)LR) {  // a literal code
         const uint32_t e2 = L.u.d.T[(uint32_t)i >> l1];
         const uint32_t l2 = e2 & 15;
-        if (!(e2 & (E_LINK | E_SLOW)) && (e2 >> 4) < 256 && l2 > 0 && l1 + l2 <= (uint32_t)LR)
+        if (l2 > 0 && !(e2 & 16) && l1 + l2 <= (uint32_t)LR)
           v = (uint16_t)e2;
       }
       L.u.d.x.pair[i] = v;

@@ -709,50 +709,13 @@ __device__ inline uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t sh) {  // (
 constexpr int REC_WAVE = 64;
 constexpr int REC_STAGE = 24576;  // 64 short-read records (~21 KB); 6 waves per CU
 
-__device__ void decode_group(const uint8_t* __restrict__ U, int64_t ulen,
-                             const int64_t* __restrict__ rec_lin, int64_t nrec,
-                             const int64_t* __restrict__ blk_pos, const int64_t* __restrict__ uoff,
-                             int64_t nblk, const int32_t* __restrict__ pt, const RecSoA& soa,
-                             int32_t* d_status, int64_t i0, uint4* stage4) {
-  const int lane = threadIdx.x;
-  const int nact = (int)min((int64_t)REC_WAVE, nrec - i0);
-  const int64_t i = i0 + lane;
-  const bool act = lane < nact;
-  const int64_t p = act ? rec_lin[i] : rec_lin[i0];
-  // block_size of every record: two aligned dwords (U is padded by 256 zero bytes)
-  const uint32_t* U32 = reinterpret_cast<const uint32_t*>(U);
-  const int32_t bs = (int32_t)funnel(U32[p >> 2], U32[(p >> 2) + 1], (uint32_t)(p & 3));
-  const int64_t n = 4 + (int64_t)bs;
-  const bool bad = act && p + n > ulen;
-  if (__any(bad)) {
-    if (bad) *d_status = ST_SHORT;
-    return;
-  }
-  const int64_t first = rec_lin[i0];
-  const int64_t lastp = rec_lin[i0 + nact - 1];
-  const int32_t lastbs = (int32_t)funnel(U32[lastp >> 2], U32[(lastp >> 2) + 1], (uint32_t)(lastp & 3));
-  const int64_t base = first & ~(int64_t)15;
-  const int64_t len = lastp + 4 + (int64_t)lastbs - base;
-  const uint32_t* W;  // dword view of the record bytes
-  int64_t off;        // byte offset of this record in W
-  if (len + 32 <= REC_STAGE) {  // the hash reads up to 12 bytes past the last record
-    // LDS-DMA: every 16-byte piece in flight at once (a register-staged loop waits per piece)
-    const uint4* src = reinterpret_cast<const uint4*>(U + base);
-    const int npiece = (int)((len + 31) / 16);
-    for (int c0 = 0; c0 < npiece; c0 += REC_WAVE)
-      if (c0 + lane < npiece)
-        __builtin_amdgcn_global_load_lds(
-            static_cast<const void*>(src + c0 + lane),
-            (__attribute__((address_space(3))) void*)(stage4 + c0), 16, 0, 0);
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    W = reinterpret_cast<const uint32_t*>(stage4);
-    off = p - base;
-  } else {
-    W = U32;
-    off = p;
-  }
-  if (!act) return;
+// Lane work of decode_group: record i (start p, n = 4 + block_size bytes) read through W, a
+// dword view in which the record starts at byte `off` (LDS staging or U itself).
+template <typename WP>
+__device__ __attribute__((always_inline)) inline void decode_one(
+    WP W, int64_t off, int64_t p, int32_t bs, int64_t n, int64_t i,
+    const int64_t* __restrict__ blk_pos, const int64_t* __restrict__ uoff, int64_t nblk,
+    const int32_t* __restrict__ pt, const RecSoA& soa) {
   const int64_t wi0 = off >> 2;
   const uint32_t sh = (uint32_t)(off & 3);
   uint32_t f[10];
@@ -794,6 +757,49 @@ __device__ void decode_group(const uint8_t* __restrict__ U, int64_t ulen,
     wi += 2;
   }
   soa.hash[i] = dq_mix64(h);
+}
+
+__device__ void decode_group(const uint8_t* __restrict__ U, int64_t ulen,
+                             const int64_t* __restrict__ rec_lin, int64_t nrec,
+                             const int64_t* __restrict__ blk_pos, const int64_t* __restrict__ uoff,
+                             int64_t nblk, const int32_t* __restrict__ pt, const RecSoA& soa,
+                             int32_t* d_status, int64_t i0, uint4* stage4) {
+  const int lane = threadIdx.x;
+  const int nact = (int)min((int64_t)REC_WAVE, nrec - i0);
+  const int64_t i = i0 + lane;
+  const bool act = lane < nact;
+  const int64_t p = act ? rec_lin[i] : rec_lin[i0];
+  // block_size of every record: two aligned dwords (U is padded by 256 zero bytes)
+  const uint32_t* U32 = reinterpret_cast<const uint32_t*>(U);
+  const int32_t bs = (int32_t)funnel(U32[p >> 2], U32[(p >> 2) + 1], (uint32_t)(p & 3));
+  const int64_t n = 4 + (int64_t)bs;
+  const bool bad = act && p + n > ulen;
+  if (__any(bad)) {
+    if (bad) *d_status = ST_SHORT;
+    return;
+  }
+  const int64_t first = rec_lin[i0];
+  const int64_t lastp = rec_lin[i0 + nact - 1];
+  const int32_t lastbs = (int32_t)funnel(U32[lastp >> 2], U32[(lastp >> 2) + 1], (uint32_t)(lastp & 3));
+  const int64_t base = first & ~(int64_t)15;
+  const int64_t len = lastp + 4 + (int64_t)lastbs - base;
+  if (len + 32 <= REC_STAGE) {  // the hash reads up to 12 bytes past the last record
+    // LDS-DMA: every 16-byte piece in flight at once (a register-staged loop waits per piece)
+    const uint4* src = reinterpret_cast<const uint4*>(U + base);
+    const int npiece = (int)((len + 31) / 16);
+    for (int c0 = 0; c0 < npiece; c0 += REC_WAVE)
+      if (c0 + lane < npiece)
+        __builtin_amdgcn_global_load_lds(
+            static_cast<const void*>(src + c0 + lane),
+            (__attribute__((address_space(3))) void*)(stage4 + c0), 16, 0, 0);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (act)  // DS reads from the staging buffer (a pointer that may be either would be flat)
+      decode_one((const __attribute__((address_space(3))) uint32_t*)stage4, p - base, p, bs, n, i,
+                 blk_pos, uoff, nblk, pt, soa);
+  } else if (act) {
+    decode_one(U32, p, p, bs, n, i, blk_pos, uoff, nblk, pt, soa);
+  }
 }
 
 // Grid-stride over groups of 64 records: a few thousand resident waves, not one dispatch per group.
