@@ -75,8 +75,9 @@ constexpr uint16_t E_LINK = 0x0200;
 constexpr uint16_t E_SLOW = 0x0100;
 // Decoded litlen entry: code length (bits 0-3), M = length/EOB/invalid (bit 4), extra-bit count
 // (bits 5-7), value (bits 8-15): the literal byte or length base - 3.  EOB and the invalid symbols
-// 286/287 are M entries with 0 extra bits and values no length base has.
-constexpr uint32_t LL_EOB = 0xFE10, LL_BAD = 0xFD10;
+// 286/287 are M entries with 0 extra bits and values 248/249, which no length base has, so
+// (e & 0xFEF0) == 0xF810 finds both.
+constexpr uint32_t LL_EOB = 0xF810, LL_BAD = 0xF910;
 DQ_HD uint16_t ent_ll(uint32_t sym, uint32_t len) {
   if (sym < 256) return (uint16_t)(sym << 8 | len);
   if (sym == 256) return (uint16_t)(LL_EOB | len);
@@ -203,8 +204,6 @@ DQ_AI uint32_t peek_bits(const uint32_t* __restrict__ W, uint32_t pos, uint32_t 
   return (uint32_t)(v >> (pos & 31)) & ((1u << n) - 1);
 }
 
-enum : int { S_NONE = 0, S_LIT = 1, S_MATCH = 2, S_EOB = 3, S_ERR = 4 };
-
 // 3-byte match descriptor at image byte `a` via two aligned dword reads.
 DQ_AI uint32_t load_desc(const LdsI& L, int a) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(L.out + (a & ~3));
@@ -231,18 +230,19 @@ DQ_AI uint32_t d_second(const LdsI& L, uint32_t e, uint32_t bb) {
 }
 
 
-// One full symbol: a literal (value in len), a match (len, dist) or EOB (len = the bit after it).
-// Straight-line: every lane does the litlen and the distance lookup (a literal lane consumes no
-// distance bits), so a wave mixing literals and matches does not execute both paths one after the
-// other.  The table
-// entries carry the values (ent_ll / ent_d): a length is value + 3 + its extra bits, a distance
-// m << s + 1 + its extra bits, each extra field one bit-field extract.
+// One full symbol: a literal (value in len, is_m false) or a match (len, dist, is_m true); returns
+// true instead when the symbol ends the run: EOB (len = the bit after it) or an invalid code
+// (len = 0xffffffff).  Straight-line: every lane does the litlen and the distance lookup (a
+// literal lane consumes no distance bits), so a wave mixing literals and matches does not execute
+// both paths one after the other.  The table entries carry the values (ent_ll / ent_d): a length
+// is value + 3 + its extra bits, a distance m << s + 1 + its extra bits, each extra field one
+// bit-field extract.
 // Literal pairs: when the root index also holds a second whole literal (pair table) and the
 // boundary between them lies before `lim` (the next bit position at which the caller looks at
 // symbol boundaries: segment start/exit, checkpoint, end of data), both are taken at once and
 // `lit2` is the second (else 0xffffffff) -- the boundaries the caller sees are unchanged.
-DQ_AI int dsym(BitR& r, const uint32_t* __restrict__ W, const LdsI& L, uint32_t p, uint32_t lim,
-               uint32_t& len, uint32_t& dist, uint32_t& lit2) {
+DQ_AI bool dsym(BitR& r, const uint32_t* __restrict__ W, const LdsI& L, uint32_t p, uint32_t lim,
+                uint32_t& len, uint32_t& dist, uint32_t& lit2, bool& is_m) {
   br_refill(r, W);  // >= 33 bits: a litlen code + its extra bits (<= 20)
   uint32_t bb = (uint32_t)r.bb;
   const uint32_t ri = bb & ((1u << LR) - 1);
@@ -251,7 +251,7 @@ DQ_AI int dsym(BitR& r, const uint32_t* __restrict__ W, const LdsI& L, uint32_t 
   if ((e & 15) == 0) e = ll_second(L, e, bb);
   const uint32_t nb = e & 15;
   const uint32_t lx = __builtin_amdgcn_ubfe(e, 5, 3);
-  const bool is_m = (e & 16) != 0;
+  is_m = (e & 16) != 0;
   len = (e >> 8) + (is_m ? 3u : 0u) + __builtin_amdgcn_ubfe(bb, nb, lx);
   const bool two = pe != 0 && p + nb < lim;  // pe != 0: the root entry is a literal
   lit2 = two ? pe >> 8 : 0xffffffffu;
@@ -264,15 +264,12 @@ DQ_AI int dsym(BitR& r, const uint32_t* __restrict__ W, const LdsI& L, uint32_t 
   dist = (__builtin_amdgcn_ubfe(e2, 12, 2) << __builtin_amdgcn_ubfe(e2, 8, 4)) + 1u +
          __builtin_amdgcn_ubfe(bb, nb2, dx);
   br_take(r, is_m ? nb2 + dx : 0u);
-  const uint32_t kind = e & 0xfff0u;
-  if (nb == 0 || kind == (LL_BAD & 0xfff0u)) return S_ERR;
-  if (!is_m) return S_LIT;
-  if (kind == (LL_EOB & 0xfff0u)) {  // M entry: the distance bits taken above are not the
-    len = p + nb;                      // stream's, so the bit after EOB is returned in len
-    return S_EOB;
+  const bool stop = nb == 0 || (e & 0xFEF0u) == 0xF810u || (is_m && (nb2 == 0 || (e2 & 0x4000u)));
+  if (stop) {  // rare: EOB (an M entry, so the distance bits taken above are not the stream's)
+    const bool eob = nb != 0 && (e & 0xFFF0u) == LL_EOB;
+    len = eob ? p + nb : 0xffffffffu;
   }
-  if (nb2 == 0 || (e2 & 0x4000u)) return S_ERR;
-  return S_MATCH;
+  return stop;
 }
 
 enum : int32_t { F_DEAD = 4 };  // speculative path found no boundary >= sB (garbage)
@@ -292,35 +289,42 @@ DQ_AI int run_seg(const uint32_t* __restrict__ W, const LdsI& L, uint32_t start,
                   uint32_t* ck = nullptr, int ckstride = 0) {
   BitR r;
   br_init(r, W, start);
-  bool counting = false;
-  int32_t cnt = 0, B = -1;
+  uint32_t p = br_pos(r);
+  uint32_t len = 0, dist = 0, lit2;
+  bool m;
+  // warm-up: to the first symbol boundary >= sB, nothing counted
+  while (p < sB) {
+    if (p >= endbits || dsym(r, W, L, p, min(sB, endbits), len, dist, lit2, m)) {
+      *Ep = (int32_t)(p < endbits && len != 0xffffffffu ? len : p);
+      *Bp = -1;
+      *cntp = 0;
+      return F_DEAD;
+    }
+    p = br_pos(r);
+  }
+  const int32_t B = (int32_t)p;
+  int32_t cnt = 0;
   int f;
   uint32_t thr = ck ? sB + CKI : 0xffffffffu;
   int j = 0;
   for (;;) {
-    const uint32_t p = br_pos(r);
-    const bool nc = !counting && p >= sB;
-    B = nc ? (int32_t)p : B;
-    counting = counting || nc;
     if (p >= thr) {  // rare: a checkpoint
       ck[j * ckstride] = ((p - sB) << 16) | (uint32_t)cnt;
       j++;
       thr = j < NCK ? thr + CKI : 0xffffffffu;
     }
-    if ((counting && p >= sE) || p >= endbits) {
+    if (p >= sE || p >= endbits) {
       *Ep = (int32_t)p;
-      f = p >= sE && counting ? F_EXIT : (counting ? F_END : F_DEAD);
+      f = p >= sE ? F_EXIT : F_END;
       break;
     }
-    uint32_t len = 0, dist = 0, lit2;
-    const uint32_t lim = min(min(thr, counting ? sE : sB), endbits);
-    const int k = dsym(r, W, L, p, lim, len, dist, lit2);
-    if (k > S_MATCH) {
-      *Ep = (int32_t)(k == S_EOB ? len : p);
-      f = !counting ? F_DEAD : (k == S_EOB ? F_EOB : F_ERR);
+    if (dsym(r, W, L, p, min(min(thr, sE), endbits), len, dist, lit2, m)) {
+      *Ep = (int32_t)(len != 0xffffffffu ? len : p);
+      f = len != 0xffffffffu ? F_EOB : F_ERR;
       break;
     }
-    cnt += counting ? (k == S_MATCH ? (int32_t)len : (lit2 != 0xffffffffu ? 2 : 1)) : 0;
+    cnt += m ? (int32_t)len : (lit2 != 0xffffffffu ? 2 : 1);
+    p = br_pos(r);
   }
   *Bp = B;
   *cntp = cnt;
@@ -361,13 +365,13 @@ DQ_AI int run_redo(const uint32_t* __restrict__ W, const LdsI& L, uint32_t s0, u
       cur = j < NCK ? ck[j * ckstride] : 0xffffffffu;
     }
     uint32_t len = 0, dist = 0, lit2;
-    const int k = dsym(r, W, L, p, min(min(thr, sE), endbits), len, dist, lit2);
-    if (k > S_MATCH) {
-      *Ep = (int32_t)(k == S_EOB ? len : p);
-      f = k == S_EOB ? F_EOB : F_ERR;
+    bool m;
+    if (dsym(r, W, L, p, min(min(thr, sE), endbits), len, dist, lit2, m)) {
+      *Ep = (int32_t)(len != 0xffffffffu ? len : p);
+      f = len != 0xffffffffu ? F_EOB : F_ERR;
       break;
     }
-    cnt += k == S_MATCH ? (int32_t)len : (lit2 != 0xffffffffu ? 2 : 1);
+    cnt += m ? (int32_t)len : (lit2 != 0xffffffffu ? 2 : 1);
   }
   *cntp = cnt;
   return f;
@@ -383,15 +387,17 @@ DQ_AI void emit_seg(const uint32_t* __restrict__ W, LdsI& L, uint32_t start, uin
     const uint32_t q = br_pos(r);
     if (q >= target || q >= endbits || p >= isize) return;
     uint32_t len = 0, dist = 0, lit2;
-    const int k = dsym(r, W, L, q, min(target, endbits), len, dist, lit2);
-    if (k == S_LIT) {
+    bool m;
+    if (dsym(r, W, L, q, min(target, endbits), len, dist, lit2, m))
+      return;  // EOB / error: already accounted for by the rounds
+    if (!m) {
       L.out[sh + p] = (uint8_t)len;
       p++;
       if (lit2 != 0xffffffffu && p < isize) {
         L.out[sh + p] = (uint8_t)lit2;
         p++;
       }
-    } else if (k == S_MATCH) {
+    } else {
       if ((int32_t)dist > p) {
         set_err(L, ST_BAD_DIST);
         return;
@@ -407,8 +413,6 @@ DQ_AI void emit_seg(const uint32_t* __restrict__ W, LdsI& L, uint32_t start, uin
       o[2] = (uint8_t)(desc >> 16);
       atomicOr(&L.bm[p >> 5], 1u << (p & 31));
       p += (int32_t)len;
-    } else {
-      return;  // EOB / error: already accounted for by the rounds
     }
   }
 }
