@@ -207,8 +207,7 @@ DQ_AI uint32_t peek_bits(const uint32_t* __restrict__ W, uint32_t pos, uint32_t 
 // 3-byte match descriptor at image byte `a` via two aligned dword reads.
 DQ_AI uint32_t load_desc(const LdsI& L, int a) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(L.out + (a & ~3));
-  const uint64_t v = ((uint64_t)w[1] << 32) | w[0];
-  return (uint32_t)(v >> (8 * (a & 3))) & 0xffffffu;
+  return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)a & 3u) & 0xffffffu;
 }
 
 // Second-level / canonical lookup for a root entry flagged E_LINK or E_SLOW.
@@ -1106,11 +1105,15 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
         const uint32_t desc = before ? cdesc : (ms == msv[k * G + G - 1] ? db[k] : da[k]);
         const int32_t len = (int32_t)(desc >> 15) + 3, D = (int32_t)(desc & 0x7fff) + 1;
         const bool copy = x < isize && ms != 0xffff && (!before || ms == cms) && x < ms + len;
-        // src = ms - D + (x - ms) mod D; x - ms <= 257: a float reciprocal + one fix-up is exact
+        // src = ms - D + (x - ms) mod D; x - ms <= 257: a float reciprocal + one fix-up is exact,
+        // needed only by bytes past the first period of an overlapping match (skipped per wave)
         const int32_t jj = x - ms;
-        const int32_t q = (int32_t)((float)jj * __builtin_amdgcn_rcpf((float)D));
-        int32_t r = jj - q * D;
-        r = r >= D ? r - D : r;
+        int32_t r = jj;
+        if (__builtin_expect(__any(copy && jj >= D), 0)) {
+          const int32_t q = (int32_t)((float)jj * __builtin_amdgcn_rcpf((float)D));
+          r = jj - q * D;
+          r = r >= D ? r - D : r;
+        }
         const int32_t src = ms - D + r;
         const bool done = !copy || src < sbk;
         fr[e] = copy ? src : x;

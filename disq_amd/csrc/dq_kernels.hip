@@ -698,7 +698,7 @@ __global__ void block_pages_kernel(const int64_t* __restrict__ uoff, int64_t nbl
 }
 
 __device__ inline uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t sh) {  // (hi:lo) >> 8 sh
-  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * sh));
+  return __builtin_amdgcn_alignbyte(hi, lo, sh);
 }
 
 // One wave per 64 consecutive records (the chain is contiguous in U).  The wave first copies the
