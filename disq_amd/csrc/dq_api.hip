@@ -662,7 +662,7 @@ static int run_pipeline(dq_ctx* ctx) {
       for (int64_t i = 0; i < nblk; i++)
         for (int k = 0; k < 16; k++) acc[k] += (double)h[16 * (size_t)i + k];
       static const char* nm[16] = {"header", "tables", "spec", "rounds", "scan", "emit",
-                                   "resolve+store", "crc", "hdr_read_lengths", "resolve_hop_next", "redo_rounds", "-",
+                                   "resolve+store", "crc", "hdr_read_lengths", "resolve_hop_next", "redo_rounds", "tables_build",
                                    "resolve_steps_jumps", "resolve_store", "resolve_jump_tail", "res_batches"};
       fprintf(stderr, "[dq] inflate3 phase cycles per BGZF block (thread 0, s_memtime):");
       for (int k = 0; k < 16; k++)

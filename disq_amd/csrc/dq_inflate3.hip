@@ -847,6 +847,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     TST(0);
     // ---- 2. tables
     build_tables(L, nlen, ndist);
+    if (TIMING && t == 0) tacc[11] += __builtin_amdgcn_s_memtime() - tlast;  // without the pair table
     if (L.misc[M_ERR]) break;
     // pair table (the header scratch is dead): root index i whose literal leaves room for a
     // second whole literal code in the remaining root bits -- the root entry of i >> l1 (its
@@ -1128,20 +1129,23 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   // Every value read is a byte of the same chain, so no barrier orders the rounds and each read
   // advances at least one hop; it ends at a literal (nxt[p] == p) or a byte before the step.
   auto jump_round = [&](int32_t b0, int32_t* fr, int32_t* xs, uint32_t& pending) {
+    // branch-free over the entries: a final entry re-reads and re-writes its own next pointer,
+    // which holds its final source already
     int32_t qv[NE];
 #pragma unroll
-    for (int e = 0; e < NE; e++) qv[e] = ((pending >> e) & 1) ? (int32_t)nxt[xs[e] - b0] : 0;
+    for (int e = 0; e < NE; e++) {
+      const bool pd = (pending >> e) & 1;
+      qv[e] = (int32_t)nxt[pd ? xs[e] - b0 : (e / G) * CH + G * t + e % G];
+    }
 #pragma unroll
     for (int e = 0; e < NE; e++) {
-      if (!((pending >> e) & 1)) continue;
+      const bool pd = (pending >> e) & 1;
       const int32_t p = xs[e], q = qv[e];
       const int32_t sbk = b0 + (e / G) * CH + ((G * t) & ~511);
-      if (q == p || q < sbk) {
-        fr[e] = q;
-        pending &= ~(1u << e);
-      } else {
-        xs[e] = q;
-      }
+      const bool fin = pd && (q == p || q < sbk);
+      fr[e] = fin ? q : fr[e];
+      xs[e] = pd && !fin ? q : p;
+      pending &= fin ? ~(1u << e) : ~0u;
       nxt[(e / G) * CH + G * t + e % G] = (uint16_t)q;
     }
   };
@@ -1180,24 +1184,28 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     uint32_t pendB = 0;
     if (more) first_hop(nbs, ncms, ncdesc, frB, xsB, pendB);
     const uint64_t tb1 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
-    // (b) batch k's 512-byte steps in order: one LDS read + write per copied byte, one barrier
+    // (b) batch k's 512-byte steps in order: one LDS read + write per copied byte, one barrier.
+    //     A step's reads are issued before the next batch's jump round that follows the previous
+    //     barrier, so their latency overlaps it.
 #pragma unroll
     for (int k = 0; k < NB; k++) {
 #pragma unroll
       for (int j = 0; j < G; j++) {
-        if (((G * t) >> 9) == j) {
-          const int32_t g0 = bs + k * CH + G * t;
-          uint8_t v[G];
+        const bool mine = ((G * t) >> 9) == j;
+        const int32_t g0 = bs + k * CH + G * t;
+        uint8_t v[G];
+        if (mine)
 #pragma unroll
           for (int i = 0; i < G; i++) v[i] = O[min(frA[k * G + i], 65535)];
+        if ((k > 0 || j > 0) && pendB) jump_round(nbs, frB, xsB, pendB);
+        if (mine)
 #pragma unroll
           for (int i = 0; i < G; i++)
-            if (g0 + i < isize && frA[k * G + i] != g0 + i) L.out[sh + g0 + i] = v[i];
-        }
+            if (g0 + i < isize) L.out[sh + g0 + i] = v[i];  // a literal rewrites its own value
         __syncthreads();
-        if (pendB) jump_round(nbs, frB, xsB, pendB);
       }
     }
+    if (pendB) jump_round(nbs, frB, xsB, pendB);
     const uint64_t tb2 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
     // (c) store the 16-byte U lines this batch completed
     const int32_t c1 = min(isize, nbs);
