@@ -105,15 +105,17 @@ struct alignas(16) LdsI {
     struct {
       uint16_t T[T_END];
       HuffCanon hl, hd;           // canonical descriptions (E_SLOW fallback)
-      uint16_t lsym[288];
-      uint8_t dsym[32];
+      uint16_t lend[16], dend[16];  // left-aligned end of the length-l codes' root range (l <= R)
+      uint16_t lent[288];         // decoded table entry of canonical position q
+      uint16_t dent[32];
       union {
         uint16_t pair[1 << LR];   // decode: second literal of a root index (lit << 4 | len), 0 none
         struct {
           uint8_t lens[320];      // litlen lengths [0, 288), distance lengths [288, 320)
           uint8_t clen[20];
           uint16_t clt[128];      // code-length code: sym << 3 | len (len 0 = invalid)
-          int32_t cntw[8][16];    // per-wave counts of each code length
+          int32_t cntw[8];        // per-wave counts of second-level tables
+          uint32_t cntp[8][8];    // per-wave counts of each code length, 16 bits per length
           uint16_t pref[320];     // root prefix of each long code, by canonical position
           uint8_t slotq[320];     // second-level table of each long code, by canonical position
         } h;
@@ -217,7 +219,7 @@ DQ_AI uint32_t ll_second(const LdsI& L, uint32_t e, uint32_t bb) {
   if (!(e & E_SLOW)) return 0u;
   int l = 0;
   const int k = canon_decode(bb, L.u.d.hl, LR + 1, &l);
-  return k < 0 ? 0u : ent_ll(L.u.d.lsym[k], (uint32_t)l);
+  return k < 0 ? 0u : L.u.d.lent[k];
 }
 DQ_AI uint32_t d_second(const LdsI& L, uint32_t e, uint32_t bb) {
   if (e & E_LINK)
@@ -225,7 +227,7 @@ DQ_AI uint32_t d_second(const LdsI& L, uint32_t e, uint32_t bb) {
   if (!(e & E_SLOW)) return 0u;
   int l = 0;
   const int k = canon_decode(bb, L.u.d.hd, DR + 1, &l);
-  return k < 0 ? 0u : ent_d(L.u.d.dsym[k], (uint32_t)l);
+  return k < 0 ? 0u : L.u.d.dent[k];
 }
 
 
@@ -466,15 +468,15 @@ DQ_AI uint64_t lanes_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0u
 // longer than the root (q0) and of all codes (qn).  Returns 0, or ST_BAD_TABLE for an
 // over-subscribed or (except a single code) incomplete code.
 template <int W0, int NW, int R>
-DQ_AI int canon_from_counts(LdsI& L, HuffCanon& h, int32_t* q0p, int32_t* qnp) {
+DQ_AI int canon_from_counts(LdsI& L, HuffCanon& h, uint16_t* end, int32_t* q0p, int32_t* qnp) {
+  uint32_t pk[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // 16-bit lanes: no carries (<= 320 symbols)
+#pragma unroll
+  for (int w = W0; w < W0 + NW; w++)
+#pragma unroll
+    for (int j = 0; j < 8; j++) pk[j] += L.u.d.x.h.cntp[w][j];
   int cnt[16];
 #pragma unroll
-  for (int l = 1; l <= 15; l++) {
-    int c = 0;
-#pragma unroll
-    for (int w = W0; w < W0 + NW; w++) c += L.u.d.x.h.cntw[w][l];
-    cnt[l] = c;
-  }
+  for (int l = 1; l <= 15; l++) cnt[l] = (int)((pk[l >> 1] >> (16 * (l & 1))) & 0xffffu);
   int left = 1, maxl = 0, q0 = 0;
   uint32_t code = 0, off = 0;
   bool over = false;
@@ -490,6 +492,7 @@ DQ_AI int canon_from_counts(LdsI& L, HuffCanon& h, int32_t* q0p, int32_t* qnp) {
     h.first[l] = (uint16_t)code;
     h.count[l] = (uint16_t)c;
     h.offs[l] = (uint16_t)off;
+    if (l <= R) end[l] = (uint16_t)((code + (uint32_t)c) << (R - l));
     off += c;
     if (l == R) q0 = (int)off;
     code = (code + c) << 1;
@@ -501,31 +504,56 @@ DQ_AI int canon_from_counts(LdsI& L, HuffCanon& h, int32_t* q0p, int32_t* qnp) {
   return 0;
 }
 
+// Root table entry of bit-reversed (left-aligned) index r: the canonical ranges of lengths 1..R
+// are consecutive in left-aligned order, so the length is 1 + the number of range ends <= r and
+// the canonical position follows from the length's first code; 0 past the short codes (a long
+// code's prefix, linked below, or no code).
+template <int R>
+DQ_AI uint16_t root_entry(const LdsI& L, const HuffCanon& h, const uint16_t* end,
+                          const uint16_t* ent, uint32_t r) {
+  int l = 1;
+#pragma unroll
+  for (int k = 1; k <= R; k++) l += (uint32_t)end[k] <= r ? 1 : 0;
+  if (l > R) return 0;
+  const int q = (int)h.offs[l] + (int)(r >> (R - l)) - (int)h.first[l];
+  return ent[q];
+}
+
 // Build both decode tables from L.u.d.x.h.lens (all threads; barriers inside).
 // Litlen symbols are handled by threads 0..319 (waves 0-4), distance symbols by wave 5.
 DQ_AI void build_tables(LdsI& L, int nlen, int ndist) {
   const int t = tid_fresh(), lane = t & 63, wv = t >> 6;
-  for (int i = t; i < T_END; i += WG) L.u.d.T[i] = 0;
+  for (int i = T_LSUB + t; i < T_DROOT; i += WG) L.u.d.T[i] = 0;  // second-level tables (the
+  for (int i = T_DSUB + t; i < T_END; i += WG) L.u.d.T[i] = 0;    // roots are written whole)
   const bool isl = t < 320, isd = t >= 320 && t < 352;
   const int sym = isl ? t : t - 320;
   const int len = isl ? (sym < nlen ? L.u.d.x.h.lens[sym] : 0)
                       : (isd && sym < ndist ? L.u.d.x.h.lens[288 + sym] : 0);
-  // rank among equal lengths inside the wave
+  // rank among equal lengths inside the wave: a wave scan of one-hot length counters packed
+  // 8 bits per length in 4 registers (<= 64 per wave: no carries)
   int rank = 0;
   if (wv < 6) {
-    for (int l = 1; l <= 15; l++) {
-      const uint64_t m = __ballot(len == l);
-      if (len == l) rank = __popcll(m & lanes_below(lane));
-      if (lane == 0) L.u.d.x.h.cntw[wv][l] = __popcll(m);
-    }
+    uint32_t c[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      c[j] = (len >> 2) == j ? 1u << (8 * (len & 3)) : 0u;
+#pragma unroll
+    for (int j = 0; j < 4; j++) c[j] = (uint32_t)wave_incl_scan((int)c[j], lane);
+    const uint32_t mine = (len >> 2) == 0 ? c[0] : (len >> 2) == 1 ? c[1] : (len >> 2) == 2 ? c[2] : c[3];
+    rank = (int)((mine >> (8 * (len & 3))) & 0xffu) - 1;
+    if (lane == 63)
+#pragma unroll
+      for (int j = 0; j < 8; j++)  // widened to 16 bits per length for the cross-wave sums
+        L.u.d.x.h.cntp[wv][j] = ((c[j >> 1] >> (16 * (j & 1))) & 0xffu) |
+                                (((c[j >> 1] >> (16 * (j & 1) + 8)) & 0xffu) << 16);
   }
   __syncthreads();
   if (t == 0) {
-    const int e = canon_from_counts<0, 5, LR>(L, L.u.d.hl, &L.misc[M_LQ0], &L.misc[M_LQN]);
+    const int e = canon_from_counts<0, 5, LR>(L, L.u.d.hl, L.u.d.lend, &L.misc[M_LQ0], &L.misc[M_LQN]);
     if (e) set_err(L, e);
   }
   if (t == 320) {
-    const int e = canon_from_counts<5, 1, DR>(L, L.u.d.hd, &L.misc[M_DQ0], &L.misc[M_DQN]);
+    const int e = canon_from_counts<5, 1, DR>(L, L.u.d.hd, L.u.d.dend, &L.misc[M_DQ0], &L.misc[M_DQN]);
     if (e) set_err(L, e);
   }
   __syncthreads();
@@ -535,22 +563,23 @@ DQ_AI void build_tables(LdsI& L, int nlen, int ndist) {
   int q = -1;  // canonical position
   uint32_t code = 0;
   if (len) {
-    if (isl) for (int w = 0; w < wv; w++) rank += L.u.d.x.h.cntw[w][len];
+    if (isl)
+      for (int w = 0; w < wv; w++) rank += (int)((L.u.d.x.h.cntp[w][len >> 1] >> (16 * (len & 1))) & 0xffffu);
     code = H.first[len] + (uint32_t)rank;
     q = H.offs[len] + rank;
-    if (isl) L.u.d.lsym[q] = (uint16_t)sym;
-    else L.u.d.dsym[q] = (uint8_t)sym;
     const uint16_t ent = isl ? ent_ll((uint32_t)sym, (uint32_t)len) : ent_d((uint32_t)sym, (uint32_t)len);
-    if (len <= R) {
-      const uint32_t rv = bitrev(code, len);
-      uint16_t* root = L.u.d.T + (isl ? 0 : T_DROOT);
-      for (uint32_t k = 0; k < (1u << (R - len)); k++) root[rv | (k << len)] = ent;
-    } else {
-      L.u.d.x.h.pref[(isl ? 0 : 288) + q] = (uint16_t)(code >> (len - R));
-    }
+    if (isl) L.u.d.lent[q] = ent;
+    else L.u.d.dent[q] = ent;
+    if (len > R) L.u.d.x.h.pref[(isl ? 0 : 288) + q] = (uint16_t)(code >> (len - R));
   }
   __syncthreads();
-  // second-level tables: thread t handles canonical position t of each alphabet
+  // root tables, one entry per thread and index (no per-code replica loops)
+  L.u.d.T[t] = root_entry<LR>(L, L.u.d.hl, L.u.d.lend, L.u.d.lent, bitrev((uint32_t)t, LR));
+  L.u.d.T[t + WG] = root_entry<LR>(L, L.u.d.hl, L.u.d.lend, L.u.d.lent, bitrev((uint32_t)(t + WG), LR));
+  if (t < (1 << DR))
+    L.u.d.T[T_DROOT + t] = root_entry<DR>(L, L.u.d.hd, L.u.d.dend, L.u.d.dent, bitrev((uint32_t)t, DR));
+  // second-level tables: thread t handles canonical position t of each alphabet (the link
+  // entries are written after the barrier below, over the root entries above)
   {
     const int q0 = isl ? L.misc[M_LQ0] : L.misc[M_DQ0];
     const int qn = isl ? L.misc[M_LQN] : L.misc[M_DQN];
@@ -560,10 +589,10 @@ DQ_AI void build_tables(LdsI& L, int nlen, int ndist) {
     const bool start = lng && (sym == q0 || L.u.d.x.h.pref[base + sym - 1] != pf);
     const uint64_t sm = __ballot(start);
     int slot = __popcll(sm & lanes_below(lane)) + (start ? 1 : 0);  // inclusive
-    if (wv < 6 && lane == 0) L.u.d.x.h.cntw[wv][0] = __popcll(sm);
+    if (wv < 6 && lane == 0) L.u.d.x.h.cntw[wv] = __popcll(sm);
     __syncthreads();
     if (isl)
-      for (int w = 0; w < wv; w++) slot += L.u.d.x.h.cntw[w][0];
+      for (int w = 0; w < wv; w++) slot += L.u.d.x.h.cntw[w];
     slot -= 1;
     if (lng) {
       const int cap = isl ? LSLOTS : DSLOTS;
