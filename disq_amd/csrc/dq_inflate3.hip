@@ -622,6 +622,12 @@ DQ_AI void build_tables(LdsI& L, int nlen, int ndist) {
 
 // Dynamic header: decode the code-length sequence (wave 0) into L.u.d.x.h.lens.
 // Returns the bit position after the header, or sets M_ERR.
+// 128 bit offsets per step: lane l decodes the symbol at offsets l and 64 + l of the window
+// (entries e = l and 64 + l); the true path from entry 0 is found by pointer doubling over the
+// entries (successor^(2^b), b < 7, by lane shuffles of both halves), then entry k takes the k-th
+// symbol of the path; repeat values are forward-filled by max-scans and runs placed by sum-scans.
+// A 128-bit window holds ~30 code-length symbols: half the steps of a 64-bit window for two more
+// dependent shuffle levels.
 DQ_AI uint32_t read_lengths(const uint32_t* __restrict__ W, LdsI& L, uint32_t P, int nlen,
                                  int ndist, uint32_t endbits, uint32_t hbase, int& nit) {
   // the header's compressed words were staged in the (not yet built) decode table: HB_WORDS
@@ -631,6 +637,11 @@ DQ_AI uint32_t read_lengths(const uint32_t* __restrict__ W, LdsI& L, uint32_t P,
   const int lane = tid_fresh() & 63;
   const int total = nlen + ndist;
   int have = 0, prev = -1;
+  // successor^(2^b) of entry h * 64 + lane, 128 = past the window; a lookup of entry y
+  auto look = [&](int v0, int v1, int y) -> int {
+    const int a = __shfl(v0, y & 63, 64), c = __shfl(v1, y & 63, 64);
+    return y >= 128 ? 128 : (y >= 64 ? c : a);
+  };
   for (int iter = 0; iter < 400 && have < total; iter++) {
     nit++;
     if (P > endbits) {
@@ -638,68 +649,90 @@ DQ_AI uint32_t read_lengths(const uint32_t* __restrict__ W, LdsI& L, uint32_t P,
       return P;
     }
     const uint32_t wi = P >> 5, off = P & 31;
-    const uint64_t lo = ((uint64_t)word(wi + 1) << 32) | word(wi);
-    const uint64_t hi = ((uint64_t)word(wi + 3) << 32) | word(wi + 2);
-    const uint32_t o = off + (uint32_t)lane;  // <= 94
-    const uint64_t x = o < 64 ? ((lo >> o) | (o ? hi << (64 - o) : 0ull)) : (hi >> (o - 64));
-    const uint32_t bits = (uint32_t)x;
-    const uint32_t ent = L.u.d.x.h.clt[bits & 127];
-    const uint32_t cl = ent & 7, s = ent >> 3;
-    const uint32_t ex = s == 16 ? 2u : s == 17 ? 3u : s == 18 ? 7u : 0u;
-    const uint32_t xv = (bits >> cl) & ((1u << ex) - 1);
-    const int rep = s < 16 ? 1 : s == 16 ? 3 + (int)xv : s == 17 ? 3 + (int)xv : 11 + (int)xv;
-    const int adv = cl ? (int)(cl + ex) : 0;
-    // the true symbol path through this window, by pointer doubling: J_b = successor^(2^b)
-    // (lane + adv; an invalid code is a self-loop, leaving the window is 64), then lane k finds the
-    // k-th symbol of the path from lane 0 -- 11 lane shuffles instead of a serial readlane walk
-    int Jb[6];
-    Jb[0] = adv ? min(lane + adv, 64) : lane;
+    const uint32_t k0 = (off + (uint32_t)lane) >> 5, sh = (off + (uint32_t)lane) & 31;
+    uint32_t bits[2];
+    bits[0] = __builtin_amdgcn_alignbit(word(wi + k0 + 1), word(wi + k0), sh);
+    bits[1] = __builtin_amdgcn_alignbit(word(wi + k0 + 3), word(wi + k0 + 2), sh);
+    int s[2], rep[2], adv[2], J[7][2];
 #pragma unroll
-    for (int b = 1; b < 6; b++) {
-      const int y = __shfl(Jb[b - 1], min(Jb[b - 1], 63), 64);
-      Jb[b] = Jb[b - 1] >= 64 ? 64 : y;
+    for (int h = 0; h < 2; h++) {
+      const uint32_t ent = L.u.d.x.h.clt[bits[h] & 127];
+      const uint32_t cl = ent & 7, sy = ent >> 3;
+      const uint32_t ex = sy == 16 ? 2u : sy == 17 ? 3u : sy == 18 ? 7u : 0u;
+      const uint32_t xv = (bits[h] >> cl) & ((1u << ex) - 1);
+      s[h] = (int)sy;
+      rep[h] = sy < 16 ? 1 : sy == 16 ? 3 + (int)xv : sy == 17 ? 3 + (int)xv : 11 + (int)xv;
+      adv[h] = cl ? (int)(cl + ex) : 0;
+      const int e = lane + 64 * h;
+      J[0][h] = adv[h] ? min(e + adv[h], 128) : e;  // an invalid code is a self-loop
     }
-    int pk = 0;  // start lane of the lane-th symbol of the path
 #pragma unroll
-    for (int b = 0; b < 6; b++) {
-      const int y = __shfl(Jb[b], min(pk, 63), 64);
-      if ((lane >> b) & 1) pk = pk >= 64 ? 64 : y;
+    for (int b = 1; b < 7; b++)
+#pragma unroll
+      for (int h = 0; h < 2; h++) J[b][h] = look(J[b - 1][0], J[b - 1][1], J[b - 1][h]);
+    // entry k = h * 64 + lane takes the k-th symbol of the path from entry 0
+    uint32_t pm[4] = {0, 0, 0, 0};  // the path as a 128-bit mask
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int k = lane + 64 * h;
+      int pk = 0;
+#pragma unroll
+      for (int b = 0; b < 7; b++) {
+        const int y = look(J[b][0], J[b][1], pk);
+        if ((k >> b) & 1) pk = pk >= 128 ? 128 : y;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; q++) pm[q] |= (pk >> 5) == q ? 1u << (pk & 31) : 0u;
     }
-    const uint64_t pbit = pk < 64 ? 1ull << pk : 0ull;
-    const uint64_t path = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(wave_incl_or((int)(uint32_t)(pbit >> 32)), 63) << 32) |
-                          (uint32_t)__builtin_amdgcn_readlane(wave_incl_or((int)(uint32_t)pbit), 63);
+#pragma unroll
+    for (int q = 0; q < 4; q++) pm[q] = (uint32_t)__builtin_amdgcn_readlane(wave_incl_or((int)pm[q]), 63);
+    bool onp[2];
+    onp[0] = (lane < 32 ? pm[0] >> lane : pm[1] >> (lane - 32)) & 1;
+    onp[1] = (lane < 32 ? pm[2] >> lane : pm[3] >> (lane - 32)) & 1;
     // take path symbols while the lengths read so far are < total
-    const bool onp = (path >> lane) & 1;
-    const int rp = onp ? rep : 0;
-    const int rinc = wave_incl_scan(rp, lane);
-    const bool take = onp && have + rinc - rp < total;
-    const uint64_t mark = __ballot(take);
-    const int lastl = 63 - __clzll(mark);  // lane 0 is always taken (have < total)
-    const int cum = have + __builtin_amdgcn_readlane(rinc, lastl);
-    const int j = lastl + __builtin_amdgcn_readlane(adv, lastl);
-    if (__any(take && adv == 0) || cum > total) {
+    int rp[2], rinc[2];
+    rp[0] = onp[0] ? rep[0] : 0;
+    rp[1] = onp[1] ? rep[1] : 0;
+    rinc[0] = wave_incl_scan(rp[0], lane);
+    rinc[1] = wave_incl_scan(rp[1], lane) + __builtin_amdgcn_readlane(rinc[0], 63);
+    bool take[2];
+    take[0] = onp[0] && have + rinc[0] - rp[0] < total;
+    take[1] = onp[1] && have + rinc[1] - rp[1] < total;
+    const uint64_t mark0 = __ballot(take[0]), mark1 = __ballot(take[1]);
+    // entry 0 is always taken (have < total)
+    const int lastl = mark1 ? 64 + 63 - __clzll(mark1) : 63 - __clzll(mark0);
+    const int ll = lastl & 63;
+    const int cum = have + (lastl >= 64 ? __builtin_amdgcn_readlane(rinc[1], ll) : __builtin_amdgcn_readlane(rinc[0], ll));
+    const int j = lastl + (lastl >= 64 ? __builtin_amdgcn_readlane(adv[1], ll) : __builtin_amdgcn_readlane(adv[0], ll));
+    if (__any((take[0] && adv[0] == 0) || (take[1] && adv[1] == 0)) || cum > total) {
       set_err(L, ST_BAD_TABLE);
       return P;
     }
-    const bool on = (mark >> lane) & 1;
-    // value written by each symbol: 0-15 literal length, 17/18 zero, 16 the previous value
-    const int v0 = s < 16 ? (int)s : 0;
-    // a repeat (16) takes the value of the nearest on-path non-repeat symbol below it, else the
-    // last value of the previous window: forward fill by a max-scan of (lane + 1) << 5 | value
-    const int key = wave_incl_max(on && s != 16 ? ((lane + 1) << 5) | v0 : 0);
-    const int val = (on && s == 16) ? (key > 0 ? (key & 31) : prev) : v0;
-    if (__any(on && s == 16 && val < 0)) {
+    // value written by each symbol: 0-15 literal length, 17/18 zero, 16 the previous value; a
+    // repeat (16) takes the value of the nearest taken non-repeat symbol below it, else the last
+    // value of the previous window: forward fill by a max-scan of (entry + 1) << 5 | value
+    int val[2];
+    {
+      const int v00 = s[0] < 16 ? s[0] : 0, v01 = s[1] < 16 ? s[1] : 0;
+      const int key0 = wave_incl_max(take[0] && s[0] != 16 ? ((lane + 1) << 5) | v00 : 0);
+      const int key1 = max(wave_incl_max(take[1] && s[1] != 16 ? ((lane + 65) << 5) | v01 : 0),
+                           __builtin_amdgcn_readlane(key0, 63));
+      val[0] = (take[0] && s[0] == 16) ? (key0 > 0 ? (key0 & 31) : prev) : v00;
+      val[1] = (take[1] && s[1] == 16) ? (key1 > 0 ? (key1 & 31) : prev) : v01;
+    }
+    if (__any((take[0] && s[0] == 16 && val[0] < 0) || (take[1] && s[1] == 16 && val[1] < 0))) {
       set_err(L, ST_BAD_TABLE);
       return P;
     }
-    const int r = on ? rep : 0;
-    const int incl = rinc;  // taken lanes precede the untaken ones on the path
-    if (on && val != 0) {  // lens is zero-filled: zero runs (up to 138) need no stores
-      for (int i = have + incl - r; i < have + incl; i++)
-        L.u.d.x.h.lens[i < nlen ? i : 288 + i - nlen] = (uint8_t)val;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int r = take[h] ? rep[h] : 0;
+      if (take[h] && val[h] != 0) {  // lens is zero-filled: zero runs (up to 138) need no stores
+        for (int i = have + rinc[h] - r; i < have + rinc[h]; i++)
+          L.u.d.x.h.lens[i < nlen ? i : 288 + i - nlen] = (uint8_t)val[h];
+      }
     }
-    const int lastlane = 63 - __clzll(mark);
-    prev = __builtin_amdgcn_readlane(val, lastlane);
+    prev = lastl >= 64 ? __builtin_amdgcn_readlane(val[1], ll) : __builtin_amdgcn_readlane(val[0], ll);
     have = cum;
     P += (uint32_t)j;
   }
