@@ -141,7 +141,7 @@ __constant__ uint8_t c_clorder3[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 
 // misc slots
 enum { M_ERR = 0, M_BFINAL, M_BTYPE, M_POS, M_A, M_LAST, M_MORE, M_MORE1, M_STLEN, M_STSRC,
        M_CARRY_MS, M_CARRY_DESC, M_NLEN, M_NDIST, M_NCODE, M_LQ0, M_LQN, M_DQ0, M_DQN, M_NEXT,
-       M_LASTF };
+       M_LASTF, M_RCNT = 28 /* and 29: redo-list counters of even / odd rounds */ };
 
 __device__ __attribute__((always_inline)) inline void set_err(LdsI& L, int32_t code) { atomicCAS(&L.misc[M_ERR], 0, code); }
 
@@ -419,15 +419,12 @@ DQ_AI void emit_seg(const uint32_t* __restrict__ W, LdsI& L, uint32_t start, uin
 }
 
 __device__ inline uint32_t gf2_mulmod(uint32_t a, uint32_t b) {  // reflected, poly 0xEDB88320
-  uint32_t m = 1u << 31, p = 0;
-  if (a == 0) return 0;
-  for (;;) {
-    if (a & m) {
-      p ^= b;
-      if ((a & (m - 1)) == 0) break;
-    }
-    m >>= 1;
-    b = b & 1 ? (b >> 1) ^ 0xEDB88320u : b >> 1;
+  // branch-free: every lane holds its own constant a, so a data-dependent loop only diverges
+  uint32_t p = 0;
+#pragma unroll
+  for (int i = 31; i >= 0; i--) {
+    p ^= ((a >> i) & 1u) ? b : 0u;
+    b = (b >> 1) ^ ((b & 1u) ? 0xEDB88320u : 0u);
   }
   return p;
 }
@@ -962,6 +959,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     if (cap >= 8) CK = reinterpret_cast<uint32_t*>(SC + nl);
     const uint32_t seg = (span + nl - 1) / nl;
     // ---- 3. speculative pass: from OV bits before the segment, counting from its first boundary
+    if (t == 0) L.misc[M_RCNT] = 0;  // round 0's redo-list counter (published by the barrier below)
     if (t < nl) {
       const uint32_t sB = a + (uint32_t)t * seg;
       const uint32_t start = t == 0 ? a : (sB > a + OV ? sB - OV : a);
@@ -979,7 +977,8 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     __syncthreads();
     TST(2);
     // ---- 4. rounds: lanes whose first boundary differs from the predecessor's exit re-decode
-    //      from that exit (compacted onto the first threads); repeat until consistent
+    //      from that exit (compacted onto the first threads by an LDS counter, one barrier per
+    //      round besides the re-decode's); repeat until consistent
     for (int round = 0; round <= nl; round++) {
       bool need = false;
       int32_t st = 0;
@@ -988,21 +987,15 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
         st = pe >> 3;
         need = (pe & 7) == F_EXIT && AB[t] != st;
       }
-      const uint64_t nm = __ballot(need);
-      if (lane == 0) L.wsum[wv] = __popcll(nm);
-      __syncthreads();
-      int off = 0, nneed = 0;
-      for (int w = 0; w < WG / 64; w++) {
-        const int c = L.wsum[w];
-        off += w < wv ? c : 0;
-        nneed += c;
-      }
+      int32_t* rc = &L.misc[M_RCNT + (round & 1)];
       if (need) {
-        const int r = off + __popcll(nm & lanes_below(lane));
+        const int r = atomicAdd(rc, 1);
         LS[r] = t;
         ST[r] = st;
       }
+      if (t == 0) L.misc[M_RCNT + ((round + 1) & 1)] = 0;  // the next round's counter
       __syncthreads();
+      const int nneed = *rc;
       if (nneed == 0) break;
       TCOUNT(10);
       const bool hi = __builtin_amdgcn_readfirstlane(t) < __builtin_amdgcn_readfirstlane(nneed);  // the few waves re-decoding
