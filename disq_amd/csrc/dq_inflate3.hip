@@ -139,8 +139,8 @@ __constant__ uint32_t c_slice_shift[WG];  // x^(8 * 128 * k) mod P, k = 0..511
 __constant__ uint8_t c_clorder3[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 // misc slots
-enum { M_ERR = 0, M_BFINAL, M_BTYPE, M_POS, M_A, M_LAST, M_MORE, M_MORE1, M_STLEN, M_STSRC,
-       M_CARRY_MS, M_CARRY_DESC, M_NLEN, M_NDIST, M_NCODE, M_LQ0, M_LQN, M_DQ0, M_DQN, M_NEXT,
+enum { M_ERR = 0, M_A = 4, M_LAST, M_MORE, M_MORE1,
+       M_CARRY_MS = 10, M_CARRY_DESC, M_LQ0 = 15, M_LQN, M_DQ0, M_DQN, M_NEXT,
        M_LASTF, M_RCNT = 28 /* and 29: redo-list counters of even / odd rounds */ };
 
 __device__ __attribute__((always_inline)) inline void set_err(LdsI& L, int32_t code) { atomicCAS(&L.misc[M_ERR], 0, code); }
@@ -782,67 +782,51 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   if (t == 0) {
     if (isize < 0 || isize > 65536) L.misc[M_ERR] = ST_ISIZE;
     else if (dbytes < 0) L.misc[M_ERR] = ST_OVERREAD;
-    L.misc[M_POS] = (int32_t)a0;
   }
   __syncthreads();
   int32_t produced = 0;
+  uint32_t pos = a0;  // bit position of the next deflate block's header
   while (L.misc[M_ERR] == 0 && produced < isize) {
     const int t = tid_fresh(), lane = t & 63, wv = t >> 6;
-    // ---- 1. block header
-    if (t == 0) {
-      const uint32_t pos = (uint32_t)L.misc[M_POS];
-      const uint32_t h = peek_bits(W, pos, 17);
-      const int32_t bfinal = (int32_t)(h & 1), btype = (int32_t)((h >> 1) & 3);
-      L.misc[M_BFINAL] = bfinal;
-      L.misc[M_BTYPE] = btype;
-      if (pos + 3 > endbits) {
-        L.misc[M_ERR] = ST_OVERREAD;
-      } else if (btype == 0) {
-        const uint32_t q = (pos + 3 + 7) & ~7u;  // byte boundary
-        const uint8_t* bp = reinterpret_cast<const uint8_t*>(W) + q / 8;
-        const uint32_t len = bp[0] | ((uint32_t)bp[1] << 8), nlen = bp[2] | ((uint32_t)bp[3] << 8);
-        if ((len ^ 0xffffu) != nlen) L.misc[M_ERR] = ST_BAD_STORED;
-        else if (q + 32 + 8 * len > endbits) L.misc[M_ERR] = ST_OVERREAD;
-        L.misc[M_STLEN] = (int32_t)len;
-        L.misc[M_STSRC] = (int32_t)(q / 8 + 4);
-        L.misc[M_POS] = (int32_t)(q + 32 + 8 * len);
-      } else if (btype == 3) {
-        L.misc[M_ERR] = ST_BAD_BLOCKTYPE;
-      } else if (btype == 1) {
-        L.misc[M_NLEN] = 288;
-        L.misc[M_NDIST] = 32;
-        L.misc[M_A] = (int32_t)(pos + 3);
-      } else {
-        const int nlen = (int)((h >> 3) & 31) + 257, ndist = (int)((h >> 8) & 31) + 1;
-        const int ncode = (int)((h >> 13) & 15) + 4;
-        if (nlen > 286 || ndist > 30) L.misc[M_ERR] = ST_BAD_TABLE;
-        L.misc[M_NLEN] = nlen;
-        L.misc[M_NDIST] = ndist;
-        L.misc[M_NCODE] = ncode;
-        L.misc[M_A] = (int32_t)(pos + 17);  // code-length code lengths
-      }
+    // ---- 1. block header: every thread reads it (the branches below are uniform, no barrier)
+    const uint32_t h = peek_bits(W, pos, 17);
+    const int32_t bfinal = (int32_t)(h & 1), btype = (int32_t)((h >> 1) & 3);
+    const int32_t herr = pos + 3 > endbits ? ST_OVERREAD : btype == 3 ? ST_BAD_BLOCKTYPE : 0;
+    if (herr) {
+      if (t == 0) L.misc[M_ERR] = herr;
+      break;
     }
-    __syncthreads();
-    if (L.misc[M_ERR]) break;
-    const int btype = L.misc[M_BTYPE];
     if (btype == 0) {  // stored block: copy
-      const int32_t len = L.misc[M_STLEN], src = L.misc[M_STSRC];
-      const uint8_t* sp = reinterpret_cast<const uint8_t*>(W) + src;
-      const int32_t n = min(len, isize - produced);
+      const uint32_t q = (pos + 3 + 7) & ~7u;  // byte boundary
+      const uint8_t* bp = reinterpret_cast<const uint8_t*>(W) + q / 8;
+      const uint32_t len = bp[0] | ((uint32_t)bp[1] << 8), nl = bp[2] | ((uint32_t)bp[3] << 8);
+      const int32_t serr = (len ^ 0xffffu) != nl ? ST_BAD_STORED : q + 32 + 8 * len > endbits ? ST_OVERREAD : 0;
+      if (serr) {
+        if (t == 0) L.misc[M_ERR] = serr;
+        break;
+      }
+      const uint8_t* sp = bp + 4;
+      const int32_t n = min((int32_t)len, isize - produced);
       for (int i = t; i < n; i += WG) L.out[sh + produced + i] = sp[i];
       produced += n;
-      const int32_t fin = L.misc[M_BFINAL];
+      pos = q + 32 + 8 * len;
       __syncthreads();
-      if (fin) break;
+      if (bfinal) break;
       continue;
     }
-    const int nlen = L.misc[M_NLEN], ndist = L.misc[M_NDIST];
+    const int nlen = btype == 1 ? 288 : (int)((h >> 3) & 31) + 257;
+    const int ndist = btype == 1 ? 32 : (int)((h >> 8) & 31) + 1;
+    if (btype == 2 && (nlen > 286 || ndist > 30)) {
+      if (t == 0) L.misc[M_ERR] = ST_BAD_TABLE;
+      break;
+    }
     if (btype == 1) {
       for (int i = t; i < 320; i += WG) L.u.d.x.h.lens[i] = fixed_len(i);
+      if (t == 0) L.misc[M_A] = (int32_t)(pos + 3);
       __syncthreads();
     } else {
-      const int ncode = L.misc[M_NCODE];
-      const uint32_t clpos = (uint32_t)L.misc[M_A];
+      const int ncode = (int)((h >> 13) & 15) + 4;
+      const uint32_t clpos = pos + 17;  // code-length code lengths
       for (int i = t; i < 320; i += WG) L.u.d.x.h.lens[i] = 0;
       const uint32_t hbase = clpos >> 5;
       if (t < HB_WORDS) reinterpret_cast<uint32_t*>(L.u.d.T)[t] = W[hbase + t];
@@ -895,11 +879,11 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
         const uint32_t a = read_lengths(W, L, clpos + 3 * (uint32_t)ncode, nlen, ndist, endbits, hbase, nit);
         (void)nit;
         if (t == 0) L.misc[M_A] = (int32_t)a;
+        // the wave that wrote the lengths checks for an EOB code (its own stores are ordered)
+        if (t == 0 && L.misc[M_ERR] == 0 && L.u.d.x.h.lens[256] == 0) set_err(L, ST_BAD_TABLE);
         if (TIMING && t == 0) tacc[8] += __builtin_amdgcn_s_memtime() - tr0;
         if (__builtin_amdgcn_readfirstlane(t) < 64) __builtin_amdgcn_s_setprio(0);
       }
-      __syncthreads();
-      if (t == 0 && L.misc[M_ERR] == 0 && L.u.d.x.h.lens[256] == 0) set_err(L, ST_BAD_TABLE);
       __syncthreads();
       if (L.misc[M_ERR]) break;
     }
@@ -1067,13 +1051,11 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       emit_seg(W, L, (uint32_t)myB, sE, endbits, myoff, isize, sh);
     }
     const int32_t nextpos = L.misc[M_NEXT];
-    const int32_t fin = L.misc[M_BFINAL];
     __syncthreads();
     TST(5);
     produced = min(isize, produced + total);
-    if (full || fin) break;
-    if (t == 0) L.misc[M_POS] = nextpos;
-    __syncthreads();
+    if (full || bfinal) break;
+    pos = (uint32_t)nextpos;
   }
   __syncthreads();
   int32_t err = L.misc[M_ERR];
