@@ -943,7 +943,10 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     if (cap >= 8) CK = reinterpret_cast<uint32_t*>(SC + nl);
     const uint32_t seg = (span + nl - 1) / nl;
     // ---- 3. speculative pass: from OV bits before the segment, counting from its first boundary
-    if (t == 0) L.misc[M_RCNT] = 0;  // round 0's redo-list counter (published by the barrier below)
+    if (t == 0) {  // published by the barrier below
+      L.misc[M_RCNT] = 0;       // round 0's redo-list counter
+      L.misc[M_LAST] = nl - 1;  // the first lane that does not exit normally (atomicMin)
+    }
     if (t < nl) {
       const uint32_t sB = a + (uint32_t)t * seg;
       const uint32_t start = t == 0 ? a : (sB > a + OV ? sB - OV : a);
@@ -1020,9 +1023,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       myF = AE[t] & 7;
       myC = AC[t];
     }
-    if (t == 0) L.misc[M_LAST] = nl - 1;
-    __syncthreads();
-    if (t < nl && myF != F_EXIT) atomicMin(&L.misc[M_LAST], t);
+    if (t < nl && myF != F_EXIT) atomicMin(&L.misc[M_LAST], t);  // initialised with the spec pass
     __syncthreads();
     const int last = L.misc[M_LAST];
     const int32_t cv = t <= last ? myC : 0;
