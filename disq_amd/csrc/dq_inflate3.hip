@@ -926,7 +926,10 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     int32_t* SE;  // speculative exit << 3 | flag
     int32_t* SC;  // speculative byte count
     uint32_t* CK = nullptr;  // checkpoints, [j * nl + lane]
-    int nl = (int)max(1u, min((uint32_t)NDEC, span / 128u));
+    // lanes: one per >= 128 bits, at most NDEC (tuning: sflags bits 8-17 cap the lanes, bits
+    // 20-29 set the minimum segment bits)
+    const uint32_t maxl = (sflags >> 8) & 1023u, minseg = (sflags >> 20) & 1023u;
+    int nl = (int)max(1u, min(maxl ? maxl : (uint32_t)NDEC, span / (minseg ? minseg : 128u)));
     if (cap >= 8) {
       nl = min(nl, cap);
       AB = reinterpret_cast<int32_t*>(L.out + ob);
@@ -1403,7 +1406,10 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
   const int64_t ngrid = sel ? nsel : nblk;
   if (ngrid <= 0) return;
   static const uint32_t ov = getenv("DQ_OV") ? (uint32_t)atoi(getenv("DQ_OV")) : OV_DEFAULT;
-  static const uint32_t sflags = getenv("DQ_STORE") ? (uint32_t)atoi(getenv("DQ_STORE")) : 2;
+  static const uint32_t sflags =
+      (getenv("DQ_STORE") ? (uint32_t)atoi(getenv("DQ_STORE")) : 2u) |
+      (getenv("DQ_NDEC") ? (uint32_t)(atoi(getenv("DQ_NDEC")) & 1023) << 8 : 0u) |
+      (getenv("DQ_SEGBITS") ? (uint32_t)(atoi(getenv("DQ_SEGBITS")) & 1023) << 20 : 0u);
   static int cfg = -1;
   if (cfg < 0) {  // DQ_CFG="nb,g" (tuning experiments: 4,1 default, 2,1 or 1,4)
     int nb = 4, g = 1;
