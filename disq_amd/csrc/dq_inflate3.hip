@@ -788,7 +788,14 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   uint32_t pos = a0;  // bit position of the next deflate block's header
   while (L.misc[M_ERR] == 0 && produced < isize) {
     const int t = tid_fresh(), lane = t & 63, wv = t >> 6;
-    // ---- 1. block header: every thread reads it (the branches below are uniform, no barrier)
+    // ---- 1. block header: every thread reads it (the branches below are uniform, no barrier).
+    //      The dynamic header's staged words and code-length code lengths are loaded with it
+    //      (their position follows from pos alone; C is padded, so a stored or fixed block near
+    //      the end reads pad bytes it never uses).
+    const uint32_t clpos = pos + 17;
+    const uint32_t hbase = clpos >> 5;
+    const uint32_t hw = t < HB_WORDS ? W[hbase + t] : 0u;
+    const uint32_t hcl = t < 19 ? peek_bits(W, clpos + 3 * t, 3) : 0u;
     const uint32_t h = peek_bits(W, pos, 17);
     const int32_t bfinal = (int32_t)(h & 1), btype = (int32_t)((h >> 1) & 3);
     const int32_t herr = pos + 3 > endbits ? ST_OVERREAD : btype == 3 ? ST_BAD_BLOCKTYPE : 0;
@@ -826,11 +833,9 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       __syncthreads();
     } else {
       const int ncode = (int)((h >> 13) & 15) + 4;
-      const uint32_t clpos = pos + 17;  // code-length code lengths
       for (int i = t; i < 320; i += WG) L.u.d.x.h.lens[i] = 0;
-      const uint32_t hbase = clpos >> 5;
-      if (t < HB_WORDS) reinterpret_cast<uint32_t*>(L.u.d.T)[t] = W[hbase + t];
-      if (t < 19) L.u.d.x.h.clen[c_clorder3[t]] = t < ncode ? (uint8_t)peek_bits(W, clpos + 3 * t, 3) : 0;
+      if (t < HB_WORDS) reinterpret_cast<uint32_t*>(L.u.d.T)[t] = hw;
+      if (t < 19) L.u.d.x.h.clen[c_clorder3[t]] = t < ncode ? (uint8_t)hcl : 0;
       __syncthreads();
       // code-length code: 7-bit table, one entry per thread (canonical decode over 19 lengths)
       if (t < 128) {

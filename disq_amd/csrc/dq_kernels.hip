@@ -706,57 +706,59 @@ __device__ inline uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t sh) {  // (
 // into the SoA, the htsjdk start pointer (block via the page table) and the raw-byte hash
 // (8-byte little-endian words, zero padded; DESIGN.md section "hash") from LDS.  Runs of records
 // longer than the staging buffer (long reads) are read straight from U.
-constexpr int REC_WAVE = 64;
-constexpr int REC_STAGE = 24576;  // 64 short-read records (~21 KB); 6 waves per CU
+constexpr int REC_WAVE = 64;      // threads per workgroup (one wave)
+constexpr int REC_GROUP = 32;     // records per group: two lanes per record split its hash words
+constexpr int REC_STAGE = 12288;  // 32 short-read records (~10.5 KB): 13 waves per CU
 
 // Lane work of decode_group: record i (start p, n = 4 + block_size bytes) read through W, a
-// dword view in which the record starts at byte `off` (LDS staging or U itself).
+// dword view in which the record starts at byte `off` (LDS staging or U itself).  Lane half 0
+// decodes the fixed fields; both halves hash the record's 8-byte words of their parity (the word
+// sum is order-free) and return the partial sum.
 template <typename WP>
-__device__ __attribute__((always_inline)) inline void decode_one(
-    WP W, int64_t off, int64_t p, int32_t bs, int64_t n, int64_t i,
+__device__ __attribute__((always_inline)) inline uint64_t decode_one(
+    WP W, int64_t off, int64_t p, int32_t bs, int64_t n, int64_t i, int half,
     const int64_t* __restrict__ blk_pos, const int64_t* __restrict__ uoff, int64_t nblk,
     const int32_t* __restrict__ pt, const RecSoA& soa) {
   const int64_t wi0 = off >> 2;
   const uint32_t sh = (uint32_t)(off & 3);
-  uint32_t f[10];
-  {
-    uint32_t w[10];
+  if (half == 0) {
+    uint32_t f[10];
+    {
+      uint32_t w[10];
 #pragma unroll
-    for (int k = 0; k < 10; k++) w[k] = W[wi0 + k];
+      for (int k = 0; k < 10; k++) w[k] = W[wi0 + k];
 #pragma unroll
-    for (int k = 0; k < 9; k++) f[k] = funnel(w[k], w[k + 1], sh);
+      for (int k = 0; k < 9; k++) f[k] = funnel(w[k], w[k + 1], sh);
+    }
+    soa.block_size[i] = bs;
+    soa.ref_id[i] = (int32_t)f[1];
+    soa.pos[i] = (int32_t)f[2];
+    soa.l_read_name[i] = (uint8_t)(f[3] & 0xff);
+    soa.mapq[i] = (uint8_t)((f[3] >> 8) & 0xff);
+    soa.bin[i] = (uint16_t)(f[3] >> 16);
+    soa.n_cigar[i] = (uint16_t)(f[4] & 0xffff);
+    soa.flag[i] = (uint16_t)(f[4] >> 16);
+    soa.l_seq[i] = (int32_t)f[5];
+    soa.next_ref_id[i] = (int32_t)f[6];
+    soa.next_pos[i] = (int32_t)f[7];
+    soa.tlen[i] = (int32_t)f[8];
+    int64_t j = pt[p >> 16];
+    while (j + 1 < nblk && uoff[j + 1] <= p) j++;
+    soa.voffset[i] = ((uint64_t)blk_pos[j] << 16) | (uint64_t)(p - uoff[j]);
   }
-  soa.block_size[i] = bs;
-  soa.ref_id[i] = (int32_t)f[1];
-  soa.pos[i] = (int32_t)f[2];
-  soa.l_read_name[i] = (uint8_t)(f[3] & 0xff);
-  soa.mapq[i] = (uint8_t)((f[3] >> 8) & 0xff);
-  soa.bin[i] = (uint16_t)(f[3] >> 16);
-  soa.n_cigar[i] = (uint16_t)(f[4] & 0xffff);
-  soa.flag[i] = (uint16_t)(f[4] >> 16);
-  soa.l_seq[i] = (int32_t)f[5];
-  soa.next_ref_id[i] = (int32_t)f[6];
-  soa.next_pos[i] = (int32_t)f[7];
-  soa.tlen[i] = (int32_t)f[8];
-  int64_t j = pt[p >> 16];
-  while (j + 1 < nblk && uoff[j + 1] <= p) j++;
-  soa.voffset[i] = ((uint64_t)blk_pos[j] << 16) | (uint64_t)(p - uoff[j]);
-  // hash
-  uint64_t h = (uint64_t)n * DQ_K_LEN;
+  // hash words k = half, half + 2, ...
+  uint64_t part = 0;
   const int64_t nw = (n + 7) / 8;
-  int64_t wi = wi0;
-  uint32_t w0 = W[wi];
-  for (int64_t k = 0; k < nw; k++) {
-    const uint32_t w1 = W[wi + 1], w2 = W[wi + 2];
+  for (int64_t k = half; k < nw; k += 2) {
+    const int64_t wi = wi0 + 2 * k;
+    const uint32_t w0 = W[wi], w1 = W[wi + 1], w2 = W[wi + 2];
     const uint32_t lo = funnel(w0, w1, sh), hi = funnel(w1, w2, sh);
     uint64_t w = ((uint64_t)hi << 32) | lo;
     const int64_t rem = n - 8 * k;
     if (rem < 8) w &= (1ull << (8 * rem)) - 1;
-    h += dq_mix64(w ^ ((uint64_t)(k + 1) * DQ_K_WORD));
-    w0 = w2;
-    wi += 2;
+    part += dq_mix64(w ^ ((uint64_t)(k + 1) * DQ_K_WORD));
   }
-  soa.hash[i] = dq_mix64(h);
+  return part;
 }
 
 __device__ void decode_group(const uint8_t* __restrict__ U, int64_t ulen,
@@ -764,10 +766,10 @@ __device__ void decode_group(const uint8_t* __restrict__ U, int64_t ulen,
                              const int64_t* __restrict__ blk_pos, const int64_t* __restrict__ uoff,
                              int64_t nblk, const int32_t* __restrict__ pt, const RecSoA& soa,
                              int32_t* d_status, int64_t i0, uint4* stage4) {
-  const int lane = threadIdx.x;
-  const int nact = (int)min((int64_t)REC_WAVE, nrec - i0);
-  const int64_t i = i0 + lane;
-  const bool act = lane < nact;
+  const int lane = threadIdx.x, r = lane & (REC_GROUP - 1), half = lane / REC_GROUP;
+  const int nact = (int)min((int64_t)REC_GROUP, nrec - i0);
+  const int64_t i = i0 + r;
+  const bool act = r < nact;
   const int64_t p = act ? rec_lin[i] : rec_lin[i0];
   // block_size of every record: two aligned dwords (U is padded by 256 zero bytes)
   const uint32_t* U32 = reinterpret_cast<const uint32_t*>(U);
@@ -783,6 +785,7 @@ __device__ void decode_group(const uint8_t* __restrict__ U, int64_t ulen,
   const int32_t lastbs = (int32_t)funnel(U32[lastp >> 2], U32[(lastp >> 2) + 1], (uint32_t)(lastp & 3));
   const int64_t base = first & ~(int64_t)15;
   const int64_t len = lastp + 4 + (int64_t)lastbs - base;
+  uint64_t part = 0;
   if (len + 32 <= REC_STAGE) {  // the hash reads up to 12 bytes past the last record
     // LDS-DMA: every 16-byte piece in flight at once (a register-staged loop waits per piece)
     const uint4* src = reinterpret_cast<const uint4*>(U + base);
@@ -795,21 +798,26 @@ __device__ void decode_group(const uint8_t* __restrict__ U, int64_t ulen,
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     if (act)  // DS reads from the staging buffer (a pointer that may be either would be flat)
-      decode_one((const __attribute__((address_space(3))) uint32_t*)stage4, p - base, p, bs, n, i,
-                 blk_pos, uoff, nblk, pt, soa);
+      part = decode_one((const __attribute__((address_space(3))) uint32_t*)stage4, p - base, p, bs,
+                        n, i, half, blk_pos, uoff, nblk, pt, soa);
   } else if (act) {
-    decode_one(U32, p, p, bs, n, i, blk_pos, uoff, nblk, pt, soa);
+    part = decode_one(U32, p, p, bs, n, i, half, blk_pos, uoff, nblk, pt, soa);
   }
+  // both halves' word sums (all lanes take part in the shuffles)
+  const uint32_t plo = (uint32_t)part, phi = (uint32_t)(part >> 32);
+  const uint64_t other = ((uint64_t)(uint32_t)__shfl_xor((int)phi, REC_GROUP, 64) << 32) |
+                         (uint32_t)__shfl_xor((int)plo, REC_GROUP, 64);
+  if (act && half == 0) soa.hash[i] = dq_mix64((uint64_t)n * DQ_K_LEN + part + other);
 }
 
-// Grid-stride over groups of 64 records: a few thousand resident waves, not one dispatch per group.
+// Grid-stride over groups of 32 records: a few thousand resident waves, not one dispatch per group.
 __global__ __launch_bounds__(64) void decode_records_kernel(
     const uint8_t* __restrict__ U, int64_t ulen, const int64_t* __restrict__ rec_lin, int64_t nrec,
     const int64_t* __restrict__ blk_pos, const int64_t* __restrict__ uoff, int64_t nblk,
     const int32_t* __restrict__ pt, RecSoA soa, int32_t* d_status) {
   __shared__ uint4 stage4[REC_STAGE / 16 + 1];
-  for (int64_t g = blockIdx.x; g * REC_WAVE < nrec; g += gridDim.x) {
-    decode_group(U, ulen, rec_lin, nrec, blk_pos, uoff, nblk, pt, soa, d_status, g * REC_WAVE,
+  for (int64_t g = blockIdx.x; g * REC_GROUP < nrec; g += gridDim.x) {
+    decode_group(U, ulen, rec_lin, nrec, blk_pos, uoff, nblk, pt, soa, d_status, g * REC_GROUP,
                  stage4);
     __syncthreads();  // this group is done with the staging buffer
   }
@@ -1317,7 +1325,7 @@ void launch_decode_records(const uint8_t* U, int64_t ulen, const int64_t* rec_li
   hipLaunchKernelGGL(block_pages_kernel, dim3((unsigned)((npages + 255) / 256)), dim3(256), 0, s,
                      uoff, nblk, pt, npages);
   hipLaunchKernelGGL(decode_records_kernel,
-                     dim3((unsigned)std::min<int64_t>((nrec + REC_WAVE - 1) / REC_WAVE, 8192)),
+                     dim3((unsigned)std::min<int64_t>((nrec + REC_GROUP - 1) / REC_GROUP, 16384)),
                      dim3(REC_WAVE), 0, s, U, ulen, rec_lin, nrec, blk_pos, uoff, nblk, pt, soa,
                      d_status);
 }
