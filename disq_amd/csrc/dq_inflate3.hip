@@ -117,7 +117,6 @@ struct alignas(16) LdsI {
           int32_t cntw[8];        // per-wave counts of second-level tables
           uint32_t cntp[8][8];    // per-wave counts of each code length, 16 bits per length
           uint16_t pref[320];     // root prefix of each long code, by canonical position
-          uint8_t slotq[320];     // second-level table of each long code, by canonical position
         } h;
       } x;
     } d;
@@ -593,25 +592,21 @@ DQ_AI void build_tables(LdsI& L, int nlen, int ndist) {
     slot -= 1;
     if (lng) {
       const int cap = isl ? LSLOTS : DSLOTS;
-      L.u.d.x.h.slotq[base + sym] = (uint8_t)min(slot, 255);
       if (start) {
         const int R2 = isl ? LR : DR;
         const uint32_t ridx = bitrev(pf, R2) + (isl ? 0 : T_DROOT);
         L.u.d.T[ridx] = slot < cap ? (uint16_t)(E_LINK | slot << 4) : E_SLOW;
       }
-    }
-  }
-  __syncthreads();
-  if (len > R) {
-    const int slot = L.u.d.x.h.slotq[(isl ? 0 : 288) + q];
-    const int cap = isl ? LSLOTS : DSLOTS;
-    if (slot < cap) {
-      const int sb = isl ? LSB : DSB;
-      const int m = len - R;
-      const uint32_t tail = bitrev(code & ((1u << m) - 1), m);
-      uint16_t* sub = L.u.d.T + (isl ? T_LSUB : T_DSUB) + (slot << sb);
-      const uint16_t ent = isl ? ent_ll((uint32_t)sym, (uint32_t)len) : ent_d((uint32_t)sym, (uint32_t)len);
-      for (uint32_t k = 0; k < (1u << (sb - m)); k++) sub[tail | (k << m)] = ent;
+      if (slot < cap) {  // this canonical position's code into its second-level table
+        const uint16_t ent = isl ? L.u.d.lent[sym] : L.u.d.dent[sym];
+        const int cl = ent & 15;
+        const uint32_t c = H.first[cl] + (uint32_t)(sym - H.offs[cl]);
+        const int sb = isl ? LSB : DSB;
+        const int m = cl - R;
+        const uint32_t tail = bitrev(c & ((1u << m) - 1), m);
+        uint16_t* sub = L.u.d.T + (isl ? T_LSUB : T_DSUB) + (slot << sb);
+        for (uint32_t k = 0; k < (1u << (sb - m)); k++) sub[tail | (k << m)] = ent;
+      }
     }
   }
   __syncthreads();
