@@ -675,16 +675,42 @@ __global__ void seg_counts_kernel(const Seg* __restrict__ segs, int64_t nseg, in
   if (s < nseg) counts[s] = segs[s].count;
 }
 
-__global__ void seg_emit_kernel(const uint8_t* __restrict__ U, const Seg* __restrict__ segs,
-                                const int64_t* __restrict__ base, int64_t nseg,
-                                int64_t* __restrict__ rec_lin) {
-  int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= nseg) return;
-  const Seg g = segs[s];
-  int64_t p = g.start, o = base[s];
-  for (int64_t k = 0; k < g.count; k++) {
-    rec_lin[o + k] = p;
-    p += 4 + (int64_t)ld32(U, p);
+// One lane per segment walks its chain again and writes the record starts.  The walk goes in
+// rounds of EMIT_R records into an LDS buffer per lane; the wave then writes each lane's run with
+// consecutive lanes on consecutive entries (coalesced), instead of 64 lanes storing 64 scattered
+// 8-byte entries per instruction.
+constexpr int EMIT_R = 32;
+__global__ __launch_bounds__(64) void seg_emit_kernel(const uint8_t* __restrict__ U,
+                                                      const Seg* __restrict__ segs,
+                                                      const int64_t* __restrict__ base, int64_t nseg,
+                                                      int64_t* __restrict__ rec_lin) {
+  __shared__ int64_t buf[64][EMIT_R + 1];
+  const int lane = threadIdx.x;
+  const int64_t s = (int64_t)blockIdx.x * 64 + lane;
+  int64_t p = 0, o = 0, left = 0;
+  if (s < nseg) {
+    const Seg g = segs[s];
+    p = g.start;
+    o = base[s];
+    left = g.count;
+  }
+  for (;;) {
+    const int n = (int)min(left, (int64_t)EMIT_R);
+    if (!__any(n > 0)) break;
+    for (int k = 0; k < n; k++) {
+      buf[lane][k] = p;
+      p += 4 + (int64_t)ld32(U, p);
+    }
+    // publish (n, o) of every lane, then write lane l's n entries with lanes 0..n-1
+    const int64_t my_o = o;
+    for (int l = 0; l < 64; l++) {
+      const int nl = __shfl(n, l, 64);
+      if (nl == 0) continue;  // uniform
+      const int64_t ol = __shfl(my_o, l, 64);
+      if (lane < nl) rec_lin[ol + lane] = buf[l][lane];
+    }
+    o += n;
+    left -= n;
   }
 }
 
