@@ -740,11 +740,15 @@ constexpr int REC_STAGE = 12288;  // 32 short-read records (~10.5 KB): 13 waves 
 // dword view in which the record starts at byte `off` (LDS staging or U itself).  Lane half 0
 // decodes the fixed fields; both halves hash the record's 8-byte words of their parity (the word
 // sum is order-free) and return the partial sum.
+struct BlockOf {  // the htsjdk block of a record start: loaded before the staging wait
+  int64_t j, u0, u1, bp;
+};
+
 template <typename WP>
 __device__ __attribute__((always_inline)) inline uint64_t decode_one(
     WP W, int64_t off, int64_t p, int32_t bs, int64_t n, int64_t i, int half,
     const int64_t* __restrict__ blk_pos, const int64_t* __restrict__ uoff, int64_t nblk,
-    const int32_t* __restrict__ pt, const RecSoA& soa) {
+    BlockOf bo, const RecSoA& soa) {
   const int64_t wi0 = off >> 2;
   const uint32_t sh = (uint32_t)(off & 3);
   if (half == 0) {
@@ -768,9 +772,13 @@ __device__ __attribute__((always_inline)) inline uint64_t decode_one(
     soa.next_ref_id[i] = (int32_t)f[6];
     soa.next_pos[i] = (int32_t)f[7];
     soa.tlen[i] = (int32_t)f[8];
-    int64_t j = pt[p >> 16];
-    while (j + 1 < nblk && uoff[j + 1] <= p) j++;
-    soa.voffset[i] = ((uint64_t)blk_pos[j] << 16) | (uint64_t)(p - uoff[j]);
+    while (bo.j + 1 < nblk && bo.u1 <= p) {  // rare: the page's first block ends before p
+      bo.j++;
+      bo.u0 = bo.u1;
+      bo.u1 = bo.j + 1 < nblk ? uoff[bo.j + 1] : INT64_MAX;
+      bo.bp = blk_pos[bo.j];
+    }
+    soa.voffset[i] = ((uint64_t)bo.bp << 16) | (uint64_t)(p - bo.u0);
   }
   // hash words k = half, half + 2, ...
   uint64_t part = 0;
@@ -806,6 +814,12 @@ __device__ void decode_group(const uint8_t* __restrict__ U, int64_t ulen,
     if (bad) *d_status = ST_SHORT;
     return;
   }
+  // the block lookups of the voffset, issued now so their latency overlaps the staging
+  BlockOf bo;
+  bo.j = pt[p >> 16];
+  bo.u0 = uoff[bo.j];
+  bo.u1 = bo.j + 1 < nblk ? uoff[bo.j + 1] : INT64_MAX;
+  bo.bp = blk_pos[bo.j];
   const int64_t first = rec_lin[i0];
   const int64_t lastp = rec_lin[i0 + nact - 1];
   const int32_t lastbs = (int32_t)funnel(U32[lastp >> 2], U32[(lastp >> 2) + 1], (uint32_t)(lastp & 3));
@@ -825,9 +839,9 @@ __device__ void decode_group(const uint8_t* __restrict__ U, int64_t ulen,
     __syncthreads();
     if (act)  // DS reads from the staging buffer (a pointer that may be either would be flat)
       part = decode_one((const __attribute__((address_space(3))) uint32_t*)stage4, p - base, p, bs,
-                        n, i, half, blk_pos, uoff, nblk, pt, soa);
+                        n, i, half, blk_pos, uoff, nblk, bo, soa);
   } else if (act) {
-    part = decode_one(U32, p, p, bs, n, i, half, blk_pos, uoff, nblk, pt, soa);
+    part = decode_one(U32, p, p, bs, n, i, half, blk_pos, uoff, nblk, bo, soa);
   }
   // both halves' word sums (all lanes take part in the shuffles)
   const uint32_t plo = (uint32_t)part, phi = (uint32_t)(part >> 32);
