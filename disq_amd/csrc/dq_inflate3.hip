@@ -1204,11 +1204,12 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     const uint64_t tb0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
     const int32_t nbs = bs + BATCH;
     const bool more = nbs < isize;
-    // carry into batch k+1: the match covering batch k's last byte, if it continues (all threads
-    // compute it, from batch k's descriptors, before (b) overwrites them)
-    int32_t ncms = -1;
-    uint32_t ncdesc = 0;
-    if (more) {
+    // carry into batch k+1: the match covering batch k's last byte, if it continues (wave 0
+    // computes it from batch k's descriptors, before (b) overwrites them, and publishes it; the
+    // slots are read right after the barrier, and rewritten only after batch k+1's steps)
+    if (more && wv == 0) {
+      int32_t ncms = -1;
+      uint32_t ncdesc = 0;
       const int32_t x = nbs - 1;
       const uint64_t m = bm64[x >> 6];  // bit 63 of the last word: every bit is at or before x
       const int32_t ms = m ? (x | 63) - (int32_t)__clzll(m) : (int32_t)L.u.r.last_start[(x >> 6) - 1];
@@ -1219,8 +1220,14 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
           ncdesc = desc;
         }
       }
+      if (lane == 0) {
+        L.misc[M_CARRY_MS] = ncms;
+        L.misc[M_CARRY_DESC] = (int32_t)ncdesc;
+      }
     }
     __syncthreads();  // every wave's jumps of batch k are done: nxt is free for batch k+1
+    const int32_t ncms = more ? L.misc[M_CARRY_MS] : -1;
+    const uint32_t ncdesc = more ? (uint32_t)L.misc[M_CARRY_DESC] : 0u;
     int32_t frB[NE], xsB[NE];
     uint32_t pendB = 0;
     if (more) first_hop(nbs, ncms, ncdesc, frB, xsB, pendB);
