@@ -140,7 +140,8 @@ __constant__ uint8_t c_clorder3[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 
 // misc slots
 enum { M_ERR = 0, M_A = 4, M_LAST, M_MORE, M_MORE1,
        M_CARRY_MS = 10, M_CARRY_DESC, M_LQ0 = 15, M_LQN, M_DQ0, M_DQN, M_NEXT,
-       M_LASTF, M_RCNT = 28 /* and 29: redo-list counters of even / odd rounds */ };
+       M_LASTF, M_RCNT = 28 /* and 29: redo-list counters of even / odd rounds */,
+       M_DIRTY = 30 /* and 31: a re-decoded exit changed, even / odd rounds */ };
 
 __device__ __attribute__((always_inline)) inline void set_err(LdsI& L, int32_t code) { atomicCAS(&L.misc[M_ERR], 0, code); }
 
@@ -983,7 +984,10 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
         LS[r] = t;
         ST[r] = st;
       }
-      if (t == 0) L.misc[M_RCNT + ((round + 1) & 1)] = 0;  // the next round's counter
+      if (t == 0) {  // the next round's counter; this round's changed-exit flag
+        L.misc[M_RCNT + ((round + 1) & 1)] = 0;
+        L.misc[M_DIRTY + (round & 1)] = 0;
+      }
       __syncthreads();
       const int nneed = *rc;
       if (nneed == 0) break;
@@ -1000,8 +1004,10 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
         // a speculative lane that found no boundary (F_DEAD) recorded no checkpoints
         const int f = run_redo(W, L, s0, sB, sE, endbits, CK ? CK + lt : nullptr, nl, SE[lt],
                                SC[lt], &E, &c, TIMING ? &jmerge : nullptr);
+        const int32_t ae = (E << 3) | f;
+        if (ae != AE[lt]) L.misc[M_DIRTY + (round & 1)] = 1;  // the successor's start moved
         AB[lt] = (int32_t)s0;
-        AE[lt] = (E << 3) | f;
+        AE[lt] = ae;
         AC[lt] = c;
         if (TIMING) {
           if (jmerge >= 0) {
@@ -1015,6 +1021,9 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       }
       if (hi) __builtin_amdgcn_s_setprio(0);
       __syncthreads();
+      // no re-decoded lane changed its exit: every successor's start still holds, so the
+      // check of another round would find nothing to do (the slot is cleared again two rounds on)
+      if (L.misc[M_DIRTY + (round & 1)] == 0) break;
     }
     TST(3);
 
