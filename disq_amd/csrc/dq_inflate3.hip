@@ -379,9 +379,16 @@ DQ_AI int run_redo(const uint32_t* __restrict__ W, const LdsI& L, uint32_t s0, u
 }
 
 // Emit from the verified boundary `start` to the first boundary >= target, output starting at
-// absolute position p; stops at isize.
+// absolute position p; stops at isize.  Literals, literal pairs and match descriptors are written
+// by the same three byte stores: a store a symbol does not need goes to this lane's dummy word
+// (wsum / small are dead during emit), so literal and match lanes do not run separate branches.
 DQ_AI void emit_seg(const uint32_t* __restrict__ W, LdsI& L, uint32_t start, uint32_t target,
                     uint32_t endbits, int32_t p, int32_t isize, int sh) {
+  typedef volatile __attribute__((address_space(3))) uint8_t lds8;
+  // three ds_write_b8 (a merged unaligned b16 store stalls): volatile keeps them apart, the LDS
+  // address space keeps them DS stores (a generic volatile pointer became flat stores)
+  uint32_t* const dummy32 = reinterpret_cast<uint32_t*>(L.wsum) + (tid_fresh() & 63);
+  lds8* const dummy = (lds8*)dummy32;
   BitR r;
   br_init(r, W, start);
   for (;;) {
@@ -391,30 +398,18 @@ DQ_AI void emit_seg(const uint32_t* __restrict__ W, LdsI& L, uint32_t start, uin
     bool m;
     if (dsym(r, W, L, q, min(target, endbits), len, dist, lit2, m))
       return;  // EOB / error: already accounted for by the rounds
-    if (!m) {
-      L.out[sh + p] = (uint8_t)len;
-      p++;
-      if (lit2 != 0xffffffffu && p < isize) {
-        L.out[sh + p] = (uint8_t)lit2;
-        p++;
-      }
-    } else {
-      if ((int32_t)dist > p) {
-        set_err(L, ST_BAD_DIST);
-        return;
-      }
-      const uint32_t desc = (dist - 1) | ((len - 3) << 15);
-      // three ds_write_b8 (a merged unaligned b16 store stalls): volatile keeps them apart, the LDS
-      // address space keeps them DS stores (a generic volatile pointer became flat stores with a
-      // full vmcnt wait after each)
-      volatile __attribute__((address_space(3))) uint8_t* o =
-          (volatile __attribute__((address_space(3))) uint8_t*)(L.out + sh + p);
-      o[0] = (uint8_t)desc;
-      o[1] = (uint8_t)(desc >> 8);
-      o[2] = (uint8_t)(desc >> 16);
-      atomicOr(&L.bm[p >> 5], 1u << (p & 31));
-      p += (int32_t)len;
+    if (m && (int32_t)dist > p) {
+      set_err(L, ST_BAD_DIST);
+      return;
     }
+    const bool two = !m && lit2 != 0xffffffffu && p + 1 < isize;
+    const uint32_t desc = (dist - 1) | ((len - 3) << 15);
+    lds8* const o = (lds8*)(L.out + sh + p);
+    o[0] = (uint8_t)(m ? desc : len);
+    *(m || two ? o + 1 : dummy) = (uint8_t)(m ? desc >> 8 : lit2);
+    *(m ? o + 2 : dummy) = (uint8_t)(desc >> 16);
+    atomicOr(m ? &L.bm[p >> 5] : dummy32, 1u << (p & 31));
+    p += m ? (int32_t)len : (two ? 2 : 1);
   }
 }
 
