@@ -308,12 +308,15 @@ DQ_AI int run_seg(const uint32_t* __restrict__ W, const LdsI& L, uint32_t start,
   int f;
   uint32_t thr = ck ? sB + CKI : 0xffffffffu;
   int j = 0;
+  // a lane crosses a checkpoint every few symbols, so some lane of the wave does on most steps:
+  // written branch-free, the step that crosses none stores to the lane's dummy word (wsum is
+  // dead during the speculative pass; `small` may hold the per-lane arrays)
+  uint32_t* const dummy = reinterpret_cast<uint32_t*>(const_cast<int32_t*>(L.wsum)) + (tid_fresh() & 15);
   for (;;) {
-    if (p >= thr) {  // rare: a checkpoint
-      ck[j * ckstride] = ((p - sB) << 16) | (uint32_t)cnt;
-      j++;
-      thr = j < NCK ? thr + CKI : 0xffffffffu;
-    }
+    const bool cross = p >= thr;
+    *(cross ? ck + j * ckstride : dummy) = ((p - sB) << 16) | (uint32_t)cnt;
+    j += cross ? 1 : 0;
+    thr = cross ? (j < NCK ? thr + CKI : 0xffffffffu) : thr;
     if (p >= sE || p >= endbits) {
       *Ep = (int32_t)p;
       f = p >= sE ? F_EXIT : F_END;
