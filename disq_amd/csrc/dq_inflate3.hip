@@ -351,23 +351,26 @@ DQ_AI int run_redo(const uint32_t* __restrict__ W, const LdsI& L, uint32_t s0, u
   int j = 0;
   for (;;) {
     const uint32_t p = br_pos(r);
-    if (p >= sE || p >= endbits) {
-      *Ep = (int32_t)p;
-      f = p >= sE ? F_EXIT : F_END;
-      break;
-    }
-    if (p >= thr) {  // rare: compare with the speculative checkpoint
-      if ((cur >> 16) == p - sB) {
+    // at a checkpoint threshold: the same boundary as the speculative run merges (one exit branch
+    // for the segment end, the data end and a merge; the threshold update is branch-free)
+    const bool cross = p >= thr;
+    const bool merge = cross && (cur >> 16) == p - sB;
+    if (p >= sE || p >= endbits || merge) {
+      if (merge) {
         *Ep = se >> 3;
         f = se & 7;
         cnt += sc - (int32_t)(cur & 0xffffu);
         if (jm) *jm = j;
-        break;
+      } else {
+        *Ep = (int32_t)p;
+        f = p >= sE ? F_EXIT : F_END;
       }
-      j++;
-      thr = j < NCK ? thr + CKI : 0xffffffffu;
-      cur = j < NCK ? ck[j * ckstride] : 0xffffffffu;
+      break;
     }
+    j += cross ? 1 : 0;
+    const uint32_t nxt = ck ? ck[min(j, NCK - 1) * ckstride] : 0xffffffffu;
+    thr = cross ? (j < NCK ? thr + CKI : 0xffffffffu) : thr;
+    cur = cross ? (j < NCK ? nxt : 0xffffffffu) : cur;
     uint32_t len = 0, dist = 0, lit2;
     bool m;
     if (dsym(r, W, L, p, min(min(thr, sE), endbits), len, dist, lit2, m)) {
