@@ -402,10 +402,10 @@ DQ_AI void emit_seg(const uint32_t* __restrict__ W, LdsI& L, uint32_t start, uin
     if (q >= target || q >= endbits || p >= isize) return;
     uint32_t len = 0, dist = 0, lit2;
     bool m;
-    if (dsym(r, W, L, q, min(target, endbits), len, dist, lit2, m))
-      return;  // EOB / error: already accounted for by the rounds
-    if (m && (int32_t)dist > p) {
-      set_err(L, ST_BAD_DIST);
+    const bool stop = dsym(r, W, L, q, min(target, endbits), len, dist, lit2, m);
+    const bool far = m && (int32_t)dist > p;  // a distance before the block's first byte
+    if (stop || far) {  // one exit branch: EOB / bad code (accounted for by the rounds) or far
+      if (!stop) set_err(L, ST_BAD_DIST);
       return;
     }
     const bool two = !m && lit2 != 0xffffffffu && p + 1 < isize;
