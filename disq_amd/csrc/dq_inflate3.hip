@@ -63,16 +63,18 @@ constexpr int RES_NXT = 2048;        // resolve batch bytes (NB * G * WG) at mos
 // 16-bit decode table layout: [litlen root | litlen subtables | dist root | dist subtables]
 constexpr int LR = 10, DR = 8;            // root bits
 constexpr int LSB = 15 - LR, DSB = 15 - DR;  // second-level index bits
-constexpr int LSLOTS = 16, DSLOTS = 4;    // second-level tables available
+constexpr int LSLOTS = 16, DSLOTS = 4;    // second-level entries: LSLOTS * 2^LSB, DSLOTS * 2^DSB
+constexpr int MAXGRP = 64;                // second-level tables (prefix groups) per alphabet
 constexpr int T_LSUB = 1 << LR;
 constexpr int T_DROOT = T_LSUB + LSLOTS * (1 << LSB);
 constexpr int T_DSUB = T_DROOT + (1 << DR);
 constexpr int T_END = T_DSUB + DSLOTS * (1 << DSB);
 constexpr int HB_WORDS = 160;             // staged dynamic-header words (aliases T)
 // Root entries whose code length field (bits 0-3) is 0 are not codes: 0 = no code (incomplete
-// table), E_LINK | slot << 4 = second-level table `slot`, E_SLOW = canonical decode.
-constexpr uint16_t E_LINK = 0x0200;
-constexpr uint16_t E_SLOW = 0x0100;
+// table); sb << 4 | off << 7 (sb = bits 4-6 != 0) = the second-level table of 2^sb entries at
+// `off` (zlib-style: sized by the longest code under the prefix, so every alphabet fits the
+// second-level area); E_SLOW = canonical decode (only past MAXGRP tables or the area).
+constexpr uint16_t E_SLOW = 0x0080;
 // Decoded litlen entry: code length (bits 0-3), M = length/EOB/invalid (bit 4), extra-bit count
 // (bits 5-7), value (bits 8-15): the literal byte or length base - 3.  EOB and the invalid symbols
 // 286/287 are M entries with 0 extra bits and values 248/249, which no length base has, so
@@ -115,6 +117,8 @@ struct alignas(16) LdsI {
           uint8_t clen[20];
           uint16_t clt[128];      // code-length code: sym << 3 | len (len 0 = invalid)
           int32_t cntw[8];        // per-wave counts of second-level tables
+          int32_t cnts[8];        // per-wave second-level entries
+          uint32_t ginfo[MAXGRP + 32];  // per second-level table (litlen, then distance): offset | sb << 16
           uint32_t cntp[8][8];    // per-wave counts of each code length, 16 bits per length
           uint16_t pref[320];     // root prefix of each long code, by canonical position
         } h;
@@ -127,14 +131,26 @@ struct alignas(16) LdsI {
     uint32_t crc4[4][256];
   } u;
   int32_t misc[32];
-  int32_t wsum[16];
-  int32_t small[8 * 7];           // per-lane arrays when the image tail is too short
+  union {
+    struct {
+      int32_t wsum[16];
+      int32_t small[8 * 7];       // per-lane arrays when the image tail is too short
+    };
+    // dummy words of the branch-free stores: 16 per wave in the speculative pass (wsum is dead,
+    // `small` may hold the arrays), one per lane in the emit (both dead)
+    uint32_t scratch[16 + 8 * 7];
+  };
 };
+static_assert(sizeof(((LdsI*)nullptr)->scratch) >= 64 * 4, "one emit dummy word per lane");
 static_assert(sizeof(LdsI) <= 81920, "two workgroups per CU");
 static_assert(HB_WORDS * 4 <= T_END * 2, "header staging fits the decode table");
 
 __constant__ uint32_t c_crc4[4][256];
-__constant__ uint32_t c_slice_shift[WG];  // x^(8 * 128 * k) mod P, k = 0..511
+// CRC slices: 132 bytes (33 words), so the 64 lanes of a wave read 64 different LDS banks (128-byte
+// slices put every lane of a wave in the same bank: a 32-way conflict on every data read)
+constexpr int CRC_SL = 132;
+static_assert(CRC_SL * WG >= 65536, "the slices cover the largest block");
+__constant__ uint32_t c_slice_shift[WG];  // x^(8 * CRC_SL * k) mod P, k = 0..511
 __constant__ uint8_t c_clorder3[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 // misc slots
@@ -176,7 +192,16 @@ DQ_AI void st_nt(uint4* d, uint4 v) {  // streaming store (nt): U is not re-read
   __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(d));
 }
 
-DQ_AI void br_init(BitR& r, const uint32_t* __restrict__ W, uint32_t bitpos) {
+// The compressed words.  (Staging a deflate block's words in the LDS image tail for the speculative
+// pass and the rounds was measured: no faster, profiles/r3a_lds_bits_ab.txt -- the refill load is
+// issued a half step ahead and is not the decode step's critical path.)
+struct GSrc {
+  const uint32_t* __restrict__ p;
+  DQ_AI uint32_t operator[](uint32_t i) const { return p[i]; }
+};
+
+template <class S>
+DQ_AI void br_init(BitR& r, const S& W, uint32_t bitpos) {
   const uint32_t wi = bitpos >> 5;
   const uint64_t lo = W[wi], hi = W[wi + 1];
   const uint32_t sh = bitpos & 31;
@@ -185,7 +210,8 @@ DQ_AI void br_init(BitR& r, const uint32_t* __restrict__ W, uint32_t bitpos) {
   r.wp = wi + 2;
   r.nw = W[r.wp];
 }
-DQ_AI void br_refill(BitR& r, const uint32_t* __restrict__ W) {
+template <class S>
+DQ_AI void br_refill(BitR& r, const S& W) {
   const bool need = r.bc <= 32;
   r.bb |= need ? (uint64_t)r.nw << r.bc : 0ull;
   r.bc += need ? 32u : 0u;
@@ -212,18 +238,18 @@ DQ_AI uint32_t load_desc(const LdsI& L, int a) {
   return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)a & 3u) & 0xffffffu;
 }
 
-// Second-level / canonical lookup for a root entry flagged E_LINK or E_SLOW.
+// Second-level / canonical lookup for a root entry that is not a code.
 DQ_AI uint32_t ll_second(const LdsI& L, uint32_t e, uint32_t bb) {
-  if (e & E_LINK)
-    return L.u.d.T[T_LSUB + (((e >> 4) & 15) << LSB) + ((bb >> LR) & ((1u << LSB) - 1))];
+  const uint32_t sb = (e >> 4) & 7;
+  if (sb) return L.u.d.T[T_LSUB + (e >> 7) + ((bb >> LR) & ((1u << sb) - 1))];
   if (!(e & E_SLOW)) return 0u;
   int l = 0;
   const int k = canon_decode(bb, L.u.d.hl, LR + 1, &l);
   return k < 0 ? 0u : L.u.d.lent[k];
 }
 DQ_AI uint32_t d_second(const LdsI& L, uint32_t e, uint32_t bb) {
-  if (e & E_LINK)
-    return L.u.d.T[T_DSUB + (((e >> 4) & 15) << DSB) + ((bb >> DR) & ((1u << DSB) - 1))];
+  const uint32_t sb = (e >> 4) & 7;
+  if (sb) return L.u.d.T[T_DSUB + (e >> 7) + ((bb >> DR) & ((1u << sb) - 1))];
   if (!(e & E_SLOW)) return 0u;
   int l = 0;
   const int k = canon_decode(bb, L.u.d.hd, DR + 1, &l);
@@ -242,7 +268,8 @@ DQ_AI uint32_t d_second(const LdsI& L, uint32_t e, uint32_t bb) {
 // boundary between them lies before `lim` (the next bit position at which the caller looks at
 // symbol boundaries: segment start/exit, checkpoint, end of data), both are taken at once and
 // `lit2` is the second (else 0xffffffff) -- the boundaries the caller sees are unchanged.
-DQ_AI bool dsym(BitR& r, const uint32_t* __restrict__ W, const LdsI& L, uint32_t p, uint32_t lim,
+template <class S>
+DQ_AI bool dsym(BitR& r, const S& W, const LdsI& L, uint32_t p, uint32_t lim,
                 uint32_t& len, uint32_t& dist, uint32_t& lit2, bool& is_m) {
   br_refill(r, W);  // >= 33 bits: a litlen code + its extra bits (<= 20)
   uint32_t bb = (uint32_t)r.bb;
@@ -285,7 +312,8 @@ constexpr uint32_t CKI = 48;    // checkpoint spacing in bits (>= the longest sy
 
 // Speculative lanes also record checkpoints: the first symbol boundary at or past sB + CKI * (j+1)
 // (offset from sB << 16 | bytes counted so far), j < NCK, at ck[j * ckstride] (nullptr: none).
-DQ_AI int run_seg(const uint32_t* __restrict__ W, const LdsI& L, uint32_t start, uint32_t sB,
+template <class S>
+DQ_AI int run_seg(const S& W, const LdsI& L, uint32_t start, uint32_t sB,
                   uint32_t sE, uint32_t endbits, int32_t* Bp, int32_t* Ep, int32_t* cntp,
                   uint32_t* ck = nullptr, int ckstride = 0) {
   BitR r;
@@ -311,7 +339,7 @@ DQ_AI int run_seg(const uint32_t* __restrict__ W, const LdsI& L, uint32_t start,
   // a lane crosses a checkpoint every few symbols, so some lane of the wave does on most steps:
   // written branch-free, the step that crosses none stores to the lane's dummy word (wsum is
   // dead during the speculative pass; `small` may hold the per-lane arrays)
-  uint32_t* const dummy = reinterpret_cast<uint32_t*>(const_cast<int32_t*>(L.wsum)) + (tid_fresh() & 15);
+  uint32_t* const dummy = const_cast<uint32_t*>(L.scratch) + (tid_fresh() & 15);
   for (;;) {
     const bool cross = p >= thr;
     *(cross ? ck + j * ckstride : dummy) = ((p - sB) << 16) | (uint32_t)cnt;
@@ -339,7 +367,8 @@ DQ_AI int run_seg(const uint32_t* __restrict__ W, const LdsI& L, uint32_t start,
 // threshold the path is compared with the speculative one: the same boundary means the same
 // decoder state, so the rest of the segment is the speculative run's (exit `se` = E << 3 | flag,
 // `sc` bytes from its first boundary) and the decode stops there.
-DQ_AI int run_redo(const uint32_t* __restrict__ W, const LdsI& L, uint32_t s0, uint32_t sB,
+template <class S>
+DQ_AI int run_redo(const S& W, const LdsI& L, uint32_t s0, uint32_t sB,
                    uint32_t sE, uint32_t endbits, const uint32_t* ck, int ckstride, int32_t se,
                    int32_t sc, int32_t* Ep, int32_t* cntp, int* jm = nullptr) {
   BitR r;
@@ -388,12 +417,13 @@ DQ_AI int run_redo(const uint32_t* __restrict__ W, const LdsI& L, uint32_t s0, u
 // absolute position p; stops at isize.  Literals, literal pairs and match descriptors are written
 // by the same three byte stores: a store a symbol does not need goes to this lane's dummy word
 // (wsum / small are dead during emit), so literal and match lanes do not run separate branches.
-DQ_AI void emit_seg(const uint32_t* __restrict__ W, LdsI& L, uint32_t start, uint32_t target,
+template <class S>
+DQ_AI void emit_seg(const S& W, LdsI& L, uint32_t start, uint32_t target,
                     uint32_t endbits, int32_t p, int32_t isize, int sh) {
   typedef volatile __attribute__((address_space(3))) uint8_t lds8;
   // three ds_write_b8 (a merged unaligned b16 store stalls): volatile keeps them apart, the LDS
   // address space keeps them DS stores (a generic volatile pointer became flat stores)
-  uint32_t* const dummy32 = reinterpret_cast<uint32_t*>(L.wsum) + (tid_fresh() & 63);
+  uint32_t* const dummy32 = L.scratch + (tid_fresh() & 63);
   lds8* const dummy = (lds8*)dummy32;
   BitR r;
   br_init(r, W, start);
@@ -576,8 +606,10 @@ DQ_AI void build_tables(LdsI& L, int nlen, int ndist) {
   L.u.d.T[t + WG] = root_entry<LR>(L, L.u.d.hl, L.u.d.lend, L.u.d.lent, bitrev((uint32_t)(t + WG), LR));
   if (t < (1 << DR))
     L.u.d.T[T_DROOT + t] = root_entry<DR>(L, L.u.d.hd, L.u.d.dend, L.u.d.dent, bitrev((uint32_t)t, DR));
-  // second-level tables: thread t handles canonical position t of each alphabet (the link
-  // entries are written after the barrier below, over the root entries above)
+  // second-level tables: thread t handles canonical position t of each alphabet.  The long codes
+  // under one root prefix are consecutive canonical positions (a group); a group's table has
+  // 2^(longest length - R) entries, placed by a scan of the sizes (the link entries are written
+  // after the barrier below, over the root entries above)
   {
     const int q0 = isl ? L.misc[M_LQ0] : L.misc[M_DQ0];
     const int qn = isl ? L.misc[M_LQN] : L.misc[M_DQN];
@@ -585,28 +617,43 @@ DQ_AI void build_tables(LdsI& L, int nlen, int ndist) {
     const bool lng = (isl || isd) && sym >= q0 && sym < qn;  // here `sym` = canonical position
     const uint16_t pf = lng ? L.u.d.x.h.pref[base + sym] : 0;
     const bool start = lng && (sym == q0 || L.u.d.x.h.pref[base + sym - 1] != pf);
+    const bool gend = lng && (sym == qn - 1 || L.u.d.x.h.pref[base + sym + 1] != pf);
+    const uint16_t ent = lng ? (isl ? L.u.d.lent[sym] : L.u.d.dent[sym]) : (uint16_t)0;
+    const int cl = ent & 15;
+    const int gsz = gend ? 1 << (cl - R) : 0;
     const uint64_t sm = __ballot(start);
     int slot = __popcll(sm & lanes_below(lane)) + (start ? 1 : 0);  // inclusive
-    if (wv < 6 && lane == 0) L.u.d.x.h.cntw[wv] = __popcll(sm);
+    int osz = wave_incl_scan(gsz, lane);                              // inclusive
+    if (lane == 63) {
+      L.u.d.x.h.cntw[wv] = __popcll(sm);
+      L.u.d.x.h.cnts[wv] = osz;
+    }
     __syncthreads();
     if (isl)
-      for (int w = 0; w < wv; w++) slot += L.u.d.x.h.cntw[w];
-    slot -= 1;
-    if (lng) {
-      const int cap = isl ? LSLOTS : DSLOTS;
-      if (start) {
-        const int R2 = isl ? LR : DR;
-        const uint32_t ridx = bitrev(pf, R2) + (isl ? 0 : T_DROOT);
-        L.u.d.T[ridx] = slot < cap ? (uint16_t)(E_LINK | slot << 4) : E_SLOW;
+      for (int w = 0; w < wv; w++) {
+        slot += L.u.d.x.h.cntw[w];
+        osz += L.u.d.x.h.cnts[w];
       }
-      if (slot < cap) {  // this canonical position's code into its second-level table
-        const uint16_t ent = isl ? L.u.d.lent[sym] : L.u.d.dent[sym];
-        const int cl = ent & 15;
+    slot -= 1;
+    const int R2 = isl ? LR : DR;
+    const int area = isl ? LSLOTS << LSB : DSLOTS << DSB;
+    const int gmax = isl ? MAXGRP : 32;
+    uint32_t* const ginfo = L.u.d.x.h.ginfo + (isl ? 0 : MAXGRP);
+    if (gend && slot < gmax) ginfo[slot] = (uint32_t)(osz - gsz) | (uint32_t)(cl - R2) << 16;
+    __syncthreads();
+    if (lng) {
+      const uint32_t gi = slot < gmax ? ginfo[slot] : 0u;
+      const int off = (int)(gi & 0xffffu), sb = (int)(gi >> 16);
+      const bool fits = slot < gmax && off + (1 << sb) <= area;
+      if (start) {
+        const uint32_t ridx = bitrev(pf, R2) + (isl ? 0 : T_DROOT);
+        L.u.d.T[ridx] = fits ? (uint16_t)(sb << 4 | off << 7) : E_SLOW;
+      }
+      if (fits) {  // this canonical position's code into its group's table
         const uint32_t c = H.first[cl] + (uint32_t)(sym - H.offs[cl]);
-        const int sb = isl ? LSB : DSB;
-        const int m = cl - R;
+        const int m = cl - R2;
         const uint32_t tail = bitrev(c & ((1u << m) - 1), m);
-        uint16_t* sub = L.u.d.T + (isl ? T_LSUB : T_DSUB) + (slot << sb);
+        uint16_t* sub = L.u.d.T + (isl ? T_LSUB : T_DSUB) + off;
         for (uint32_t k = 0; k < (1u << (sb - m)); k++) sub[tail | (k << m)] = ent;
       }
     }
@@ -947,6 +994,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     SC = SE + nl;
     if (cap >= 8) CK = reinterpret_cast<uint32_t*>(SC + nl);
     const uint32_t seg = (span + nl - 1) / nl;
+    const GSrc gsrc{W};
     // ---- 3. speculative pass: from OV bits before the segment, counting from its first boundary
     if (t == 0) {  // published by the barrier below
       L.misc[M_RCNT] = 0;       // round 0's redo-list counter
@@ -959,7 +1007,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       int32_t B = -1, E = 0, c = 0;
       if (CK)
         for (int j = 0; j < NCK; j++) CK[j * nl + t] = 0xffffffffu;
-      const int f = run_seg(W, L, start, sB, sE, endbits, &B, &E, &c, CK ? CK + t : nullptr, nl);
+      const int f = run_seg(gsrc, L, start, sB, sE, endbits, &B, &E, &c, CK ? CK + t : nullptr, nl);
       AB[t] = B;
       AE[t] = (E << 3) | f;
       AC[t] = c;
@@ -1003,7 +1051,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
         int jmerge = -1;
         const uint32_t sB = a + (uint32_t)lt * seg;
         // a speculative lane that found no boundary (F_DEAD) recorded no checkpoints
-        const int f = run_redo(W, L, s0, sB, sE, endbits, CK ? CK + lt : nullptr, nl, SE[lt],
+        const int f = run_redo(gsrc, L, s0, sB, sE, endbits, CK ? CK + lt : nullptr, nl, SE[lt],
                                SC[lt], &E, &c, TIMING ? &jmerge : nullptr);
         const int32_t ae = (E << 3) | f;
         if (ae != AE[lt]) L.misc[M_DIRTY + (round & 1)] = 1;  // the successor's start moved
@@ -1062,7 +1110,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     // ---- emit
     if (t <= last && myoff < isize) {
       const uint32_t sE = t == nl - 1 ? 0xffffffffu : a + (uint32_t)(t + 1) * seg;
-      emit_seg(W, L, (uint32_t)myB, sE, endbits, myoff, isize, sh);
+      emit_seg(gsrc, L, (uint32_t)myB, sE, endbits, myoff, isize, sh);
     }
     const int32_t nextpos = L.misc[M_NEXT];
     __syncthreads();
@@ -1304,13 +1352,13 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   for (int x = t; x < head; x += WG) dstU[x] = O[x];
   for (int x = head + 16 * lines_done + t; x < isize; x += WG) dstU[x] = O[x];
   TST(6);
-  // ---- 7. CRC32: thread t hashes the 128-byte slice ending (511 - t) * 128 bytes before isize
+  // ---- 7. CRC32: thread t hashes the CRC_SL-byte slice ending (511 - t) * CRC_SL bytes before isize
   if (verify_crc) {
     __syncthreads();  // the resolve scratch is dead: the CRC tables reuse it
     for (int i = t; i < 1024; i += WG) (&L.u.crc4[0][0])[i] = (&c_crc4[0][0])[i];
     __syncthreads();
-    const int32_t e = isize - (WG - 1 - t) * 128;
-    const int32_t s0 = max(0, e - 128);
+    const int32_t e = isize - (WG - 1 - t) * CRC_SL;
+    const int32_t s0 = max(0, e - CRC_SL);
     uint32_t cr = 0;
     if (e > 0) {
       int32_t x = s0;
@@ -1372,9 +1420,12 @@ struct HostTables {
     uint32_t p = 1u << 30;  // x^1
     x2n[0] = p;
     for (int k = 1; k < 32; k++) x2n[k] = p = h_mul(p, p);
-    // x^(8 * 128 * k) mod P: x^1024 = x2n[10]; powers by repeated multiplication
+    // x^(8 * CRC_SL * k) mod P: x^1056 = x^1024 * x^32 = x2n[10] * x2n[5]; powers by repeated
+    // multiplication
+    static_assert(CRC_SL == 132, "x^(8 * CRC_SL) below");
+    const uint32_t step = h_mul(x2n[10], x2n[5]);
     slice[0] = 1u << 31;  // x^0
-    for (int k = 1; k < WG; k++) slice[k] = h_mul(slice[k - 1], x2n[10]);
+    for (int k = 1; k < WG; k++) slice[k] = h_mul(slice[k - 1], step);
     uint32_t x8 = 1u << 31;          // x^0
     const uint32_t x8step = x2n[3];  // x^8
     for (int n = 0; n <= 65536; n++) {
@@ -1427,14 +1478,17 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
       (getenv("DQ_STORE") ? (uint32_t)atoi(getenv("DQ_STORE")) : 2u) |
       (getenv("DQ_NDEC") ? (uint32_t)(atoi(getenv("DQ_NDEC")) & 1023) << 8 : 0u) |
       (getenv("DQ_SEGBITS") ? (uint32_t)(atoi(getenv("DQ_SEGBITS")) & 1023) << 20 : 0u);
-  static int cfg = -1;
-  if (cfg < 0) {  // DQ_CFG="nb,g" (tuning experiments: 4,1 default, 2,1 or 1,4)
+  // DQ_CFG="nb,g" (tuning experiments: 4,1 default, 2,1 or 1,4); a function-local static const is
+  // initialised once, thread-safely (dq_decode_file_multi launches from one host thread per device)
+  static const int cfg = [] {
     int nb = 4, g = 1;
     if (const char* e = getenv("DQ_CFG")) sscanf(e, "%d,%d", &nb, &g);
-    cfg = g == 4 ? 1 : nb == 2 ? 4 : 0;
-  }
+    return g == 4 ? 1 : nb == 2 ? 4 : 0;
+  }();
+  // DQ_LDSPAD: extra dynamic LDS per workgroup (occupancy experiments: 80000 = one workgroup per CU)
+  static const unsigned ldspad = getenv("DQ_LDSPAD") ? (unsigned)atoi(getenv("DQ_LDSPAD")) : 0u;
 #define DQ_LAUNCH(TM, NBT, GT)                                                                  \
-  hipLaunchKernelGGL((inflate_block_kernel<TM, NBT, GT>), dim3((unsigned)ngrid), dim3(WG), 0, s, C, \
+  hipLaunchKernelGGL((inflate_block_kernel<TM, NBT, GT>), dim3((unsigned)ngrid), dim3(WG), ldspad, s, C, \
                      blk_pos, blk_csize, blk_usize, uoff, ngrid, U, status, verify_crc, crc_init, tim, ov, \
                      sflags, sel)
 #define DQ_CFGS(TM)                       \

@@ -3,12 +3,14 @@
 htsjdk hands each BGZF member to java.util.zip.Inflater (zlib): any valid raw-DEFLATE stream must
 inflate.  The records below keep their fields but carry quality strings drawn from a skewed byte
 distribution (two frequent values, 254 rare ones), so zlib's literal/length code has dozens of
-codes longer than the 10-bit root table under more distinct root prefixes than the kernel has
-second-level tables (16): those codes take the canonical slow path.  The same stream is also
-compressed with fixed Huffman codes (Z_FIXED) and stored (level 0).  Parity: the decompressed
-stream equals zlib's, every partition equals the oracle's.  The CPU test checks that the fixtures
-do reach the slow path (a DEFLATE header parser counts the prefixes), so the GPU test cannot pass
-vacuously."""
+codes longer than the 10-bit root table under more distinct root prefixes (> 16) than round 2's
+fixed second-level tables held: the variable-size second-level tables (one per prefix, sized by
+its longest code) take all of them.  A hand-built block with more prefixes than the kernel keeps
+tables for (MAXGRP = 64) reaches the canonical slow path, and one with long DISTANCE codes under 5
+prefixes the distance tables.  The same stream is also compressed with fixed Huffman codes
+(Z_FIXED) and stored (level 0).  Parity: the decompressed stream equals zlib's, every partition
+equals the oracle's.  The CPU tests check the fixtures' shapes (a DEFLATE header parser counts the
+prefixes), so the GPU tests cannot pass vacuously."""
 import struct
 import zlib
 
@@ -20,7 +22,8 @@ from oracle import oracle as O
 
 import bamutil as B
 
-LR, LSLOTS = 10, 16  # litlen root bits and second-level tables of dq_inflate3.hip
+LR, LSLOTS = 10, 16  # litlen root bits of dq_inflate3.hip; round 2's fixed second-level tables
+MAXGRP = 64  # second-level litlen tables the kernel keeps (dq_inflate3.hip); more -> slow path
 
 
 def skewed_stream(n=3000, seed=31, rare=0.03):
@@ -115,9 +118,9 @@ def stream():
     return skewed_stream()
 
 
-def test_fixtures_reach_the_slow_path(stream):
-    """Every dynamic member of the level 1/6/9 files needs more second-level tables than the
-    kernel has: the canonical fallback decodes part of every block."""
+def test_fixtures_need_many_second_level_tables(stream):
+    """Every dynamic member of the level 1/6/9 files has long codes under more root prefixes than
+    16 (the fixed tables of round 2, which sent the rest to the canonical slow path)."""
     for level in (1, 6, 9):
         bodies = [member(stream[a:a + B.BLOCK_U], level)[18:-8]
                   for a in range(0, len(stream), B.BLOCK_U)]
@@ -145,8 +148,8 @@ def test_gpu_inflate_long_codes_fixed_and_stored(stream, level, strategy):
     assert np.array_equal(b["hash"], ref["hash"])
 
 
-# ---- a hand-built dynamic block whose DISTANCE code needs the slow path: 10 nine-bit distance
-# codes under 5 distinct 8-bit prefixes (the kernel has 4 second-level distance tables).
+# ---- a hand-built dynamic block with long DISTANCE codes: 10 nine-bit distance codes under 5
+# distinct 8-bit prefixes (round 2 had 4 fixed second-level distance tables and a slow path).
 DR, DSLOTS = 8, 4
 LBASE = [3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31, 35, 43, 51, 59, 67, 83, 99, 115,
          131, 163, 195, 227, 258]
@@ -175,9 +178,10 @@ class _Writer:
         return self.v.to_bytes((self.n + 7) // 8, "little")
 
 
-def deflate_long_distances(data: bytes, stride: int) -> bytes:
+def deflate_long_distances(data: bytes, stride: int, ll_lens=LL_LENS, d_lens=D_LENS) -> bytes:
     """One final dynamic block of `data`: matches at k * stride (k = 1..5, cycling) of <= 42
     bytes where the bytes repeat, literals elsewhere."""
+    LL_LENS, D_LENS = ll_lens, d_lens
     llc, dc = _canonical(LL_LENS), _canonical(D_LENS)
     w = _Writer()
     w.bits(1, 1)
@@ -209,13 +213,13 @@ def deflate_long_distances(data: bytes, stride: int) -> bytes:
             w.bits(d - DBASE[ds], DEXT[ds])
             i += n
         else:
-            w.code(llc[data[i]], 9)
+            w.code(llc[data[i]], LL_LENS[data[i]])
             i += 1
-    w.code(llc[256], 3)
+    w.code(llc[256], LL_LENS[256])
     return w.bytes()
 
 
-def long_distance_bam():
+def long_distance_bam(ll_lens=LL_LENS):
     r = synth.generate(50, seed=33, nthreads=2)
     u = B.inflate_all(r.bam)
     head = u[:B.header_len(u)]
@@ -223,7 +227,7 @@ def long_distance_bam():
     stride = len(rec)
     assert stride == 129
     body = rec * 450  # 58,050 bytes: one member
-    deflated = deflate_long_distances(body, stride)
+    deflated = deflate_long_distances(body, stride, ll_lens)
     assert zlib.decompress(deflated, -15) == body
     hdr = b"\x1f\x8b\x08\x04\x00\x00\x00\x00\x00\xff\x06\x00BC\x02\x00"
     m = hdr + struct.pack("<H", 18 + len(deflated) + 8 - 1) + deflated
@@ -248,6 +252,40 @@ def test_long_distance_fixture():
 def test_gpu_inflate_distance_slow_path():
     from disq_amd import _lib
     bam, u = long_distance_bam()
+    split = 8 * 1024
+    with _lib.Context(split_size=split, verify_crc=True, device=0) as c:
+        c.open_bytes(bam)
+        b = c.read(with_raw=False)
+        got = c.inflated()
+    assert np.array_equal(got, np.frombuffer(u, np.uint8))
+    ref = np.concatenate(O.OracleBam(bam).read_partitions(split))
+    assert len(b["voffset"]) == len(ref) == 490
+    assert np.array_equal(b["voffset"], ref["voffset"])
+    assert np.array_equal(b["hash"], ref["hash"])
+
+
+# ---- a hand-built literal/length code with 160 eleven-bit codes (literals 118..255, EOB and the
+# lengths 257..277) under 80 distinct 10-bit prefixes: more than MAXGRP, so the codes of the last
+# 16 prefixes take the canonical slow path; 118 seven-bit literals fill the rest (Kraft sum 1).
+LL_MANY = [7] * 118 + [11] * 160 + [0] * 8
+
+
+def test_many_prefix_fixture():
+    assert sum(2.0 ** -n for n in LL_MANY if n) == 1.0
+    cc = _canonical(LL_MANY)
+    prefixes = {cc[s] >> (ln - LR) for s, ln in enumerate(LL_MANY) if ln > LR}
+    assert len(prefixes) == 80 > MAXGRP
+    bam, u = long_distance_bam(LL_MANY)
+    assert B.inflate_all(bam) == u
+    # the records' bytes use literals under the slow-path prefixes (the last 16 in code order)
+    slow = {s for s, ln in enumerate(LL_MANY) if ln > LR and (cc[s] >> 1) >= 1024 - 16}
+    assert slow & set(u)
+
+
+@pytest.mark.gpu
+def test_gpu_inflate_litlen_slow_path():
+    from disq_amd import _lib
+    bam, u = long_distance_bam(LL_MANY)
     split = 8 * 1024
     with _lib.Context(split_size=split, verify_crc=True, device=0) as c:
         c.open_bytes(bam)
