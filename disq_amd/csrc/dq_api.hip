@@ -595,28 +595,27 @@ static int run_pipeline(dq_ctx* ctx) {
     launch_chain2(ctx->cbuf(), L, ctx->cand.as<Cand>(), d_ncand, ncand,
                   ctx->voff.as<int64_t>(), ctx->blk_pos.as<int64_t>(), ctx->blk_cs.as<int32_t>(),
                   ctx->blk_us.as<int32_t>(), capb, d_nblk, d_broken, is_eof, s);
-  int64_t nblk = 0;
-  if ((rc = get_i64(ctx, d_nblk, &nblk))) return rc;
-  int32_t broken = 0;
-  HIPCHK(hipMemcpy(&broken, d_broken, 4, hipMemcpyDeviceToHost));
   // The chain must start at the file start (htsjdk reads from block 0); a shard's chain starts
-  // at the guesser's first block in its first split (the first valid candidate).
+  // at the guesser's first block in its first split (the first valid candidate).  The first
+  // valid candidate and the chain's first block come from a device reduction: one small copy
+  // brings them back with the block count and the broken flag.
+  unsigned long long* d_cc = reinterpret_cast<unsigned long long*>(ctx->scal.as<char>() + 128);
+  HIPCHK(hipMemsetAsync(d_cc, 0xff, 16, s));
+  if (ncand > 0)
+    launch_chain_check(ctx->cand.as<Cand>(), d_ncand, capc, ctx->blk_pos.as<int64_t>(), d_nblk, d_cc, s);
+  alignas(8) unsigned char sc[144];
+  HIPCHK(hipMemcpyAsync(sc, ctx->scal.p, sizeof sc, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  int64_t nblk = 0;
+  int32_t broken = 0;
+  unsigned long long minvalid = 0, p0 = 0;
+  memcpy(&broken, sc + 4, 4);
+  memcpy(&nblk, sc + 64, 8);
+  memcpy(&minvalid, sc + 128, 8);
+  memcpy(&p0, sc + 136, 8);
   int64_t chain_start = 0;
-  if (ctx->shard && !ctx->chunk_mode && ncand > 0) {
-    std::vector<Cand> ch((size_t)ncand);
-    HIPCHK(hipMemcpy(ch.data(), ctx->cand.p, sizeof(Cand) * (size_t)ncand, hipMemcpyDeviceToHost));
-    chain_start = L;
-    for (const Cand& c : ch)
-      if (c.valid == 1) {
-        chain_start = c.pos;
-        break;
-      }
-  }
-  if (!broken && ncand > 0) {
-    int64_t p0 = 0;
-    HIPCHK(hipMemcpy(&p0, ctx->blk_pos.p, sizeof(int64_t), hipMemcpyDeviceToHost));
-    if (p0 != chain_start) broken = 1;
-  }
+  if (ctx->shard && !ctx->chunk_mode && ncand > 0) chain_start = minvalid == ~0ull ? L : (int64_t)minvalid;
+  if (!broken && ncand > 0 && (int64_t)p0 != chain_start) broken = 1;
   if (broken) {  // walk htsjdk headers from the start (false-positive or non-BC headers present)
     int64_t capw = L / 26 + 2;
     if ((rc = ensure_all(ctx, ctx->blk_pos, sizeof(int64_t) * (size_t)capw))) return rc;
@@ -672,20 +671,22 @@ static int run_pipeline(dq_ctx* ctx) {
   }
   dbg(s, "inflate", nblk, ulen);
   HIPCHK(hipEventRecord(ctx->ev[2], s));
-  {
-    std::vector<int32_t> st((size_t)nblk);
-    if (nblk) HIPCHK(hipMemcpyAsync(st.data(), ctx->status.p, sizeof(int32_t) * (size_t)nblk,
-                                    hipMemcpyDeviceToHost, s));
+  {  // the first failed block, by a device reduction: one word back instead of the status array
+    unsigned long long* d_bad = reinterpret_cast<unsigned long long*>(ctx->scal.as<char>() + 144);
+    HIPCHK(hipMemsetAsync(d_bad, 0xff, 8, s));
+    launch_first_bad(ctx->status.as<int32_t>(), nullptr, nblk, d_bad, s);
+    unsigned long long bad = 0;
+    HIPCHK(hipMemcpyAsync(&bad, d_bad, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    for (int64_t b = 0; b < nblk; b++)
-      if (st[(size_t)b] != ST_OK) {
-        int64_t pos = 0;
-        HIPCHK(hipMemcpy(&pos, ctx->blk_pos.as<int64_t>() + b, 8, hipMemcpyDeviceToHost));
-        char msg[256];
-        snprintf(msg, sizeof msg, "%s in BGZF block at %lld", status_name(st[(size_t)b]),
-                 (long long)pos);
-        RET(DQ_EFORMAT, msg);
-      }
+    if (bad != ~0ull) {
+      int32_t st = 0;
+      int64_t pos = 0;
+      HIPCHK(hipMemcpy(&st, ctx->status.as<int32_t>() + bad, 4, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(&pos, ctx->blk_pos.as<int64_t>() + bad, 8, hipMemcpyDeviceToHost));
+      char msg[256];
+      snprintf(msg, sizeof msg, "%s in BGZF block at %lld", status_name(st), (long long)pos);
+      RET(DQ_EFORMAT, msg);
+    }
   }
   if (ctx->text_mode) {  // BGZF text: lines are planned by text_run
     ctx->stats = dq_stats{};
@@ -1541,6 +1542,11 @@ static int run_span(dq_ctx* ctx, const dq_traversal* tr, dq_stats* out) {
   const int64_t nsplit = (int64_t)plans.size();
   std::vector<uint64_t> cb, ce;            // span chunks, partition order
   std::vector<int64_t> part_first((size_t)nsplit + 1, 0);
+  // traverseUnplacedUnmapped: the partition whose chunk holds the start of the last linear bin
+  // also reads the unplaced-unmapped tail from there to the end of the file, after its interval
+  // records (AbstractBinarySamSource.java:116-129) -- one more chunk, kept by tail_keep
+  const bool want_tail = tr->traverse_unplaced_unmapped && ctx->solb != -1 && ctx->ncc >= 1;
+  int64_t tail_chunk = -1;
   for (int64_t i = 0; i < nsplit; i++) {
     part_first[(size_t)i] = (int64_t)cb.size();
     const SplitPlan& P = plans[(size_t)i];
@@ -1549,6 +1555,12 @@ static int run_span(dq_ctx* ctx, const dq_traversal* tr, dq_stats* out) {
       if (c.b < vb) continue;
       cb.push_back(c.b - vb);
       ce.push_back(c.e - vb);
+    }
+    if (want_tail && P.vstart + vb <= (uint64_t)ctx->solb && (uint64_t)ctx->solb < P.vend + vb &&
+        (uint64_t)ctx->solb >= vb) {
+      tail_chunk = (int64_t)cb.size();
+      cb.push_back((uint64_t)ctx->solb - vb);
+      ce.push_back(((uint64_t)ctx->flen << 16) | 0xffff);
     }
   }
   part_first[(size_t)nsplit] = (int64_t)cb.size();
@@ -1612,16 +1624,21 @@ static int run_span(dq_ctx* ctx, const dq_traversal* tr, dq_stats* out) {
     }
     HIPCHK(hipEventRecord(ctx->ev[6], s));
     {
-      std::vector<int32_t> st((size_t)nblk);
-      if (nblk) HIPCHK(hipMemcpyAsync(st.data(), ctx->status.p, 4 * (size_t)nblk, hipMemcpyDeviceToHost, s));
+      // the first failed selected block, by a device reduction (one word back)
+      unsigned long long* d_bad = reinterpret_cast<unsigned long long*>(ctx->scal.as<char>() + 144);
+      HIPCHK(hipMemsetAsync(d_bad, 0xff, 8, s));
+      if (nsel) launch_first_bad(ctx->status.as<int32_t>(), ctx->sel.as<int32_t>(), nsel, d_bad, s);
+      unsigned long long bad = 0;
+      HIPCHK(hipMemcpyAsync(&bad, d_bad, 8, hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
-      for (int32_t j : sel)
-        if (st[(size_t)j] != ST_OK) {
-          char msg[256];
-          snprintf(msg, sizeof msg, "%s in BGZF block at %lld", status_name(st[(size_t)j]),
-                   (long long)(bp[(size_t)j] + ctx->base));
-          RET(DQ_EFORMAT, msg);
-        }
+      if (bad != ~0ull) {
+        int32_t st = 0;
+        HIPCHK(hipMemcpy(&st, ctx->status.as<int32_t>() + bad, 4, hipMemcpyDeviceToHost));
+        char msg[256];
+        snprintf(msg, sizeof msg, "%s in BGZF block at %lld", status_name(st),
+                 (long long)(bp[(size_t)bad] + ctx->base));
+        RET(DQ_EFORMAT, msg);
+      }
     }
     // 4. windowed record chains
     const int64_t SEG = 64 * 1024;
@@ -1730,6 +1747,12 @@ static int run_span(dq_ctx* ctx, const dq_traversal* tr, dq_stats* out) {
                              ctx->span_idx.as<int64_t>(), nidx, ctx->iv_ref.as<int32_t>(),
                              ctx->iv_start.as<int32_t>(), ctx->iv_end.as<int32_t>(),
                              ctx->iv_begin.as<int32_t>(), ctx->n_ref, ctx->keep.as<uint8_t>(), s);
+      if (tail_chunk >= 0) {
+        unsigned long long* d_first = reinterpret_cast<unsigned long long*>(ctx->scal.as<char>() + 152);
+        HIPCHK(hipMemsetAsync(d_first, 0xff, 8, s));
+        launch_tail_keep(ctx->span_idx.as<int64_t>(), d_off, (int)tail_chunk, ctx->f_ref.as<int32_t>(),
+                         d_first, ctx->keep.as<uint8_t>(), nidx, s);
+      }
       launch_keep_to_i32(ctx->keep.as<uint8_t>(), nidx, ctx->span_keep32.as<int32_t>(), s);
       if ((rc = ensure_scan(ctx, nidx))) return rc;
       launch_exclusive_scan_i32(ctx->span_keep32.as<int32_t>(), ctx->span_off.as<int64_t>(), nidx,
@@ -2660,8 +2683,8 @@ int dq_run_resident(dq_ctx* ctx, const dq_traversal* tr, dq_stats* stats) {
     RET(DQ_EINVAL, "Traversing mapped reads only is not supported.");
   if (int rc0 = check_tail_reachable(ctx, tr)) return rc0;
   int rc;
-  if (tr && tr->has_intervals && tr->n > 0 && !tr->traverse_unplaced_unmapped && ctx->have_bai &&
-      !ctx->o.full_traversal && !ctx->chunk_mode) {
+  if (tr && tr->has_intervals && tr->n > 0 && ctx->have_bai && !ctx->o.full_traversal &&
+      !ctx->chunk_mode) {
     // .bai span run: only the spans' blocks are inflated; the partition plans come from a full
     // run of the open file (made once here if there is none yet)
     if (!ctx->plan_cached) {

@@ -116,11 +116,22 @@ struct alignas(16) LdsI {
           uint8_t lens[320];      // litlen lengths [0, 288), distance lengths [288, 320)
           uint8_t clen[20];
           uint16_t clt[128];      // code-length code: sym << 3 | len (len 0 = invalid)
-          int32_t cntw[8];        // per-wave counts of second-level tables
-          int32_t cnts[8];        // per-wave second-level entries
-          uint32_t ginfo[MAXGRP + 32];  // per second-level table (litlen, then distance): offset | sb << 16
-          uint32_t cntp[8][8];    // per-wave counts of each code length, 16 bits per length
-          uint16_t pref[320];     // root prefix of each long code, by canonical position
+          union {
+            struct {              // build_tables
+              int32_t cntw[8];    // per-wave counts of second-level tables
+              int32_t cnts[8];    // per-wave second-level entries
+              uint32_t ginfo[MAXGRP + 32];  // per second-level table (litlen, then distance): offset | sb << 16
+              uint32_t cntp[8][8];  // per-wave counts of each code length, 16 bits per length
+              uint16_t pref[320];   // root prefix of each long code, by canonical position
+            };
+            struct {              // read_lengths: one 128-bit window per wave
+              uint8_t exitm[8][16];  // window w entered at offset e < 16 -> entry offset into w + 1
+              int32_t ent[9];        // true entry offset of each window (255: none)
+              int32_t wt[8];         // lengths the window's path symbols write
+              int32_t lv[8];         // the window's last non-repeat value (-1 none)
+              int32_t endp;          // bit position after the last code-length symbol
+            };
+          };
         } h;
       } x;
     } d;
@@ -661,35 +672,38 @@ DQ_AI void build_tables(LdsI& L, int nlen, int ndist) {
   __syncthreads();
 }
 
-// Dynamic header: decode the code-length sequence (wave 0) into L.u.d.x.h.lens.
+// Dynamic header: decode the code-length sequence into L.u.d.x.h.lens, all eight waves at once.
 // Returns the bit position after the header, or sets M_ERR.
-// 128 bit offsets per step: lane l decodes the symbol at offsets l and 64 + l of the window
-// (entries e = l and 64 + l); the true path from entry 0 is found by pointer doubling over the
-// entries (successor^(2^b), b < 7, by lane shuffles of both halves), then entry k takes the k-th
-// symbol of the path; repeat values are forward-filled by max-scans and runs placed by sum-scans.
-// A 128-bit window holds ~30 code-length symbols: half the steps of a 64-bit window for two more
-// dependent shuffle levels.
-DQ_AI uint32_t read_lengths(const uint32_t* __restrict__ W, LdsI& L, uint32_t P, int nlen,
-                                 int ndist, uint32_t endbits, uint32_t hbase, int& nit) {
+// Wave w takes the 128-bit window w of a 1024-bit pass: lane l decodes the symbol at offsets l and
+// 64 + l of its window (entries e = l and 64 + l) and the window's successor table is doubled
+// (successor^(2^b), b < 7, by lane shuffles of both halves).  A window's true path enters at one of
+// its first 14 offsets (a code-length symbol is at most 7 + 7 bits), so each wave first maps every
+// such entry to its exit into the next window; one thread chains the eight maps from the pass's
+// start, and every wave then takes the path from its true entry: entry k of the window takes the
+// k-th symbol of the path.  Repeat values are forward-filled by max-scans and runs placed by
+// sum-scans, across windows through per-window totals (zero runs need no stores: the lengths are
+// zero-filled).  Round 2 ran this serially over the windows in wave 0 (~25k cycles per header).
+DQ_AI uint32_t read_lengths(LdsI& L, uint32_t P, int nlen, int ndist, uint32_t endbits, uint32_t hbase) {
   // the header's compressed words were staged in the (not yet built) decode table: HB_WORDS
   // words cover the longest possible header (17 + 57 + 320 * 14 bits)
   const uint32_t* hb = reinterpret_cast<const uint32_t*>(L.u.d.T);
   auto word = [&](uint32_t i) -> uint32_t { return hb[min(i - hbase, (uint32_t)HB_WORDS - 1)]; };
-  const int lane = tid_fresh() & 63;
+  auto& H = L.u.d.x.h;
+  const int t = tid_fresh(), lane = t & 63, w = t >> 6;
   const int total = nlen + ndist;
-  int have = 0, prev = -1;
+  int have = 0, prev = -1;  // workgroup-uniform
   // successor^(2^b) of entry h * 64 + lane, 128 = past the window; a lookup of entry y
   auto look = [&](int v0, int v1, int y) -> int {
     const int a = __shfl(v0, y & 63, 64), c = __shfl(v1, y & 63, 64);
     return y >= 128 ? 128 : (y >= 64 ? c : a);
   };
-  for (int iter = 0; iter < 400 && have < total; iter++) {
-    nit++;
+  for (int pass = 0; pass < 8 && have < total; pass++) {
     if (P > endbits) {
       set_err(L, ST_OVERREAD);
       return P;
     }
-    const uint32_t wi = P >> 5, off = P & 31;
+    const uint32_t Wb = P + 128u * (uint32_t)w;
+    const uint32_t wi = Wb >> 5, off = Wb & 31;
     const uint32_t k0 = (off + (uint32_t)lane) >> 5, sh = (off + (uint32_t)lane) & 31;
     uint32_t bits[2];
     bits[0] = __builtin_amdgcn_alignbit(word(wi + k0 + 1), word(wi + k0), sh);
@@ -697,7 +711,7 @@ DQ_AI uint32_t read_lengths(const uint32_t* __restrict__ W, LdsI& L, uint32_t P,
     int s[2], rep[2], adv[2], J[7][2];
 #pragma unroll
     for (int h = 0; h < 2; h++) {
-      const uint32_t ent = L.u.d.x.h.clt[bits[h] & 127];
+      const uint32_t ent = H.clt[bits[h] & 127];
       const uint32_t cl = ent & 7, sy = ent >> 3;
       const uint32_t ex = sy == 16 ? 2u : sy == 17 ? 3u : sy == 18 ? 7u : 0u;
       const uint32_t xv = (bits[h] >> cl) & ((1u << ex) - 1);
@@ -711,12 +725,35 @@ DQ_AI uint32_t read_lengths(const uint32_t* __restrict__ W, LdsI& L, uint32_t P,
     for (int b = 1; b < 7; b++)
 #pragma unroll
       for (int h = 0; h < 2; h++) J[b][h] = look(J[b - 1][0], J[b - 1][1], J[b - 1][h]);
-    // entry k = h * 64 + lane takes the k-th symbol of the path from entry 0
+    {  // exit of the path entered at offset `lane` (< 16): its last position inside the window
+       // (largest jumps that stay inside), then that symbol's successor
+      int x = lane & 15;
+#pragma unroll
+      for (int b = 6; b >= 0; b--) {
+        const int y = look(J[b][0], J[b][1], x);
+        x = y < 128 ? y : x;
+      }
+      const int ax = look(adv[0], adv[1], x);
+      const int ex = ax ? x + ax - 128 : 255;  // 255: the path meets an invalid code
+      if (lane < 16) H.exitm[w][lane] = (uint8_t)(ex >= 0 && ex < 16 ? ex : 255);
+    }
+    __syncthreads();
+    if (t == 0) {
+      int e = 0;
+      for (int v = 0; v < 8; v++) {
+        H.ent[v] = e;
+        e = e < 16 ? H.exitm[v][e] : 255;
+      }
+      H.ent[8] = e;
+    }
+    __syncthreads();
+    const int entry = H.ent[w];
+    // entry k = h * 64 + lane takes the k-th symbol of the path from `entry`
     uint32_t pm[4] = {0, 0, 0, 0};  // the path as a 128-bit mask
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const int k = lane + 64 * h;
-      int pk = 0;
+      int pk = entry < 128 ? entry : 128;
 #pragma unroll
       for (int b = 0; b < 7; b++) {
         const int y = look(J[b][0], J[b][1], pk);
@@ -730,55 +767,78 @@ DQ_AI uint32_t read_lengths(const uint32_t* __restrict__ W, LdsI& L, uint32_t P,
     bool onp[2];
     onp[0] = (lane < 32 ? pm[0] >> lane : pm[1] >> (lane - 32)) & 1;
     onp[1] = (lane < 32 ? pm[2] >> lane : pm[3] >> (lane - 32)) & 1;
-    // take path symbols while the lengths read so far are < total
+    // lengths written by the path symbols before each entry; the last non-repeat value
     int rp[2], rinc[2];
     rp[0] = onp[0] ? rep[0] : 0;
     rp[1] = onp[1] ? rep[1] : 0;
     rinc[0] = wave_incl_scan(rp[0], lane);
     rinc[1] = wave_incl_scan(rp[1], lane) + __builtin_amdgcn_readlane(rinc[0], 63);
+    const int v00 = s[0] < 16 ? s[0] : 0, v01 = s[1] < 16 ? s[1] : 0;
+    const int key0 = wave_incl_max(onp[0] && s[0] != 16 ? ((lane + 1) << 5) | v00 : 0);
+    const int key1 = max(wave_incl_max(onp[1] && s[1] != 16 ? ((lane + 65) << 5) | v01 : 0),
+                         __builtin_amdgcn_readlane(key0, 63));
+    if (lane == 63) {
+      H.wt[w] = rinc[1];
+      H.lv[w] = key1 > 0 ? (key1 & 31) : -1;
+    }
+    __syncthreads();
+    int have_w = have, prev_w = prev, wsum = 0, lvall = prev;
+    for (int v = 0; v < 8; v++) {
+      const int wt = H.wt[v], lv = H.lv[v];
+      if (v < w) {
+        have_w += wt;
+        prev_w = lv >= 0 ? lv : prev_w;
+      }
+      wsum += wt;
+      lvall = lv >= 0 ? lv : lvall;
+    }
+    // take path symbols while the lengths read so far are < total
     bool take[2];
-    take[0] = onp[0] && have + rinc[0] - rp[0] < total;
-    take[1] = onp[1] && have + rinc[1] - rp[1] < total;
-    const uint64_t mark0 = __ballot(take[0]), mark1 = __ballot(take[1]);
-    // entry 0 is always taken (have < total)
-    const int lastl = mark1 ? 64 + 63 - __clzll(mark1) : 63 - __clzll(mark0);
-    const int ll = lastl & 63;
-    const int cum = have + (lastl >= 64 ? __builtin_amdgcn_readlane(rinc[1], ll) : __builtin_amdgcn_readlane(rinc[0], ll));
-    const int j = lastl + (lastl >= 64 ? __builtin_amdgcn_readlane(adv[1], ll) : __builtin_amdgcn_readlane(adv[0], ll));
-    if (__any((take[0] && adv[0] == 0) || (take[1] && adv[1] == 0)) || cum > total) {
-      set_err(L, ST_BAD_TABLE);
-      return P;
-    }
-    // value written by each symbol: 0-15 literal length, 17/18 zero, 16 the previous value; a
-    // repeat (16) takes the value of the nearest taken non-repeat symbol below it, else the last
-    // value of the previous window: forward fill by a max-scan of (entry + 1) << 5 | value
+    take[0] = onp[0] && have_w + rinc[0] - rp[0] < total;
+    take[1] = onp[1] && have_w + rinc[1] - rp[1] < total;
     int val[2];
-    {
-      const int v00 = s[0] < 16 ? s[0] : 0, v01 = s[1] < 16 ? s[1] : 0;
-      const int key0 = wave_incl_max(take[0] && s[0] != 16 ? ((lane + 1) << 5) | v00 : 0);
-      const int key1 = max(wave_incl_max(take[1] && s[1] != 16 ? ((lane + 65) << 5) | v01 : 0),
-                           __builtin_amdgcn_readlane(key0, 63));
-      val[0] = (take[0] && s[0] == 16) ? (key0 > 0 ? (key0 & 31) : prev) : v00;
-      val[1] = (take[1] && s[1] == 16) ? (key1 > 0 ? (key1 & 31) : prev) : v01;
-    }
-    if (__any((take[0] && s[0] == 16 && val[0] < 0) || (take[1] && s[1] == 16 && val[1] < 0))) {
+    val[0] = (take[0] && s[0] == 16) ? (key0 > 0 ? (key0 & 31) : prev_w) : v00;
+    val[1] = (take[1] && s[1] == 16) ? (key1 > 0 ? (key1 & 31) : prev_w) : v01;
+    if ((take[0] && (adv[0] == 0 || (s[0] == 16 && val[0] < 0))) ||
+        (take[1] && (adv[1] == 0 || (s[1] == 16 && val[1] < 0))))
       set_err(L, ST_BAD_TABLE);
-      return P;
-    }
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const int r = take[h] ? rep[h] : 0;
       if (take[h] && val[h] != 0) {  // lens is zero-filled: zero runs (up to 138) need no stores
-        for (int i = have + rinc[h] - r; i < have + rinc[h]; i++)
-          L.u.d.x.h.lens[i < nlen ? i : 288 + i - nlen] = (uint8_t)val[h];
+        for (int i = have_w + rinc[h] - r; i < have_w + rinc[h] && i < total; i++)
+          H.lens[i < nlen ? i : 288 + i - nlen] = (uint8_t)val[h];
       }
     }
-    prev = lastl >= 64 ? __builtin_amdgcn_readlane(val[1], ll) : __builtin_amdgcn_readlane(val[0], ll);
-    have = cum;
-    P += (uint32_t)j;
+    // the window where the lengths reach total publishes the header's end (and checks the last
+    // symbol does not run past total)
+    if (have_w < total && have_w + H.wt[w] >= total) {
+      const uint64_t mark0 = __ballot(take[0]), mark1 = __ballot(take[1]);
+      const int lastl = mark1 ? 64 + 63 - __clzll(mark1) : 63 - __clzll(mark0);
+      const int ll = lastl & 63;
+      const int cum = have_w + (lastl >= 64 ? __builtin_amdgcn_readlane(rinc[1], ll) : __builtin_amdgcn_readlane(rinc[0], ll));
+      const int j = lastl + (lastl >= 64 ? __builtin_amdgcn_readlane(adv[1], ll) : __builtin_amdgcn_readlane(adv[0], ll));
+      if (lane == 0) {
+        if (cum > total) set_err(L, ST_BAD_TABLE);
+        H.endp = (int32_t)(Wb + (uint32_t)j);
+      }
+    }
+    have += wsum;
+    prev = lvall;
+    const uint32_t nextP = P + 1024u + (uint32_t)H.ent[8];
+    if (have < total && H.ent[8] >= 16) {  // the path met an invalid code before total
+      set_err(L, ST_BAD_TABLE);
+      return P;
+    }
+    __syncthreads();  // H.endp / lens visible; ent, wt, lv reused by the next pass
+    if (L.misc[M_ERR]) return P;
+    P = nextP;
   }
-  if (have < total) set_err(L, ST_BAD_TABLE);
-  return P;
+  if (have < total) {
+    set_err(L, ST_BAD_TABLE);
+    return P;
+  }
+  return (uint32_t)H.endp;
 }
 
 template <bool TIMING, int NB, int G>
@@ -919,22 +979,19 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       }
       __syncthreads();
       if (L.misc[M_ERR]) break;
-      if (wv == 0) {
-        // the serial critical path of the block: win issue arbitration against the other
-        // workgroup's waves on this SIMD (the guard must be provably wave-uniform)
-        if (__builtin_amdgcn_readfirstlane(t) < 64) __builtin_amdgcn_s_setprio(3);
+      {
         const uint64_t tr0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
-        int nit = 0;
-        const uint32_t a = read_lengths(W, L, clpos + 3 * (uint32_t)ncode, nlen, ndist, endbits, hbase, nit);
-        (void)nit;
+        const uint32_t a = read_lengths(L, clpos + 3 * (uint32_t)ncode, nlen, ndist, endbits, hbase);
         if (t == 0) L.misc[M_A] = (int32_t)a;
-        // the wave that wrote the lengths checks for an EOB code (its own stores are ordered)
-        if (t == 0 && L.misc[M_ERR] == 0 && L.u.d.x.h.lens[256] == 0) set_err(L, ST_BAD_TABLE);
         if (TIMING && t == 0) tacc[8] += __builtin_amdgcn_s_memtime() - tr0;
-        if (__builtin_amdgcn_readfirstlane(t) < 64) __builtin_amdgcn_s_setprio(0);
       }
       __syncthreads();
       if (L.misc[M_ERR]) break;
+      // an EOB code is required
+      if (L.u.d.x.h.lens[256] == 0) {
+        if (t == 0) L.misc[M_ERR] = ST_BAD_TABLE;
+        break;
+      }
     }
     TST(0);
     // ---- 2. tables

@@ -68,6 +68,12 @@ void launch_chain2(const uint8_t* C, int64_t L, const Cand* cand, const int64_t*
                    const int64_t* voff, int64_t* blk_pos, int32_t* blk_csize, int32_t* blk_usize,
                    int64_t blk_cap, int64_t* d_nblk, int32_t* d_broken, int32_t eof_in_buf,
                    hipStream_t s);
+// out[0] = min pos of the valid candidates (out initialised to all ones), out[1] = blk_pos[0].
+void launch_chain_check(const Cand* cand, const int64_t* d_ncand, int64_t cap, const int64_t* blk_pos,
+                        const int64_t* d_nblk, unsigned long long* out, hipStream_t s);
+// out[0] = the first block index (through sel when given) whose status is not ST_OK.
+void launch_first_bad(const int32_t* status, const int32_t* sel, int64_t n, unsigned long long* out,
+                      hipStream_t s);
 // Serial fallback chain walk (one lane) over htsjdk headers from `start`.
 void launch_chain_serial(const uint8_t* C, int64_t clen, int64_t start, int64_t* blk_pos,
                          int32_t* blk_csize, int32_t* blk_usize, int64_t cap, int64_t* d_nblk,
@@ -195,6 +201,10 @@ void launch_span_ranges(const uint64_t* voffset, int64_t nrec, const uint64_t* c
                         const uint64_t* cend, int64_t nchunk, int64_t* first, int64_t* count,
                         hipStream_t s);
 void launch_keep_to_i32(const uint8_t* keep, int64_t n, int32_t* out, hipStream_t s);
+// Span-run unplaced tail: keep flags of chunk k's entries (idx[off[k]..off[k+1])) = from the first
+// record with refID == -1 on (*first: device scratch, initialised to all ones).
+void launch_tail_keep(const int64_t* idx, const int64_t* off, int k, const int32_t* ref,
+                      unsigned long long* first, uint8_t* keep, int64_t max_n, hipStream_t s);
 void launch_gather_i64(const int64_t* src, const int64_t* pos, int64_t n, int64_t* dst,
                        hipStream_t s);
 void launch_compact_kept(const int64_t* idx, const uint8_t* keep, const int64_t* off, int64_t n,

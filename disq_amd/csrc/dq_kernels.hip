@@ -1282,6 +1282,48 @@ void launch_chain2(const uint8_t* C, int64_t L, const Cand* cand, const int64_t*
                      eof_in_buf);
 }
 
+// Chain start of a shard (the first valid candidate: the guesser's first block of its first
+// split) as a device min-reduction, plus a copy of the chain's first block position, so the host
+// reads both with the block count in one small copy.  out[0] = min valid pos (initialised to
+// all ones by the caller), out[1] = blk_pos[0].
+__global__ void chain_check_kernel(const Cand* __restrict__ cand, const int64_t* __restrict__ ncand,
+                                   const int64_t* __restrict__ blk_pos, const int64_t* __restrict__ d_nblk,
+                                   unsigned long long* __restrict__ out) {
+  const int64_t n = *ncand;
+  unsigned long long best = ~0ull;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    if (cand[i].valid == 1) best = min(best, (unsigned long long)cand[i].pos);
+  for (int o = 32; o >= 1; o >>= 1) best = min(best, (unsigned long long)__shfl_xor(best, o, 64));
+  if ((threadIdx.x & 63) == 0 && best != ~0ull) atomicMin(&out[0], best);
+  if (blockIdx.x == 0 && threadIdx.x == 0) out[1] = *d_nblk > 0 ? (unsigned long long)blk_pos[0] : ~0ull;
+}
+
+// First block whose status is not ST_OK: a device min-reduction of the block index into out[0]
+// (initialised to all ones by the caller); the host reads one word instead of the status array.
+__global__ void first_bad_kernel(const int32_t* __restrict__ status, const int32_t* __restrict__ sel,
+                                 int64_t n, unsigned long long* __restrict__ out) {
+  unsigned long long best = ~0ull;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = sel ? (int64_t)sel[i] : i;
+    if (status[b] != 0) best = min(best, (unsigned long long)b);
+  }
+  for (int o = 32; o >= 1; o >>= 1) best = min(best, (unsigned long long)__shfl_xor(best, o, 64));
+  if ((threadIdx.x & 63) == 0 && best != ~0ull) atomicMin(out, best);
+}
+
+void launch_chain_check(const Cand* cand, const int64_t* d_ncand, int64_t cap, const int64_t* blk_pos,
+                        const int64_t* d_nblk, unsigned long long* out, hipStream_t s) {
+  const unsigned g = (unsigned)std::min<int64_t>(1024, std::max<int64_t>(1, (cap + 255) / 256));
+  hipLaunchKernelGGL(chain_check_kernel, dim3(g), dim3(256), 0, s, cand, d_ncand, blk_pos, d_nblk, out);
+}
+
+void launch_first_bad(const int32_t* status, const int32_t* sel, int64_t n, unsigned long long* out,
+                      hipStream_t s) {
+  if (n <= 0) return;
+  const unsigned g = (unsigned)std::min<int64_t>(1024, (n + 255) / 256);
+  hipLaunchKernelGGL(first_bad_kernel, dim3(g), dim3(256), 0, s, status, sel, n, out);
+}
+
 void launch_chain_serial(const uint8_t* C, int64_t clen, int64_t start, int64_t* blk_pos,
                          int32_t* blk_csize, int32_t* blk_usize, int64_t cap, int64_t* d_nblk,
                          int32_t* d_status, hipStream_t s) {
@@ -1448,6 +1490,34 @@ void launch_span_ranges(const uint64_t* voffset, int64_t nrec, const uint64_t* c
   if (nchunk <= 0) return;
   hipLaunchKernelGGL(span_ranges_kernel, dim3((unsigned)((nchunk + 255) / 256)), dim3(256), 0, s,
                      voffset, nrec, cbeg, cend, nchunk, first, count);
+}
+
+// The unplaced-unmapped tail of a span run (BAMFileIndexUnmappedIterator, H/BAMFileReader2.java:
+// 1199-1206, after queryUnmapped's seek to the start of the last linear bin): of the records
+// idx[off[k]], .. idx[off[k+1]-1] of the tail chunk k, skip until the first with refID == -1 and
+// keep every one from there.  Pass 1: the first such entry (min-reduction into *first, initialised
+// to all ones); pass 2: the keep flags of the chunk's entries.
+__global__ void tail_first_kernel(const int64_t* __restrict__ idx, const int64_t* __restrict__ off, int k,
+                                  const int32_t* __restrict__ ref, unsigned long long* __restrict__ first) {
+  const int64_t a = off[k], b = off[k + 1];
+  unsigned long long best = ~0ull;
+  for (int64_t i = a + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < b; i += (int64_t)gridDim.x * blockDim.x)
+    if (ref[idx[i]] == -1) best = min(best, (unsigned long long)i);
+  for (int o = 32; o >= 1; o >>= 1) best = min(best, (unsigned long long)__shfl_xor(best, o, 64));
+  if ((threadIdx.x & 63) == 0 && best != ~0ull) atomicMin(first, best);
+}
+__global__ void tail_keep_kernel(const int64_t* __restrict__ off, int k,
+                                 const unsigned long long* __restrict__ first, uint8_t* __restrict__ keep) {
+  const int64_t a = off[k], b = off[k + 1];
+  const unsigned long long f = *first;
+  for (int64_t i = a + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < b; i += (int64_t)gridDim.x * blockDim.x)
+    keep[i] = (unsigned long long)i >= f ? 1 : 0;
+}
+void launch_tail_keep(const int64_t* idx, const int64_t* off, int k, const int32_t* ref,
+                      unsigned long long* first, uint8_t* keep, int64_t max_n, hipStream_t s) {
+  const unsigned g = (unsigned)std::min<int64_t>(1024, std::max<int64_t>(1, (max_n + 255) / 256));
+  hipLaunchKernelGGL(tail_first_kernel, dim3(g), dim3(256), 0, s, idx, off, k, ref, first);
+  hipLaunchKernelGGL(tail_keep_kernel, dim3(g), dim3(256), 0, s, off, k, first, keep);
 }
 
 void launch_keep_to_i32(const uint8_t* keep, int64_t n, int32_t* out, hipStream_t s) {

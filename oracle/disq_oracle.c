@@ -1038,6 +1038,149 @@ int dqo_run_partitions(const uint8_t* data, int64_t len, const int64_t* starts,
   return j.err ? DQO_EFORMAT : 0;
 }
 
+/* ------------------------------------------------------------------ interval traversal, all
+ * partitions (bench-scale parity of the GPU span runs): per partition, the records of the .bai span
+ * of the optimized intervals clipped to the partition chunk (AbstractBinarySamSource.java:102-112;
+ * spans = 0 reads the whole chunk) that overlap an interval (the filter of :113-115), then, when
+ * asked, the unplaced-unmapped tail of the partition holding the start of the last linear bin
+ * (:116-129).  q = optimized intervals (sorted, disjoint per reference), so the overlap test is a
+ * binary search equal to dqo_record_overlaps.  Per-partition count + ordered digest, as
+ * dqo_run_partitions. */
+typedef struct {
+  const uint8_t* data;
+  int64_t len;
+  const int64_t *starts, *ends;
+  int64_t n;
+  const uint8_t* bai;
+  int64_t bai_len;
+  const int32_t *qr, *qs, *qe;
+  int64_t nq;
+  int unplaced, spans;
+  int64_t solb, ncc;
+  int64_t* counts;
+  uint64_t* digests;
+  int64_t next;
+  pthread_mutex_t mu;
+  int err;
+} tjob_t;
+
+static int q_overlaps(const tjob_t* j, const dqo_rec* r) {
+  const int32_t astart = r->pos + 1;
+  const int32_t aend = ((r->flag & 4) && astart != 0) ? astart : r->align_end;
+  /* first interval of r's reference whose end >= astart */
+  int64_t lo = 0, hi = j->nq;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) / 2;
+    if (j->qr[mid] < r->ref_id || (j->qr[mid] == r->ref_id && qend(j->qe[mid]) < astart)) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < j->nq && j->qr[lo] == r->ref_id && j->qs[lo] <= aend;
+}
+
+static void* tworker(void* arg) {
+  tjob_t* j = (tjob_t*)arg;
+  dqo_file* f = dqo_open_mem(j->data, j->len, 0);
+  int32_t nr, dummy;
+  uint64_t first;
+  if (dqo_read_header(f, &nr, &first, &dummy, 0) != 0) {
+    j->err = 1;
+    dqo_close(f);
+    return NULL;
+  }
+  rdr r;
+  rdr_init(&r, f);
+  uint8_t* buf = NULL;
+  int64_t bufcap = 0, spcap = 0;
+  uint64_t *sb = NULL, *se = NULL;
+  for (;;) {
+    pthread_mutex_lock(&j->mu);
+    int64_t i = j->next++;
+    pthread_mutex_unlock(&j->mu);
+    if (i >= j->n) break;
+    uint64_t vs, ve;
+    int64_t cnt = 0;
+    uint64_t dig = 0;
+    int res = first_read(&r, j->starts[i], j->ends[i], &vs, &ve);
+    if (res < 0) { j->err = 1; break; }
+    if (res == 1) {
+      /* the chunks to read: the clipped span, or the whole chunk */
+      int64_t nsp = 1;
+      if (j->nq > 0 && j->spans) {
+        nsp = dqo_bai_span(j->bai, j->bai_len, j->qr, j->qs, j->qe, j->nq, vs, ve, NULL, NULL, 0);
+        if (nsp < 0) { j->err = 1; break; }
+      }
+      if (nsp > spcap) {
+        spcap = nsp + 16;
+        sb = (uint64_t*)realloc(sb, sizeof(uint64_t) * (size_t)spcap);
+        se = (uint64_t*)realloc(se, sizeof(uint64_t) * (size_t)spcap);
+      }
+      if (j->nq > 0 && j->spans) dqo_bai_span(j->bai, j->bai_len, j->qr, j->qs, j->qe, j->nq, vs, ve, sb, se, nsp);
+      else { sb[0] = vs; se[0] = ve; }
+      for (int64_t k = 0; j->nq > 0 && k < nsp; k++) {
+        if (rdr_seek(&r, sb[k]) != 0) continue;
+        for (;;) {
+          uint64_t v = rdr_ptr(&r);
+          if (v >= se[k]) break;
+          int32_t bs;
+          int rr = read_record(&r, &buf, &bufcap, &bs);
+          if (rr <= 0) { if (rr < 0) j->err = 1; break; }
+          dqo_rec rec;
+          fill_rec(&rec, v, buf, bs);
+          if (!q_overlaps(j, &rec)) continue;
+          dig += mix64(rec.hash + ((uint64_t)cnt + 1) * 0x9E3779B97F4A7C15ULL);
+          cnt++;
+        }
+      }
+      if (j->unplaced && j->solb != -1 && j->ncc >= 1 && vs <= (uint64_t)j->solb &&
+          (uint64_t)j->solb < ve && rdr_seek(&r, (uint64_t)j->solb) == 0) {
+        int skipping = 1;  /* BAMFileIndexUnmappedIterator */
+        for (;;) {
+          uint64_t v = rdr_ptr(&r);
+          int32_t bs;
+          int rr = read_record(&r, &buf, &bufcap, &bs);
+          if (rr <= 0) { if (rr < 0) j->err = 1; break; }
+          if (skipping && rd32(buf + 4) != -1) continue;
+          skipping = 0;
+          (void)v;
+          uint64_t h = dqo_record_hash(buf, 4 + (int64_t)bs);
+          dig += mix64(h + ((uint64_t)cnt + 1) * 0x9E3779B97F4A7C15ULL);
+          cnt++;
+        }
+      }
+    }
+    j->counts[i] = cnt;
+    j->digests[i] = dig;
+  }
+  free(sb);
+  free(se);
+  free(buf);
+  rdr_free(&r);
+  dqo_close(f);
+  return NULL;
+}
+
+int dqo_run_partitions_traversal(const uint8_t* data, int64_t len, const int64_t* starts,
+                                 const int64_t* ends, int64_t n, int nthreads,
+                                 const uint8_t* bai, int64_t bai_len, const int32_t* q_ref,
+                                 const int32_t* q_start, const int32_t* q_end, int64_t nq,
+                                 int unplaced, int spans, int64_t* counts, uint64_t* digests) {
+  if (nthreads < 1) nthreads = 1;
+  tjob_t j;
+  memset(&j, 0, sizeof j);
+  j.data = data; j.len = len; j.starts = starts; j.ends = ends; j.n = n;
+  j.bai = bai; j.bai_len = bai_len; j.qr = q_ref; j.qs = q_start; j.qe = q_end; j.nq = nq;
+  j.unplaced = unplaced; j.spans = spans; j.counts = counts; j.digests = digests;
+  int32_t nref;
+  if (dqo_bai_info(bai, bai_len, &nref, &j.solb, &j.ncc) != 0) return DQO_EFORMAT;
+  pthread_mutex_init(&j.mu, NULL);
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
+  for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, tworker, &j);
+  for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+  free(th);
+  pthread_mutex_destroy(&j.mu);
+  return j.err ? DQO_EFORMAT : 0;
+}
+
 /* ================================================================== BGZF text (VCF) path
  * TextInputFormat over a BGZF file with Disq's splittable codecs: per split, the lines Hadoop's
  * LineRecordReader returns.  Restated, as a literal simulation:

@@ -138,6 +138,14 @@ int64_t dqo_inflate_file(dqo_file* f, uint8_t* out, int64_t cap);
 int dqo_run_partitions(const uint8_t* data, int64_t len, const int64_t* starts,
                        const int64_t* ends, int64_t n_splits, int nthreads, int64_t* counts,
                        uint64_t* digests, int64_t* ubytes);
+/* Interval traversal of every partition on nthreads threads: per partition the records of the
+ * .bai span of the optimized intervals q (sorted, disjoint; spans = 0: the whole chunk) that
+ * overlap q, plus the unplaced-unmapped tail when `unplaced`; count + ordered digest. */
+int dqo_run_partitions_traversal(const uint8_t* data, int64_t len, const int64_t* starts,
+                                 const int64_t* ends, int64_t n, int nthreads,
+                                 const uint8_t* bai, int64_t bai_len, const int32_t* q_ref,
+                                 const int32_t* q_start, const int32_t* q_end, int64_t nq,
+                                 int unplaced, int spans, int64_t* counts, uint64_t* digests);
 
 #ifdef __cplusplus
 }

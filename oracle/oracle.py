@@ -108,6 +108,10 @@ def lib():
         L.dqo_run_partitions.argtypes = [C.c_void_p, C.c_int64, P(C.c_int64), P(C.c_int64),
                                          C.c_int64, C.c_int, P(C.c_int64), P(C.c_uint64),
                                          P(C.c_int64)]
+        L.dqo_run_partitions_traversal.argtypes = [
+            C.c_void_p, C.c_int64, P(C.c_int64), P(C.c_int64), C.c_int64, C.c_int, C.c_void_p,
+            C.c_int64, P(C.c_int32), P(C.c_int32), P(C.c_int32), C.c_int64, C.c_int, C.c_int,
+            P(C.c_int64), P(C.c_uint64)]
     return _lib
 
 
@@ -557,3 +561,28 @@ def run_partitions(data: bytes, splits, nthreads):
     if rc != 0:
         raise OracleError("run_partitions failed")
     return cnt, dig, ub
+
+
+def run_partitions_traversal(data: bytes, splits, nthreads, bai: bytes, intervals,
+                             unplaced=False, spans=True):
+    """Interval traversal of every partition (count, digest) on nthreads threads, as
+    OracleBam.read_partitions(traversal=(intervals, unplaced), bai=..., spans=...) followed by
+    stream_digest per partition, but in C: the bench-scale parity of the GPU span runs."""
+    buf = np.frombuffer(data, np.uint8)
+    b = np.frombuffer(bai, np.uint8)
+    q = optimize_intervals(intervals) if intervals else []
+    r = np.array([i[0] for i in q] or [0], np.int32)
+    s = np.array([i[1] for i in q] or [0], np.int32)
+    e = np.array([i[2] for i in q] or [0], np.int32)
+    n = len(splits)
+    st = np.array([a for a, _ in splits], np.int64)
+    en = np.array([x for _, x in splits], np.int64)
+    cnt = np.zeros(n, np.int64)
+    dig = np.zeros(n, np.uint64)
+    rc = lib().dqo_run_partitions_traversal(
+        buf.ctypes.data, len(buf), _p(st, C.c_int64), _p(en, C.c_int64), n, nthreads,
+        b.ctypes.data, len(b), _p(r, C.c_int32), _p(s, C.c_int32), _p(e, C.c_int32), len(q),
+        int(unplaced), int(spans), _p(cnt, C.c_int64), _p(dig, C.c_uint64))
+    if rc != 0:
+        raise OracleError("run_partitions_traversal failed")
+    return cnt, dig

@@ -24,11 +24,11 @@ def intervals(n, lo, hi, ref=0, seed=3, min_len=20, max_len=5000):
     return [(ref, int(s), int(min(hi, s + l - 1))) for s, l in zip(st, ln)]
 
 
-def gpu_span(data, bai, split, ivs, full=False):
+def gpu_span(data, bai, split, ivs, full=False, unplaced=False):
     with _lib.Context(split_size=split, verify_crc=True, full_traversal=full) as c:
         c.open_bytes(data)
         c.set_index(bai)
-        st = c.run_resident((ivs, False))
+        st = c.run_resident((ivs, unplaced))
         cnt, dig = c.partition_digests()
     return st, cnt, dig
 
@@ -85,3 +85,21 @@ def test_long_read_spans_grow_windows():
     st, cnt, dig = gpu_span(w.bam, w.bai, 256 * 1024, ivs)
     ocnt, odig = oracle_parts(ob, 256 * 1024, ivs, w.bai)
     assert np.array_equal(cnt, ocnt) and np.array_equal(dig, odig)
+
+
+@pytest.mark.parametrize("split", [1 << 20, 256 * 1024])
+def test_wgs_spans_with_unplaced_tail(split):
+    """traverseUnplacedUnmapped in a span run: the partition holding the start of the last linear
+    bin appends the unplaced-unmapped tail after its interval records
+    (AbstractBinarySamSource.java:116-129); every partition = the oracle's traversal."""
+    w = synth.generate(60000, seed=29, bai=True, nthreads=8, unplaced_fraction=0.02)
+    ivs = intervals(400, 1, 290000, seed=7, max_len=600)
+    st, cnt, dig = gpu_span(w.bam, w.bai, split, ivs, unplaced=True)
+    ocnt, odig = O.run_partitions_traversal(w.bam, O.path_splits(len(w.bam), split), 4, w.bai,
+                                            ivs, True)
+    c0, _ = O.run_partitions_traversal(w.bam, O.path_splits(len(w.bam), split), 4, w.bai, ivs,
+                                       False)
+    assert ocnt.sum() > c0.sum() + 500  # the tail is there
+    assert np.array_equal(cnt, ocnt)
+    assert np.array_equal(dig, odig)
+    assert st.n_filtered == int(ocnt.sum())

@@ -46,3 +46,40 @@ def test_span_is_clipped_to_the_chunk():
     right = O.bai_span(a.bai, q, mid, ve)
     assert all(vs <= b and e <= mid for b, e in left)
     assert all(mid <= b and e <= ve for b, e in right)
+
+
+def _py_parts(ob, split, ivs, bai, unplaced, spans):
+    parts = iter(ob.read_partitions(split, traversal=(ivs, unplaced), bai=bai, spans=spans))
+    cnt, dig = [], []
+    for _, _, ch in ob.plan(split):
+        if ch is None:
+            cnt.append(0)
+            dig.append(0)
+            continue
+        p = next(parts)
+        cnt.append(len(p))
+        dig.append(O.stream_digest(p["hash"]))
+    return np.array(cnt), np.array(dig, np.uint64)
+
+
+@pytest.mark.parametrize("unplaced", [False, True])
+@pytest.mark.parametrize("spans", [True, False])
+def test_c_traversal_equals_the_restatement(unplaced, spans):
+    """oracle.run_partitions_traversal (C, threaded, binary-search overlap test: the bench-scale
+    interval-mode oracle) = read_partitions + stream_digest (the restatement the GPU tests use),
+    with and without the unplaced-unmapped tail (AbstractBinarySamSource.java:116-129)."""
+    w = synth.generate(20000, seed=4, bai=True, unplaced_fraction=0.01, nthreads=4)
+    ob = O.OracleBam(w.bam)
+    rng = np.random.default_rng(2)
+    ivs = [(0, int(s), int(s + rng.integers(10, 3000))) for s in rng.integers(1, 99000, size=80)]
+    ivs += [(1, 1, 0), (5, 100, 200)]  # an open-ended interval; a contig with no reads
+    split = 256 * 1024
+    splits = O.path_splits(len(w.bam), split)
+    cnt, dig = O.run_partitions_traversal(w.bam, splits, 4, w.bai, ivs, unplaced, spans)
+    pcnt, pdig = _py_parts(ob, split, ivs, w.bai, unplaced, spans)
+    assert cnt.sum() > 0 and len(cnt) > 3
+    assert np.array_equal(cnt, pcnt)
+    assert np.array_equal(dig, pdig)
+    if unplaced:
+        c0, _ = O.run_partitions_traversal(w.bam, splits, 4, w.bai, ivs, False, spans)
+        assert cnt.sum() > c0.sum()  # the tail is there
