@@ -27,7 +27,10 @@ def _need(path: str) -> str:
 
 
 def gpu_lib_path() -> str:
-    return _need(GPU_LIB)
+    # DQ_GPU_LIB: an alternative build of the same library (A/B of compile-time kernel variants in
+    # one GPU session; tools/gpu_variant_ab.sh); never set by the product path
+    alt = os.environ.get("DQ_GPU_LIB")
+    return _need(alt if alt else GPU_LIB)
 
 
 def synth_lib_path() -> str:

@@ -316,17 +316,20 @@ enum : int32_t { F_DEAD = 4 };  // speculative path found no boundary >= sB (gar
 // Decode from `start`; output is counted from the first symbol boundary >= sB (*Bp) and the
 // run stops at the first boundary >= sE (*Ep).  Returns F_EXIT / F_EOB (*Ep = bit after EOB) /
 // F_ERR / F_END (ran off the data) / F_DEAD (no boundary >= sB before an error, EOB or the end).
-constexpr int NCK = 8;          // checkpoints per speculative lane
-constexpr uint32_t CKI = 48;    // checkpoint spacing in bits (>= the longest symbol: a symbol
+constexpr int NCK_MAX = 16;     // checkpoints per speculative lane (runtime nck <= NCK_MAX)
+constexpr int NCK_DEFAULT = 8;
+constexpr uint32_t CKI_DEFAULT = 48;  // checkpoint spacing in bits (>= the longest symbol: a symbol
                                 // crosses at most one threshold; most paths re-synchronise
                                 // within ~100 bits, segments are ~160-1000 bits)
 
 // Speculative lanes also record checkpoints: the first symbol boundary at or past sB + CKI * (j+1)
-// (offset from sB << 16 | bytes counted so far), j < NCK, at ck[j * ckstride] (nullptr: none).
+// (offset from sB << 16 | bytes counted so far), j < nck, at ck[j * ckstride] (nullptr: none).
+// A spacing below the longest symbol only loses merges: a merge needs equal bit positions, and
+// equal positions at symbol boundaries are equal decoder states whatever the checkpoint index.
 template <class S>
 DQ_AI int run_seg(const S& W, const LdsI& L, uint32_t start, uint32_t sB,
                   uint32_t sE, uint32_t endbits, int32_t* Bp, int32_t* Ep, int32_t* cntp,
-                  uint32_t* ck = nullptr, int ckstride = 0) {
+                  uint32_t* ck, int ckstride, uint32_t CKI, int NCK) {
   BitR r;
   br_init(r, W, start);
   uint32_t p = br_pos(r);
@@ -381,7 +384,7 @@ DQ_AI int run_seg(const S& W, const LdsI& L, uint32_t start, uint32_t sB,
 template <class S>
 DQ_AI int run_redo(const S& W, const LdsI& L, uint32_t s0, uint32_t sB,
                    uint32_t sE, uint32_t endbits, const uint32_t* ck, int ckstride, int32_t se,
-                   int32_t sc, int32_t* Ep, int32_t* cntp, int* jm = nullptr) {
+                   int32_t sc, int32_t* Ep, int32_t* cntp, uint32_t CKI, int NCK, int* jm = nullptr) {
   BitR r;
   br_init(r, W, s0);
   int32_t cnt = 0;
@@ -847,7 +850,10 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     const int32_t* __restrict__ blk_csize, const int32_t* __restrict__ blk_usize,
     const int64_t* __restrict__ uoff, int64_t nblk, uint8_t* __restrict__ U,
     int32_t* __restrict__ status, int32_t verify_crc, const uint32_t* __restrict__ crc_init,
-    uint64_t* __restrict__ tim, uint32_t OV, uint32_t sflags, const int32_t* __restrict__ sel) {
+    uint64_t* __restrict__ tim, uint32_t OV, uint32_t sflags, const int32_t* __restrict__ sel,
+    uint32_t ckcfg) {
+  const uint32_t CKI = ckcfg & 255u;        // checkpoint spacing (bits)
+  const int NCK = (int)(ckcfg >> 8) & 31;   // checkpoints per lane
   __shared__ LdsI L;
   // DQ_TIMING: thread 0 accumulates s_memtime cycles per phase (tim != nullptr only then)
   uint64_t tacc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -1023,7 +1029,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     const uint32_t span = endbits - a;
     // per-lane arrays live in the not-yet-written tail of the output image
     const int ob = (sh + produced + 3) & ~3;
-    const int cap = (sh + isize - ob) / (4 * (7 + NCK));
+    const int cap = (sh + isize - ob) / (4 * (7 + NCK));  // NCK: this launch's checkpoints
     int32_t* AB;  // verified start (first boundary >= segment start), -1 none
     int32_t* AE;  // exit << 3 | flag
     int32_t* AC;  // output bytes in [B, E)
@@ -1064,7 +1070,8 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       int32_t B = -1, E = 0, c = 0;
       if (CK)
         for (int j = 0; j < NCK; j++) CK[j * nl + t] = 0xffffffffu;
-      const int f = run_seg(gsrc, L, start, sB, sE, endbits, &B, &E, &c, CK ? CK + t : nullptr, nl);
+      const int f = run_seg(gsrc, L, start, sB, sE, endbits, &B, &E, &c, CK ? CK + t : nullptr, nl,
+                            CKI, NCK);
       AB[t] = B;
       AE[t] = (E << 3) | f;
       AC[t] = c;
@@ -1109,7 +1116,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
         const uint32_t sB = a + (uint32_t)lt * seg;
         // a speculative lane that found no boundary (F_DEAD) recorded no checkpoints
         const int f = run_redo(gsrc, L, s0, sB, sE, endbits, CK ? CK + lt : nullptr, nl, SE[lt],
-                               SC[lt], &E, &c, TIMING ? &jmerge : nullptr);
+                               SC[lt], &E, &c, CKI, NCK, TIMING ? &jmerge : nullptr);
         const int32_t ae = (E << 3) | f;
         if (ae != AE[lt]) L.misc[M_DIRTY + (round & 1)] = 1;  // the successor's start moved
         AB[lt] = (int32_t)s0;
@@ -1542,12 +1549,20 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
     if (const char* e = getenv("DQ_CFG")) sscanf(e, "%d,%d", &nb, &g);
     return g == 4 ? 1 : nb == 2 ? 4 : 0;
   }();
+  // checkpoints: DQ_CKI bits apart (8..255), DQ_NCK of them (1..NCK_MAX)
+  static const uint32_t ckcfg = [] {
+    uint32_t cki = getenv("DQ_CKI") ? (uint32_t)atoi(getenv("DQ_CKI")) : CKI_DEFAULT;
+    uint32_t nck = getenv("DQ_NCK") ? (uint32_t)atoi(getenv("DQ_NCK")) : (uint32_t)NCK_DEFAULT;
+    cki = std::min(255u, std::max(8u, cki));
+    nck = std::min((uint32_t)NCK_MAX, std::max(1u, nck));
+    return cki | nck << 8;
+  }();
   // DQ_LDSPAD: extra dynamic LDS per workgroup (occupancy experiments: 80000 = one workgroup per CU)
   static const unsigned ldspad = getenv("DQ_LDSPAD") ? (unsigned)atoi(getenv("DQ_LDSPAD")) : 0u;
 #define DQ_LAUNCH(TM, NBT, GT)                                                                  \
   hipLaunchKernelGGL((inflate_block_kernel<TM, NBT, GT>), dim3((unsigned)ngrid), dim3(WG), ldspad, s, C, \
                      blk_pos, blk_csize, blk_usize, uoff, ngrid, U, status, verify_crc, crc_init, tim, ov, \
-                     sflags, sel)
+                     sflags, sel, ckcfg)
 #define DQ_CFGS(TM)                       \
   switch (cfg) {                          \
     case 1: DQ_LAUNCH(TM, 1, 4); break;   \
