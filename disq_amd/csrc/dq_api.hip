@@ -2389,7 +2389,11 @@ int dq_decode_file_multi(dq_ctx* ctx, const char* path, const int32_t* devices, 
     o.device = devices[r];
     dq_ctx* c = nullptr;
     if ((s.rc = dq_ctx_create(&c, &o))) {
-      s.err = "dq_ctx_create failed on device " + std::to_string(devices[r]);
+      // dq_ctx_create hands back an allocated context on its error paths too: keep its message,
+      // then free it
+      s.err = "dq_ctx_create failed on device " + std::to_string(devices[r]) +
+              (c ? std::string(": ") + dq_last_error(c) : std::string());
+      if (c) dq_ctx_destroy(c);
       return;
     }
     int64_t halo = 4 << 20;

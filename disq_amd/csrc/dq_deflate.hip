@@ -15,11 +15,13 @@
 // hash-chain link, kept in global scratch), then the stripe's positions update the table.  Lane t
 // then owns bytes [255 t, 255 t + 255) and parses them greedily on its own: at each position the
 // longest match of >= 3 bytes among the previous SHORT bytes and the first CHAIN links of its hash
-// chain, clamped to its segment's end, so lanes never wait for each other.  Symbols are coded
-// with the fixed Huffman code (BTYPE 01): a lane's bit count is known as it goes, so each lane
-// stages its bits in its own global-memory slot; an exclusive scan of the counts places every
-// lane's bits, which are OR-ed into the LDS image of the block (the input is dead by then) and
-// stored with 16-byte writes.  A block whose code would not fit BSIZE is stored (BTYPE 00).
+// chain, clamped to its segment's end, so lanes never wait for each other.  Symbols go to a
+// per-lane staging slot and to LDS histograms; wave 0 builds the literal/length code and wave 1
+// the distance code (a rank sort, Moffat-Katajainen minimum-redundancy lengths, a Kraft fix-up
+// capping them at 15), the code-length sequence is run-length coded; the block is coded dynamic
+// (BTYPE 10) or fixed (01), whichever is shorter.  Each lane's bit count gives its offset by an
+// exclusive scan; every lane OR-s its bits into the LDS image of the block (the input is dead by
+// then), stored with 16-byte writes.  A block whose code would not fit BSIZE is stored (BTYPE 00).
 // CRC32: per-lane table CRC over the segment, combined with x^(8 n) mod P multipliers.
 #include "dq_internal.h"
 

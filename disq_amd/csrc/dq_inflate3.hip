@@ -7,24 +7,28 @@
 // A BGZF block is an independent raw-DEFLATE stream of <= 64 KiB output, so blocks are decoded
 // independently: one 512-thread workgroup per block, the whole output image in LDS (two
 // workgroups per CU: 80 KiB of LDS each).  Per deflate block of the stream:
-//   1. header   -- thread 0 reads BFINAL/BTYPE/HLIT/HDIST/HCLEN; 19 threads read the code-length
-//                  code lengths; 128 threads fill its 7-bit decode table; wave 0 decodes the
-//                  code-length sequence 64 bit offsets at a time (every lane decodes the symbol
-//                  at its offset, the true path is walked with readlane, runs are placed by a
-//                  wave scan).
-//   2. tables   -- canonical codes are assigned in parallel (per-wave ballots give each symbol
-//                  its rank among equal lengths); 10-bit litlen / 8-bit distance root tables of
-//                  16-bit entries that carry the decoded value (literal byte, length base and
-//                  extra-bit count, distance base and extra-bit count: ent_ll / ent_d) plus 32 /
-//                  128-entry second-level tables for longer codes, so every code decodes with at
-//                  most two LDS reads and no arithmetic on the symbol number.
-//   3. spec     -- the bit range is cut into NDEC segments; lane t starts decoding at the first
-//                  bit of segment t (an arbitrary bit) and records its EXIT: the first litlen-mode
-//                  symbol boundary at or past the start of segment t+1.  Huffman codes
-//                  self-synchronise, so an exit is almost always on the true symbol path.
-//   4. rounds   -- lane t re-decodes from lane t-1's exit, counting output bytes; a lane whose
-//                  exit changed triggers a re-decode of its successor (Jacobi iteration: lane 0
-//                  starts on the true path, so round r has verified lanes 0..r).
+//   1. header   -- every thread reads BFINAL/BTYPE/HLIT/HDIST/HCLEN; 19 threads read the
+//                  code-length code lengths; 128 threads fill its 7-bit decode table; the eight
+//                  waves decode the code-length sequence, one 128-bit window each: every lane
+//                  decodes the symbols at two offsets, the window's successor table is doubled by
+//                  lane shuffles, each window's exits are chained across the windows by one
+//                  thread, and runs are placed by wave scans (read_lengths).
+//   2. tables   -- canonical codes are assigned in parallel (wave scans of one-hot length
+//                  counters give each symbol its rank among equal lengths); 10-bit litlen / 8-bit
+//                  distance root tables of 16-bit entries that carry the decoded value (literal
+//                  byte, length base and extra-bit count, distance base and extra-bit count:
+//                  ent_ll / ent_d) plus variable-size second-level tables for longer codes (one per
+//                  root prefix, sized by its longest code), so every code decodes with at most two
+//                  LDS reads and no arithmetic on the symbol number.
+//   3. spec     -- the bit range is cut into NDEC segments; lane t decodes from OV bits before
+//                  segment t (warm-up), counts output from its first symbol boundary at or after
+//                  the segment start and stops at its EXIT, the first boundary at or after the next
+//                  segment; it also records checkpoints (its first boundary past every CKI bits).
+//                  Huffman codes self-synchronise, so an exit is almost always on the true path.
+//   4. rounds   -- lanes whose first boundary differs from the predecessor's exit re-decode from
+//                  that exit (compacted onto the first threads by an LDS counter) until they meet
+//                  the speculative path at a checkpoint (same bit position = same decoder state),
+//                  then take the rest of the speculative run; repeat while an exit changed.
 //   5. emit     -- an exclusive scan of the per-lane byte counts gives every lane its output
 //                  offset; lanes decode once more, writing literals into the LDS image and, for
 //                  each match, a 3-byte descriptor (dist-1 | len-3 << 15) at its first byte plus a
@@ -32,12 +36,13 @@
 // Then, for the whole BGZF block:
 //   6. resolve  -- lastStart[w] = last match start at or before the end of bitmap word w (a max
 //                  scan), so the owner of any byte is found in O(1).  Batches of NB chunks of 512
-//                  bytes: (a) every byte follows its copy chain (start - dist + (offset mod dist))
-//                  through static data only until it reaches a literal or a byte of an earlier
-//                  chunk -- the NB chains of a thread advance together, no barriers; (b) chunk by
-//                  chunk, one LDS read + write per byte and one barrier; (c) the batch's 16-byte
-//                  lines are stored to U while the next batch follows its chains.
-//   7. CRC32    -- slice-by-4 per thread over a 128-byte slice, combined across threads by
+//                  bytes: (a) every byte's first hop (owner, descriptor, copy source start - dist +
+//                  (offset mod dist)) is published as a 16-bit next pointer, then pointer jumping
+//                  (barrier-free) until a literal or a byte before the byte's 512-byte step; (b)
+//                  step by step, one LDS read + write per byte and one barrier; (c) the batch's
+//                  16-byte lines are stored to U.  Batches are software-pipelined (batch k+1's hops
+//                  and jumps run between batch k's steps).
+//   7. CRC32    -- slice-by-4 per thread over a 132-byte slice, combined across threads by
 //                  multiplying with x^(8n) mod P (precomputed per slice index); compared with the
 //                  gzip trailer.
 // Output stops at ISIZE (Inflater.inflate(buf, 0, ISIZE) semantics); fewer bytes is an error.

@@ -257,8 +257,11 @@ class HtsjdkReadsRddStorage:
     def write(self, rdd: HtsjdkReadsRdd, path: str, tempPartsDirectory: Optional[str] = None):
         """BamSink.save (D/impl/formats/bam/BamSink.java:32-69) with GPU BGZF compression: each
         partition's records as a headerless BGZF part (HeaderlessBamOutputFormat, no terminator),
-        the header as its own BGZF blocks (BAMFileWriter.writeHeader), the 28-byte EOF block, then
-        the parts merged in partition order (Merger.mergeParts) into `path`."""
+        the header as its own BGZF blocks, the 28-byte EOF block, then the parts merged in
+        partition order (Merger.mergeParts) into `path`; the temporary parts directory is deleted
+        after the merge (BamSink.java:67-68).  The header bytes are the ones the file was read
+        with (header.raw), not re-encoded from a SAMFileHeader as BAMFileWriter.writeHeader does:
+        for a header read by this package they are the same BAM header."""
         header = rdd.getHeader()
         if not header.raw:
             raise ValueError("header has no BAM encoding")
@@ -278,6 +281,9 @@ class HtsjdkReadsRddStorage:
         with open(path, "wb") as fh:
             for d in pieces:
                 fh.write(d)
+        if tempPartsDirectory:  # fileSystemWrapper.delete(tempPartsDirectory)
+            import shutil
+            shutil.rmtree(tempPartsDirectory, ignore_errors=True)
         return path
 
     @staticmethod
@@ -355,19 +361,62 @@ class HtsjdkVariantsRddStorage:
                 ctx.text_set_intervals([(iv.getContig(), iv.getStart(), iv.getEnd())
                                         for iv in intervals])
             b = ctx.text_read(True)
-            with _lib.Context(split_size=0, device=self._device) as hc:  # the header lines
-                hc.text_open_path(path)
-                hb = hc.text_read(False)
         d, do, ln, po = b["data"], b["data_offset"], b["line_len"], b["part_offset"]
         parts = [VariantsPartition(bytes(d[do[k]:do[k] + ln[k]]) for k in range(po[p], po[p + 1]))
                  for p in range(len(po) - 1)]
-        header = []
-        for k in range(len(hb["line_len"])):
-            line = bytes(hb["data"][hb["data_offset"][k]:hb["data_offset"][k] + hb["line_len"][k]])
-            if not line.startswith(b"#"):
+        return HtsjdkVariantsRdd(vcf_header_lines(path), VariantsRDD(parts))
+
+
+def vcf_header_lines(path: str, max_bytes: int = 64 << 20):
+    """The leading '#' lines of a BGZF VCF, read from a prefix of the file: BGZF members are
+    inflated from the start (on the driver, as VcfSource.getVCFCodec reads the header through
+    htsjdk, D/impl/formats/vcf/VcfSource.java:60-86) only until the first line that does not start
+    with '#'.  Terminators as Hadoop's LineReader: LF, CR LF, lone CR; a UTF-8 BOM on the first
+    line is dropped (LineRecordReader.skipUtfByteOrderMark)."""
+    import struct
+    import zlib
+    lines, buf, first, read = [], b"", True, 0
+    with open(path, "rb") as fh:
+        while read < max_bytes:
+            hdr = fh.read(12)
+            if len(hdr) < 12:
                 break
-            header.append(line)
-        return HtsjdkVariantsRdd(header, VariantsRDD(parts))
+            if hdr[:4] != b"\x1f\x8b\x08\x04":
+                raise ValueError(f"{path}: not a BGZF member at {read}")
+            xlen = struct.unpack_from("<H", hdr, 10)[0]
+            extra = fh.read(xlen)
+            bsize, k = None, 0
+            while k + 4 <= len(extra):  # the BC subfield holds BSIZE
+                si1, si2, slen = extra[k], extra[k + 1], struct.unpack_from("<H", extra, k + 2)[0]
+                if si1 == 66 and si2 == 67 and slen == 2:
+                    bsize = struct.unpack_from("<H", extra, k + 4)[0] + 1
+                k += 4 + slen
+            if bsize is None:
+                raise ValueError(f"{path}: BGZF member without a BC subfield at {read}")
+            body = fh.read(bsize - 12 - xlen)
+            read += bsize
+            buf += zlib.decompress(body[:-8], -15)
+            if first and buf.startswith(b"\xef\xbb\xbf"):
+                buf = buf[3:]
+            first = False if buf else first
+            # complete lines (a CR at the very end may be the first half of a CR LF)
+            pos = 0
+            while True:
+                i = min([x for x in (buf.find(b"\n", pos), buf.find(b"\r", pos)) if x >= 0],
+                        default=-1)
+                if i < 0 or (buf[i:i + 1] == b"\r" and i + 1 == len(buf)):
+                    break
+                line = buf[pos:i]
+                if not line.startswith(b"#"):
+                    return lines
+                lines.append(line)
+                pos = i + (2 if buf[i:i + 2] == b"\r\n" else 1)
+            buf = buf[pos:]
+            if buf and not buf.startswith(b"#"):
+                return lines
+    if buf.startswith(b"#"):  # a header line that runs to the end of the file
+        lines.append(buf.rstrip(b"\r"))
+    return lines
 
 
 class BAMSBIIndexer:

@@ -14,9 +14,11 @@
  *       BgzfBlockGuesser.java:76-149)
  *     + getFirstReadInPartition/BamRecordGuesser (BamSource.java:110-153,
  *       D/impl/formats/bam/BamRecordGuesser.java:34-194)                    dq_plan
- *   BamSource.getIterator(SamReader, SAMFileSpan) (BamSource.java:172-175)  dq_decode
+ *   BamSource.getIterator(SamReader, SAMFileSpan) (BamSource.java:172-175), one Spark task
+ *                                                      dq_decode_chunk (dq_decode on a resident file)
  *   BamSource.createIndexIterator + queryUnmapped tail
- *     (BamSource.java:177-182; AbstractBinarySamSource.java:86-134)       dq_decode_filtered
+ *     (BamSource.java:177-182; AbstractBinarySamSource.java:86-134)
+ *                                    dq_decode_chunk_filtered (dq_decode_filtered on a resident file)
  *   AbstractBinarySamSource.getReads, whole RDD (AbstractBinarySamSource.java:42-136)  dq_read
  *   AbstractSamSource.getFileHeader (D/impl/formats/sam/AbstractSamSource.java:32-49)
  *                                                                           dq_read_header
@@ -349,9 +351,10 @@ void dq_text_batch_free(dq_text_batch* b);
  * of 65280 bytes (htsjdk DEFAULT_UNCOMPRESSED_BLOCK_SIZE, the last one shorter), each compressed
  * on the GPU into one BGZF member ('BC' extra field, BSIZE, CRC32, ISIZE).  No EOF terminator is
  * written (BamSink appends BlockCompressedStreamConstants.EMPTY_GZIP_BLOCK once, after all parts).
- * The DEFLATE bit stream is this library's own (LZ77 + fixed Huffman, or stored when that does
- * not fit): the blocks inflate to exactly htsjdk's block contents; the compressed bytes differ
- * from java.util.zip.Deflater's.  *out is malloc'ed (dq_free). */
+ * The DEFLATE bit stream is this library's own (LZ77 + a dynamic Huffman code per block, the
+ * fixed code when that is shorter, stored when neither fits): the blocks inflate to exactly
+ * htsjdk's block contents; the compressed bytes differ from java.util.zip.Deflater's.  *out is
+ * malloc'ed (dq_free). */
 int dq_bgzf_compress(dq_ctx* ctx, const uint8_t* data, int64_t len, uint8_t** out, int64_t* out_len);
 /* The same over the resident decompressed stream of the open file (benchmark / round trip): the
  * result stays in HBM (dq_bgzf_fetch copies it out); *ms = device time. */

@@ -107,3 +107,20 @@ def test_vcf_overlap_uses_info_end():
     assert O.vcf_overlaps(lines[0], [("chr1", end, end)])
     assert not O.vcf_overlaps(lines[0], [("chr1", end + 1, end + 10)])
     assert not O.vcf_overlaps(lines[0], [("chr2", pos, end)])
+
+
+def test_vcf_header_lines_from_a_prefix():
+    """HtsjdkVariantsRddStorage.read's header: the leading '#' lines, read by inflating only the
+    first BGZF members (no second full-file read), equal the plain VCF's '#' lines."""
+    import os
+    from disq_amd.storage import vcf_header_lines
+    g = os.path.join(os.path.dirname(__file__), "golden")
+    plain = open(os.path.join(g, "test.vcf"), "rb").read().split(b"\n")
+    want = []
+    for ln in plain:
+        if not ln.startswith(b"#"):
+            break
+        want.append(ln.rstrip(b"\r"))
+    assert vcf_header_lines(os.path.join(g, "test.vcf.bgz")) == want
+    hs = vcf_header_lines(os.path.join(g, "HiSeq.10000.vcf.bgz"))
+    assert hs[0].startswith(b"##fileformat") and hs[-1].startswith(b"#CHROM")
