@@ -143,6 +143,8 @@ struct alignas(16) LdsI {
     struct {
       uint16_t last_start[1024];  // last match start <= end of 64-bit bitmap word (0xffff none)
       uint16_t nxt[RES_NXT];      // next pointer of each byte of the batch
+      int32_t carry_ms[32];       // the match carried into batch k + 1 (start, -1 none), and its
+      uint32_t carry_desc[32];    // descriptor: read before any step overwrites a descriptor
     } r;
     uint32_t crc4[4][256];
   } u;
@@ -171,7 +173,7 @@ __constant__ uint8_t c_clorder3[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 
 
 // misc slots
 enum { M_ERR = 0, M_A = 4, M_LAST, M_MORE, M_MORE1,
-       M_CARRY_MS = 10, M_CARRY_DESC, M_LQ0 = 15, M_LQN, M_DQ0, M_DQN, M_NEXT,
+       M_LQ0 = 15, M_LQN, M_DQ0, M_DQN, M_NEXT,
        M_LASTF, M_RCNT = 28 /* and 29: redo-list counters of even / odd rounds */,
        M_DIRTY = 30 /* and 31: a re-decoded exit changed, even / odd rounds */ };
 
@@ -1217,7 +1219,6 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       const int v = max(ex, ls[k]);
       L.u.r.last_start[2 * t + k] = v < 0 ? (uint16_t)0xffff : (uint16_t)v;
     }
-    if (t == 0) L.misc[M_CARRY_MS] = -1;
     __syncthreads();
   }
   uint8_t* dstU = U + ub;
@@ -1325,36 +1326,35 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   int32_t cms = -1;     // carry into the current batch
   uint32_t cdesc = 0;
   first_hop(0, cms, cdesc, frA, xsA, pendA);
+  // the carries into every batch, while every descriptor is intact (off the batches' critical
+  // path: round 2 had wave 0 compute each one in front of the batch barrier)
+  if (t < (isize + BATCH - 1) / BATCH) {
+    int32_t ncms = -1;
+    uint32_t ncdesc = 0;
+    const int32_t x = (t + 1) * BATCH - 1;  // batch t's last byte
+    if (x + 1 < isize) {
+      const uint64_t m = bm64[x >> 6];  // bit 63 of the last word: every bit is at or before x
+      const int32_t ms = m ? (x | 63) - (int32_t)__clzll(m) : (int32_t)L.u.r.last_start[(x >> 6) - 1];
+      if (ms != 0xffff) {
+        const uint32_t desc = load_desc(L, sh + ms);
+        if (ms + (int32_t)(desc >> 15) + 3 > x + 1) {
+          ncms = ms;
+          ncdesc = desc;
+        }
+      }
+    }
+    L.u.r.carry_ms[t] = ncms;
+    L.u.r.carry_desc[t] = ncdesc;
+  }
   __syncthreads();
   for (int hop = 0; pendA != 0 && hop < WG + 2; hop++) jump_round(0, frA, xsA, pendA);
   for (int32_t bs = 0; bs < isize; bs += BATCH) {
     const uint64_t tb0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
     const int32_t nbs = bs + BATCH;
     const bool more = nbs < isize;
-    // carry into batch k+1: the match covering batch k's last byte, if it continues (wave 0
-    // computes it from batch k's descriptors, before (b) overwrites them, and publishes it; the
-    // slots are read right after the barrier, and rewritten only after batch k+1's steps)
-    if (more && wv == 0) {
-      int32_t ncms = -1;
-      uint32_t ncdesc = 0;
-      const int32_t x = nbs - 1;
-      const uint64_t m = bm64[x >> 6];  // bit 63 of the last word: every bit is at or before x
-      const int32_t ms = m ? (x | 63) - (int32_t)__clzll(m) : (int32_t)L.u.r.last_start[(x >> 6) - 1];
-      if (ms != 0xffff) {
-        const uint32_t desc = ms < bs ? cdesc : load_desc(L, sh + ms);
-        if ((ms >= bs || ms == cms) && ms + (int32_t)(desc >> 15) + 3 > nbs) {
-          ncms = ms;
-          ncdesc = desc;
-        }
-      }
-      if (lane == 0) {
-        L.misc[M_CARRY_MS] = ncms;
-        L.misc[M_CARRY_DESC] = (int32_t)ncdesc;
-      }
-    }
     __syncthreads();  // every wave's jumps of batch k are done: nxt is free for batch k+1
-    const int32_t ncms = more ? L.misc[M_CARRY_MS] : -1;
-    const uint32_t ncdesc = more ? (uint32_t)L.misc[M_CARRY_DESC] : 0u;
+    const int32_t ncms = more ? L.u.r.carry_ms[bs / BATCH] : -1;
+    const uint32_t ncdesc = more ? L.u.r.carry_desc[bs / BATCH] : 0u;
     int32_t frB[NE], xsB[NE];
     uint32_t pendB = 0;
     if (more) first_hop(nbs, ncms, ncdesc, frB, xsB, pendB);
