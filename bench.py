@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--gb", type=float, default=12.5, help="compressed GB of the file per GPU")
+    ap.add_argument("--shape", choices=("wgs", "longread"), default="wgs",
+                    help="wgs: configs[1]/[2] (2x150 bp pairs); longread: configs[4] (ONT-like "
+                         "10-100 kb reads, 1 %% of 0.5-2 Mb, records spanning many BGZF blocks)")
     ap.add_argument("--split-size", type=int, default=0, help="Disq splitSize (0 = 32 MiB)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--halo", type=int, default=4 << 20, help="initial halo bytes")
@@ -64,6 +67,11 @@ def parse():
     ap.add_argument("--intervals", type=int, default=10000,
                     help="BED-like intervals for the N = 1 interval-filter measurement (0 = skip)")
     ap.add_argument("--e2e", type=int, default=1, help="N = 1 end-to-end measurement (0 = skip)")
+    ap.add_argument("--gen-budget-s", type=float, default=150.0,
+                    help="N > 1: generation seconds per rank before the ranks tile a chunk pool")
+    ap.add_argument("--e2e-window-gb", type=float, default=2.0,
+                    help="end-to-end: compressed GB per window")
+    ap.add_argument("--e2e-depth", type=int, default=3, help="end-to-end: overlapping windows")
     return ap.parse_args()
 
 
@@ -113,21 +121,43 @@ def main():
     # ---- workload: this rank's byte range of one logical N x args.gb GB file
     os.environ["DQ_SYNTH_PROGRESS"] = "1"
     t0 = time.time()
-    probe = synth.generate(20000, seed=args.seed, nthreads=gen_threads)
+    shape = synth.LONGREAD if args.shape == "longread" else synth.WGS
+    per_chunk = 2000 if shape == synth.LONGREAD else 20000
+    probe = synth.generate(per_chunk, seed=args.seed, nthreads=gen_threads, shape=shape)
+    probe_s = time.time() - t0  # one chunk, on one thread
     per_rec = len(probe.bam) / probe.n_records
     n_total = int(args.gb * 1e9 / per_rec) * world
-    nchunks = synth.chunk_count(n_total)
+    nchunks = synth.chunk_count(n_total, shape=shape)
     k0, k1 = rank * nchunks // world, (rank + 1) * nchunks // world
-    want_bai = world == 1 and args.intervals > 0
+    want_bai = world == 1 and args.intervals > 0 and shape == synth.WGS
+    # Generation budget: zlib level 5 (htsjdk's) costs ~1 thread-second per chunk, so with few
+    # threads per rank (an 8-GPU node under a small CPU quota) the ranks generate a pool of
+    # distinct chunks and tile it over their byte range (the blocks are the same level-5 BGZF
+    # members; positions then repeat every pool instead of rising over the whole file).  N = 1
+    # and any rank that fits the budget generate every chunk.
+    est = (k1 - k0) * probe_s / max(1, gen_threads)
+    pool = None
+    if world > 1 and est > args.gen_budget_s:
+        pool = max(2 * gen_threads, int(args.gen_budget_s * gen_threads / max(probe_s, 1e-3)))
     log(f"[bench] rank {rank}: chunks [{k0}, {k1}) of {nchunks} ({n_total} records in the file), "
-        f"{gen_threads} threads")
-    res, free = synth.generate(n_total, seed=args.seed, nthreads=gen_threads, as_buffer=True,
-                               bai=want_bai, unplaced_fraction=0.005,
-                               chunks=None if world == 1 else (k0, k1))
-    gen_s = time.time() - t0
-    own_len = res.bam_len
+        f"{gen_threads} threads, estimated {est:.0f} s" + (f", pool of {pool} chunks" if pool else ""))
     import ctypes
-    own_np = np.ctypeslib.as_array((ctypes.c_uint8 * own_len).from_address(res.bam))
+    if pool is None or pool >= k1 - k0:
+        res, free = synth.generate(n_total, seed=args.seed, nthreads=gen_threads, as_buffer=True,
+                                   bai=want_bai, unplaced_fraction=0.005, shape=shape,
+                                   chunks=None if world == 1 else (k0, k1))
+        own_len = res.bam_len
+        own_np = np.ctypeslib.as_array((ctypes.c_uint8 * own_len).from_address(res.bam))
+        gen_desc = {"distinct_chunks": k1 - k0, "tiled_chunks": 0}
+    else:
+        own_np, free = tiled_rank_bytes(synth, n_total, args.seed, gen_threads, k0, k1, nchunks,
+                                        pool, shape)
+        own_len = len(own_np)
+        res = None
+        gen_desc = {"distinct_chunks": pool + (1 if k0 == 0 else 0),
+                    "tiled_chunks": (k1 - k0) - pool - (1 if k0 == 0 else 0),
+                    "note": "a pool of distinct level-5 chunks tiled over the rank's range"}
+    gen_s = time.time() - t0
     lens = [own_len]
     if dist is not None:
         t = torch.tensor([own_len], dtype=torch.int64, device=cdev)
@@ -157,7 +187,7 @@ def main():
     rs.reserve(0)
     torch.cuda.synchronize()
     h2d_s = time.time() - t0
-    bai = ctypes.string_at(res.bai, res.bai_len) if (want_bai and res.bai) else None
+    bai = ctypes.string_at(res.bai, res.bai_len) if (want_bai and res is not None and res.bai) else None
     cpu_data = own_np.copy() if (world == 1 and args.cpu_seconds > 0) else None
     own_host = torch.from_numpy(own_np.copy()) if (rehearsal and world > 1) else None
     del own_np
@@ -273,7 +303,7 @@ def main():
         if cpu_data is not None:
             cpu, parity = cpu_baseline(cpu_data, ctx, rs, shard, file_len, header, args, ncores)
         if args.e2e:
-            e2e = end_to_end(cpu_data, args)
+            e2e = end_to_end(cpu_data, args, digest, header)
     if rehearsal and world > 1 and rank == 0:
         # the whole logical file, generated at once, through the oracle: its digest must equal
         # the digest folded from the shards
@@ -300,9 +330,13 @@ def main():
             "dtype": "u8",
             "data": "synthetic (seeded generator, htsjdk BGZF conventions, deflate level 5)",
             "config": {
-                "workload": f"configs[2]: one synthetic 30x-WGS-shaped coordinate-sorted BAM of "
-                            f"{world} x {args.gb} GB (100 GB at 8 GPUs), 2x150 bp pairs, 0.5 % "
-                            f"unplaced-unmapped tail, byte-range sharded with halo stitching",
+                "workload": (f"configs[2]: one synthetic 30x-WGS-shaped coordinate-sorted BAM of "
+                             f"{world} x {args.gb} GB (100 GB at 8 GPUs), 2x150 bp pairs, 0.5 % "
+                             f"unplaced-unmapped tail, byte-range sharded with halo stitching"
+                             if shape == synth.WGS else
+                             f"configs[4]: one synthetic long-read coordinate-sorted BAM of "
+                             f"{world} x {args.gb} GB, ONT-like reads of 10-100 kb (1 % of "
+                             f"0.5-2 Mb) whose records span many BGZF blocks, 0.5 % unplaced"),
                 "parallelism": f"1 file, {world} byte-range shard(s), halo over "
                                + ("gloo (REHEARSAL on one GPU, not a measurement)" if rehearsal
                                   else "RCCL p2p"),
@@ -321,6 +355,7 @@ def main():
                     "plan": round(stats.ms_plan, 2), "records": round(stats.ms_records, 2),
                     "total": round(stats.ms_total, 2)},
                 "generator_s": round(gen_s, 1),
+                "generator": dict(gen_desc, threads_per_rank=gen_threads),
                 "interval_mode": interval_mode,
                 "end_to_end": e2e,
                 "parity": parity,
@@ -359,6 +394,40 @@ def main():
         sys.exit(3)
     if (interval_mode or {}).get("parity") and interval_mode["parity"].get("status") != "match":
         sys.exit(3)
+
+
+def tiled_rank_bytes(synth, n_total, seed, threads, k0, k1, nchunks, pool, shape=0):
+    """A rank's bytes [chunks k0, k1) from a pool of distinct chunks: chunk 0 (the header) and the
+    last chunk (unplaced tail + EOF block) are generated as themselves; the pool [a, a + pool) of
+    mid-file chunks is generated once and repeated, the remainder taken from its front."""
+    import ctypes
+    import numpy as np
+    pieces = []
+    a = k0 + 1 if k0 == 0 else k0
+    last = k1 == nchunks
+    b = k1 - 1 if last else k1
+    pool = max(1, min(pool, b - a))
+
+    def gen(lo, hi):
+        r, fr = synth.generate(n_total, seed=seed, nthreads=threads, as_buffer=True,
+                               unplaced_fraction=0.005, chunks=(lo, hi), shape=shape)
+        arr = np.ctypeslib.as_array((ctypes.c_uint8 * r.bam_len).from_address(r.bam)).copy()
+        fr()
+        return arr
+    if k0 == 0:
+        pieces.append(gen(0, 1))
+    if b > a:
+        # the pool, chunk by chunk boundaries known: generate it as single chunks in parallel
+        # calls is serial in the library, so generate it whole and tile it whole
+        whole = gen(a, a + pool)
+        reps, rem = divmod(b - a, pool)
+        pieces += [whole] * reps
+        if rem:
+            pieces.append(gen(a, a + rem))
+    if last:
+        pieces.append(gen(k1 - 1, k1))
+    out = np.concatenate(pieces)
+    return out, (lambda: None)
 
 
 def make_intervals(seqs, n, seed=3):
@@ -509,35 +578,87 @@ def cpu_baseline(data, ctx, rs, shard, file_len, header, args, ncores):
     return cpu, parity
 
 
-def end_to_end(data, args):
-    """Page-cached file -> host SoA + raw records (one whole read, not timed with the steps):
-    the file is in /dev/shm (RAM, as the page cache would hold it); dq_open_path streams it to
-    HBM through pinned staging buffers, the pipeline runs, and dq_read copies every record's
-    SoA row and raw bytes back to host memory."""
+def end_to_end(data, args, resident_digest=None, header=None):
+    """Page-cached file -> host SoA + raw records, every stage overlapped (one whole read, not
+    timed with the steps): the file is in /dev/shm (RAM, as the page cache would hold it) and is
+    read in windows of whole partitions by `depth` contexts on their own host threads and HIP
+    streams (disq_amd.stream): one window's file -> pinned -> HBM copy, another's pipeline and a
+    third's export of every record's SoA row and raw bytes to host memory (dq_read) run at once,
+    as Disq's tasks overlap their prefetcher's reads with decoding
+    (SeekableByteChannelPrefetcher.java:253-298).  The whole-file digest must equal the resident
+    run's."""
     if data is None:
         return None
-    from disq_amd import _lib
+    from disq_amd import _lib, stream
     path = f"/dev/shm/disq_bench_{os.getpid()}.bam"
     try:
         with open(path, "wb") as f:
             f.write(memoryview(data))
-        with _lib.Context(split_size=args.split_size, verify_crc=not args.no_crc) as c:
-            t0 = time.perf_counter()
-            c.open_path(path)
-            t1 = time.perf_counter()
-            st = c.run_resident()
-            t2 = time.perf_counter()
+        if header is None:
+            with _lib.Context() as hc:
+                header = hc.header_from_prefix(bytes(data[:1 << 20]))
+        exported = {"records": 0, "raw": 0, "soa": 0, "digests": []}
+        keep = []
+        lk = __import__("threading").Lock()
+
+        def export(k, c, shard):
             b = c.read(with_raw=True)
-            t3 = time.perf_counter()
-        n = len(b["voffset"])
-        raw = 0 if b["raw"] is None else len(b["raw"])
-        del b
-        return {"seconds": round(t3 - t0, 3), "decompressed_gbs": round(st.owned_bytes / (t3 - t0) / 1e9, 3),
-                "reads_per_s": round(n / (t3 - t0), 1),
-                "open_h2d_s": round(t1 - t0, 3), "pipeline_s": round(t2 - t1, 3),
-                "d2h_soa_raw_s": round(t3 - t2, 3), "raw_gb": round(raw / 1e9, 3),
-                "path": "page cache (/dev/shm) -> pinned staging -> HBM -> pipeline -> host SoA + "
-                        "raw bytes (dq_open_path + dq_read)"}
+            n = len(b["voffset"])
+            raw = 0 if b["raw"] is None else len(b["raw"])
+            # the consumer's view: the last record's raw bytes end where its offsets say
+            assert raw == (int(b["raw_offset"][-1]) + 4 + int(b["block_size"][-1]) if n else 0)
+            with lk:
+                exported["records"] += n
+                exported["raw"] += raw
+                exported["soa"] += sum(int(b[k2].nbytes) for k2, _ in _lib.FIELDS if k2 in b)
+                exported["digests"].append((shard.p0, b["part_digest"].copy()))
+        window = int(args.e2e_window_gb * 1e9)
+        # the contexts and their pinned export arenas are set up before the read (an executor's
+        # long-lived buffers): a window's records land there by DMA, and the consumer is done with
+        # them when the next window of that context is exported
+        t0 = time.perf_counter()
+        arena = int(window * 3.7)  # U + SoA of a window (2.85 + ~0.55 x its compressed bytes)
+        ctxs = []
+        for _ in range(args.e2e_depth):
+            c = _lib.Context(split_size=args.split_size, verify_crc=not args.no_crc)
+            c.set_export_arena(arena)
+            ctxs.append(c)
+        setup_s = time.perf_counter() - t0
+        try:
+            res = stream.stream_read(path, len(data), header, window=window, depth=args.e2e_depth,
+                                     split_size=args.split_size, verify_crc=not args.no_crc,
+                                     on_window=export, contexts=ctxs)
+        finally:
+            del keep[:]
+            for c in ctxs:
+                c.close()
+        secs = res["seconds"]
+        from disq_amd import parallel as P
+        dg = [0] * len(res["digests"])
+        for p0, d in exported["digests"]:  # the partition digests of the exported host batches
+            for i, x in enumerate(d):
+                dg[p0 + i] = int(x)
+        exported_digest = P.fold_digest(dg)
+        out = {"seconds": round(secs, 3),
+               "decompressed_gbs": round(res["owned_bytes"] / secs / 1e9, 3),
+               "reads_per_s": round(exported["records"] / secs, 1),
+               "windows": res["windows"], "depth": args.e2e_depth,
+               "window_gb": args.e2e_window_gb,
+               "stage_seconds_summed_over_windows": {
+                   "open_h2d": round(res["open_s"], 3), "pipeline": round(res["run_s"], 3),
+                   "d2h_soa_raw": round(res["on_window_s"], 3)},
+               "overlap": round((res["open_s"] + res["run_s"] + res["on_window_s"]) / secs, 2),
+               "records": exported["records"], "raw_gb": round(exported["raw"] / 1e9, 3),
+               "soa_gb": round(exported["soa"] / 1e9, 3),
+               "digest": f"{res['digest']:016x}",
+               "digest_match": None if resident_digest is None else res["digest"] == resident_digest,
+               "exported_digest_match": exported_digest == res["digest"],
+               "setup_s_untimed": round(setup_s, 2),
+               "arena_gb_per_context": round(arena / 1e9, 2),
+               "path": "page cache (/dev/shm) -> pinned staging -> HBM -> pipeline -> host SoA + "
+                       "raw bytes, windows of whole partitions on overlapping contexts "
+                       "(disq_amd.stream + dq_open_shard_path + dq_read)"}
+        return out
     except Exception as e:  # noqa: BLE001
         return {"error": f"{type(e).__name__}: {e}"}
     finally:

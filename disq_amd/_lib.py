@@ -52,7 +52,8 @@ class DqBatch(C.Structure):
                 ("raw_len", C.c_int64),
                 ("n_partitions", C.c_int64),
                 ("part_offset", C.POINTER(C.c_int64)),
-                ("part_digest", C.POINTER(C.c_uint64))]
+                ("part_digest", C.POINTER(C.c_uint64)),
+                ("in_arena", C.c_int32), ("reserved", C.c_int32)]
 
 
 class DqTextBatch(C.Structure):
@@ -107,7 +108,8 @@ EXPORTS = ("dq_ctx_create", "dq_ctx_destroy", "dq_last_error", "dq_version", "dq
            "dq_decode_chunk_filtered", "dq_debug_guess_all", "dq_text_open_memory",
            "dq_text_open_path", "dq_text_run", "dq_text_read", "dq_text_batch_free",
            "dq_bgzf_compress", "dq_bgzf_compress_resident", "dq_bgzf_fetch",
-           "dq_text_set_index", "dq_text_set_intervals", "dq_decode_file_multi")
+           "dq_text_set_index", "dq_text_set_intervals", "dq_decode_file_multi",
+           "dq_set_export_arena")
 
 _lib = None
 _lock = threading.Lock()
@@ -162,6 +164,7 @@ def lib():
         L.dq_debug_inflated.argtypes = [vp, vp, C.c_int64, P(C.c_int64)]
         L.dq_debug_guess_all.argtypes = [vp, vp, C.c_int64, P(C.c_int64)]
         L.dq_batch_free.argtypes = [P(DqBatch)]
+        L.dq_set_export_arena.argtypes = [vp, C.c_int64]
         L.dq_text_open_memory.argtypes = [vp, vp, C.c_int64]
         L.dq_text_open_path.argtypes = [vp, C.c_char_p]
         L.dq_text_run.argtypes = [vp, C.c_int32, P(DqStats)]
@@ -492,6 +495,12 @@ class Context:
             check(self._h, lib().dq_decode_filtered(self._h, vstart, vend, C.byref(t),
                                                     int(with_raw), C.byref(bp)))
         return batch_to_numpy(bp)
+
+    def set_export_arena(self, nbytes):
+        """dq_set_export_arena: later batches of this context land in `nbytes` of pinned host
+        memory by DMA; an arena batch's arrays are valid until the next batch of the context
+        (a streaming consumer's recycled buffers)."""
+        check(self._h, lib().dq_set_export_arena(self._h, int(nbytes)))
 
     def read(self, with_raw=True, traversal=None):
         bp = C.POINTER(DqBatch)()

@@ -116,6 +116,11 @@ struct dq_ctx {
   uint8_t* pin[2] = {nullptr, nullptr};
   size_t pin_cap = 0;
   hipEvent_t pin_ev[2] = {nullptr, nullptr};
+  // dq_set_export_arena: batches land in this pinned arena (DMA, no staging copies), valid until
+  // the next batch of the context
+  uint8_t* arena = nullptr;
+  size_t arena_cap = 0;
+  DevBuf x_bs4, x_boff, x_voff, x_parts;  // batch export: raw offsets, voffsets, digests
   int64_t h2d_bytes = 0;            // compressed bytes copied host -> device by the last open
   const uint8_t* cbuf() const { return cext ? cext : C.as<uint8_t>(); }
   // kernel 1
@@ -1275,28 +1280,6 @@ static int make_batch(dq_ctx* ctx, const std::vector<std::pair<int64_t, int64_t>
   dq_batch* b = (dq_batch*)calloc(1, sizeof(dq_batch));
   if (!b) RET(DQ_ENOMEM, "out of host memory");
   b->n_records = n;
-  const size_t m = (size_t)std::max<int64_t>(1, n);
-  b->voffset = (uint64_t*)host_alloc(8 * m);
-  b->block_size = (int32_t*)host_alloc(4 * m);
-  b->ref_id = (int32_t*)host_alloc(4 * m);
-  b->pos = (int32_t*)host_alloc(4 * m);
-  b->l_seq = (int32_t*)host_alloc(4 * m);
-  b->next_ref_id = (int32_t*)host_alloc(4 * m);
-  b->next_pos = (int32_t*)host_alloc(4 * m);
-  b->tlen = (int32_t*)host_alloc(4 * m);
-  b->flag = (uint16_t*)host_alloc(2 * m);
-  b->bin = (uint16_t*)host_alloc(2 * m);
-  b->n_cigar = (uint16_t*)host_alloc(2 * m);
-  b->mapq = (uint8_t*)host_alloc(m);
-  b->l_read_name = (uint8_t*)host_alloc(m);
-  b->hash = (uint64_t*)host_alloc(8 * m);
-  b->raw_offset = (int64_t*)host_alloc(8 * m);
-  if (!b->voffset || !b->block_size || !b->ref_id || !b->pos || !b->l_seq || !b->next_ref_id ||
-      !b->next_pos || !b->tlen || !b->flag || !b->bin || !b->n_cigar || !b->mapq ||
-      !b->l_read_name || !b->hash || !b->raw_offset) {
-    dq_batch_free(b);
-    RET(DQ_ENOMEM, "out of host memory");
-  }
   int rc = 0;
   auto fail = [&](int code) {
     dq_batch_free(b);
@@ -1363,57 +1346,116 @@ static int make_batch(dq_ctx* ctx, const std::vector<std::pair<int64_t, int64_t>
     rows = dst;
     first = 0;
   }
+  // per-record work on the device: raw offsets (an exclusive scan of 4 + block_size), voffsets in
+  // file coordinates, the partitions' ordered digests; the host only receives arrays
+  const int64_t np = std::max<int64_t>(0, (int64_t)part_bounds.size() - 1);
+  const size_t m = (size_t)std::max<int64_t>(1, n);
+  int64_t raw_len = 0;
+  const uint64_t* d_voff = rows.voffset + first;
   if (n > 0) {
-    auto d2h = [&](const void* dbase, size_t esz, void* dst) {
-      return d2h_large(ctx, dst, (const char*)dbase + (size_t)first * esz, (size_t)n * esz);
+    if ((rc = ensure_all(ctx, ctx->x_bs4, 4 * m)) || (rc = ensure_all(ctx, ctx->x_boff, 8 * (m + 1))) ||
+        (rc = ensure_scan(ctx, n)))
+      return fail(rc);
+    launch_bs_plus4(rows.block_size + first, n, ctx->x_bs4.as<int32_t>(), s);
+    launch_exclusive_scan_i32(ctx->x_bs4.as<int32_t>(), ctx->x_boff.as<int64_t>(), n,
+                              ctx->tmp.as<int64_t>(), s);
+    if (ctx->base) {
+      if ((rc = ensure_all(ctx, ctx->x_voff, 8 * m))) return fail(rc);
+      launch_add_u64(d_voff, n, (uint64_t)ctx->base << 16, ctx->x_voff.as<uint64_t>(), s);
+      d_voff = ctx->x_voff.as<uint64_t>();
+    }
+    XCHK(hipMemcpyAsync(&raw_len, ctx->x_boff.as<int64_t>() + n, 8, hipMemcpyDeviceToHost, s));
+  }
+  std::vector<PartRange> pr((size_t)np + 1);
+  for (int64_t p = 0; p < np; p++) pr[(size_t)p] = {part_bounds[(size_t)p], part_bounds[(size_t)p + 1], 0};
+  if (np > 0 && n > 0) {
+    if ((rc = ensure_all(ctx, ctx->x_parts, sizeof(PartRange) * (size_t)(np + 1)))) return fail(rc);
+    XCHK(hipMemcpyAsync(ctx->x_parts.p, pr.data(), sizeof(PartRange) * (size_t)np, hipMemcpyHostToDevice, s));
+    launch_partition_digest2(rows.hash + first, ctx->x_parts.as<PartRange>(), np, s);
+  }
+  XCHK(hipStreamSynchronize(s));  // raw_len
+  b->raw_len = raw_len;
+  // host arrays: the pinned arena when it is set and large enough, else heap memory
+  const size_t soa_bytes = 8 * ((8 * m + 7) / 8) * 3 + 8 * ((4 * m + 7) / 8) * 7 +
+                           8 * ((2 * m + 7) / 8) * 3 + 8 * ((m + 7) / 8) * 2;
+  const size_t want = soa_bytes + (with_raw ? (size_t)std::max<int64_t>(1, raw_len) : 0) + 64 * 20;
+  const bool in_arena = ctx->arena && want <= ctx->arena_cap;
+  size_t used = 0;
+  auto halloc = [&](size_t bytes) -> void* {
+    if (!in_arena) return host_alloc(bytes);
+    void* p = ctx->arena + used;
+    used += (bytes + 63) & ~(size_t)63;
+    return p;
+  };
+  b->in_arena = in_arena ? 1 : 0;
+  b->voffset = (uint64_t*)halloc(8 * m);
+  b->block_size = (int32_t*)halloc(4 * m);
+  b->ref_id = (int32_t*)halloc(4 * m);
+  b->pos = (int32_t*)halloc(4 * m);
+  b->l_seq = (int32_t*)halloc(4 * m);
+  b->next_ref_id = (int32_t*)halloc(4 * m);
+  b->next_pos = (int32_t*)halloc(4 * m);
+  b->tlen = (int32_t*)halloc(4 * m);
+  b->flag = (uint16_t*)halloc(2 * m);
+  b->bin = (uint16_t*)halloc(2 * m);
+  b->n_cigar = (uint16_t*)halloc(2 * m);
+  b->mapq = (uint8_t*)halloc(m);
+  b->l_read_name = (uint8_t*)halloc(m);
+  b->hash = (uint64_t*)halloc(8 * m);
+  b->raw_offset = (int64_t*)halloc(8 * m);
+  if (!b->voffset || !b->block_size || !b->ref_id || !b->pos || !b->l_seq || !b->next_ref_id ||
+      !b->next_pos || !b->tlen || !b->flag || !b->bin || !b->n_cigar || !b->mapq ||
+      !b->l_read_name || !b->hash || !b->raw_offset)
+    return fail(DQ_ENOMEM);
+  if (n > 0) {
+    // pinned destination: one DMA per array; heap: through the staging buffers
+    auto d2h = [&](const void* src, size_t bytes, void* dst) -> int {
+      if (in_arena) {
+        HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+        return 0;
+      }
+      return d2h_large(ctx, dst, src, bytes);
     };
-    if ((rc = d2h(rows.voffset, 8, b->voffset)) || (rc = d2h(rows.block_size, 4, b->block_size)) ||
-        (rc = d2h(rows.ref_id, 4, b->ref_id)) || (rc = d2h(rows.pos, 4, b->pos)) ||
-        (rc = d2h(rows.l_seq, 4, b->l_seq)) || (rc = d2h(rows.next_ref_id, 4, b->next_ref_id)) ||
-        (rc = d2h(rows.next_pos, 4, b->next_pos)) || (rc = d2h(rows.tlen, 4, b->tlen)) ||
-        (rc = d2h(rows.flag, 2, b->flag)) || (rc = d2h(rows.bin, 2, b->bin)) ||
-        (rc = d2h(rows.n_cigar, 2, b->n_cigar)) || (rc = d2h(rows.mapq, 1, b->mapq)) ||
-        (rc = d2h(rows.l_read_name, 1, b->l_read_name)) || (rc = d2h(rows.hash, 8, b->hash)))
+    auto fld = [&](const void* dbase, size_t esz, void* dst) {
+      return d2h((const char*)dbase + (size_t)first * esz, (size_t)n * esz, dst);
+    };
+    if ((rc = d2h(d_voff, 8 * (size_t)n, b->voffset)) || (rc = fld(rows.block_size, 4, b->block_size)) ||
+        (rc = fld(rows.ref_id, 4, b->ref_id)) || (rc = fld(rows.pos, 4, b->pos)) ||
+        (rc = fld(rows.l_seq, 4, b->l_seq)) || (rc = fld(rows.next_ref_id, 4, b->next_ref_id)) ||
+        (rc = fld(rows.next_pos, 4, b->next_pos)) || (rc = fld(rows.tlen, 4, b->tlen)) ||
+        (rc = fld(rows.flag, 2, b->flag)) || (rc = fld(rows.bin, 2, b->bin)) ||
+        (rc = fld(rows.n_cigar, 2, b->n_cigar)) || (rc = fld(rows.mapq, 1, b->mapq)) ||
+        (rc = fld(rows.l_read_name, 1, b->l_read_name)) || (rc = fld(rows.hash, 8, b->hash)) ||
+        (rc = d2h(ctx->x_boff.p, 8 * (size_t)n, b->raw_offset)))
       return fail(rc);
   }
-  if (ctx->base)
-    for (int64_t i = 0; i < n; i++) b->voffset[i] += (uint64_t)ctx->base << 16;
-  int64_t raw_len = 0;
-  for (int64_t i = 0; i < n; i++) {
-    b->raw_offset[i] = raw_len;
-    raw_len += 4 + (int64_t)b->block_size[i];
-  }
-  b->raw_len = raw_len;
   if (with_raw && n > 0) {
-    b->raw = (uint8_t*)host_alloc((size_t)std::max<int64_t>(1, raw_len));
+    b->raw = (uint8_t*)halloc((size_t)std::max<int64_t>(1, raw_len));
     if (!b->raw) return fail(DQ_ENOMEM);
     if (direct) {  // consecutive chain records are contiguous in U
       int64_t lo = 0;
       XCHK(hipMemcpy(&lo, ctx->rec_lin.as<int64_t>() + first, 8, hipMemcpyDeviceToHost));
-      if ((rc = d2h_large(ctx, b->raw, ctx->U.as<uint8_t>() + lo, (size_t)raw_len))) return fail(rc);
+      if (in_arena) XCHK(hipMemcpyAsync(b->raw, ctx->U.as<uint8_t>() + lo, (size_t)raw_len, hipMemcpyDeviceToHost, s));
+      else if ((rc = d2h_large(ctx, b->raw, ctx->U.as<uint8_t>() + lo, (size_t)raw_len))) return fail(rc);
     } else {
-      if ((rc = ensure_all(ctx, ctx->x_off, 8 * (size_t)n)) ||
-          (rc = ensure_all(ctx, ctx->x_raw, (size_t)raw_len)))
-        return fail(rc);
-      XCHK(hipMemcpyAsync(ctx->x_off.p, b->raw_offset, 8 * (size_t)n, hipMemcpyHostToDevice, s));
+      if ((rc = ensure_all(ctx, ctx->x_raw, (size_t)raw_len))) return fail(rc);
       launch_gather_raw(ctx->U.as<uint8_t>(), ctx->rec_lin.as<int64_t>(), ctx->f_bs.as<int32_t>(),
-                        d_idx, 0, n, ctx->x_off.as<int64_t>(), ctx->x_raw.as<uint8_t>(), s);
-      if ((rc = d2h_large(ctx, b->raw, ctx->x_raw.p, (size_t)raw_len))) return fail(rc);
+                        d_idx, 0, n, ctx->x_boff.as<int64_t>(), ctx->x_raw.as<uint8_t>(), s);
+      if (in_arena) XCHK(hipMemcpyAsync(b->raw, ctx->x_raw.p, (size_t)raw_len, hipMemcpyDeviceToHost, s));
+      else if ((rc = d2h_large(ctx, b->raw, ctx->x_raw.p, (size_t)raw_len))) return fail(rc);
     }
   }
-#undef XCHK
-  b->n_partitions = (int64_t)part_bounds.size() - 1;
-  if (b->n_partitions < 0) b->n_partitions = 0;
-  b->part_offset = (int64_t*)malloc(sizeof(int64_t) * (size_t)(b->n_partitions + 1));
-  b->part_digest = (uint64_t*)calloc((size_t)b->n_partitions + 1, sizeof(uint64_t));
+  b->n_partitions = np;
+  b->part_offset = (int64_t*)malloc(sizeof(int64_t) * (size_t)(np + 1));
+  b->part_digest = (uint64_t*)calloc((size_t)np + 1, sizeof(uint64_t));
   if (!b->part_offset || !b->part_digest) return fail(DQ_ENOMEM);
-  for (int64_t p = 0; p <= b->n_partitions; p++) b->part_offset[p] = part_bounds[(size_t)p];
-  for (int64_t p = 0; p < b->n_partitions; p++) {
-    uint64_t d = 0;
-    for (int64_t k = b->part_offset[p]; k < b->part_offset[p + 1]; k++)
-      d += dq_mix64(b->hash[k] + (uint64_t)(k - b->part_offset[p] + 1) * DQ_K_LEN);
-    b->part_digest[p] = d;
+  for (int64_t p = 0; p <= np; p++) b->part_offset[p] = part_bounds[(size_t)p];
+  if (np > 0 && n > 0) {
+    XCHK(hipMemcpyAsync(pr.data(), ctx->x_parts.p, sizeof(PartRange) * (size_t)np, hipMemcpyDeviceToHost, s));
   }
+  XCHK(hipStreamSynchronize(s));
+  for (int64_t p = 0; p < np; p++) b->part_digest[p] = n > 0 ? pr[(size_t)p].digest : 0;
+#undef XCHK
   *out = b;
   return 0;
 }
@@ -1855,9 +1897,41 @@ static void reset_open(dq_ctx* ctx, int64_t len) {
 // Bytes [off, off + len) of an open file into C (plus the 4 KiB zero pad): read() into two pinned
 // staging buffers in turn, each copied asynchronously while the next piece is read from the page
 // cache (the role of Disq's 2 x 4 MB NIO prefetcher, SeekableByteChannelPrefetcher.java:45).
+// The same by DMA straight from the file's page-cache pages: the range is mapped read-only and
+// registered with the device (page pinning, no byte copies), one copy reads it into C.  Returns
+// 1 when mapping or registration is not available (the caller then copies through staging).
+static int upload_file_range_mapped(dq_ctx* ctx, int fd, int64_t off, int64_t len) {
+  static const bool enabled = !(getenv("DQ_MMAP") && atoi(getenv("DQ_MMAP")) == 0);
+  if (!enabled || len < (64 << 20)) return 1;
+  const int64_t pg = (int64_t)sysconf(_SC_PAGESIZE);
+  const int64_t a = off & ~(pg - 1), d = off - a, mlen = len + d;
+  void* p = mmap(nullptr, (size_t)mlen, PROT_READ, MAP_SHARED, fd, (off_t)a);
+  if (p == MAP_FAILED) return 1;
+  if (hipHostRegister(p, (size_t)mlen, hipHostRegisterReadOnly) != hipSuccess) {
+    (void)hipGetLastError();
+    munmap(p, (size_t)mlen);
+    return 1;
+  }
+  int rc = ensure_all(ctx, ctx->C, (size_t)len + 4096);
+  hipError_t e = hipSuccess;
+  if (!rc) {
+    e = hipMemcpyAsync(ctx->C.as<uint8_t>(), (const uint8_t*)p + d, (size_t)len, hipMemcpyHostToDevice, ctx->s);
+    if (e == hipSuccess) e = hipMemsetAsync(ctx->C.as<uint8_t>() + len, 0, 4096, ctx->s);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->s);
+  }
+  (void)hipHostUnregister(p);
+  munmap(p, (size_t)mlen);
+  if (rc) return rc;
+  if (e != hipSuccess) RET(DQ_EDEVICE, std::string("file range H2D: ") + hipGetErrorString(e));
+  reset_open(ctx, len);
+  ctx->h2d_bytes = len;
+  return 0;
+}
+
 static int upload_file_range(dq_ctx* ctx, int fd, int64_t off, int64_t len) {
   constexpr size_t PIECE = PIN_PIECE;
   int rc;
+  if ((rc = upload_file_range_mapped(ctx, fd, off, len)) != 1) return rc;
   if ((rc = ensure_all(ctx, ctx->C, (size_t)len + 4096))) return rc;
   if ((rc = ensure_pinned(ctx))) return rc;
   bool used[2] = {false, false};
@@ -2101,6 +2175,7 @@ void dq_ctx_destroy(dq_ctx* ctx) {
     if (ctx->pin_ev[k]) (void)hipEventDestroy(ctx->pin_ev[k]);
     if (ctx->pin[k]) (void)hipHostFree(ctx->pin[k]);
   }
+  if (ctx->arena) (void)hipHostFree(ctx->arena);
   if (ctx->s) (void)hipStreamDestroy(ctx->s);
   delete ctx;
 }
@@ -2993,8 +3068,26 @@ int dq_bgzf_fetch(dq_ctx* ctx, uint8_t* host_out, int64_t cap) {
   return 0;
 }
 
+int dq_set_export_arena(dq_ctx* ctx, int64_t bytes) {
+  if (!ctx || bytes < 0) return DQ_EINVAL;
+  ON_DEVICE(ctx);
+  if (ctx->arena) (void)hipHostFree(ctx->arena);
+  ctx->arena = nullptr;
+  ctx->arena_cap = 0;
+  if (bytes == 0) return 0;
+  HIPCHK(hipHostMalloc((void**)&ctx->arena, (size_t)bytes, hipHostMallocDefault));
+  ctx->arena_cap = (size_t)bytes;
+  return 0;
+}
+
 void dq_batch_free(dq_batch* b) {
   if (!b) return;
+  if (b->in_arena) {  // the arrays live in the context's export arena
+    free(b->part_offset);
+    free(b->part_digest);
+    free(b);
+    return;
+  }
   free(b->voffset);
   free(b->block_size);
   free(b->ref_id);

@@ -181,6 +181,8 @@ void launch_sbi_sample(const uint64_t* voffset, int64_t nrec, int64_t g, uint64_
 void launch_partition_ranges(const SplitPlan* plans, int64_t nsplit, const int64_t* rec_lin,
                              const uint64_t* voffset, int64_t nrec, PartRange* parts,
                              int32_t* d_status, hipStream_t s);
+void launch_bs_plus4(const int32_t* bs, int64_t n, int32_t* out, hipStream_t s);
+void launch_add_u64(const uint64_t* in, int64_t n, uint64_t add, uint64_t* out, hipStream_t s);
 void launch_partition_digest2(const uint64_t* hash, PartRange* parts, int64_t nparts,
                               hipStream_t s);
 void launch_partition_digest_idx(const uint64_t* hash, const int64_t* kept, PartRange* parts,

@@ -1420,6 +1420,28 @@ void launch_partition_ranges(const SplitPlan* plans, int64_t nsplit, const int64
                      plans, nsplit, rec_lin, voffset, nrec, parts, d_status);
 }
 
+// Batch export helpers: 4 + block_size of each record (the raw-offset scan's input), and voffsets
+// translated by a shard's base.
+__global__ void bs_plus4_kernel(const int32_t* __restrict__ bs, int64_t n, int32_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = 4 + bs[i];
+}
+__global__ void add_u64_kernel(const uint64_t* __restrict__ in, int64_t n, uint64_t add,
+                               uint64_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = in[i] + add;
+}
+void launch_bs_plus4(const int32_t* bs, int64_t n, int32_t* out, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(bs_plus4_kernel, dim3((unsigned)std::min<int64_t>(4096, (n + 255) / 256)),
+                     dim3(256), 0, s, bs, n, out);
+}
+void launch_add_u64(const uint64_t* in, int64_t n, uint64_t add, uint64_t* out, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(add_u64_kernel, dim3((unsigned)std::min<int64_t>(4096, (n + 255) / 256)),
+                     dim3(256), 0, s, in, n, add, out);
+}
+
 void launch_partition_digest2(const uint64_t* hash, PartRange* parts, int64_t nparts, hipStream_t s) {
   if (nparts <= 0) return;
   hipLaunchKernelGGL(partition_digest_kernel, dim3((unsigned)nparts, DIG_SPLIT), dim3(256), 0, s,

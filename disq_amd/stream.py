@@ -27,14 +27,16 @@ from . import parallel as P
 def stream_read(read_bytes, file_len: int, header: bytes,
                 window: int = 8 << 30, depth: int = 2, split_size: int = 0,
                 use_nio: bool = False, hadoop_block_size: int = 0, device: int = 0,
-                verify_crc: bool = True, halo: int = 4 << 20, on_window=None) -> dict:
+                verify_crc: bool = True, halo: int = 4 << 20, on_window=None,
+                contexts=None) -> dict:
     """Decode the whole file in windows of ~`window` compressed bytes on one GPU.
 
     read_bytes(a, b) returns the file's bytes [a, b) (page cache, host memory or a generator), or
     read_bytes is a path: the library reads each window itself (dq_open_shard_path).
     on_window(k, ctx, shard), if given, runs on the window's context after its pipeline (e.g. to
-    export records with ctx.read()).  Returns the per-partition counts and digests, the whole-file
-    digest, record and decompressed byte totals, and timings."""
+    export records with ctx.read()).  contexts: `depth` open Contexts to use (e.g. set up with an
+    export arena beforehand); they stay open.  Returns the per-partition counts and digests, the
+    whole-file digest, record and decompressed byte totals, and timings."""
     from . import _lib
     split_opts = dict(split_size=split_size, use_nio=use_nio, hadoop_block_size=hadoop_block_size)
     nwin = max(1, math.ceil(file_len / max(1, window)))
@@ -42,16 +44,21 @@ def stream_read(read_bytes, file_len: int, header: bytes,
     nsplit = len(P.path_splits(file_len, **split_opts))
     counts = np.zeros(nsplit, np.int64)
     digests = np.zeros(nsplit, np.uint64)
-    totals = {"records": 0, "owned_bytes": 0, "compressed_read": 0, "ms_device": 0.0}
+    totals = {"records": 0, "owned_bytes": 0, "compressed_read": 0, "ms_device": 0.0,
+              "open_s": 0.0, "run_s": 0.0, "on_window_s": 0.0}
     lock = threading.Lock()
     nxt = [0]
     errors = []
 
-    def worker():
+    import contextlib
+
+    def worker(slot):
         try:
-            with _lib.Context(split_size=split_size, use_nio=use_nio,
-                              hadoop_block_size=hadoop_block_size, verify_crc=verify_crc,
-                              device=device) as c:
+            cm = (contextlib.nullcontext(contexts[slot]) if contexts is not None else
+                  _lib.Context(split_size=split_size, use_nio=use_nio,
+                               hadoop_block_size=hadoop_block_size, verify_crc=verify_crc,
+                               device=device))
+            with cm as c:
                 while True:
                     with lock:
                         k = nxt[0]
@@ -63,12 +70,15 @@ def stream_read(read_bytes, file_len: int, header: bytes,
                     while True:
                         end = min(file_len, s.hi + h)
                         try:
+                            t0 = time.perf_counter()
                             if isinstance(read_bytes, str):
                                 c.open_shard_path(read_bytes, s.lo, end - s.lo, s.p0, s.p1, header)
                             else:
                                 c.open_shard(read_bytes(s.lo, end), s.lo, file_len, s.p0, s.p1,
                                              header)
+                            t1 = time.perf_counter()
                             st = c.run_resident()
+                            t2 = time.perf_counter()
                             break
                         except _lib.DqError as e:
                             if "halo too small" in str(e) and end < file_len:
@@ -76,9 +86,14 @@ def stream_read(read_bytes, file_len: int, header: bytes,
                                 continue
                             raise
                     cnt, dig = c.partition_digests()
+                    t3 = time.perf_counter()
                     if on_window is not None:
                         on_window(k, c, s)
+                    t4 = time.perf_counter()
                     with lock:
+                        totals["open_s"] += t1 - t0
+                        totals["run_s"] += t2 - t1
+                        totals["on_window_s"] += t4 - t3
                         counts[s.p0:s.p1] = cnt
                         digests[s.p0:s.p1] = dig
                         totals["records"] += st.n_records
@@ -90,7 +105,8 @@ def stream_read(read_bytes, file_len: int, header: bytes,
                 errors.append(e)
 
     t0 = time.perf_counter()
-    th = [threading.Thread(target=worker) for _ in range(max(1, min(depth, len(plan))))]
+    nth = max(1, min(depth if contexts is None else len(contexts), len(plan)))
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(nth)]
     for t in th:
         t.start()
     for t in th:

@@ -108,6 +108,8 @@ typedef struct dq_batch {
   int64_t n_partitions;
   int64_t* part_offset;  /* n_partitions + 1 entries: partition p = [part_offset[p], [p+1]) */
   uint64_t* part_digest; /* ordered digest of each partition's record hashes */
+  int32_t in_arena;      /* 1: the arrays live in the context's export arena (dq_set_export_arena) */
+  int32_t reserved;
 } dq_batch;
 
 /* Interval traversal (HtsjdkReadsTraversalParameters, D/HtsjdkReadsTraversalParameters.java):
@@ -361,6 +363,12 @@ int dq_bgzf_compress(dq_ctx* ctx, const uint8_t* data, int64_t len, uint8_t** ou
 int dq_bgzf_compress_resident(dq_ctx* ctx, int64_t* out_len, double* ms);
 int dq_bgzf_fetch(dq_ctx* ctx, uint8_t* host_out, int64_t cap);
 
+/* Export arena: batches of this context (dq_read, dq_decode*) place their arrays in `bytes` of
+ * pinned host memory owned by the context, copied by DMA with no staging copies (a batch that does
+ * not fit takes heap memory as before).  An arena batch's arrays stay valid until the next batch
+ * of the context, dq_set_export_arena or dq_ctx_destroy: a streaming consumer's recycled buffers
+ * (one Spark task's records at a time).  bytes = 0 releases the arena. */
+int dq_set_export_arena(dq_ctx* ctx, int64_t bytes);
 void dq_batch_free(dq_batch* b);
 void dq_free(void* p);
 

@@ -95,6 +95,22 @@ def test_long_reads():
         assert_parity(s.bam, split)
 
 
+def test_long_reads_2000_records():
+    """configs[4] shape at >= 2,000 records (BamSource.java:110-153: the guesser walks up to
+    MAX_READ_SIZE positions; BamRecordGuesser.java:34-52): ONT-like 10-100 kb reads and 1 % of
+    0.5-2 Mb whose records span up to ~46 BGZF blocks; every partition field by field, the
+    decompressed stream and the plan equal the oracle's, at split sizes down to 1 MiB (many splits
+    start inside a record)."""
+    s = synth.generate(2000, seed=41, shape=synth.LONGREAD, records_per_chunk=250, nthreads=8)
+    assert s.n_records == 2000
+    big = np.frombuffer(s.bam, np.uint8)
+    assert len(big) > 40 << 20
+    for split in (1 << 20, 8 << 20):
+        b = assert_parity(s.bam, split)
+        assert len(b["voffset"]) >= 2000
+        assert int(b["block_size"].max()) > 4 * 65536  # records spanning many blocks
+
+
 @pytest.fixture(scope="module")
 def anysam():
     return synth.generate(1000, shape=synth.ANYSAM, bai=True)
