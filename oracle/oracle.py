@@ -42,6 +42,9 @@ HADOOP_LOCAL_BLOCK_SIZE = 32 * 1024 * 1024  # fs.local.block.size default (Hadoo
 
 
 def build() -> str:
+    # DQ_ORACLE_LIB: another build of the same sources (tools/oracle_asan.sh: the ASan/UBSan one)
+    if os.environ.get("DQ_ORACLE_LIB"):
+        return os.environ["DQ_ORACLE_LIB"]
     if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(
         os.path.join(_HERE, "disq_oracle.c")
     ):

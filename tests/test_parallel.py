@@ -451,6 +451,58 @@ def test_exchange_path_on_nccl_world1(tmp_path):
 
 
 @pytest.mark.gpu
+def test_resident_shard_in_place_halo_growth():
+    """The in-place RCCL branch of read_shard_exchange without a second GPU: rank 0 of 2 holds
+    its bytes in a ResidentShard, the halo lands in `recv` by a device-to-device copy (what the
+    nccl irecv does), a halo too small for the straddling record is grown x4 -- reserve()
+    reallocates and must keep the own bytes -- and the span decoded in place
+    (dq_open_shard_device) equals the oracle's partitions of that shard."""
+    import torch
+    from disq_amd import _lib, synth
+    r = synth.generate(60000, seed=29, nthreads=8, unplaced_fraction=0.005)
+    data, split = r.bam, 1 << 20
+    n = len(data)
+    offsets = [0, n // 2, n]
+    plan = P.shard_plan(n, 2, offsets, split_size=split)
+    s = plan[0]
+    assert not s.empty and s.hi > offsets[1]
+    full = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda:0")  # "rank 1's" HBM
+    rs = P.ResidentShard(full[:offsets[1]].clone(), torch.device("cuda:0"))
+    with _lib.Context(split_size=split) as hc:
+        header = hc.header_from_prefix(data[:1 << 20])
+    ob = O.OracleBam(data)
+    oplan = ob.plan(split)
+    parts = iter(ob.read_partitions(split))
+    want = {i: next(parts) for i, (_, _, ch) in enumerate(oplan) if ch is not None}
+    halo, grown, caps = 256, 0, []
+    while True:
+        tr = [(a, b) for _, rr, a, b in P.halo_transfers(plan, offsets, n, halo) if rr == 0]
+        rs.reserve(sum(b - a for a, b in tr))
+        caps.append(rs.cap)
+        pos = 0
+        for a, b in tr:  # the receive: HBM to HBM
+            rs.recv[pos:pos + b - a].copy_(full[a:b])
+            pos += b - a
+        torch.cuda.synchronize()
+        ptr, ln = rs.span(s.lo - offsets[0])
+        try:
+            with _lib.Context(split_size=split) as c:
+                c.open_shard_device(ptr, ln, s.lo, n, s.p0, s.p1, header)
+                b = c.read(with_raw=False)
+            break
+        except _lib.DqError as e:
+            assert "halo too small" in str(e)
+            halo *= 4
+            grown += 1
+    assert grown >= 1 and len(set(caps)) >= 2  # the buffer was reallocated at least once
+    assert torch.equal(rs.own, full[:offsets[1]])  # the own bytes survived the reallocation
+    got = np.concatenate([want[p] for p in range(s.p0, s.p1) if p in want])
+    assert len(b["voffset"]) == len(got)
+    for f in FIELDS:
+        assert np.array_equal(b[f], got[f]), f
+
+
+@pytest.mark.gpu
 def test_unplaced_tail_needs_the_file_end():
     """queryUnmapped reads to the end of the file: a shard that stops earlier refuses
     traverseUnplacedUnmapped instead of returning a cut tail; the last shard runs it, with the
