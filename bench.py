@@ -72,6 +72,9 @@ def parse():
     ap.add_argument("--e2e-window-gb", type=float, default=2.0,
                     help="end-to-end: compressed GB per window")
     ap.add_argument("--e2e-depth", type=int, default=3, help="end-to-end: overlapping windows")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="generation rehearsal: generate rank 0's share of an N-rank run under "
+                         "the N-rank thread budget, report the time as JSON and exit (no GPU work)")
     return ap.parse_args()
 
 
@@ -103,7 +106,8 @@ def main():
     rehearsal = os.environ.get("DQ_BENCH_REHEARSAL") == "1"
     if rehearsal:
         local = 0
-    torch.cuda.set_device(local)
+    if not args.emulate_world:
+        torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     cdev = torch.device("cpu") if rehearsal else dev  # where collective tensors live
     dist = None
@@ -114,7 +118,9 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=dev)
     aff, quota, ncores = usable_cores()
-    gen_threads = max(1, min(32, ncores // max(1, local_world)))
+    # the generation's world: this run's, or the one a rehearsal emulates (rank 0 of it)
+    gworld = args.emulate_world or world
+    gen_threads = max(1, min(32, ncores // max(1, args.emulate_world or local_world)))
 
     from disq_amd import _lib, parallel as P, synth
 
@@ -126,10 +132,10 @@ def main():
     probe = synth.generate(per_chunk, seed=args.seed, nthreads=gen_threads, shape=shape)
     probe_s = time.time() - t0  # one chunk, on one thread
     per_rec = len(probe.bam) / probe.n_records
-    n_total = int(args.gb * 1e9 / per_rec) * world
+    n_total = int(args.gb * 1e9 / per_rec) * gworld
     nchunks = synth.chunk_count(n_total, shape=shape)
-    k0, k1 = rank * nchunks // world, (rank + 1) * nchunks // world
-    want_bai = world == 1 and args.intervals > 0 and shape == synth.WGS
+    k0, k1 = rank * nchunks // gworld, (rank + 1) * nchunks // gworld
+    want_bai = gworld == 1 and args.intervals > 0 and shape == synth.WGS
     # Generation budget: zlib level 5 (htsjdk's) costs ~1 thread-second per chunk, so with few
     # threads per rank (an 8-GPU node under a small CPU quota) the ranks generate a pool of
     # distinct chunks and tile it over their byte range (the blocks are the same level-5 BGZF
@@ -137,7 +143,7 @@ def main():
     # and any rank that fits the budget generate every chunk.
     est = (k1 - k0) * probe_s / max(1, gen_threads)
     pool = None
-    if world > 1 and est > args.gen_budget_s:
+    if gworld > 1 and est > args.gen_budget_s:
         pool = max(2 * gen_threads, int(args.gen_budget_s * gen_threads / max(probe_s, 1e-3)))
     log(f"[bench] rank {rank}: chunks [{k0}, {k1}) of {nchunks} ({n_total} records in the file), "
         f"{gen_threads} threads, estimated {est:.0f} s" + (f", pool of {pool} chunks" if pool else ""))
@@ -145,7 +151,7 @@ def main():
     if pool is None or pool >= k1 - k0:
         res, free = synth.generate(n_total, seed=args.seed, nthreads=gen_threads, as_buffer=True,
                                    bai=want_bai, unplaced_fraction=0.005, shape=shape,
-                                   chunks=None if world == 1 else (k0, k1))
+                                   chunks=None if gworld == 1 else (k0, k1))
         own_len = res.bam_len
         own_np = np.ctypeslib.as_array((ctypes.c_uint8 * own_len).from_address(res.bam))
         gen_desc = {"distinct_chunks": k1 - k0, "tiled_chunks": 0}
@@ -158,6 +164,17 @@ def main():
                     "tiled_chunks": (k1 - k0) - pool - (1 if k0 == 0 else 0),
                     "note": "a pool of distinct level-5 chunks tiled over the rank's range"}
     gen_s = time.time() - t0
+    if args.emulate_world:
+        free()
+        print(json.dumps({
+            "rehearsal": f"generation of rank 0 of {gworld} (bench.py --gpus {gworld}), no GPU work",
+            "gb_per_rank": args.gb, "shape": args.shape, "threads_per_rank": gen_threads,
+            "usable_cores": ncores, "host_cores": aff, "cgroup_cpu_quota": quota,
+            "chunks_of_rank": k1 - k0, "chunks_in_file": nchunks, "probe_chunk_s": round(probe_s, 3),
+            "estimated_full_s": round(est, 1), "gen_budget_s": args.gen_budget_s,
+            "generator": gen_desc, "own_gb": round(own_len / 1e9, 3),
+            "generator_s": round(gen_s, 1)}), flush=True)
+        return
     lens = [own_len]
     if dist is not None:
         t = torch.tensor([own_len], dtype=torch.int64, device=cdev)

@@ -139,10 +139,11 @@ struct dq_ctx {
   int64_t header_bytes = 0;
   DevBuf d_ref_len;
   // planning
-  DevBuf plans;
+  DevBuf plans, plan_best;  // plan_best: the record guesser's per-split minima (planning scratch)
   std::vector<SplitPlan> plans_h;
   // records
   DevBuf segs, segcnt, segbase, rec_lin, pages;
+  DevBuf long_ent, long_cnt;  // long records' pieces (decode_records: hashed by many threads)
   DevBuf f_voff, f_bs, f_ref, f_pos, f_lseq, f_nref, f_npos, f_tlen, f_flag, f_bin, f_ncig, f_mapq,
       f_lrn, f_hash;
   int64_t nrec = 0;
@@ -260,6 +261,24 @@ int ensure_all(dq_ctx* ctx, DevBuf& b, size_t bytes) {
 // recursion): every scan sizes it for its own n.
 int ensure_scan(dq_ctx* ctx, int64_t n) {
   return ensure_all(ctx, ctx->tmp, sizeof(int64_t) * (size_t)(4 * (n / 1024 + 1) + 4096));
+}
+
+// Kernel 3's decode of ctx->rec_lin[0, nrec) into the SoA (+ the page table and the long-record
+// piece list it needs as scratch).
+int decode_records(dq_ctx* ctx, int64_t nrec, int64_t nblk, int32_t* d_stat, hipStream_t s) {
+  int rc;
+  const int64_t ulen = ctx->ulen;
+  const int64_t lcap = long_list_cap(ulen, nrec);
+  if ((rc = ensure_all(ctx, ctx->pages, 4 * (size_t)((ulen >> 16) + 1))) ||
+      (rc = ensure_all(ctx, ctx->long_ent, 8 * (size_t)lcap)) ||
+      (rc = ensure_all(ctx, ctx->long_cnt, 8)))
+    return rc;
+  HIPCHK(hipMemsetAsync(d_stat, 0, 4, s));
+  launch_decode_records(ctx->U.as<uint8_t>(), ulen, ctx->rec_lin.as<int64_t>(), nrec,
+                        ctx->blk_pos.as<int64_t>(), ctx->uoff.as<int64_t>(), nblk,
+                        ctx->pages.as<int32_t>(), ctx->soa(), d_stat, ctx->long_ent.as<uint64_t>(),
+                        lcap, ctx->long_cnt.as<unsigned long long>(), s);
+  return 0;
 }
 
 const char* status_name(int32_t st) {
@@ -507,9 +526,8 @@ std::vector<Interval> optimize(std::vector<Interval> v) {
 
 // DQ_DEBUG=1: synchronise and report after every pipeline stage.
 bool dbg_on() {
-  static int v = -1;
-  if (v < 0) v = getenv("DQ_DEBUG") ? 1 : 0;
-  return v == 1;
+  static const bool v = getenv("DQ_DEBUG") != nullptr;  // initialised once, thread-safely
+  return v;
 }
 void dbg(hipStream_t s, const char* what, long long a = 0, long long b = 0) {
   if (!dbg_on()) return;
@@ -651,20 +669,20 @@ static int run_pipeline(dq_ctx* ctx) {
     if (!crc_init) RET(DQ_EDEVICE, "CRC32 table initialisation failed on this device");
     static const bool timing = getenv("DQ_TIMING") != nullptr;
     uint64_t* tim = nullptr;
-    if (timing) HIPCHK(hipMalloc(&tim, sizeof(uint64_t) * 16 * (size_t)std::max<int64_t>(1, nblk)));
+    if (timing) HIPCHK(hipMalloc(&tim, sizeof(uint64_t) * 24 * (size_t)std::max<int64_t>(1, nblk)));
     HIPCHK(hipEventRecord(ctx->ev[5], s));
     launch_inflate3(ctx->cbuf(), ctx->blk_pos.as<int64_t>(), ctx->blk_cs.as<int32_t>(),
                     ctx->blk_us.as<int32_t>(), ctx->uoff.as<int64_t>(), nblk, ctx->U.as<uint8_t>(),
                     ctx->status.as<int32_t>(), ctx->o.verify_crc, crc_init, tim, s);
     HIPCHK(hipEventRecord(ctx->ev[6], s));
     if (timing) {
-      std::vector<uint64_t> h(16 * (size_t)nblk);
+      std::vector<uint64_t> h(24 * (size_t)nblk);
       HIPCHK(hipMemcpyAsync(h.data(), tim, 8 * h.size(), hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
       (void)hipFree(tim);
-      double acc[16] = {0};
+      double acc[24] = {0};
       for (int64_t i = 0; i < nblk; i++)
-        for (int k = 0; k < 16; k++) acc[k] += (double)h[16 * (size_t)i + k];
+        for (int k = 0; k < 24; k++) acc[k] += (double)h[24 * (size_t)i + k];
       static const char* nm[16] = {"header", "tables", "spec", "rounds", "scan", "emit",
                                    "resolve+store", "crc", "hdr_read_lengths", "resolve_hop_next", "redo_rounds", "tables_build",
                                    "resolve_steps_jumps", "resolve_store", "resolve_jump_tail", "res_batches"};
@@ -672,6 +690,12 @@ static int run_pipeline(dq_ctx* ctx) {
       for (int k = 0; k < 16; k++)
         if (nm[k][0] != '-') fprintf(stderr, " %s=%.0f", nm[k], acc[k] / (double)std::max<int64_t>(1, nblk));
       fprintf(stderr, "\n");
+      const double nb = (double)std::max<int64_t>(1, nblk);
+      fprintf(stderr, "[dq] first deflate block: header=%.0f tables=%.0f spec=%.0f rounds=%.0f emit=%.0f; "
+              "later ones: header=%.0f tables=%.0f spec=%.0f rounds=%.0f emit=%.0f; deflate blocks per "
+              "BGZF block %.3f\n", acc[16] / nb, acc[17] / nb, acc[18] / nb, acc[19] / nb, acc[21] / nb,
+              (acc[0] - acc[16]) / nb, (acc[1] - acc[17]) / nb, (acc[2] - acc[18]) / nb,
+              (acc[3] - acc[19]) / nb, (acc[5] - acc[21]) / nb, acc[22] / nb);
     }
   }
   dbg(s, "inflate", nblk, ulen);
@@ -770,11 +794,21 @@ static int run_pipeline(dq_ctx* ctx) {
   launch_plan_blocks(ctx->cand.as<Cand>(), d_ncand, ctx->blk_pos.as<int64_t>(),
                      ctx->blk_us.as<int32_t>(), ctx->uoff.as<int64_t>(), d_nblk,
                      ctx->plans.as<SplitPlan>(), nsplit, s);
+  if ((rc = ensure_all(ctx, ctx->plan_best, 16 * (size_t)nsplit))) return rc;
   launch_first_record(ctx->U.as<uint8_t>(), ulen, is_eof, ctx->d_ref_len.as<int32_t>(), ctx->n_ref,
                       ctx->blk_pos.as<int64_t>(), ctx->uoff.as<int64_t>(), d_nblk,
-                      ctx->plans.as<SplitPlan>(), nsplit, s);
+                      ctx->plans.as<SplitPlan>(), nsplit, ctx->plan_best.as<unsigned long long>(), s);
   HIPCHK(hipMemcpyAsync(ctx->plans_h.data(), ctx->plans.p, sizeof(SplitPlan) * (size_t)nsplit,
                         hipMemcpyDeviceToHost, s));
+  }
+  // block statistics (DEFLATE payload bytes, the shard's chain end and owned bytes) by a device
+  // reduction, back with the same synchronisation (the block table itself stays in HBM)
+  uint64_t bstat[4] = {0, 0, 0, 0};
+  {
+    uint64_t* d_bs = reinterpret_cast<uint64_t*>(ctx->scal.as<char>() + 160);
+    launch_block_stats(ctx->blk_pos.as<int64_t>(), ctx->blk_cs.as<int32_t>(), ctx->uoff.as<int64_t>(),
+                       nblk, ulen, splits.empty() ? 0 : splits.back().second, d_bs, s);
+    HIPCHK(hipMemcpyAsync(bstat, d_bs, sizeof bstat, hipMemcpyDeviceToHost, s));
   }
   HIPCHK(hipStreamSynchronize(s));
   HIPCHK(hipEventRecord(ctx->ev[3], s));
@@ -805,16 +839,26 @@ static int run_pipeline(dq_ctx* ctx) {
   }
   // ---- Kernel 3: record chain, SoA decode, hashes
   int64_t nrec = 0;
-  const int64_t SEG = 64 * 1024;  // record-chain segment: one wave walks it
+  // record-chain segment: one wave finds its first record start by the guesser, one lane walks it.
+  // 64 KiB for short reads (~180 records to walk); for long records, ~16 typical records (the
+  // median 10-record span the planning's guesser chained), so the speculation does not run the
+  // guesser over every byte of segments that no record starts in (long reads, configs[4])
+  int64_t SEG = 64 * 1024;
+  {
+    std::vector<int32_t> sp;
+    for (auto& P : ctx->plans_h)
+      if (P.rec_lin >= 0 && P.rec_span > 0) sp.push_back(P.rec_span);
+    if (!sp.empty()) {
+      std::nth_element(sp.begin(), sp.begin() + sp.size() / 2, sp.end());
+      const int64_t want = 16 * (int64_t)sp[sp.size() / 2] / 10;
+      while (SEG < want && SEG < (4 << 20)) SEG <<= 1;
+    }
+  }
   // record starts wanted: all of U, or (shard) those in blocks at or before the last split end
   int64_t chain_end = ulen;
   if (ctx->shard && !is_eof && nblk > 0) {
-    std::vector<int64_t> bp((size_t)nblk);
-    HIPCHK(hipMemcpy(bp.data(), ctx->blk_pos.p, 8 * (size_t)nblk, hipMemcpyDeviceToHost));
-    const int64_t last_end = splits.back().second;
-    const int64_t j = std::upper_bound(bp.begin(), bp.end(), last_end) - bp.begin();
-    if (j >= nblk) RET(DQ_EFORMAT, "shard halo too small: no BGZF block after the last split");
-    HIPCHK(hipMemcpy(&chain_end, ctx->uoff.as<int64_t>() + j, 8, hipMemcpyDeviceToHost));
+    if ((int64_t)bstat[3] >= nblk) RET(DQ_EFORMAT, "shard halo too small: no BGZF block after the last split");
+    chain_end = (int64_t)bstat[1];
   }
   if (start_lin >= 0 && start_lin < chain_end) {
     const int64_t nseg = (chain_end - start_lin + SEG - 1) / SEG;
@@ -856,11 +900,7 @@ static int run_pipeline(dq_ctx* ctx) {
     for (auto* b : b4) if ((rc = ensure_all(ctx, *b, 4 * nr))) return rc;
     for (auto* b : b2) if ((rc = ensure_all(ctx, *b, 2 * nr))) return rc;
     for (auto* b : b1) if ((rc = ensure_all(ctx, *b, nr))) return rc;
-    if ((rc = ensure_all(ctx, ctx->pages, 4 * (size_t)((ulen >> 16) + 1)))) return rc;
-    HIPCHK(hipMemsetAsync(d_stat, 0, 4, s));
-    launch_decode_records(ctx->U.as<uint8_t>(), ulen, ctx->rec_lin.as<int64_t>(), nrec,
-                          ctx->blk_pos.as<int64_t>(), ctx->uoff.as<int64_t>(), nblk,
-                          ctx->pages.as<int32_t>(), ctx->soa(), d_stat, s);
+    if ((rc = decode_records(ctx, nrec, nblk, d_stat, s))) return rc;
   }
   dbg(s, "decode", nrec);
   ctx->nrec = nrec;
@@ -900,29 +940,11 @@ static int run_pipeline(dq_ctx* ctx) {
   S.ms_scan = ev_ms(ctx->ev[0], ctx->ev[1]);
   S.ms_inflate = ev_ms(ctx->ev[5], ctx->ev[6]);  // the inflate kernel (CRC32 fused)
   S.ms_crc = 0;                                   // fused into the inflate kernel
-  {
-    // DEFLATE payload bytes = sum over blocks of (BSIZE + 1 - 26): csize - 18 header - 8 trailer;
-    // owned bytes = the decompressed bytes of the blocks that start inside the splits (the
-    // whole stream for a whole file; over the shards of a file they add up to its size)
-    std::vector<int32_t> cs((size_t)nblk);
-    std::vector<int64_t> bp((size_t)nblk);
-    if (nblk) {
-      HIPCHK(hipMemcpyAsync(cs.data(), ctx->blk_cs.p, 4 * (size_t)nblk, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipMemcpyAsync(bp.data(), ctx->blk_pos.p, 8 * (size_t)nblk, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipStreamSynchronize(s));
-    }
-    int64_t db = 0;
-    for (int32_t c : cs) db += c - 26;
-    S.deflate_bytes = db;
-    S.owned_bytes = ulen;
-    if (ctx->shard && nblk) {
-      const int64_t last_end = splits.back().second;
-      const int64_t j = std::lower_bound(bp.begin(), bp.end(), last_end) - bp.begin();
-      int64_t u = ulen;
-      if (j < nblk) HIPCHK(hipMemcpy(&u, ctx->uoff.as<int64_t>() + j, 8, hipMemcpyDeviceToHost));
-      S.owned_bytes = u;
-    }
-  }
+  // DEFLATE payload bytes = sum over blocks of (BSIZE + 1 - 26): csize - 18 header - 8 trailer;
+  // owned bytes = the decompressed bytes of the blocks that start inside the splits (the whole
+  // stream for a whole file; over the shards of a file they add up to its size)
+  S.deflate_bytes = (int64_t)bstat[0];
+  S.owned_bytes = ctx->shard && nblk ? (int64_t)bstat[2] : ulen;
   S.ms_plan = ev_ms(ctx->ev[2], ctx->ev[3]);
   S.ms_records = ev_ms(ctx->ev[3], ctx->ev[4]);
   S.ms_total = ev_ms(ctx->ev[0], ctx->ev[4]);
@@ -1751,10 +1773,7 @@ static int run_span(dq_ctx* ctx, const dq_traversal* tr, dq_stats* out) {
     if (nrec > 0) {
       launch_seg_emit2(ctx->U.as<uint8_t>(), ctx->ulen, ctx->segs.as<Seg>(),
                        ctx->segbase.as<int64_t>(), nseg, ctx->rec_lin.as<int64_t>(), s);
-      HIPCHK(hipMemsetAsync(d_stat, 0, 4, s));
-      launch_decode_records(ctx->U.as<uint8_t>(), ctx->ulen, ctx->rec_lin.as<int64_t>(), nrec,
-                            ctx->blk_pos.as<int64_t>(), ctx->uoff.as<int64_t>(), nblk,
-                            ctx->pages.as<int32_t>(), ctx->soa(), d_stat, s);
+      if ((rc = decode_records(ctx, nrec, nblk, d_stat, s))) return rc;
     }
     // 5. records of every span chunk, kernel 4, per-partition digests of the kept records
     int64_t nidx = 0;

@@ -863,7 +863,9 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   const int NCK = (int)(ckcfg >> 8) & 31;   // checkpoints per lane
   __shared__ LdsI L;
   // DQ_TIMING: thread 0 accumulates s_memtime cycles per phase (tim != nullptr only then)
-  uint64_t tacc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  // [0..15] phases over the BGZF block; [16..21] phases 0-5 of its first deflate block; [22] the
+  // number of deflate blocks
+  uint64_t tacc[24] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t tlast = TIMING ? __builtin_amdgcn_s_memtime() : 0;
 #define TST(i)                                            \
   do {                                                    \
@@ -1187,6 +1189,11 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     __syncthreads();
     TST(5);
     produced = min(isize, produced + total);
+    if (TIMING && t == 0) {
+      if (tacc[22] == 0)
+        for (int i = 0; i < 6; i++) tacc[16 + i] = tacc[i];
+      tacc[22] += 1;
+    }
     if (full || bfinal) break;
     pos = (uint32_t)nextpos;
   }
@@ -1456,7 +1463,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   }
   TST(7);
   if (TIMING && t == 0)
-    for (int i = 0; i < 16; i++) tim[(int64_t)blockIdx.x * 16 + i] = tacc[i];
+    for (int i = 0; i < 24; i++) tim[(int64_t)blockIdx.x * 24 + i] = tacc[i];
 }
 
 uint32_t h_mul(uint32_t a, uint32_t b) {

@@ -94,6 +94,11 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
                      int32_t* status, int32_t verify_crc, const uint32_t* crc_init, uint64_t* tim,
                      hipStream_t s, const int32_t* sel = nullptr, int64_t nsel = 0);
 
+// out[0] = sum of (csize - 26) over the blocks; out[1] / out[2] = uoff of the first block starting
+// after / at or after x (ulen if none); out[3] = the index of the first block starting after x.
+void launch_block_stats(const int64_t* blk_pos, const int32_t* blk_cs, const int64_t* uoff,
+                        int64_t nblk, int64_t ulen, int64_t x, uint64_t* out, hipStream_t s);
+
 // Split planning (a2-a4).
 constexpr int64_t SPLIT_FROM_SBI = -2;  // SplitPlan.first_blk of a chunk taken from a .sbi
 struct SplitPlan {
@@ -103,16 +108,18 @@ struct SplitPlan {
   int64_t rec_lin;       // linear U offset of the first record (-1 = empty partition)
   uint64_t vstart, vend;
   int32_t status;        // 0 ok; 100 = needs more data; else error
-  int32_t pad;
+  int32_t rec_span;      // bytes of the <= 10 records chained from rec_lin (segment sizing)
 };
 void launch_plan_blocks(const Cand* cand, const int64_t* d_ncand, const int64_t* blk_pos,
                         const int32_t* blk_usize, const int64_t* uoff, const int64_t* d_nblk,
                         SplitPlan* plans, int64_t nsplit, hipStream_t s);
 void launch_guess_all(const uint8_t* U, int64_t ulen, int32_t u_is_eof, const int32_t* ref_len,
                       int32_t n_ref, uint8_t* flag, hipStream_t s);
+// best: 2 * nsplit words of device scratch
 void launch_first_record(const uint8_t* U, int64_t ulen, int32_t u_is_eof, const int32_t* ref_len,
                          int32_t n_ref, const int64_t* blk_pos, const int64_t* uoff,
-                         const int64_t* d_nblk, SplitPlan* plans, int64_t nsplit, hipStream_t s);
+                         const int64_t* d_nblk, SplitPlan* plans, int64_t nsplit,
+                         unsigned long long* best, hipStream_t s);
 
 // Kernel 3: record chain over U from `start_lin`.
 struct Seg {
@@ -167,10 +174,13 @@ struct RecSoA {
   uint8_t* l_read_name;
   uint64_t* hash;
 };
-// pt: (ulen >> 16) + 1 int32 scratch (block page table)
+// pt: (ulen >> 16) + 1 int32 scratch (block page table); long_ent: long_list_cap(ulen, nrec)
+// entries (the pieces of the records hashed by many threads), long_cnt: one device counter
+int64_t long_list_cap(int64_t ulen, int64_t nrec);
 void launch_decode_records(const uint8_t* U, int64_t ulen, const int64_t* rec_lin, int64_t nrec,
                            const int64_t* blk_pos, const int64_t* uoff, int64_t nblk, int32_t* pt,
-                           RecSoA soa, int32_t* d_status, hipStream_t s);
+                           RecSoA soa, int32_t* d_status, uint64_t* long_ent, int64_t long_cap,
+                           unsigned long long* long_cnt, hipStream_t s);
 
 struct PartRange {
   int64_t begin, end;   // record index range in the chain

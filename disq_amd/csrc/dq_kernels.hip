@@ -301,12 +301,35 @@ __device__ int check_internal(const uint8_t* U, int64_t ulen, int u_is_eof, cons
   if ((flags & 4) == 0 && (seq_len == 0 || n_cig == 0)) return 0;
   if ((e = rd_ok(v + 36, name_len, ulen, u_is_eof))) return e;
   if (U[v + 36 + name_len - 1] != 0) return 0;
-  for (int i = 0; i < name_len - 1; i++) {
-    int8_t b = (int8_t)U[v + 36 + i];
-    if (!((b >= '!' && b <= '?') || (b >= 'A' && b <= '~'))) return 0;
+  for (int i = 0; i < name_len - 1; i += 16) {  // 16 name bytes per round of loads
+    uint8_t b16[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) b16[k] = i + k < name_len - 1 ? U[v + 36 + i + k] : (uint8_t)'A';
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const int8_t b = (int8_t)b16[k];
+      if (!((b >= '!' && b <= '?') || (b >= 'A' && b <= '~'))) return 0;
+    }
   }
   int64_t cp = v + 36 + name_len;
-  for (int i = 0; i < n_cig; i++) {
+  int i = 0;
+  // the ops 8 at a time from nine aligned dwords, all loads in flight (a long read's CIGAR has
+  // thousands of ops: one dependent byte-load round trip per op made the guesser the planning's
+  // critical path); the checks keep the op order
+  const uint32_t* U32 = reinterpret_cast<const uint32_t*>(U);
+  for (; i + 8 <= n_cig && cp + 32 <= ulen; i += 8, cp += 32) {
+    const uint32_t sh = (uint32_t)(cp & 3);
+    uint32_t d[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) d[k] = U32[(cp >> 2) + k];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int32_t op = (int32_t)__builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+      if (op == -1) return 3;
+      if ((op & 0xf) > 8) return 0;
+    }
+  }
+  for (; i < n_cig; i++) {
     if ((e = rd_ok(cp, 4, ulen, u_is_eof))) return e;
     int32_t op = ld32(U, cp);
     if (op == -1) return 3;
@@ -450,50 +473,70 @@ __global__ void plan_blocks_kernel(const Cand* __restrict__ cand, const int64_t*
 }
 
 // BamSource.getFirstReadInPartition: first position (<= 10,000,000 scanned) where the guesser
-// fires.  One workgroup per split, 256 positions per step, first hit by ballot + LDS min.
+// fires.  FR_K workgroups per split scan interleaved 256-position steps (a split that starts
+// inside a 2 Mb read has ~1.5 MB of positions before its first record: one workgroup stepping
+// through them was the planning's critical path); hits go to the split's minimum by a 64-bit
+// atomic, and a workgroup stops once its next step starts past the current minimum -- every
+// position below the final minimum was checked by the workgroup that owns its step.
+// first_record_final_kernel then fills the plan (one thread per split).
+constexpr int FR_K = 16;
 __global__ __launch_bounds__(256) void first_record_kernel(
     const uint8_t* __restrict__ U, int64_t ulen, int32_t u_is_eof, const int32_t* __restrict__ ref_len,
-    int32_t n_ref, const int64_t* __restrict__ blk_pos, const int64_t* __restrict__ uoff,
-    const int64_t* __restrict__ d_nblk, SplitPlan* __restrict__ plans, int64_t nsplit) {
-  __shared__ int64_t best;
-  __shared__ int32_t need;
-  int64_t i = blockIdx.x;
+    int32_t n_ref, const SplitPlan* __restrict__ plans, int64_t nsplit,
+    unsigned long long* __restrict__ best_all) {
+  __shared__ unsigned long long cur;
+  const int64_t i = blockIdx.x / FR_K, k = blockIdx.x % FR_K;
+  if (i >= nsplit) return;
+  const SplitPlan& P = plans[i];
+  if (P.first_blk < 0 || P.status != 0) return;
+  unsigned long long* best = best_all + i;  // the minimum hit; best[nsplit]: a "need more data" seen
+  const int64_t lo = P.u_lo;
+  const int64_t hi = min(P.u_hi, lo + (int64_t)10000000);
+  for (int64_t b = lo + 256 * k; b < hi; b += 256 * FR_K) {
+    if (threadIdx.x == 0) cur = __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const bool stop = (unsigned long long)b > cur;
+    __syncthreads();
+    if (stop) break;
+    const int64_t v = b + threadIdx.x;
+    if (v < hi) {
+      const int r = check_record_start(U, ulen, u_is_eof, ref_len, n_ref, v);
+      if (r == 1 || r == 4) atomicMin(best, (unsigned long long)v);
+      if (r == 4) atomicOr(best + nsplit, 1ull);
+    }
+  }
+}
+
+__global__ void first_record_final_kernel(const uint8_t* __restrict__ U, int64_t ulen, int32_t u_is_eof,
+                                          const int32_t* __restrict__ ref_len, int32_t n_ref,
+                                          const int64_t* __restrict__ blk_pos,
+                                          const int64_t* __restrict__ uoff,
+                                          const int64_t* __restrict__ d_nblk,
+                                          SplitPlan* __restrict__ plans, int64_t nsplit,
+                                          const unsigned long long* __restrict__ best_all) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nsplit) return;
   SplitPlan& P = plans[i];
   if (P.first_blk < 0 || P.status != 0) return;
-  const int64_t lo = P.u_lo;
-  const int64_t hi = min(P.u_hi, lo + (int64_t)10000000);
-  if (threadIdx.x == 0) {
-    best = INT64_MAX;
-    need = 0;
-  }
-  __syncthreads();
-  for (int64_t b = lo; b < hi; b += 256) {
-    int64_t v = b + threadIdx.x;
-    if (v < hi) {
-      int r = check_record_start(U, ulen, u_is_eof, ref_len, n_ref, v);
-      if (r == 1) atomicMin((unsigned long long*)&best, (unsigned long long)v);
-      if (r == 4) atomicMin((unsigned long long*)&best, (unsigned long long)v), need = 1;
+  const unsigned long long best = best_all[i];
+  if (best != ~0ull) {
+    // a "need more data" at the minimum position means the answer is unknown here
+    const int64_t v = (int64_t)best;
+    if (best_all[nsplit + i] && check_record_start(U, ulen, u_is_eof, ref_len, n_ref, v) == 4) {
+      P.status = 100;  // caller must extend the buffer
+      return;
     }
-    __syncthreads();
-    if (best != INT64_MAX) break;
-    __syncthreads();
+    const int64_t nb = *d_nblk;
+    const int64_t j = block_of(uoff, nb, v);
+    P.rec_lin = v;
+    P.vstart = ((uint64_t)blk_pos[j] << 16) | (uint64_t)(v - uoff[j]);
+    // bytes of the (up to) 10 records the guesser chained from v: the host sizes the record
+    // chain's segments by the typical record length
+    int64_t q = v;
+    for (int k = 0; k < 10 && q + 4 <= ulen; k++) q += 4 + (int64_t)(uint32_t)ld32(U, q);
+    P.rec_span = (int32_t)min(q - v, (int64_t)INT32_MAX);
   }
-  if (threadIdx.x == 0) {
-    if (best != INT64_MAX) {
-      // a "need more data" at the minimum position means the answer is unknown here
-      int64_t v = best;
-      if (need && check_record_start(U, ulen, u_is_eof, ref_len, n_ref, v) == 4) {
-        P.status = 100;  // caller must extend the buffer
-        return;
-      }
-      int64_t nb = *d_nblk;
-      int64_t j = block_of(uoff, nb, v);
-      P.rec_lin = v;
-      P.vstart = ((uint64_t)blk_pos[j] << 16) | (uint64_t)(v - uoff[j]);
-    }
-    P.vend = ((uint64_t)P.split_end << 16) | 0xffff;
-  }
+  P.vend = ((uint64_t)P.split_end << 16) | 0xffff;
 }
 
 // ------------------------------------------------------------------ Kernel 3: record chain
@@ -748,7 +791,7 @@ template <typename WP>
 __device__ __attribute__((always_inline)) inline uint64_t decode_one(
     WP W, int64_t off, int64_t p, int32_t bs, int64_t n, int64_t i, int half,
     const int64_t* __restrict__ blk_pos, const int64_t* __restrict__ uoff, int64_t nblk,
-    BlockOf bo, const RecSoA& soa) {
+    BlockOf bo, const RecSoA& soa, bool hash = true) {
   const int64_t wi0 = off >> 2;
   const uint32_t sh = (uint32_t)(off & 3);
   if (half == 0) {
@@ -780,9 +823,9 @@ __device__ __attribute__((always_inline)) inline uint64_t decode_one(
     }
     soa.voffset[i] = ((uint64_t)bo.bp << 16) | (uint64_t)(p - bo.u0);
   }
-  // hash words k = half, half + 2, ...
+  // hash words k = half, half + 2, ... (a long record's words are hashed by long_hash_kernel)
   uint64_t part = 0;
-  const int64_t nw = (n + 7) / 8;
+  const int64_t nw = hash ? (n + 7) / 8 : 0;
   for (int64_t k = half; k < nw; k += 2) {
     const int64_t wi = wi0 + 2 * k;
     const uint32_t w0 = W[wi], w1 = W[wi + 1], w2 = W[wi + 2];
@@ -795,11 +838,24 @@ __device__ __attribute__((always_inline)) inline uint64_t decode_one(
   return part;
 }
 
+// Long records (long reads: 10 kb - 2 Mb, records of 15 KB - 3 MB) are hashed by many threads:
+// two lanes walking a record of ~100 KB word by word made the records stage 2x the inflate on a
+// long-read file.  decode_group appends every PIECE-byte piece of a record longer than LONG_N to a
+// list and writes 0 to its hash; long_hash_kernel adds each piece's word sum (the sum is
+// order-free) into the hash slot; long_hash_final_kernel applies the length term and mix64.
+constexpr int64_t LONG_N = 2048;
+constexpr int64_t LONG_PIECE = 32768;
+struct LongList {
+  uint64_t* ent;                // record index << 16 | piece
+  int64_t cap;
+  unsigned long long* cnt;      // entries appended
+};
+
 __device__ void decode_group(const uint8_t* __restrict__ U, int64_t ulen,
                              const int64_t* __restrict__ rec_lin, int64_t nrec,
                              const int64_t* __restrict__ blk_pos, const int64_t* __restrict__ uoff,
                              int64_t nblk, const int32_t* __restrict__ pt, const RecSoA& soa,
-                             int32_t* d_status, int64_t i0, uint4* stage4) {
+                             int32_t* d_status, int64_t i0, uint4* stage4, LongList ll) {
   const int lane = threadIdx.x, r = lane & (REC_GROUP - 1), half = lane / REC_GROUP;
   const int nact = (int)min((int64_t)REC_GROUP, nrec - i0);
   const int64_t i = i0 + r;
@@ -826,6 +882,7 @@ __device__ void decode_group(const uint8_t* __restrict__ U, int64_t ulen,
   const int64_t base = first & ~(int64_t)15;
   const int64_t len = lastp + 4 + (int64_t)lastbs - base;
   uint64_t part = 0;
+  bool lng = false;
   if (len + 32 <= REC_STAGE) {  // the hash reads up to 12 bytes past the last record
     // LDS-DMA: every 16-byte piece in flight at once (a register-staged loop waits per piece)
     const uint4* src = reinterpret_cast<const uint4*>(U + base);
@@ -841,24 +898,131 @@ __device__ void decode_group(const uint8_t* __restrict__ U, int64_t ulen,
       part = decode_one((const __attribute__((address_space(3))) uint32_t*)stage4, p - base, p, bs,
                         n, i, half, blk_pos, uoff, nblk, bo, soa);
   } else if (act) {
-    part = decode_one(U32, p, p, bs, n, i, half, blk_pos, uoff, nblk, bo, soa);
+    lng = n > LONG_N;
+    part = decode_one(U32, p, p, bs, n, i, half, blk_pos, uoff, nblk, bo, soa, !lng);
+    if (lng && half == 0) {  // its pieces go to long_hash_kernel
+      const int64_t np = (n + LONG_PIECE - 1) / LONG_PIECE;
+      const int64_t e0 = (int64_t)atomicAdd(ll.cnt, (unsigned long long)np);
+      for (int64_t j = 0; j < np && e0 + j < ll.cap; j++) ll.ent[e0 + j] = (uint64_t)i << 16 | (uint64_t)j;
+    }
   }
   // both halves' word sums (all lanes take part in the shuffles)
   const uint32_t plo = (uint32_t)part, phi = (uint32_t)(part >> 32);
   const uint64_t other = ((uint64_t)(uint32_t)__shfl_xor((int)phi, REC_GROUP, 64) << 32) |
                          (uint32_t)__shfl_xor((int)plo, REC_GROUP, 64);
-  if (act && half == 0) soa.hash[i] = dq_mix64((uint64_t)n * DQ_K_LEN + part + other);
+  if (act && half == 0) soa.hash[i] = lng ? 0ull : dq_mix64((uint64_t)n * DQ_K_LEN + part + other);
+}
+
+// One workgroup per piece of a long record (grid-stride over the list): thread t sums the words
+// of pairs t, t + 256, ... of the piece (five dword loads per pair, consecutive lanes on
+// consecutive pairs), a workgroup reduction, one 64-bit atomic add into the record's hash slot.
+constexpr int LH_THREADS = 256;
+__global__ __launch_bounds__(LH_THREADS) void long_hash_kernel(
+    const uint8_t* __restrict__ U, const int64_t* __restrict__ rec_lin, const uint64_t* __restrict__ ent,
+    const unsigned long long* __restrict__ cnt, int64_t cap, uint64_t* __restrict__ hash) {
+  __shared__ uint64_t wsum[LH_THREADS / 64];
+  const int64_t ne = min((int64_t)*cnt, cap);
+  const uint32_t* U32 = reinterpret_cast<const uint32_t*>(U);
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  for (int64_t e = blockIdx.x; e < ne; e += gridDim.x) {
+    const uint64_t x = ent[e];
+    const int64_t i = (int64_t)(x >> 16), j = (int64_t)(x & 0xffff);
+    const int64_t p = rec_lin[i];
+    const uint32_t sh = (uint32_t)(p & 3);
+    const int32_t bs = (int32_t)funnel(U32[p >> 2], U32[(p >> 2) + 1], sh);
+    const int64_t n = 4 + (int64_t)bs, nw = (n + 7) / 8;
+    const int64_t k0 = j * (LONG_PIECE / 8), k1 = min(nw, k0 + LONG_PIECE / 8);
+    uint64_t part = 0;
+#pragma unroll 4
+    for (int64_t k = k0 + 2 * t; k < k1; k += 2 * LH_THREADS) {
+      const int64_t wi = (p >> 2) + 2 * k;
+      const uint32_t w0 = U32[wi], w1 = U32[wi + 1], w2 = U32[wi + 2], w3 = U32[wi + 3], w4 = U32[wi + 4];
+      uint64_t a = ((uint64_t)funnel(w1, w2, sh) << 32) | funnel(w0, w1, sh);
+      uint64_t b = ((uint64_t)funnel(w3, w4, sh) << 32) | funnel(w2, w3, sh);
+      const int64_t ra = n - 8 * k, rb = ra - 8;
+      if (ra < 8) a &= (1ull << (8 * ra)) - 1;
+      if (rb < 8 && rb > 0) b &= (1ull << (8 * rb)) - 1;
+      part += dq_mix64(a ^ ((uint64_t)(k + 1) * DQ_K_WORD));
+      if (k + 1 < k1) part += dq_mix64(b ^ ((uint64_t)(k + 2) * DQ_K_WORD));
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+      const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)part, o, 64);
+      const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(part >> 32), o, 64);
+      part += ((uint64_t)hi << 32) | lo;
+    }
+    if (lane == 0) wsum[wv] = part;
+    __syncthreads();
+    if (t == 0) {
+      uint64_t s = 0;
+      for (int w = 0; w < LH_THREADS / 64; w++) s += wsum[w];
+      atomicAdd((unsigned long long*)&hash[i], (unsigned long long)s);
+    }
+    __syncthreads();
+  }
+}
+
+// Per-run block statistics without copying the block table to the host: out[0] += sum of the
+// DEFLATE payload bytes (csize - 26) over the blocks; block 0 also writes out[1] = uoff of the
+// first block whose start is > x (upper bound; ulen past the last), out[2] = the same for >= x
+// (lower bound).  out[0] must be zero on entry.
+__global__ __launch_bounds__(256) void block_stats_kernel(const int64_t* __restrict__ blk_pos,
+                                                          const int32_t* __restrict__ blk_cs,
+                                                          const int64_t* __restrict__ uoff, int64_t nblk,
+                                                          int64_t ulen, int64_t x, uint64_t* out) {
+  uint64_t acc = 0;
+  for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nblk;
+       b += (int64_t)gridDim.x * blockDim.x)
+    acc += (uint64_t)(int64_t)(blk_cs[b] - 26);
+  for (int o = 32; o >= 1; o >>= 1) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)acc, o, 64);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(acc >> 32), o, 64);
+    acc += ((uint64_t)hi << 32) | lo;
+  }
+  if ((threadIdx.x & 63) == 0 && acc) atomicAdd((unsigned long long*)out, (unsigned long long)acc);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    int64_t lo = 0, hi = nblk;  // first blk_pos > x
+    while (lo < hi) {
+      const int64_t m = (lo + hi) >> 1;
+      if (blk_pos[m] <= x) lo = m + 1;
+      else hi = m;
+    }
+    out[1] = (uint64_t)(lo < nblk ? uoff[lo] : ulen);
+    out[3] = (uint64_t)lo;
+    lo = 0, hi = nblk;  // first blk_pos >= x
+    while (lo < hi) {
+      const int64_t m = (lo + hi) >> 1;
+      if (blk_pos[m] < x) lo = m + 1;
+      else hi = m;
+    }
+    out[2] = (uint64_t)(lo < nblk ? uoff[lo] : ulen);
+  }
+}
+
+__global__ void long_hash_final_kernel(const uint8_t* __restrict__ U, const int64_t* __restrict__ rec_lin,
+                                       const uint64_t* __restrict__ ent,
+                                       const unsigned long long* __restrict__ cnt, int64_t cap,
+                                       uint64_t* __restrict__ hash) {
+  const int64_t ne = min((int64_t)*cnt, cap);
+  const uint32_t* U32 = reinterpret_cast<const uint32_t*>(U);
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < ne;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t x = ent[e];
+    if (x & 0xffff) continue;  // one entry per record: its first piece
+    const int64_t i = (int64_t)(x >> 16), p = rec_lin[i];
+    const int32_t bs = (int32_t)funnel(U32[p >> 2], U32[(p >> 2) + 1], (uint32_t)(p & 3));
+    hash[i] = dq_mix64((uint64_t)(4 + (int64_t)bs) * DQ_K_LEN + hash[i]);
+  }
 }
 
 // Grid-stride over groups of 32 records: a few thousand resident waves, not one dispatch per group.
 __global__ __launch_bounds__(64) void decode_records_kernel(
     const uint8_t* __restrict__ U, int64_t ulen, const int64_t* __restrict__ rec_lin, int64_t nrec,
     const int64_t* __restrict__ blk_pos, const int64_t* __restrict__ uoff, int64_t nblk,
-    const int32_t* __restrict__ pt, RecSoA soa, int32_t* d_status) {
+    const int32_t* __restrict__ pt, RecSoA soa, int32_t* d_status, LongList ll) {
   __shared__ uint4 stage4[REC_STAGE / 16 + 1];
   for (int64_t g = blockIdx.x; g * REC_GROUP < nrec; g += gridDim.x) {
     decode_group(U, ulen, rec_lin, nrec, blk_pos, uoff, nblk, pt, soa, d_status, g * REC_GROUP,
-                 stage4);
+                 stage4, ll);
     __syncthreads();  // this group is done with the staging buffer
   }
 }
@@ -1357,10 +1521,15 @@ void launch_guess_all(const uint8_t* U, int64_t ulen, int32_t u_is_eof, const in
 
 void launch_first_record(const uint8_t* U, int64_t ulen, int32_t u_is_eof, const int32_t* ref_len,
                          int32_t n_ref, const int64_t* blk_pos, const int64_t* uoff,
-                         const int64_t* d_nblk, SplitPlan* plans, int64_t nsplit, hipStream_t s) {
+                         const int64_t* d_nblk, SplitPlan* plans, int64_t nsplit,
+                         unsigned long long* best, hipStream_t s) {
   if (nsplit <= 0) return;
-  hipLaunchKernelGGL(first_record_kernel, dim3((unsigned)nsplit), dim3(256), 0, s, U, ulen,
-                     u_is_eof, ref_len, n_ref, blk_pos, uoff, d_nblk, plans, nsplit);
+  (void)hipMemsetAsync(best, 0xff, 8 * (size_t)nsplit, s);       // minima: all ones
+  (void)hipMemsetAsync(best + nsplit, 0, 8 * (size_t)nsplit, s);  // "need more data" flags
+  hipLaunchKernelGGL(first_record_kernel, dim3((unsigned)(nsplit * FR_K)), dim3(256), 0, s, U, ulen,
+                     u_is_eof, ref_len, n_ref, plans, nsplit, best);
+  hipLaunchKernelGGL(first_record_final_kernel, dim3((unsigned)((nsplit + 63) / 64)), dim3(64), 0, s,
+                     U, ulen, u_is_eof, ref_len, n_ref, blk_pos, uoff, d_nblk, plans, nsplit, best);
 }
 
 void launch_seg_spec(const uint8_t* U, int64_t ulen, int32_t u_is_eof, int64_t chain_end,
@@ -1399,17 +1568,37 @@ void launch_seg_emit2(const uint8_t* U, int64_t, const Seg* segs, const int64_t*
                      base, nseg, rec_lin);
 }
 
+void launch_block_stats(const int64_t* blk_pos, const int32_t* blk_cs, const int64_t* uoff,
+                        int64_t nblk, int64_t ulen, int64_t x, uint64_t* out, hipStream_t s) {
+  (void)hipMemsetAsync(out, 0, 4 * sizeof(uint64_t), s);
+  const int64_t g = std::max<int64_t>(1, std::min<int64_t>(1024, (nblk + 255) / 256));
+  hipLaunchKernelGGL(block_stats_kernel, dim3((unsigned)g), dim3(256), 0, s, blk_pos, blk_cs, uoff,
+                     nblk, ulen, x, out);
+}
+
+int64_t long_list_cap(int64_t ulen, int64_t nrec) {
+  return ulen / LONG_PIECE + std::min(nrec, ulen / LONG_N) + 1;
+}
+
 void launch_decode_records(const uint8_t* U, int64_t ulen, const int64_t* rec_lin, int64_t nrec,
                            const int64_t* blk_pos, const int64_t* uoff, int64_t nblk, int32_t* pt,
-                           RecSoA soa, int32_t* d_status, hipStream_t s) {
+                           RecSoA soa, int32_t* d_status, uint64_t* long_ent, int64_t long_cap,
+                           unsigned long long* long_cnt, hipStream_t s) {
   if (nrec <= 0 || nblk <= 0) return;
   const int64_t npages = (ulen >> 16) + 1;
   hipLaunchKernelGGL(block_pages_kernel, dim3((unsigned)((npages + 255) / 256)), dim3(256), 0, s,
                      uoff, nblk, pt, npages);
+  (void)hipMemsetAsync(long_cnt, 0, sizeof(unsigned long long), s);
+  const LongList ll{long_ent, long_cap, long_cnt};
   hipLaunchKernelGGL(decode_records_kernel,
                      dim3((unsigned)std::min<int64_t>((nrec + REC_GROUP - 1) / REC_GROUP, 16384)),
                      dim3(REC_WAVE), 0, s, U, ulen, rec_lin, nrec, blk_pos, uoff, nblk, pt, soa,
-                     d_status);
+                     d_status, ll);
+  // the long records' pieces (an empty list costs two tiny launches that read the count)
+  hipLaunchKernelGGL(long_hash_kernel, dim3(2048), dim3(LH_THREADS), 0, s, U, rec_lin, long_ent,
+                     long_cnt, long_cap, soa.hash);
+  hipLaunchKernelGGL(long_hash_final_kernel, dim3(64), dim3(256), 0, s, U, rec_lin, long_ent,
+                     long_cnt, long_cap, soa.hash);
 }
 
 void launch_partition_ranges(const SplitPlan* plans, int64_t nsplit, const int64_t* rec_lin,
