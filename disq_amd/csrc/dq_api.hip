@@ -1154,15 +1154,16 @@ static int text_run(dq_ctx* ctx, int32_t drop_hash) {
 
 // ------------------------------------------------------------------ BGZF deflate (write path)
 // htsjdk BlockCompressedOutputStream over a byte stream in HBM: blocks of 65280 bytes compressed
-// in batches (the per-lane bit staging is 80 KiB per block), packed into ctx->z_out.
+// in batches (per block 512 KiB of staged symbols and 256 KiB of match-finder buckets), packed
+// into ctx->z_out.
 static int bgzf_compress_dev(dq_ctx* ctx, const uint8_t* d_src, int64_t len, double* ms) {
   if (!deflate_tables(ctx->o.device)) RET(DQ_EDEVICE, "deflate table initialisation failed");
   hipStream_t s = ctx->s;
   const int64_t nblk = bgzf_block_count(len);
-  const int64_t batch = std::min<int64_t>(std::max<int64_t>(nblk, 1), 8192);
+  const int64_t batch = std::min<int64_t>(std::max<int64_t>(nblk, 1), 2048);
   int rc;
   if ((rc = ensure_all(ctx, ctx->z_stage, bgzf_stage_bytes(batch)))) return rc;
-  if ((rc = ensure_all(ctx, ctx->z_link, (size_t)batch * 65536 * 2))) return rc;
+  if ((rc = ensure_all(ctx, ctx->z_link, bgzf_link_bytes(batch)))) return rc;
   if ((rc = ensure_all(ctx, ctx->z_slots, (size_t)batch * 65536))) return rc;
   if ((rc = ensure_all(ctx, ctx->z_size, 4 * (size_t)batch))) return rc;
   if ((rc = ensure_all(ctx, ctx->z_off, 8 * (size_t)batch))) return rc;
@@ -1916,11 +1917,12 @@ static void reset_open(dq_ctx* ctx, int64_t len) {
 // Bytes [off, off + len) of an open file into C (plus the 4 KiB zero pad): read() into two pinned
 // staging buffers in turn, each copied asynchronously while the next piece is read from the page
 // cache (the role of Disq's 2 x 4 MB NIO prefetcher, SeekableByteChannelPrefetcher.java:45).
-// The same by DMA straight from the file's page-cache pages: the range is mapped read-only and
-// registered with the device (page pinning, no byte copies), one copy reads it into C.  Returns
-// 1 when mapping or registration is not available (the caller then copies through staging).
+// DQ_MMAP=1: the same by DMA straight from the file's page-cache pages (the range mapped read-only
+// and registered with the device, one copy into C).  Measured slower than the staging path (page
+// registration of 2 GB windows: end-to-end 14.9-19.9 GB/s against 27.5-35.3 GB/s,
+// profiles/r3s_e2e_ab.txt), so it is off by default.  Returns 1 when it is off or unavailable.
 static int upload_file_range_mapped(dq_ctx* ctx, int fd, int64_t off, int64_t len) {
-  static const bool enabled = !(getenv("DQ_MMAP") && atoi(getenv("DQ_MMAP")) == 0);
+  static const bool enabled = getenv("DQ_MMAP") && atoi(getenv("DQ_MMAP")) == 1;
   if (!enabled || len < (64 << 20)) return 1;
   const int64_t pg = (int64_t)sysconf(_SC_PAGESIZE);
   const int64_t a = off & ~(pg - 1), d = off - a, mlen = len + d;
@@ -3096,7 +3098,7 @@ int dq_set_export_arena(dq_ctx* ctx, int64_t bytes) {
   if (bytes == 0) return 0;
   HIPCHK(hipHostMalloc((void**)&ctx->arena, (size_t)bytes, hipHostMallocDefault));
   ctx->arena_cap = (size_t)bytes;
-  return 0;
+  return ensure_pinned(ctx);  // the upload staging too: every long-lived host buffer up front
 }
 
 void dq_batch_free(dq_batch* b) {

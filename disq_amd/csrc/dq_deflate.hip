@@ -9,22 +9,36 @@
 // kernel's own (java.util.zip.Deflater's exact bit stream is not reproduced): the output is valid
 // BGZF whose blocks inflate to exactly htsjdk's block contents.
 //
-// One 256-thread workgroup per block, the block's bytes in LDS.  Match candidates first: the
-// positions are walked in stripes of 256 (one per thread); each position reads, from an LDS table
-// keyed by a hash of its next 3 bytes, the last position of an earlier stripe with that hash (its
-// hash-chain link, kept in global scratch), then the stripe's positions update the table.  Lane t
-// then owns bytes [255 t, 255 t + 255) and parses them greedily on its own: at each position the
-// longest match of >= 3 bytes among the previous SHORT bytes and the first CHAIN links of its hash
-// chain, clamped to its segment's end, so lanes never wait for each other.  Symbols go to a
-// per-lane staging slot and to LDS histograms; wave 0 builds the literal/length code and wave 1
-// the distance code (a rank sort, Moffat-Katajainen minimum-redundancy lengths, a Kraft fix-up
-// capping them at 15), the code-length sequence is run-length coded; the block is coded dynamic
-// (BTYPE 10) or fixed (01), whichever is shorter.  Each lane's bit count gives its offset by an
-// exclusive scan; every lane OR-s its bits into the LDS image of the block (the input is dead by
-// then), stored with 16-byte writes.  A block whose code would not fit BSIZE is stored (BTYPE 00).
+// One 256-thread workgroup per block, the block's bytes in LDS (79 KB: 2 workgroups per CU).
+//   1. Match finder: every position with a 3-byte suffix goes into one of 2048 hash buckets, in
+//      ascending order inside its bucket (counts by LDS atomics, bucket starts by a scan, then an
+//      ordered scatter in stripes of 256 positions: the lanes of a wave with equal hashes are
+//      found by one ballot per hash bit, and the four waves take their bucket cursors in turn).
+//      A position's candidates are the entries before it in its bucket, most recent first: a
+//      contiguous run of the bucket list, so a search issues all its candidate loads at once
+//      instead of chasing zlib's hash-chain links one dependent load at a time.
+//   2. Parse: lane t parses from its segment start [255 t, 255 t + 255) with zlib-style lazy
+//      evaluation (a match shorter than `lazy` is deferred while the next position's is longer),
+//      the longest match among `chain` candidates (stopping at `nice`), matches running on past
+//      the segment end.  A parse step depends on its position alone, so two parses that reach the
+//      same position continue identically: from its exit, each lane keeps parsing until it hits a
+//      symbol boundary of a later lane's parse (usually within a few symbols) and records the
+//      merge; one thread then follows the merges from lane 0, which gives every lane the part of
+//      its symbols (and continuation) on the block's one parse.  The result is the parse a
+//      single sequential pass would make: no matches are cut at lane boundaries.
+//      (Parameters from tools/deflate_model.c: chain 48, lazy 24, nice 48 model a 2.82 ratio on
+//      the synthetic WGS stream, zlib level 5 -- htsjdk's -- 2.86.)
+//   3. Codes: histograms of the parse; wave 0 builds the literal/length code and wave 1 the
+//      distance code (a rank sort, Moffat-Katajainen minimum-redundancy lengths, a Kraft fix-up
+//      capping them at 15), the code-length sequence is run-length coded; the block is coded
+//      dynamic (BTYPE 10) or fixed (01), whichever is shorter.
+//   4. Emit: each lane's bit count gives its offset by an exclusive scan; every lane OR-s its bits
+//      into the LDS image of the block (the input is dead by then).  A block whose code would not
+//      fit BSIZE (or whose parse overflowed its staging) is stored (BTYPE 00).
 // CRC32: per-lane table CRC over the segment, combined with x^(8 n) mod P multipliers.
 #include "dq_internal.h"
 
+#include <algorithm>
 #include <mutex>
 
 namespace dq {
@@ -33,14 +47,18 @@ namespace {
 constexpr int DWG = 256;                 // threads per block
 constexpr int BLK_U = 65280;             // htsjdk DEFAULT_UNCOMPRESSED_BLOCK_SIZE
 constexpr int SEG = BLK_U / DWG;         // 255 bytes per lane
-constexpr int SHORT = 8;                 // distances 1..SHORT always tried
-constexpr int CHAIN = 6;                 // hash-chain links tried
-constexpr int HBITS = 11;                // LDS head table: 2048 entries
+constexpr int HBITS = 11;                // hash buckets (LDS counts / offsets: 8 KB)
 constexpr int MAXM = 258;
-constexpr int SLOT_WORDS = 256;          // staged symbols per lane: <= 255 + the end of block
+constexpr int WIN = 32768;               // DEFLATE window
+constexpr int OWN_WORDS = 288;           // a lane's own symbols (<= 255 + the last step's <= 32 deferrals)
+constexpr int CONT_WORDS = 224;          // its continuation past its segment end
+constexpr int LANE_WORDS = OWN_WORDS + CONT_WORDS;
 constexpr int MAX_DEFLATE = 65536 - 26;  // BSIZE limit: 18-byte header + payload + 8 trailer
+constexpr int MAXCAND = 128;             // candidates per match search at most (cfg.chain)
 
 __constant__ uint32_t c_dcrc[256];
+__constant__ uint16_t c_lbase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
+                                     35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
 __constant__ uint32_t c_x2n[32];  // x^(2^k) mod P (reflected)
 
 __device__ inline uint32_t gf2_mul(uint32_t a, uint32_t b) {  // reflected, poly 0xEDB88320
@@ -96,13 +114,16 @@ __device__ inline void fixed_ll(int sym, uint32_t& code, int& len) {
 struct alignas(16) DLds {
   uint8_t in[65536 + 16];     // the block's bytes; later the deflate image (<= 65510 bytes)
   uint32_t crc_t[256];
-  uint32_t lane_bits[DWG];
+  uint32_t lane_bits[DWG];    // the parse's exit of each lane; later its bit count, bit offset
   uint32_t lane_crc[DWG];
-  uint16_t lane_nsym[DWG];
-  int32_t head[1 << HBITS];   // hash heads; then histograms, code tables and scratch (H_* below)
+  uint32_t lane_mrg[DWG];     // continuation: merge lane | symbol index << 9 | count << 18 | over << 27
+  uint32_t lane_eff[DWG];     // effective symbols: own start | continuation count << 9 | EFF_* flags
+  uint16_t lane_nsym[DWG];    // own symbols
+  int32_t head[1 << HBITS];   // bucket counts -> ends; then histograms, code tables (H_* below)
   int32_t misc[8];
 };
-// word offsets inside DLds::head once the hash heads are dead
+constexpr uint32_t EFF_REACHED = 1u << 18, EFF_EOB = 1u << 19;
+// word offsets inside DLds::head once the buckets are dead
 enum { H_LL = 0, H_D = 288, H_CL = 320, C_LL = 352, C_D = 640, C_CL = 672, H_TOK = 704,
        H_SORT = 864, H_W = 1152, H_LEN = 1440, H_LEN_D = 1728, H_LEN_CL = 1760, H_SORT_D = 1792,
        H_W_D = 1824, H_CNT = 1856, H_CNT_D = 1890, H_BL = 1924, H_END = 1956 };
@@ -243,13 +264,113 @@ __device__ inline uint32_t hash3(const uint8_t* in, int p) {
   return (v * 2654435761u) >> (32 - HBITS);
 }
 
+__device__ inline int sym_bytes(uint32_t w) {  // uncompressed bytes of a staged symbol
+  const uint32_t ll = sym_ll(w);
+  return ll < 256 ? 1 : (int)c_lbase[ll - 257] + (int)sym_lx(w);
+}
+__device__ inline uint64_t lanes_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
+
+// Match finder over the block's hash buckets: bl holds every position with a >= 3-byte suffix,
+// grouped by bucket (hash3) and ascending inside a bucket; gi[p] is p's index in bl; the bucket of
+// hash h ends at head[h] (it starts where bucket h - 1 ends).  The candidates of p are the
+// entries before gi[p] in its bucket, most recent first -- consecutive words of bl, so all of a
+// search's candidate loads are in flight together (no pointer chasing as in zlib's hash chains).
+struct Finder {
+  const DLds& L;
+  const uint16_t* __restrict__ bl;
+  const uint16_t* __restrict__ gi;
+  int n, chain, nice;
+  // longest match (>= 3, else 0) at p, at most lim bytes; *dist its distance
+  __device__ int find(int p, int lim, int* dist) const {
+    *dist = 0;
+    if (lim < 3 || p + 3 > n) return 0;
+    const uint32_t h = hash3(L.in, p);
+    const int g = gi[p];
+    const int lo = max(h ? L.head[h - 1] : 0, g - chain);
+    const uint32_t p4 = ld4(L.in, p);
+    int best = 0, bd = 0;
+    for (int i0 = g - 1; i0 >= lo && best < nice; i0 -= 8) {
+      int q8[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) q8[k] = i0 - k >= lo ? (int)bl[i0 - k] : -1;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int q = q8[k];
+        if (q < 0 || p - q > WIN || best >= nice || best >= lim) break;
+        // only a candidate that also matches the byte at `best` can win: test the 4 bytes ending
+        // there first (zlib's scan_end test), so most candidates cost two compares, not a walk
+        if (best >= 3 && ld4(L.in, q + best - 3) != ld4(L.in, p + best - 3)) continue;
+        uint32_t x = ld4(L.in, q) ^ p4;
+        if (x & 0xffffffu) continue;  // a hash collision
+        int l = 0;
+        while (x == 0 && l + 4 < lim) {
+          l += 4;
+          x = ld4(L.in, q + l) ^ ld4(L.in, p + l);
+        }
+        l = x ? l + (int)(__builtin_ctz(x) >> 3) : l + 4;
+        l = min(l, lim);
+        if (l > best) {
+          best = l;
+          bd = p - q;
+        }
+      }
+    }
+    *dist = bd;
+    return best >= 3 ? best : 0;
+  }
+};
+
+__device__ inline uint32_t lit_word(uint32_t b) { return b; }
+__device__ inline uint32_t match_word(int len, int d) {
+  int sym, nx, xv, ds, dnx, dxv;
+  len_code(len, sym, nx, xv);
+  dist_code(d, ds, dnx, dxv);
+  return (uint32_t)sym | ((uint32_t)xv << 9) | ((uint32_t)ds << 14) | ((uint32_t)dxv << 19);
+}
+
+// One parse step at p (zlib-style lazy evaluation: while the match at the next position is
+// longer and the current one shorter than `lazy`, emit a literal and move on): appends its
+// symbols to w[*ns...] and returns the new position.  The step depends on p alone, so two parses
+// that reach the same position continue identically (the merge rule below).
+__device__ int parse_step(const Finder& F, int lazy, int p, uint32_t* w, int* ns) {
+  const int n = F.n;
+  int d = 0, l = F.find(p, min(MAXM, n - p), &d);
+  while (l && l < lazy && p + 1 < n) {
+    int d2 = 0;
+    const int l2 = F.find(p + 1, min(MAXM, n - p - 1), &d2);
+    if (l2 <= l) break;
+    w[(*ns)++] = lit_word(F.L.in[p]);
+    p++;
+    l = l2;
+    d = d2;
+  }
+  if (l) {
+    w[(*ns)++] = match_word(l, d);
+    return p + l;
+  }
+  w[(*ns)++] = lit_word(F.L.in[p]);
+  return p + 1;
+}
+
+// Runs f(word) over lane t's effective symbols: its own from the merge index, then its
+// continuation, when the parse reaches it (EFF_REACHED).
+template <class Fn>
+__device__ inline void for_each_sym(const DLds& L, const uint32_t* lane_w, int t, Fn f) {
+  const uint32_t e = L.lane_eff[t];
+  if (!(e & EFF_REACHED)) return;
+  const int k0 = (int)(e & 511), nc = (int)((e >> 9) & 511), ns = L.lane_nsym[t];
+  for (int k = k0; k < ns; k++) f(lane_w[k]);
+  for (int k = 0; k < nc; k++) f(lane_w[OWN_WORDS + k]);
+}
+
 __global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __restrict__ src,
                                                            int64_t n_in, int64_t blk0,
                                                            int64_t nblk, uint32_t* __restrict__ stage,
                                                            uint16_t* __restrict__ link,
                                                            uint8_t* __restrict__ out_slots,
                                                            int32_t* __restrict__ out_size,
-                                                           uint64_t* __restrict__ tim) {
+                                                           uint64_t* __restrict__ tim, int chain,
+                                                           int lazy, int nice) {
   __shared__ DLds L;
   uint64_t tm[8];
   int ti = 0;
@@ -260,12 +381,13 @@ __global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __rest
   DTS();
   const int64_t b = (int64_t)blockIdx.x;  // block within this launch
   if (b >= nblk) return;
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int64_t base = (blk0 + b) * (int64_t)BLK_U;
   const int n = (int)min<int64_t>(BLK_U, n_in - base);
   // load (16-byte loads where aligned)
   for (int i = t; i < 256; i += DWG) L.crc_t[i] = c_dcrc[i];
-  for (int i = t; i < (1 << HBITS); i += DWG) L.head[i] = -1;
+  for (int i = t; i < (1 << HBITS); i += DWG) L.head[i] = 0;
+  if (t < 8) L.misc[t] = 0;
   {
     const uint8_t* s = src + base;
     const int head = (int)((16 - (reinterpret_cast<uintptr_t>(s) & 15)) & 15);
@@ -280,6 +402,7 @@ __global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __rest
       for (int k = 0; k < 16; k++) d[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
     }
     for (int i = h + 16 * nv + t; i < n; i += DWG) L.in[i] = s[i];
+    if (t < 16) L.in[n + t] = 0;  // the 4-byte compares read up to 3 bytes past the end
   }
   __syncthreads();
   DTS();
@@ -290,87 +413,147 @@ __global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __rest
     for (int i = s0; i < s1; i++) c = L.crc_t[(c ^ L.in[i]) & 0xff] ^ (c >> 8);
     L.lane_crc[t] = gf2_mul(x8n((uint32_t)(n - s1)), c);
   }
-  // ---- hash-chain links: stripe r = positions [256 r, 256 r + 256), one per thread
-  uint16_t* lk = link + b * 65536;
+  // ---- hash buckets of every position with a 3-byte suffix: counts, then bucket ends by a scan
+  for (int p = t; p + 3 <= n; p += DWG) atomicAdd(&L.head[hash3(L.in, p)], 1);
+  __syncthreads();
+  {  // exclusive scan of the 2048 counts: 8 per thread
+    constexpr int PER = (1 << HBITS) / DWG;
+    int v[PER], sum = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      v[k] = L.head[PER * t + k];
+      sum += v[k];
+    }
+    int inc = sum;
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += y;
+    }
+    if (lane == 63) L.lane_mrg[wv] = (uint32_t)inc;
+    __syncthreads();
+    int off = inc - sum;
+    for (int w = 0; w < wv; w++) off += (int)L.lane_mrg[w];
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      L.head[PER * t + k] = off;  // the bucket's cursor: its start, advanced by the scatter
+      off += v[k];
+    }
+  }
+  __syncthreads();
+  // ---- ordered scatter: positions in stripes of 256, ascending inside each bucket.  Inside a
+  //      wave the lanes with equal hashes are found by one ballot per hash bit; the four waves of
+  //      a stripe take their cursors in turn (one barrier each).  Afterwards head[h] is the end
+  //      of bucket h.
+  uint16_t* bl = link + b * (2 * 65536);
+  uint16_t* gi = bl + 65536;
   for (int r = 0; r * DWG < n; r++) {
     const int p = r * DWG + t;
-    uint32_t h = 0;
-    int q = -1;
-    if (p + 3 <= n) {
-      h = hash3(L.in, p);
-      q = L.head[h];
+    const bool valid = p + 3 <= n;
+    const uint32_t h = valid ? hash3(L.in, p) : 0u;
+    uint64_t m = __ballot(valid);
+#pragma unroll
+    for (int k = 0; k < HBITS; k++) {
+      const bool bit = (h >> k) & 1u;
+      const uint64_t bk = __ballot(bit);
+      m &= bit ? bk : ~bk;
     }
-    if (p < n) lk[p] = q < 0 ? (uint16_t)0xffff : (uint16_t)q;
-    __syncthreads();
-    if (p + 3 <= n) atomicMax(&L.head[h], p);
-    __syncthreads();
+    const uint64_t bel = m & lanes_below(lane);
+    int rank = 0;
+    for (int w = 0; w < DWG / 64; w++) {
+      if (wv == w && valid) {
+        rank = L.head[h] + __popcll(bel);
+        if (lane == 63 || !(m >> (lane + 1))) L.head[h] = rank + 1;  // the group's last lane
+      }
+      __syncthreads();
+    }
+    if (valid) {
+      bl[rank] = (uint16_t)p;
+      gi[p] = (uint16_t)rank;
+    }
   }
   __threadfence_block();
   __syncthreads();
-  // ---- greedy LZ77 over the segment: symbols into the lane's staging slot, histograms in LDS
-  int32_t* H = L.head;  // the hash heads are dead from here
+  DTS();
+  // ---- speculative parse: lane t from its segment start to the first symbol boundary at or past
+  //      its end (a match may run on past it)
+  uint32_t* lane_w = stage + ((int64_t)b * DWG + t) * LANE_WORDS;
+  const Finder F{L, bl, gi, n, min(chain, MAXCAND), nice};
+  {
+    int ns = 0, p = s0;
+    while (p < s1) p = parse_step(F, lazy, p, lane_w, &ns);
+    L.lane_nsym[t] = (uint16_t)ns;
+    L.lane_bits[t] = (uint32_t)p;  // exit
+    L.lane_eff[t] = 0;
+  }
+  __threadfence_block();
+  __syncthreads();
+  // ---- continuation: from its exit, lane t parses on until it reaches a symbol boundary of a
+  //      later lane's speculative parse (the same position continues identically), skipping
+  //      lanes whose whole parse it overruns
+  {
+    int E = (int)L.lane_bits[t], u = t + 1, k = 0, nc = 0;
+    int pu = min(n, u * SEG);
+    bool over = false;
+    for (;;) {
+      if (u >= DWG || E >= n) {
+        u = DWG;
+        k = 0;
+        break;
+      }
+      const int nu = L.lane_nsym[u];
+      const uint32_t* uw = stage + ((int64_t)b * DWG + u) * LANE_WORDS;
+      while (k < nu && pu < E) pu += sym_bytes(uw[k++]);
+      if (pu == E) break;  // merged: lane u's symbols from k on
+      if (k == nu) {       // lane u's whole parse lies before E
+        u++;
+        k = 0;
+        pu = min(n, u * SEG);
+        continue;
+      }
+      if (nc > CONT_WORDS - 40) {  // (a step appends at most lazy + 1 <= 33 symbols)
+        over = true;
+        break;
+      }
+      int nn = OWN_WORDS + nc;
+      E = parse_step(F, lazy, E, lane_w, &nn);
+      nc = nn - OWN_WORDS;
+    }
+    L.lane_mrg[t] = (uint32_t)u | ((uint32_t)k << 9) | ((uint32_t)nc << 18) | (over ? 1u << 27 : 0u);
+  }
+  __threadfence_block();
+  __syncthreads();
+  // ---- the parse of the block: lane 0, then the lane each continuation merged into
+  if (t == 0) {
+    int cur = 0, k0 = 0;
+    for (int it = 0; it <= DWG; it++) {
+      const uint32_t m = L.lane_mrg[cur];
+      if ((m >> 27) & 1u) {
+        L.misc[7] = 2;  // a continuation overflowed: the block is stored
+        break;
+      }
+      const int u = (int)(m & 511), k = (int)((m >> 9) & 511);
+      L.lane_eff[cur] = (uint32_t)k0 | (m & (511u << 18)) >> 9 | EFF_REACHED | (u >= DWG ? EFF_EOB : 0u);
+      if (u >= DWG) break;
+      cur = u;
+      k0 = k;
+    }
+  }
+  int32_t* H = L.head;  // the buckets are dead from here
+  __syncthreads();
   for (int i = t; i < H_CL + 32; i += DWG) H[i] = 0;
   __syncthreads();
-  DTS();
-  uint32_t* sw = stage + ((int64_t)b * DWG + t) * SLOT_WORDS;
-  int ns = 0;
-  for (int p = s0; p < s1;) {
-    int best = 0, bd = 0;
-    if (p + 3 <= s1) {
-      const uint32_t p4 = ld4(L.in, p);
-      const int lim = min(MAXM, s1 - p);
-      auto try_q = [&](int q) {
-        uint32_t x = (ld4(L.in, q) ^ p4);
-        if (x & 0xffffffu) return;
-        // extend 4 bytes at a time; the first differing byte ends the match
-        int l = 0;
-        while (x == 0 && l + 4 < lim) {
-          l += 4;
-          x = ld4(L.in, q + l) ^ ld4(L.in, p + l);
-        }
-        l = x ? l + (int)(__builtin_ctz(x) >> 3) : l + 4;
-        l = min(l, lim);
-        if (l > best) {
-          best = l;
-          bd = p - q;
-        }
-      };
-      for (int d = 1; d <= SHORT && d <= p && best < lim; d++) try_q(p - d);
-      // links were stored by this workgroup before the barrier (fenced); nothing read them since,
-      // so no stale L1 line can hold them
-      int q = lk[p];
-      // links only go back: stop at DEFLATE's 32 KiB window
-      for (int k = 0; k < CHAIN && q != 0xffff && p - q <= 32768 && best < lim; k++) {
-        if (p - q > SHORT) try_q(q);
-        q = lk[q];
-      }
-    }
-    if (best >= 3) {
-      int sym, nx, xv, ds, dnx, dxv;
-      len_code(best, sym, nx, xv);
-      dist_code(bd, ds, dnx, dxv);
-      sw[ns++] = (uint32_t)sym | ((uint32_t)xv << 9) | ((uint32_t)ds << 14) | ((uint32_t)dxv << 19);
-      atomicAdd(&H[H_LL + sym], 1);
-      atomicAdd(&H[H_D + ds], 1);
-      p += best;
-    } else {
-      sw[ns++] = L.in[p];
-      atomicAdd(&H[H_LL + L.in[p]], 1);
-      p++;
-    }
-  }
-  // the lane holding the block's last byte ends the deflate block
-  const int last_lane = n > 0 ? (n - 1) / SEG : 0;
-  if (t == last_lane) {
-    sw[ns++] = 256;
-    atomicAdd(&H[H_LL + 256], 1);
-  }
-  L.lane_nsym[t] = (uint16_t)ns;
+  // histograms of the effective symbols
+  for_each_sym(L, lane_w, t, [&](uint32_t x) {
+    const uint32_t ll = sym_ll(x);
+    atomicAdd(&H[H_LL + ll], 1);
+    if (ll > 256) atomicAdd(&H[H_D + sym_d(x)], 1);
+  });
+  if (L.lane_eff[t] & EFF_EOB) atomicAdd(&H[H_LL + 256], 1);
+  const bool over = L.misc[7] == 2;
   __threadfence_block();
   __syncthreads();
   DTS();
   // ---- dynamic Huffman codes: wave 0 the literal/length alphabet, wave 1 the distances
-  const int lane = t & 63, wv = t >> 6;
   if (wv == 0) build_lengths(H + H_LL, 286, 15, H + H_SORT, H + H_W, H + H_LEN, H + H_CNT, lane);
   if (wv == 1) build_lengths(H + H_D, 30, 15, H + H_SORT_D, H + H_W_D, H + H_LEN_D, H + H_CNT_D, lane);
   __syncthreads();
@@ -430,8 +613,7 @@ __global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __rest
     const uint32_t* cll = reinterpret_cast<const uint32_t*>(H + C_LL);
     const uint32_t* cd = reinterpret_cast<const uint32_t*>(H + C_D);
     uint32_t bdyn = 0, bfix = 0;
-    for (int k = 0; k < ns; k++) {
-      const uint32_t x = sw[k];
+    for_each_sym(L, lane_w, t, [&](uint32_t x) {
       const int ll = (int)sym_ll(x);
       int extra = 0;
       if (ll > 256) {
@@ -442,6 +624,10 @@ __global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __rest
       }
       bdyn += (cll[ll] >> 16) + extra;
       bfix += fixed_len_of(ll) + extra;
+    });
+    if (L.lane_eff[t] & EFF_EOB) {
+      bdyn += cll[256] >> 16;
+      bfix += 7;
     }
     L.lane_bits[t] = bdyn;
     // fixed totals: the sort scratch is dead
@@ -504,7 +690,7 @@ __global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __rest
   uint8_t* o = out_slots + b * 65536;
   const uint32_t crc = (uint32_t)L.misc[1];
   // stored when the code is no shorter than the bytes themselves (and always when it would not fit)
-  const bool stored = dbytes > min(MAX_DEFLATE, n + 5);
+  const bool stored = over || dbytes > min(MAX_DEFLATE, n + 5);
   int payload;
   if (!stored) {
     // ---- the header, then every lane's symbols, OR-ed into the LDS image (the input is dead)
@@ -538,8 +724,7 @@ __global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __rest
       const uint32_t* cll = reinterpret_cast<const uint32_t*>(H + C_LL);
       const uint32_t* cd = reinterpret_cast<const uint32_t*>(H + C_D);
       ImgOut io(img, L.lane_bits[t]);
-      for (int k = 0; k < ns; k++) {
-        const uint32_t x = sw[k];
+      for_each_sym(L, lane_w, t, [&](uint32_t x) {
         const int ll = (int)sym_ll(x);
         io.put(cll[ll] & 0xffff, (int)(cll[ll] >> 16));
         if (ll > 256) {
@@ -550,7 +735,8 @@ __global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __rest
           const int dx = dextra_bits(d);
           if (dx) io.put(sym_dx(x), dx);
         }
-      }
+      });
+      if (L.lane_eff[t] & EFF_EOB) io.put(cll[256] & 0xffff, (int)(cll[256] >> 16));
       io.flush();
     }
     __syncthreads();
@@ -608,7 +794,8 @@ DefTables g_def[64];
 }  // namespace
 
 int64_t bgzf_block_count(int64_t n) { return n <= 0 ? 0 : (n + BLK_U - 1) / BLK_U; }
-size_t bgzf_stage_bytes(int64_t nblk) { return (size_t)nblk * DWG * SLOT_WORDS * 4; }
+size_t bgzf_stage_bytes(int64_t nblk) { return (size_t)nblk * DWG * LANE_WORDS * 4; }
+size_t bgzf_link_bytes(int64_t nblk) { return (size_t)nblk * 2 * 65536 * sizeof(uint16_t); }
 
 bool deflate_tables(int device) {
   if (device < 0 || device >= 64) return false;
@@ -649,8 +836,15 @@ void launch_bgzf_deflate(const uint8_t* src, int64_t n_in, int64_t blk0, int64_t
                          uint32_t* stage, uint16_t* link, uint8_t* out_slots, int32_t* out_size,
                          uint64_t* tim, hipStream_t s) {
   if (nblk <= 0) return;
+  // DQ_DEFLATE="chain,lazy,nice": match-search effort (default 48,24,48; zlib level 5 is 32,16,32
+  // with hash chains, tools/deflate_model.c)
+  static const int3 cfg = [] {
+    int c = 48, l = 24, n = 48;
+    if (const char* e = getenv("DQ_DEFLATE")) sscanf(e, "%d,%d,%d", &c, &l, &n);
+    return make_int3(std::max(1, std::min(c, MAXCAND)), std::max(0, std::min(l, 32)), std::max(3, n));
+  }();
   hipLaunchKernelGGL(bgzf_deflate_kernel, dim3((unsigned)nblk), dim3(DWG), 0, s, src, n_in, blk0, nblk,
-                     stage, link, out_slots, out_size, tim);
+                     stage, link, out_slots, out_size, tim, cfg.x, cfg.y, cfg.z);
 }
 
 void launch_bgzf_pack(const uint8_t* slots, const int32_t* size, const int64_t* off, int64_t nblk,

@@ -266,6 +266,7 @@ void launch_text_gather(const uint8_t* U, const int64_t* vstart, const int32_t* 
 // ------------------------------------------------------------------ BGZF deflate (write path)
 int64_t bgzf_block_count(int64_t n);
 size_t bgzf_stage_bytes(int64_t nblk);
+size_t bgzf_link_bytes(int64_t nblk);
 bool deflate_tables(int device);
 // Blocks [blk0, blk0 + nblk) of src[0, n_in) (65280 bytes each) into fixed 64 KiB slots.
 void launch_bgzf_deflate(const uint8_t* src, int64_t n_in, int64_t blk0, int64_t nblk,

@@ -594,21 +594,26 @@ __device__ int walk_win(const uint8_t* U, int64_t ulen, int u_is_eof, int64_t st
   return 0;
 }
 
-// One wave per segment (grid-stride: a few thousand resident waves instead of one dispatch per
-// segment): the first guesser hit at or after the segment start, 64 positions per step.
-__global__ __launch_bounds__(64) void seg_spec_kernel(const uint8_t* __restrict__ U, int64_t ulen,
+// One workgroup of NT threads per segment (grid-stride: a few thousand resident workgroups instead
+// of one dispatch per segment): the first guesser hit at or after the segment start, NT positions
+// per step.  Short reads: one wave (the first record is a few hundred bytes in); long reads: a
+// 256-thread workgroup, since the first record start after a segment start lies a size-biased
+// half record (~160 KB on the long-read file) in.
+template <int NT>
+__global__ __launch_bounds__(NT) void seg_spec_kernel(const uint8_t* __restrict__ U, int64_t ulen,
                                                       int32_t u_is_eof,
                                                       const int32_t* __restrict__ ref_len,
                                                       int32_t n_ref, Seg* __restrict__ segs,
                                                       int64_t nseg, int64_t seg_bytes,
                                                       int64_t start_lin, int64_t chain_end) {
+  __shared__ unsigned long long hit_min;
   for (int64_t s = blockIdx.x; s < nseg; s += gridDim.x) {
     const int64_t sb = start_lin + s * seg_bytes;
     const int64_t se = min(chain_end, sb + seg_bytes);
     int64_t best = INT64_MAX;
     if (s == 0) {
       best = start_lin;
-    } else {
+    } else if (NT == 64) {
       for (int64_t b = sb; b < se; b += 64) {
         const int64_t v = b + threadIdx.x;
         const bool hit = v < se && check_record_start<3>(U, ulen, u_is_eof, ref_len, n_ref, v) == 1;
@@ -618,6 +623,20 @@ __global__ __launch_bounds__(64) void seg_spec_kernel(const uint8_t* __restrict_
           break;
         }
       }
+    } else {
+      if (threadIdx.x == 0) hit_min = ~0ull;
+      __syncthreads();
+      for (int64_t b = sb; b < se; b += NT) {
+        const int64_t v = b + threadIdx.x;
+        if (v < se && check_record_start<3>(U, ulen, u_is_eof, ref_len, n_ref, v) == 1)
+          atomicMin(&hit_min, (unsigned long long)v);
+        __syncthreads();
+        const bool done = hit_min != ~0ull;
+        __syncthreads();  // every thread has read hit_min before the next step's atomics
+        if (done) break;
+      }
+      if (hit_min != ~0ull) best = (int64_t)hit_min;
+      __syncthreads();  // hit_min is read by every thread before the next segment resets it
     }
     if (threadIdx.x == 0) {
       Seg g;
@@ -1537,8 +1556,12 @@ void launch_seg_spec(const uint8_t* U, int64_t ulen, int32_t u_is_eof, int64_t c
                      int32_t n_ref, Seg* segs, int64_t nseg, int64_t seg_bytes, int64_t start_lin,
                      hipStream_t s) {
   if (nseg <= 0) return;
-  hipLaunchKernelGGL(seg_spec_kernel, dim3((unsigned)std::min<int64_t>(nseg, 16384)), dim3(64), 0, s, U, ulen, u_is_eof,
-                     ref_len, n_ref, segs, nseg, seg_bytes, start_lin, chain_end);
+  if (seg_bytes > 64 * 1024)  // long records (segments sized from the guesser's record span)
+    hipLaunchKernelGGL(seg_spec_kernel<256>, dim3((unsigned)std::min<int64_t>(nseg, 16384)), dim3(256), 0, s, U,
+                       ulen, u_is_eof, ref_len, n_ref, segs, nseg, seg_bytes, start_lin, chain_end);
+  else
+    hipLaunchKernelGGL(seg_spec_kernel<64>, dim3((unsigned)std::min<int64_t>(nseg, 16384)), dim3(64), 0, s, U,
+                       ulen, u_is_eof, ref_len, n_ref, segs, nseg, seg_bytes, start_lin, chain_end);
   hipLaunchKernelGGL(seg_walk_kernel, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, U, ulen,
                      u_is_eof, segs, nseg, seg_bytes, start_lin, chain_end);
 }
