@@ -238,26 +238,24 @@ def main():
                     raise
                 err = 1
         # descriptors of every shard: [err, owned bytes, records, counts..., digests...]
-        d = torch.zeros(3 + 2 * maxp, dtype=torch.int64)
+        d = np.zeros(3 + 2 * maxp, dtype=np.int64)
         d[0] = err
         if st is not None:
             d[1], d[2] = st.owned_bytes, st.n_records
-            d[3:3 + len(cnt)] = torch.from_numpy(cnt)
-            d[3 + maxp:3 + maxp + len(dig)] = torch.from_numpy(dig.view(np.int64))
+            d[3:3 + len(cnt)] = cnt
+            d[3 + maxp:3 + maxp + len(dig)] = dig.view(np.int64)
         if dist is not None:
             rows = [torch.zeros(3 + 2 * maxp, dtype=torch.int64, device=cdev) for _ in range(world)]
-            dist.all_gather(rows, d.to(cdev))
-            every = torch.stack([r.cpu() for r in rows])
+            dist.all_gather(rows, torch.from_numpy(d).to(cdev))
+            every = torch.stack([r.cpu() for r in rows]).numpy()
         else:
             every = d[None]
         if int(every[:, 0].max()) != 0:
             return None
-        digests = [0] * nsplit
+        digests = np.zeros(nsplit, dtype=np.uint64)
         for r, s in enumerate(plan):
-            row = every[r]
-            for i in range(s.p1 - s.p0):
-                digests[s.p0 + i] = int(row[3 + maxp + i]) & P.M64
-        return st, int(every[:, 1].sum()), int(every[:, 2].sum()), P.fold_digest(digests)
+            digests[s.p0:s.p1] = every[r, 3 + maxp:3 + maxp + s.p1 - s.p0].view(np.uint64)
+        return st, int(every[:, 1].sum()), int(every[:, 2].sum()), P.fold_digest_np(digests)
 
     def barrier():
         torch.cuda.synchronize()

@@ -571,8 +571,15 @@ static int run_pipeline(dq_ctx* ctx) {
   HIPCHK(hipMemsetAsync(ctx->scan_over.p, 0, sizeof(int32_t), s));
   launch_bgzf_scan(ctx->cbuf(), L, L, ctx->slots.as<Cand>(), 0, ctx->counts.as<int32_t>(),
                    nch, nullptr, ctx->scan_over.as<int32_t>(), s);
+  if ((rc = ensure_scan(ctx, nch))) return rc;
+  // the candidate count (scan of the chunk counts) and the overflow count come back together;
+  // only a file with dense BGZF regions (n_over > 0) takes the second pass and a second trip
+  launch_exclusive_scan_i32(ctx->counts.as<int32_t>(), ctx->offs.as<int64_t>(), nch,
+                            ctx->tmp.as<int64_t>(), s);
+  int64_t ncand = 0;
   int32_t n_over = 0;
   HIPCHK(hipMemcpyAsync(&n_over, ctx->scan_over.p, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(&ncand, ctx->offs.as<int64_t>() + nch, 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   if (n_over > SCAN_OVER_MAX) RET(DQ_EFORMAT, "too many dense BGZF regions");
   if (n_over > 0) {  // chunks with more than SCAN_CAP magic positions: second pass
@@ -586,13 +593,11 @@ static int run_pipeline(dq_ctx* ctx) {
     HIPCHK(hipMemcpyAsync(&bad, ctx->scan_over.p, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     if (bad < 0) RET(DQ_EFORMAT, "more than 640 BGZF magic positions in a 16 KiB window");
+    launch_exclusive_scan_i32(ctx->counts.as<int32_t>(), ctx->offs.as<int64_t>(), nch,
+                              ctx->tmp.as<int64_t>(), s);
+    if ((rc = get_i64(ctx, ctx->offs.as<int64_t>() + nch, &ncand))) return rc;
   }
-  if ((rc = ensure_scan(ctx, nch))) return rc;
-  launch_exclusive_scan_i32(ctx->counts.as<int32_t>(), ctx->offs.as<int64_t>(), nch,
-                            ctx->tmp.as<int64_t>(), s);
   dbg(s, "scan", nch, n_over);
-  int64_t ncand = 0;
-  if ((rc = get_i64(ctx, ctx->offs.as<int64_t>() + nch, &ncand))) return rc;
   ctx->ncand = ncand;
   const int64_t capc = std::max<int64_t>(1, ncand);
   if ((rc = ensure_all(ctx, ctx->cand, sizeof(Cand) * (size_t)capc))) return rc;
@@ -614,6 +619,9 @@ static int run_pipeline(dq_ctx* ctx) {
   if ((rc = ensure_all(ctx, ctx->blk_us, sizeof(int32_t) * (size_t)capb))) return rc;
   // a shard's bytes end inside the file: the end of the buffer is not EOF
   const int32_t is_eof = (!ctx->shard || ctx->base + L >= ctx->file_len) ? 1 : 0;
+  // blk_us zeroed past the chain: the scan below runs over all capb entries before the block count
+  // is known on the host, and its total is the decompressed length
+  HIPCHK(hipMemsetAsync(ctx->blk_us.p, 0, sizeof(int32_t) * (size_t)capb, s));
   if (ncand > 0)
     launch_chain2(ctx->cbuf(), L, ctx->cand.as<Cand>(), d_ncand, ncand,
                   ctx->voff.as<int64_t>(), ctx->blk_pos.as<int64_t>(), ctx->blk_cs.as<int32_t>(),
@@ -626,8 +634,15 @@ static int run_pipeline(dq_ctx* ctx) {
   HIPCHK(hipMemsetAsync(d_cc, 0xff, 16, s));
   if (ncand > 0)
     launch_chain_check(ctx->cand.as<Cand>(), d_ncand, capc, ctx->blk_pos.as<int64_t>(), d_nblk, d_cc, s);
+  // block offsets in U (exclusive scan of ISIZE) over the capb candidates' slots
+  if ((rc = ensure_all(ctx, ctx->uoff, sizeof(int64_t) * (size_t)(capb + 1)))) return rc;
+  if ((rc = ensure_scan(ctx, capb))) return rc;
+  launch_exclusive_scan_i32(ctx->blk_us.as<int32_t>(), ctx->uoff.as<int64_t>(), capb,
+                            ctx->tmp.as<int64_t>(), s);
   alignas(8) unsigned char sc[144];
+  int64_t ulen = 0;
   HIPCHK(hipMemcpyAsync(sc, ctx->scal.p, sizeof sc, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(&ulen, ctx->uoff.as<int64_t>() + capb, 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   int64_t nblk = 0;
   int32_t broken = 0;
@@ -647,16 +662,15 @@ static int run_pipeline(dq_ctx* ctx) {
     launch_chain_serial(ctx->cbuf(), L, chain_start, ctx->blk_pos.as<int64_t>(),
                         ctx->blk_cs.as<int32_t>(), ctx->blk_us.as<int32_t>(), capw, d_nblk, d_stat, s);
     if ((rc = get_i64(ctx, d_nblk, &nblk))) return rc;
+    if ((rc = ensure_all(ctx, ctx->uoff, sizeof(int64_t) * (size_t)(nblk + 1)))) return rc;
+    if ((rc = ensure_scan(ctx, nblk))) return rc;
+    launch_exclusive_scan_i32(ctx->blk_us.as<int32_t>(), ctx->uoff.as<int64_t>(), nblk,
+                              ctx->tmp.as<int64_t>(), s);
+    if ((rc = get_i64(ctx, ctx->uoff.as<int64_t>() + nblk, &ulen))) return rc;
   }
   dbg(s, "chain", nblk, broken);
   ctx->nblk = nblk;
   if (nblk == 0 && L > 0) RET(DQ_EFORMAT, "no BGZF blocks found");
-  if ((rc = ensure_all(ctx, ctx->uoff, sizeof(int64_t) * (size_t)(nblk + 1)))) return rc;
-  if ((rc = ensure_scan(ctx, nblk))) return rc;
-  launch_exclusive_scan_i32(ctx->blk_us.as<int32_t>(), ctx->uoff.as<int64_t>(), nblk,
-                            ctx->tmp.as<int64_t>(), s);
-  int64_t ulen = 0;
-  if ((rc = get_i64(ctx, ctx->uoff.as<int64_t>() + nblk, &ulen))) return rc;
   ctx->ulen = ulen;
   HIPCHK(hipEventRecord(ctx->ev[1], s));
   // ---- Kernel 2: inflate
@@ -700,22 +714,27 @@ static int run_pipeline(dq_ctx* ctx) {
   }
   dbg(s, "inflate", nblk, ulen);
   HIPCHK(hipEventRecord(ctx->ev[2], s));
-  {  // the first failed block, by a device reduction: one word back instead of the status array
-    unsigned long long* d_bad = reinterpret_cast<unsigned long long*>(ctx->scal.as<char>() + 144);
-    HIPCHK(hipMemsetAsync(d_bad, 0xff, 8, s));
-    launch_first_bad(ctx->status.as<int32_t>(), nullptr, nblk, d_bad, s);
-    unsigned long long bad = 0;
+  // the first failed block, by a device reduction: one word back instead of the status array.  A
+  // shard (header supplied by the caller, U not read on the host before planning) takes the word
+  // back with the planning's results; a whole file checks it before its header is read from U.
+  unsigned long long* d_bad = reinterpret_cast<unsigned long long*>(ctx->scal.as<char>() + 144);
+  const bool defer_bad = ctx->shard && !ctx->header_only && !ctx->text_mode;
+  unsigned long long bad = ~0ull;
+  HIPCHK(hipMemsetAsync(d_bad, 0xff, 8, s));
+  launch_first_bad(ctx->status.as<int32_t>(), nullptr, nblk, d_bad, s);
+  auto bad_block = [&]() -> int {
+    int32_t st = 0;
+    int64_t pos = 0;
+    HIPCHK(hipMemcpy(&st, ctx->status.as<int32_t>() + bad, 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&pos, ctx->blk_pos.as<int64_t>() + bad, 8, hipMemcpyDeviceToHost));
+    char msg[256];
+    snprintf(msg, sizeof msg, "%s in BGZF block at %lld", status_name(st), (long long)pos);
+    RET(DQ_EFORMAT, msg);
+  };
+  if (!defer_bad) {
     HIPCHK(hipMemcpyAsync(&bad, d_bad, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    if (bad != ~0ull) {
-      int32_t st = 0;
-      int64_t pos = 0;
-      HIPCHK(hipMemcpy(&st, ctx->status.as<int32_t>() + bad, 4, hipMemcpyDeviceToHost));
-      HIPCHK(hipMemcpy(&pos, ctx->blk_pos.as<int64_t>() + bad, 8, hipMemcpyDeviceToHost));
-      char msg[256];
-      snprintf(msg, sizeof msg, "%s in BGZF block at %lld", status_name(st), (long long)pos);
-      RET(DQ_EFORMAT, msg);
-    }
+    if (bad != ~0ull) return bad_block();
   }
   if (ctx->text_mode) {  // BGZF text: lines are planned by text_run
     ctx->stats = dq_stats{};
@@ -810,7 +829,9 @@ static int run_pipeline(dq_ctx* ctx) {
                        nblk, ulen, splits.empty() ? 0 : splits.back().second, d_bs, s);
     HIPCHK(hipMemcpyAsync(bstat, d_bs, sizeof bstat, hipMemcpyDeviceToHost, s));
   }
+  if (defer_bad) HIPCHK(hipMemcpyAsync(&bad, d_bad, 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  if (bad != ~0ull) return bad_block();  // before any planning status: the inflate failed first
   HIPCHK(hipEventRecord(ctx->ev[3], s));
   dbg(s, "plan", nsplit);
   int64_t start_lin = ctx->chunk_mode ? ctx->plans_h[0].rec_lin : no_guess ? ctx->header_bytes : -1;
@@ -869,8 +890,15 @@ static int run_pipeline(dq_ctx* ctx) {
     launch_seg_spec(ctx->U.as<uint8_t>(), ulen, is_eof, chain_end, ctx->d_ref_len.as<int32_t>(), ctx->n_ref,
                     ctx->segs.as<Seg>(), nseg, SEG, start_lin, s);
     launch_seg_link(ctx->segs.as<Seg>(), nseg, SEG, start_lin, chain_end, d_broken, s);
+    // the link check and the record count come back together; a broken link (a guesser false
+    // positive) is repaired serially and the count taken again
+    if ((rc = ensure_scan(ctx, nseg))) return rc;
+    launch_seg_counts(ctx->segs.as<Seg>(), nseg, ctx->segcnt.as<int64_t>(), s);
+    launch_exclusive_scan_i64(ctx->segcnt.as<int64_t>(), ctx->segbase.as<int64_t>(), nseg,
+                              ctx->tmp.as<int64_t>(), s);
     int32_t br = 0;
     HIPCHK(hipMemcpyAsync(&br, d_broken, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&nrec, ctx->segbase.as<int64_t>() + nseg, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     if (br) {
       launch_seg_fix2(ctx->U.as<uint8_t>(), ulen, is_eof, chain_end, ctx->segs.as<Seg>(), nseg, SEG, start_lin,
@@ -880,13 +908,12 @@ static int run_pipeline(dq_ctx* ctx) {
       HIPCHK(hipStreamSynchronize(s));
       if (st == 4) RET(DQ_EFORMAT, "shard halo too small: the record chain runs past the shard bytes");
       if (st) RET(DQ_EFORMAT, st == ST_BAD_CODE ? "Invalid record length" : "truncated record chain");
+      launch_seg_counts(ctx->segs.as<Seg>(), nseg, ctx->segcnt.as<int64_t>(), s);
+      launch_exclusive_scan_i64(ctx->segcnt.as<int64_t>(), ctx->segbase.as<int64_t>(), nseg,
+                                ctx->tmp.as<int64_t>(), s);
+      if ((rc = get_i64(ctx, ctx->segbase.as<int64_t>() + nseg, &nrec))) return rc;
     }
     dbg(s, "segs", nseg, br);
-    launch_seg_counts(ctx->segs.as<Seg>(), nseg, ctx->segcnt.as<int64_t>(), s);
-    if ((rc = ensure_scan(ctx, nseg))) return rc;
-    launch_exclusive_scan_i64(ctx->segcnt.as<int64_t>(), ctx->segbase.as<int64_t>(), nseg,
-                              ctx->tmp.as<int64_t>(), s);
-    if ((rc = get_i64(ctx, ctx->segbase.as<int64_t>() + nseg, &nrec))) return rc;
     const size_t nr = (size_t)std::max<int64_t>(1, nrec);
     if ((rc = ensure_all(ctx, ctx->rec_lin, 8 * nr))) return rc;
     launch_seg_emit2(ctx->U.as<uint8_t>(), ulen, ctx->segs.as<Seg>(), ctx->segbase.as<int64_t>(),

@@ -289,19 +289,30 @@ struct Finder {
     const int lo = max(h ? L.head[h - 1] : 0, g - chain);
     const uint32_t p4 = ld4(L.in, p);
     int best = 0, bd = 0;
-    for (int i0 = g - 1; i0 >= lo && best < nice; i0 -= 8) {
+    for (int i0 = g - 1; i0 >= lo && best < nice && best < lim; i0 -= 8) {
+      // a batch of 8 candidates: their positions (global) and first / scan-end words (LDS) are
+      // all loaded before any is tested, so the batch costs about one load latency of each kind
       int q8[8];
 #pragma unroll
       for (int k = 0; k < 8; k++) q8[k] = i0 - k >= lo ? (int)bl[i0 - k] : -1;
+      // only a candidate that also matches the byte at `best` can win: the 4 bytes ending there
+      // are tested first (zlib's scan_end test), with the best length at the batch start
+      const bool use_e = best >= 3;
+      const int be = use_e ? best - 3 : 0;
+      const uint32_t pe = ld4(L.in, p + be);
+      uint32_t x8[8], e8[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int q = q8[k] >= 0 ? q8[k] : p;
+        x8[k] = ld4(L.in, q) ^ p4;
+        e8[k] = ld4(L.in, q + be) ^ pe;
+      }
 #pragma unroll
       for (int k = 0; k < 8; k++) {
         const int q = q8[k];
-        if (q < 0 || p - q > WIN || best >= nice || best >= lim) break;
-        // only a candidate that also matches the byte at `best` can win: test the 4 bytes ending
-        // there first (zlib's scan_end test), so most candidates cost two compares, not a walk
-        if (best >= 3 && ld4(L.in, q + best - 3) != ld4(L.in, p + best - 3)) continue;
-        uint32_t x = ld4(L.in, q) ^ p4;
-        if (x & 0xffffffu) continue;  // a hash collision
+        if (q < 0 || p - q > WIN) break;
+        if ((x8[k] & 0xffffffu) || (use_e && e8[k])) continue;  // a hash collision / no match at best
+        uint32_t x = x8[k];
         int l = 0;
         while (x == 0 && l + 4 < lim) {
           l += 4;
@@ -313,6 +324,7 @@ struct Finder {
           best = l;
           bd = p - q;
         }
+        if (best >= nice || best >= lim) break;
       }
     }
     *dist = bd;

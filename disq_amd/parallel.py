@@ -339,6 +339,21 @@ def fold_digest(digests: Sequence[int], first_index: int = 0) -> int:
     return d
 
 
+def fold_digest_np(digests, first_index: int = 0) -> int:
+    """fold_digest over a uint64 array, vectorised (uint64 arithmetic wraps mod 2^64)."""
+    import numpy as np
+    z = np.asarray(digests, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = z ^ (np.arange(first_index + 1, first_index + 1 + len(z), dtype=np.uint64)
+                 * np.uint64(K_WORD))
+        z ^= z >> np.uint64(30)
+        z *= np.uint64(0xBF58476D1CE4E5B9)
+        z ^= z >> np.uint64(27)
+        z *= np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+        return int(z.sum(dtype=np.uint64))
+
+
 def broadcast_header(header_reader, read_prefix, file_len: int, rank: int, world: int,
                      group=None) -> bytes:
     """Rank 0 reads the decompressed header from the file's first bytes (growing the prefix) and

@@ -52,6 +52,14 @@ def test_fold_digest_definition():
     assert P.fold_digest(d[1:], first_index=1) + P.mix64(5 ^ P.K_WORD) & P.M64 == want
 
 
+def test_fold_digest_np_equals_fold_digest():
+    rng = np.random.default_rng(5)
+    d = rng.integers(0, 2 ** 63, 373, dtype=np.int64).astype(np.uint64) * np.uint64(2) + np.uint64(1)
+    assert P.fold_digest_np(d) == P.fold_digest([int(x) for x in d])
+    assert P.fold_digest_np(d[7:], first_index=7) == P.fold_digest([int(x) for x in d[7:]], 7)
+    assert P.fold_digest_np(np.zeros(0, np.uint64)) == 0
+
+
 def _oracle_decoder(full: bytes, split: int, need: int = 0):
     """Oracle stand-in for the GPU shard decoder; `need` = halo bytes it demands past the shard
     end (the library's "shard halo too small" error otherwise), to exercise halo growth."""
