@@ -289,7 +289,8 @@ struct Finder {
     const int lo = max(h ? L.head[h - 1] : 0, g - chain);
     const uint32_t p4 = ld4(L.in, p);
     int best = 0, bd = 0;
-    for (int i0 = g - 1; i0 >= lo && best < nice && best < lim; i0 -= 8) {
+    const int cap = min(lim, nice);
+    for (int i0 = g - 1; i0 >= lo && best < cap; i0 -= 8) {
       // a batch of 8 candidates: their positions (global) and first / scan-end words (LDS) are
       // all loaded before any is tested, so the batch costs about one load latency of each kind
       int q8[8];
@@ -312,20 +313,32 @@ struct Finder {
         const int q = q8[k];
         if (q < 0 || p - q > WIN) break;
         if ((x8[k] & 0xffffffu) || (use_e && e8[k])) continue;  // a hash collision / no match at best
+        // compared up to `cap` only: the first candidate that reaches it ends the search (the
+        // same choice as comparing every candidate in full), and only that one is extended on
         uint32_t x = x8[k];
         int l = 0;
-        while (x == 0 && l + 4 < lim) {
+        while (x == 0 && l + 4 < cap) {
           l += 4;
           x = ld4(L.in, q + l) ^ ld4(L.in, p + l);
         }
         l = x ? l + (int)(__builtin_ctz(x) >> 3) : l + 4;
-        l = min(l, lim);
+        l = min(l, cap);
         if (l > best) {
           best = l;
           bd = p - q;
         }
-        if (best >= nice || best >= lim) break;
+        if (best >= cap) break;
       }
+    }
+    if (best >= cap && cap < lim) {  // the winner, extended to the end of its match
+      const int q = p - bd;
+      int l = cap;
+      uint32_t x = 0;
+      while (x == 0 && l < lim) {
+        x = ld4(L.in, q + l) ^ ld4(L.in, p + l);
+        l += x ? (int)(__builtin_ctz(x) >> 3) : 4;
+      }
+      best = min(l, lim);
     }
     *dist = bd;
     return best >= 3 ? best : 0;
