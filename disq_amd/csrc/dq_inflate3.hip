@@ -190,7 +190,6 @@ struct BitR {
   uint32_t wp;    // word index of the next word to enter bb (br_pos = 32 * wp - bc)
   uint32_t nw;    // W[wp]
 };
-
 #define DQ_AI __device__ __attribute__((always_inline)) inline
 
 // The thread index behind an empty volatile asm: values derived from it cannot be hoisted out of
@@ -323,8 +322,7 @@ enum : int32_t { F_DEAD = 4 };  // speculative path found no boundary >= sB (gar
 // Decode from `start`; output is counted from the first symbol boundary >= sB (*Bp) and the
 // run stops at the first boundary >= sE (*Ep).  Returns F_EXIT / F_EOB (*Ep = bit after EOB) /
 // F_ERR / F_END (ran off the data) / F_DEAD (no boundary >= sB before an error, EOB or the end).
-constexpr int NCK_MAX = 16;     // checkpoints per speculative lane (runtime nck <= NCK_MAX)
-constexpr int NCK_DEFAULT = 8;
+constexpr int NCK_DEFAULT = 8;  // checkpoints per speculative lane
 constexpr uint32_t CKI_DEFAULT = 48;  // checkpoint spacing in bits (>= the longest symbol: a symbol
                                 // crosses at most one threshold; most paths re-synchronise
                                 // within ~100 bits, segments are ~160-1000 bits)
@@ -857,10 +855,11 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     const int32_t* __restrict__ blk_csize, const int32_t* __restrict__ blk_usize,
     const int64_t* __restrict__ uoff, int64_t nblk, uint8_t* __restrict__ U,
     int32_t* __restrict__ status, int32_t verify_crc, const uint32_t* __restrict__ crc_init,
-    uint64_t* __restrict__ tim, uint32_t OV, uint32_t sflags, const int32_t* __restrict__ sel,
-    uint32_t ckcfg) {
-  const uint32_t CKI = ckcfg & 255u;        // checkpoint spacing (bits)
-  const int NCK = (int)(ckcfg >> 8) & 31;   // checkpoints per lane
+    uint64_t* __restrict__ tim, uint32_t OV, uint32_t sflags, const int32_t* __restrict__ sel) {
+  // compile-time checkpoints (the spacing/count sweep's choice, profiles/r3ij_*): the decode loops
+  // fold the threshold updates and hold fewer SGPRs (spec + rounds -8 k cycles per block, r3y)
+  constexpr uint32_t CKI = CKI_DEFAULT;
+  constexpr int NCK = NCK_DEFAULT;
   __shared__ LdsI L;
   // DQ_TIMING: thread 0 accumulates s_memtime cycles per phase (tim != nullptr only then)
   // [0..15] phases over the BGZF block; [16..21] phases 0-5 of its first deflate block; [22] the
@@ -1561,20 +1560,12 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
     if (const char* e = getenv("DQ_CFG")) sscanf(e, "%d,%d", &nb, &g);
     return g == 4 ? 1 : nb == 2 ? 4 : 0;
   }();
-  // checkpoints: DQ_CKI bits apart (8..255), DQ_NCK of them (1..NCK_MAX)
-  static const uint32_t ckcfg = [] {
-    uint32_t cki = getenv("DQ_CKI") ? (uint32_t)atoi(getenv("DQ_CKI")) : CKI_DEFAULT;
-    uint32_t nck = getenv("DQ_NCK") ? (uint32_t)atoi(getenv("DQ_NCK")) : (uint32_t)NCK_DEFAULT;
-    cki = std::min(255u, std::max(8u, cki));
-    nck = std::min((uint32_t)NCK_MAX, std::max(1u, nck));
-    return cki | nck << 8;
-  }();
   // DQ_LDSPAD: extra dynamic LDS per workgroup (occupancy experiments: 80000 = one workgroup per CU)
   static const unsigned ldspad = getenv("DQ_LDSPAD") ? (unsigned)atoi(getenv("DQ_LDSPAD")) : 0u;
 #define DQ_LAUNCH(TM, NBT, GT)                                                                  \
   hipLaunchKernelGGL((inflate_block_kernel<TM, NBT, GT>), dim3((unsigned)ngrid), dim3(WG), ldspad, s, C, \
                      blk_pos, blk_csize, blk_usize, uoff, ngrid, U, status, verify_crc, crc_init, tim, ov, \
-                     sflags, sel, ckcfg)
+                     sflags, sel)
 #define DQ_CFGS(TM)                       \
   switch (cfg) {                          \
     case 1: DQ_LAUNCH(TM, 1, 4); break;   \
