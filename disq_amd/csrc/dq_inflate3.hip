@@ -895,16 +895,6 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   const int32_t dbytes = csize - 26;
   const uint32_t endbits = a0 + 8u * (uint32_t)max(dbytes, 0);
 
-#ifdef DQ_WARM
-  // one load per 128-byte line of the block's DEFLATE data, all at once: the decode passes'
-  // scattered first reads then hit L2 instead of waiting on HBM one lane at a time.  The words
-  // are folded into a value checked against an opaque condition at the end (kept, never true).
-  uint32_t warm = 0;
-  {
-    const int nwords = (int)((endbits + 31) >> 5) + 2;
-    for (int i = 32 * t; i < nwords; i += 32 * WG) warm ^= W[i];
-  }
-#endif
   for (int i = t; i < 2048; i += WG) L.bm[i] = 0;
   if (t < 32) L.misc[t] = 0;
   if (t == 0) {
@@ -1473,9 +1463,6 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   TST(7);
   if (TIMING && t == 0)
     for (int i = 0; i < 24; i++) tim[(int64_t)blockIdx.x * 24 + i] = tacc[i];
-#ifdef DQ_WARM
-  if (tid_fresh() == WG && warm == 0x9E3779B9u) status[b] = ST_HANG;  // never: tid < WG
-#endif
 }
 
 uint32_t h_mul(uint32_t a, uint32_t b) {
