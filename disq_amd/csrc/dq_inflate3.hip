@@ -172,7 +172,7 @@ __constant__ uint32_t c_slice_shift[WG];  // x^(8 * CRC_SL * k) mod P, k = 0..51
 __constant__ uint8_t c_clorder3[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 // misc slots
-enum { M_ERR = 0, M_A = 4, M_LAST, M_MORE, M_MORE1,
+enum { M_ERR = 0, M_SLOW = 1 /* an E_SLOW root entry in this deflate block's tables */, M_A = 4, M_LAST, M_MORE, M_MORE1,
        M_LQ0 = 15, M_LQN, M_DQ0, M_DQN, M_NEXT,
        M_LASTF, M_RCNT = 28 /* and 29: redo-list counters of even / odd rounds */,
        M_DIRTY = 30 /* and 31: a re-decoded exit changed, even / odd rounds */ };
@@ -255,17 +255,24 @@ DQ_AI uint32_t load_desc(const LdsI& L, int a) {
   return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)a & 3u) & 0xffffffu;
 }
 
-// Second-level / canonical lookup for a root entry that is not a code.
+// Second-level / canonical lookup for a root entry that is not a code.  SLOW = false (no E_SLOW
+// entry in this deflate block's tables, M_SLOW): one read, with no nested branch -- a "no code"
+// root entry (0: only in an incomplete code, which has no long codes) reads the first entry of the
+// zero-filled, unused second-level area, so it still decodes as an invalid code.
+template <bool SLOW>
 DQ_AI uint32_t ll_second(const LdsI& L, uint32_t e, uint32_t bb) {
   const uint32_t sb = (e >> 4) & 7;
+  if (!SLOW) return L.u.d.T[T_LSUB + (e >> 7) + ((bb >> LR) & ((1u << sb) - 1))];
   if (sb) return L.u.d.T[T_LSUB + (e >> 7) + ((bb >> LR) & ((1u << sb) - 1))];
   if (!(e & E_SLOW)) return 0u;
   int l = 0;
   const int k = canon_decode(bb, L.u.d.hl, LR + 1, &l);
   return k < 0 ? 0u : L.u.d.lent[k];
 }
+template <bool SLOW>
 DQ_AI uint32_t d_second(const LdsI& L, uint32_t e, uint32_t bb) {
   const uint32_t sb = (e >> 4) & 7;
+  if (!SLOW) return L.u.d.T[T_DSUB + (e >> 7) + ((bb >> DR) & ((1u << sb) - 1))];
   if (sb) return L.u.d.T[T_DSUB + (e >> 7) + ((bb >> DR) & ((1u << sb) - 1))];
   if (!(e & E_SLOW)) return 0u;
   int l = 0;
@@ -285,7 +292,7 @@ DQ_AI uint32_t d_second(const LdsI& L, uint32_t e, uint32_t bb) {
 // boundary between them lies before `lim` (the next bit position at which the caller looks at
 // symbol boundaries: segment start/exit, checkpoint, end of data), both are taken at once and
 // `lit2` is the second (else 0xffffffff) -- the boundaries the caller sees are unchanged.
-template <class S>
+template <bool SLOW, class S>
 DQ_AI bool dsym(BitR& r, const S& W, const LdsI& L, uint32_t p, uint32_t lim,
                 uint32_t& len, uint32_t& dist, uint32_t& lit2, bool& is_m) {
   br_refill(r, W);  // >= 33 bits: a litlen code + its extra bits (<= 20)
@@ -293,7 +300,7 @@ DQ_AI bool dsym(BitR& r, const S& W, const LdsI& L, uint32_t p, uint32_t lim,
   const uint32_t ri = bb & ((1u << LR) - 1);
   uint32_t e = L.u.d.T[ri];
   const uint32_t pe = L.u.d.x.pair[ri];
-  if ((e & 15) == 0) e = ll_second(L, e, bb);
+  if ((e & 15) == 0) e = ll_second<SLOW>(L, e, bb);
   const uint32_t nb = e & 15;
   const uint32_t lx = __builtin_amdgcn_ubfe(e, 5, 3);
   is_m = (e & 16) != 0;
@@ -304,7 +311,7 @@ DQ_AI bool dsym(BitR& r, const S& W, const LdsI& L, uint32_t p, uint32_t lim,
   br_refill(r, W);  // >= 33 bits: a distance code + its extra bits (<= 28)
   bb = (uint32_t)r.bb;
   uint32_t e2 = L.u.d.T[T_DROOT + (bb & ((1u << DR) - 1))];
-  if (is_m && (e2 & 15) == 0) e2 = d_second(L, e2, bb);
+  if (is_m && (e2 & 15) == 0) e2 = d_second<SLOW>(L, e2, bb);
   const uint32_t nb2 = e2 & 15, dx = __builtin_amdgcn_ubfe(e2, 4, 4);
   dist = (__builtin_amdgcn_ubfe(e2, 12, 2) << __builtin_amdgcn_ubfe(e2, 8, 4)) + 1u +
          __builtin_amdgcn_ubfe(bb, nb2, dx);
@@ -331,7 +338,7 @@ constexpr uint32_t CKI_DEFAULT = 48;  // checkpoint spacing in bits (>= the long
 // (offset from sB << 16 | bytes counted so far), j < nck, at ck[j * ckstride] (nullptr: none).
 // A spacing below the longest symbol only loses merges: a merge needs equal bit positions, and
 // equal positions at symbol boundaries are equal decoder states whatever the checkpoint index.
-template <class S>
+template <bool SLOW, class S>
 DQ_AI int run_seg(const S& W, const LdsI& L, uint32_t start, uint32_t sB,
                   uint32_t sE, uint32_t endbits, int32_t* Bp, int32_t* Ep, int32_t* cntp,
                   uint32_t* ck, int ckstride, uint32_t CKI, int NCK) {
@@ -342,7 +349,7 @@ DQ_AI int run_seg(const S& W, const LdsI& L, uint32_t start, uint32_t sB,
   bool m;
   // warm-up: to the first symbol boundary >= sB, nothing counted
   while (p < sB) {
-    if (p >= endbits || dsym(r, W, L, p, min(sB, endbits), len, dist, lit2, m)) {
+    if (p >= endbits || dsym<SLOW>(r, W, L, p, min(sB, endbits), len, dist, lit2, m)) {
       *Ep = (int32_t)(p < endbits && len != 0xffffffffu ? len : p);
       *Bp = -1;
       *cntp = 0;
@@ -369,7 +376,7 @@ DQ_AI int run_seg(const S& W, const LdsI& L, uint32_t start, uint32_t sB,
       f = p >= sE ? F_EXIT : F_END;
       break;
     }
-    if (dsym(r, W, L, p, min(min(thr, sE), endbits), len, dist, lit2, m)) {
+    if (dsym<SLOW>(r, W, L, p, min(min(thr, sE), endbits), len, dist, lit2, m)) {
       *Ep = (int32_t)(len != 0xffffffffu ? len : p);
       f = len != 0xffffffffu ? F_EOB : F_ERR;
       break;
@@ -386,7 +393,7 @@ DQ_AI int run_seg(const S& W, const LdsI& L, uint32_t start, uint32_t sB,
 // threshold the path is compared with the speculative one: the same boundary means the same
 // decoder state, so the rest of the segment is the speculative run's (exit `se` = E << 3 | flag,
 // `sc` bytes from its first boundary) and the decode stops there.
-template <class S>
+template <bool SLOW, class S>
 DQ_AI int run_redo(const S& W, const LdsI& L, uint32_t s0, uint32_t sB,
                    uint32_t sE, uint32_t endbits, const uint32_t* ck, int ckstride, int32_t se,
                    int32_t sc, int32_t* Ep, int32_t* cntp, uint32_t CKI, int NCK, int* jm = nullptr) {
@@ -421,7 +428,7 @@ DQ_AI int run_redo(const S& W, const LdsI& L, uint32_t s0, uint32_t sB,
     cur = cross ? (j < NCK ? nxt : 0xffffffffu) : cur;
     uint32_t len = 0, dist = 0, lit2;
     bool m;
-    if (dsym(r, W, L, p, min(min(thr, sE), endbits), len, dist, lit2, m)) {
+    if (dsym<SLOW>(r, W, L, p, min(min(thr, sE), endbits), len, dist, lit2, m)) {
       *Ep = (int32_t)(len != 0xffffffffu ? len : p);
       f = len != 0xffffffffu ? F_EOB : F_ERR;
       break;
@@ -436,7 +443,7 @@ DQ_AI int run_redo(const S& W, const LdsI& L, uint32_t s0, uint32_t sB,
 // absolute position p; stops at isize.  Literals, literal pairs and match descriptors are written
 // by the same three byte stores: a store a symbol does not need goes to this lane's dummy word
 // (wsum / small are dead during emit), so literal and match lanes do not run separate branches.
-template <class S>
+template <bool SLOW, class S>
 DQ_AI void emit_seg(const S& W, LdsI& L, uint32_t start, uint32_t target,
                     uint32_t endbits, int32_t p, int32_t isize, int sh) {
   typedef volatile __attribute__((address_space(3))) uint8_t lds8;
@@ -451,7 +458,7 @@ DQ_AI void emit_seg(const S& W, LdsI& L, uint32_t start, uint32_t target,
     if (q >= target || q >= endbits || p >= isize) return;
     uint32_t len = 0, dist = 0, lit2;
     bool m;
-    const bool stop = dsym(r, W, L, q, min(target, endbits), len, dist, lit2, m);
+    const bool stop = dsym<SLOW>(r, W, L, q, min(target, endbits), len, dist, lit2, m);
     const bool far = m && (int32_t)dist > p;  // a distance before the block's first byte
     if (stop || far) {  // one exit branch: EOB / bad code (accounted for by the rounds) or far
       if (!stop) set_err(L, ST_BAD_DIST);
@@ -667,6 +674,7 @@ DQ_AI void build_tables(LdsI& L, int nlen, int ndist) {
       if (start) {
         const uint32_t ridx = bitrev(pf, R2) + (isl ? 0 : T_DROOT);
         L.u.d.T[ridx] = fits ? (uint16_t)(sb << 4 | off << 7) : E_SLOW;
+        if (!fits) L.misc[M_SLOW] = 1;  // the decode passes take the canonical fallback
       }
       if (fits) {  // this canonical position's code into its group's table
         const uint32_t c = H.first[cl] + (uint32_t)(sym - H.offs[cl]);
@@ -910,6 +918,8 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     //      The dynamic header's staged words and code-length code lengths are loaded with it
     //      (their position follows from pos alone; C is padded, so a stored or fixed block near
     //      the end reads pad bytes it never uses).
+    if (t == 0) L.misc[M_SLOW] = 0;  // read after build_tables' barriers; the last read of the
+                                     // previous deflate block's flag precedes the emit barrier
     const uint32_t clpos = pos + 17;
     const uint32_t hbase = clpos >> 5;
     const uint32_t hw = t < HB_WORDS ? W[hbase + t] : 0u;
@@ -1030,6 +1040,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     __syncthreads();
     TST(1);
     const uint32_t a = (uint32_t)L.misc[M_A];
+    const bool slow = L.misc[M_SLOW] != 0;  // uniform: the canonical fallback is rare
     if (a > endbits) {
       if (t == 0) L.misc[M_ERR] = ST_OVERREAD;
       break;
@@ -1078,8 +1089,10 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       int32_t B = -1, E = 0, c = 0;
       if (CK)
         for (int j = 0; j < NCK; j++) CK[j * nl + t] = 0xffffffffu;
-      const int f = run_seg(gsrc, L, start, sB, sE, endbits, &B, &E, &c, CK ? CK + t : nullptr, nl,
-                            CKI, NCK);
+      const int f = slow ? run_seg<true>(gsrc, L, start, sB, sE, endbits, &B, &E, &c,
+                                         CK ? CK + t : nullptr, nl, CKI, NCK)
+                         : run_seg<false>(gsrc, L, start, sB, sE, endbits, &B, &E, &c,
+                                          CK ? CK + t : nullptr, nl, CKI, NCK);
       AB[t] = B;
       AE[t] = (E << 3) | f;
       AC[t] = c;
@@ -1123,8 +1136,12 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
         int jmerge = -1;
         const uint32_t sB = a + (uint32_t)lt * seg;
         // a speculative lane that found no boundary (F_DEAD) recorded no checkpoints
-        const int f = run_redo(gsrc, L, s0, sB, sE, endbits, CK ? CK + lt : nullptr, nl, SE[lt],
-                               SC[lt], &E, &c, CKI, NCK, TIMING ? &jmerge : nullptr);
+        const int f = slow ? run_redo<true>(gsrc, L, s0, sB, sE, endbits, CK ? CK + lt : nullptr,
+                                            nl, SE[lt], SC[lt], &E, &c, CKI, NCK,
+                                            TIMING ? &jmerge : nullptr)
+                           : run_redo<false>(gsrc, L, s0, sB, sE, endbits, CK ? CK + lt : nullptr,
+                                             nl, SE[lt], SC[lt], &E, &c, CKI, NCK,
+                                             TIMING ? &jmerge : nullptr);
         const int32_t ae = (E << 3) | f;
         if (ae != AE[lt]) L.misc[M_DIRTY + (round & 1)] = 1;  // the successor's start moved
         AB[lt] = (int32_t)s0;
@@ -1182,7 +1199,8 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     // ---- emit
     if (t <= last && myoff < isize) {
       const uint32_t sE = t == nl - 1 ? 0xffffffffu : a + (uint32_t)(t + 1) * seg;
-      emit_seg(gsrc, L, (uint32_t)myB, sE, endbits, myoff, isize, sh);
+      if (slow) emit_seg<true>(gsrc, L, (uint32_t)myB, sE, endbits, myoff, isize, sh);
+      else emit_seg<false>(gsrc, L, (uint32_t)myB, sE, endbits, myoff, isize, sh);
     }
     const int32_t nextpos = L.misc[M_NEXT];
     __syncthreads();
