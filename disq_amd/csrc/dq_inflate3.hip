@@ -212,9 +212,14 @@ DQ_AI void st_nt(uint4* d, uint4 v) {  // streaming store (nt): U is not re-read
 // The compressed words.  (Staging a deflate block's words in the LDS image tail for the speculative
 // pass and the rounds was measured: no faster, profiles/r3a_lds_bits_ab.txt -- the refill load is
 // issued a half step ahead and is not the decode step's critical path.)
+// A word index becomes a 32-bit byte offset from the block's (uniform) base: the load takes the
+// SGPR-base + VGPR-offset form, with no 64-bit address arithmetic per refill.  (A buffer resource
+// costs 4 more SGPRs, which the kernel spills: 4 v_readlane per load.)
 struct GSrc {
   const uint32_t* __restrict__ p;
-  DQ_AI uint32_t operator[](uint32_t i) const { return p[i]; }
+  DQ_AI uint32_t operator[](uint32_t i) const {
+    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(p) + (i << 2));
+  }
 };
 
 template <class S>
@@ -230,7 +235,7 @@ DQ_AI void br_init(BitR& r, const S& W, uint32_t bitpos) {
 template <class S>
 DQ_AI void br_refill(BitR& r, const S& W) {
   const bool need = r.bc <= 32;
-  r.bb |= need ? (uint64_t)r.nw << r.bc : 0ull;
+  r.bb |= (uint64_t)(need ? r.nw : 0u) << r.bc;  // one 32-bit select instead of a 64-bit one
   r.bc += need ? 32u : 0u;
   r.wp += need ? 1u : 0u;
   r.nw = W[r.wp];
@@ -366,9 +371,11 @@ DQ_AI int run_seg(const S& W, const LdsI& L, uint32_t start, uint32_t sB,
   // written branch-free, the step that crosses none stores to the lane's dummy word (wsum is
   // dead during the speculative pass; `small` may hold the per-lane arrays)
   uint32_t* const dummy = const_cast<uint32_t*>(L.scratch) + (tid_fresh() & 15);
+  uint32_t* ckp = ck;  // checkpoint j (advanced, not multiplied out)
   for (;;) {
     const bool cross = p >= thr;
-    *(cross ? ck + j * ckstride : dummy) = ((p - sB) << 16) | (uint32_t)cnt;
+    *(cross ? ckp : dummy) = ((p - sB) << 16) | (uint32_t)cnt;
+    ckp += cross ? ckstride : 0;
     j += cross ? 1 : 0;
     thr = cross ? (j < NCK ? thr + CKI : 0xffffffffu) : thr;
     if (p >= sE || p >= endbits) {
@@ -403,6 +410,7 @@ DQ_AI int run_redo(const S& W, const LdsI& L, uint32_t s0, uint32_t sB,
   int f;
   uint32_t thr = ck ? sB + CKI : 0xffffffffu;
   uint32_t cur = ck ? ck[0] : 0xffffffffu;
+  const uint32_t* ckq = ck;  // checkpoint min(j, NCK - 1)
   int j = 0;
   for (;;) {
     const uint32_t p = br_pos(r);
@@ -423,7 +431,8 @@ DQ_AI int run_redo(const S& W, const LdsI& L, uint32_t s0, uint32_t sB,
       break;
     }
     j += cross ? 1 : 0;
-    const uint32_t nxt = ck ? ck[min(j, NCK - 1) * ckstride] : 0xffffffffu;
+    ckq += cross && j < NCK ? ckstride : 0;
+    const uint32_t nxt = ck ? *ckq : 0xffffffffu;
     thr = cross ? (j < NCK ? thr + CKI : 0xffffffffu) : thr;
     cur = cross ? (j < NCK ? nxt : 0xffffffffu) : cur;
     uint32_t len = 0, dist = 0, lit2;
@@ -967,37 +976,45 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       __syncthreads();
       // code-length code: 7-bit table, one entry per thread (canonical decode over 19 lengths)
       if (t < 128) {
-        int cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         uint8_t cl[19];
 #pragma unroll
         for (int s = 0; s < 19; s++) cl[s] = L.u.d.x.h.clen[s];
+        // length counts packed 8 bits per length: 0-3 in pk[0], 4-7 in pk[1]
+        uint32_t pk[2] = {0u, 0u};
 #pragma unroll
-        for (int s = 0; s < 19; s++)
-#pragma unroll
-          for (int l = 1; l <= 7; l++) cnt[l] += cl[s] == l;
-        int left = 1, code = 0, first = 0;
+        for (int s = 0; s < 19; s++) {
+          const uint32_t inc = 1u << (8 * (cl[s] & 3));
+          pk[0] += cl[s] < 4 ? inc : 0u;
+          pk[1] += cl[s] >= 4 ? inc : 0u;
+        }
+        // the codes of lengths 1..7 occupy consecutive left-aligned ranges: the length of index
+        // rv is 1 + the number of range ends at or below it (as root_entry), its rank among that
+        // length's codes follows from the length's first code
+        int left = 1, code = 0, len = 1, first_l = 0;
         bool ok = true;
-        uint16_t ent = 0;
-        const uint32_t rv = bitrev((uint32_t)t, 7);
+        const int rv = (int)bitrev((uint32_t)t, 7);
 #pragma unroll
         for (int l = 1; l <= 7; l++) {
-          left = (left << 1) - cnt[l];
-          if (left < 0) ok = false;
-          first = code;
-          code = (code + cnt[l]) << 1;
-          const int c = (int)(rv >> (7 - l));
-          if (ent == 0 && c - first >= 0 && c - first < cnt[l]) {
-            int k = c - first, s2 = 0;
-#pragma unroll
-            for (int s = 0; s < 19; s++)
-              if (cl[s] == l) {
-                if (k == 0) s2 = s;
-                k--;
-              }
-            ent = (uint16_t)((s2 << 3) | l);
-          }
+          const int c = (int)((pk[l >> 2] >> (8 * (l & 3))) & 0xffu);
+          left = (left << 1) - c;
+          ok = ok && left >= 0;
+          first_l = len == l ? code : first_l;
+          code += c;
+          len += (code << (7 - l)) <= rv ? 1 : 0;  // end of the length-l range
+          code <<= 1;
         }
-        if (left != 0) ok = false;  // the code-length code must be complete
+        ok = ok && left == 0;  // the code-length code must be complete
+        uint16_t ent = 0;
+        if (len <= 7) {  // the k-th symbol of length len (one pass, no divergence over lengths)
+          int k = (rv >> (7 - len)) - first_l, s2 = 0;
+#pragma unroll
+          for (int s = 0; s < 19; s++) {
+            const bool is = cl[s] == len;
+            s2 = is && k == 0 ? s : s2;
+            k -= is ? 1 : 0;
+          }
+          ent = (uint16_t)((s2 << 3) | len);
+        }
         L.u.d.x.h.clt[t] = ent;
         if (t == 0 && !ok) set_err(L, ST_BAD_TABLE);
       }
