@@ -263,7 +263,7 @@ DQ_AI uint32_t load_desc(const LdsI& L, int a) {
 // Second-level / canonical lookup for a root entry that is not a code.  SLOW = false (no E_SLOW
 // entry in this deflate block's tables, M_SLOW): one read, with no nested branch -- a "no code"
 // root entry (0: only in an incomplete code, which has no long codes) reads the first entry of the
-// zero-filled, unused second-level area, so it still decodes as an invalid code.
+// unused second-level area, an invalid-code sentinel (build_tables).
 template <bool SLOW>
 DQ_AI uint32_t ll_second(const LdsI& L, uint32_t e, uint32_t bb) {
   const uint32_t sb = (e >> 4) & 7;
@@ -321,7 +321,10 @@ DQ_AI bool dsym(BitR& r, const S& W, const LdsI& L, uint32_t p, uint32_t lim,
   dist = (__builtin_amdgcn_ubfe(e2, 12, 2) << __builtin_amdgcn_ubfe(e2, 8, 4)) + 1u +
          __builtin_amdgcn_ubfe(bb, nb2, dx);
   br_take(r, is_m ? nb2 + dx : 0u);
-  const bool stop = nb == 0 || (e & 0xFEF0u) == 0xF810u || (is_m && (nb2 == 0 || (e2 & 0x4000u)));
+  // SLOW = false: a code-less index reads the invalid sentinels build_tables leaves at the first
+  // second-level entries, so no entry here has code length 0
+  const bool stop = (SLOW && nb == 0) || (e & 0xFEF0u) == 0xF810u ||
+                    (is_m && ((SLOW && nb2 == 0) || (e2 & 0x4000u)));
   if (stop) {  // rare: EOB (an M entry, so the distance bits taken above are not the stream's)
     const bool eob = nb != 0 && (e & 0xFFF0u) == LL_EOB;
     len = eob ? p + nb : 0xffffffffu;
@@ -372,18 +375,19 @@ DQ_AI int run_seg(const S& W, const LdsI& L, uint32_t start, uint32_t sB,
   // dead during the speculative pass; `small` may hold the per-lane arrays)
   uint32_t* const dummy = const_cast<uint32_t*>(L.scratch) + (tid_fresh() & 15);
   uint32_t* ckp = ck;  // checkpoint j (advanced, not multiplied out)
+  const uint32_t sEe = min(sE, endbits);  // one compare (one branch) for both ends
   for (;;) {
     const bool cross = p >= thr;
     *(cross ? ckp : dummy) = ((p - sB) << 16) | (uint32_t)cnt;
     ckp += cross ? ckstride : 0;
     j += cross ? 1 : 0;
     thr = cross ? (j < NCK ? thr + CKI : 0xffffffffu) : thr;
-    if (p >= sE || p >= endbits) {
+    if (p >= sEe) {
       *Ep = (int32_t)p;
       f = p >= sE ? F_EXIT : F_END;
       break;
     }
-    if (dsym<SLOW>(r, W, L, p, min(min(thr, sE), endbits), len, dist, lit2, m)) {
+    if (dsym<SLOW>(r, W, L, p, min(thr, sEe), len, dist, lit2, m)) {
       *Ep = (int32_t)(len != 0xffffffffu ? len : p);
       f = len != 0xffffffffu ? F_EOB : F_ERR;
       break;
@@ -411,6 +415,7 @@ DQ_AI int run_redo(const S& W, const LdsI& L, uint32_t s0, uint32_t sB,
   uint32_t thr = ck ? sB + CKI : 0xffffffffu;
   uint32_t cur = ck ? ck[0] : 0xffffffffu;
   const uint32_t* ckq = ck;  // checkpoint min(j, NCK - 1)
+  const uint32_t sEe = min(sE, endbits);
   int j = 0;
   for (;;) {
     const uint32_t p = br_pos(r);
@@ -418,7 +423,7 @@ DQ_AI int run_redo(const S& W, const LdsI& L, uint32_t s0, uint32_t sB,
     // for the segment end, the data end and a merge; the threshold update is branch-free)
     const bool cross = p >= thr;
     const bool merge = cross && (cur >> 16) == p - sB;
-    if (p >= sE || p >= endbits || merge) {
+    if (p >= sEe || merge) {
       if (merge) {
         *Ep = se >> 3;
         f = se & 7;
@@ -437,7 +442,7 @@ DQ_AI int run_redo(const S& W, const LdsI& L, uint32_t s0, uint32_t sB,
     cur = cross ? (j < NCK ? nxt : 0xffffffffu) : cur;
     uint32_t len = 0, dist = 0, lit2;
     bool m;
-    if (dsym<SLOW>(r, W, L, p, min(min(thr, sE), endbits), len, dist, lit2, m)) {
+    if (dsym<SLOW>(r, W, L, p, min(thr, sEe), len, dist, lit2, m)) {
       *Ep = (int32_t)(len != 0xffffffffu ? len : p);
       f = len != 0xffffffffu ? F_EOB : F_ERR;
       break;
@@ -462,12 +467,13 @@ DQ_AI void emit_seg(const S& W, LdsI& L, uint32_t start, uint32_t target,
   lds8* const dummy = (lds8*)dummy32;
   BitR r;
   br_init(r, W, start);
+  const uint32_t te = min(target, endbits);
   for (;;) {
     const uint32_t q = br_pos(r);
-    if (q >= target || q >= endbits || p >= isize) return;
+    if (q >= te || p >= isize) return;
     uint32_t len = 0, dist = 0, lit2;
     bool m;
-    const bool stop = dsym<SLOW>(r, W, L, q, min(target, endbits), len, dist, lit2, m);
+    const bool stop = dsym<SLOW>(r, W, L, q, te, len, dist, lit2, m);
     const bool far = m && (int32_t)dist > p;  // a distance before the block's first byte
     if (stop || far) {  // one exit branch: EOB / bad code (accounted for by the rounds) or far
       if (!stop) set_err(L, ST_BAD_DIST);
@@ -586,8 +592,11 @@ DQ_AI uint16_t root_entry(const LdsI& L, const HuffCanon& h, const uint16_t* end
 // Litlen symbols are handled by threads 0..319 (waves 0-4), distance symbols by wave 5.
 DQ_AI void build_tables(LdsI& L, int nlen, int ndist) {
   const int t = tid_fresh(), lane = t & 63, wv = t >> 6;
-  for (int i = T_LSUB + t; i < T_DROOT; i += WG) L.u.d.T[i] = 0;  // second-level tables (the
-  for (int i = T_DSUB + t; i < T_END; i += WG) L.u.d.T[i] = 0;    // roots are written whole)
+  // second-level tables (the roots are written whole); their first entries are invalid-code
+  // sentinels (code length 1), which a complete code's first table overwrites: only an incomplete
+  // code (no long codes) has code-less root indices, and those read them (ll_second / d_second)
+  for (int i = T_LSUB + t; i < T_DROOT; i += WG) L.u.d.T[i] = i == T_LSUB ? (uint16_t)(LL_BAD | 1u) : 0;
+  for (int i = T_DSUB + t; i < T_END; i += WG) L.u.d.T[i] = i == T_DSUB ? (uint16_t)0x4001u : 0;
   const bool isl = t < 320, isd = t >= 320 && t < 352;
   const int sym = isl ? t : t - 320;
   const int len = isl ? (sym < nlen ? L.u.d.x.h.lens[sym] : 0)

@@ -296,3 +296,92 @@ def test_gpu_inflate_litlen_slow_path():
     assert len(b["voffset"]) == len(ref) == 490
     assert np.array_equal(b["voffset"], ref["voffset"])
     assert np.array_equal(b["hash"], ref["hash"])
+
+
+# ---- an incomplete distance code: a single one-bit code (symbol 14: distances 129..192, 6 extra
+# bits), which zlib's inflate accepts (inflate_table: an incomplete code is allowed only as one
+# code of length 1).  Half of the 8-bit distance root indices have no code: the kernel's common
+# path sends them to the invalid-code sentinel of the unused second-level area (dq_inflate3.hip
+# build_tables), so a stream that uses one must fail like zlib ("invalid distance code").
+D_ONE = [0] * 14 + [1] + [0] * 15
+
+
+def deflate_one_distance(data: bytes, d: int, bad: bool = False) -> bytes:
+    """One final dynamic block of `data` with LL_LENS and D_ONE: matches at distance d where the
+    bytes repeat (<= 42 long), literals elsewhere.  bad: the first match's distance code is the
+    code-less bit 1."""
+    llc = _canonical(LL_LENS)
+    w = _Writer()
+    w.bits(1, 1)
+    w.bits(2, 2)
+    w.bits(286 - 257, 5)
+    w.bits(30 - 1, 5)
+    w.bits(19 - 4, 4)
+    order = [16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15]
+    cl = [4 if s < 16 else 0 for s in range(19)]
+    for s in order:
+        w.bits(cl[s], 3)
+    clc = _canonical(cl)
+    for ln in LL_LENS + D_ONE:
+        w.code(clc[ln], 4)
+    assert DBASE[14] <= d < DBASE[15]
+    i, first = 0, True
+    while i < len(data):
+        n = 0
+        while d <= i and n < 42 and i + n < len(data) and data[i + n] == data[i + n - d]:
+            n += 1
+        if n >= 3:
+            ls = max(j for j in range(17) if LBASE[j] <= n)
+            w.code(llc[257 + ls], LL_LENS[257 + ls])
+            w.bits(n - LBASE[ls], LEXT[ls])
+            w.bits(1 if (bad and first) else 0, 1)  # the one distance code is the bit 0
+            w.bits(d - DBASE[14], DEXT[14])
+            first = False
+            i += n
+        else:
+            w.code(llc[data[i]], LL_LENS[data[i]])
+            i += 1
+    w.code(llc[256], LL_LENS[256])
+    return w.bytes()
+
+
+def one_distance_bam(bad=False):
+    r = synth.generate(50, seed=33, nthreads=2)
+    u = B.inflate_all(r.bam)
+    head = u[:B.header_len(u)]
+    rec = B.make_record(0, 5000, b"r", 58)
+    body = rec * 450
+    deflated = deflate_one_distance(body, len(rec), bad)
+    hdr = b"\x1f\x8b\x08\x04\x00\x00\x00\x00\x00\xff\x06\x00BC\x02\x00"
+    m = hdr + struct.pack("<H", 18 + len(deflated) + 8 - 1) + deflated
+    m += struct.pack("<II", zlib.crc32(body) & 0xffffffff, len(body))
+    return member(head, 6) + m + member(rec * 40, 6) + B.EOF_BLOCK, head + body + rec * 40, deflated
+
+
+def test_one_distance_fixture():
+    bam, u, deflated = one_distance_bam()
+    assert zlib.decompress(deflated, -15) == u[B.header_len(u):][:58050]
+    assert B.inflate_all(bam) == u
+    _, _, bad = one_distance_bam(bad=True)
+    with pytest.raises(zlib.error, match="invalid distance code"):
+        zlib.decompress(bad, -15)
+
+
+@pytest.mark.gpu
+def test_gpu_inflate_incomplete_distance_code():
+    from disq_amd import _lib
+    bam, u, _ = one_distance_bam()
+    split = 8 * 1024
+    with _lib.Context(split_size=split, verify_crc=True, device=0) as c:
+        c.open_bytes(bam)
+        b = c.read(with_raw=False)
+        got = c.inflated()
+    assert np.array_equal(got, np.frombuffer(u, np.uint8))
+    ref = np.concatenate(O.OracleBam(bam).read_partitions(split))
+    assert len(b["voffset"]) == len(ref) == 490
+    assert np.array_equal(b["hash"], ref["hash"])
+    bad, _, _ = one_distance_bam(bad=True)
+    with _lib.Context(split_size=split, verify_crc=True, device=0) as c:
+        c.open_bytes(bad)
+        with pytest.raises(_lib.DqError):
+            c.run_resident()
