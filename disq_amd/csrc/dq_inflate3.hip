@@ -355,15 +355,23 @@ DQ_AI int run_seg(const S& W, const LdsI& L, uint32_t start, uint32_t sB,
   uint32_t p = br_pos(r);
   uint32_t len = 0, dist = 0, lit2;
   bool m;
-  // warm-up: to the first symbol boundary >= sB, nothing counted
-  while (p < sB) {
-    if (p >= endbits || dsym<SLOW>(r, W, L, p, min(sB, endbits), len, dist, lit2, m)) {
-      *Ep = (int32_t)(p < endbits && len != 0xffffffffu ? len : p);
+  // warm-up: to the first symbol boundary >= sB, nothing counted (one compare per step: the
+  // data end is folded into the bound and tested once after the loop)
+  const uint32_t sBe = min(sB, endbits);
+  while (p < sBe) {
+    if (dsym<SLOW>(r, W, L, p, sBe, len, dist, lit2, m)) {
+      *Ep = (int32_t)(len != 0xffffffffu ? len : p);
       *Bp = -1;
       *cntp = 0;
       return F_DEAD;
     }
     p = br_pos(r);
+  }
+  if (p < sB) {  // the data ended first
+    *Ep = (int32_t)p;
+    *Bp = -1;
+    *cntp = 0;
+    return F_DEAD;
   }
   const int32_t B = (int32_t)p;
   int32_t cnt = 0;
@@ -532,44 +540,42 @@ DQ_AI int wave_incl_max(int v) {  // values >= -1
 }
 DQ_AI uint64_t lanes_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
 
-// Canonical description of one alphabet from the per-wave length counts (one thread; the
-// W * 15 count reads are independent and issued together).  Also stores the number of codes no
-// longer than the root (q0) and of all codes (qn).  Returns 0, or ST_BAD_TABLE for an
-// over-subscribed or (except a single code) incomplete code.
+// Canonical description of one alphabet from the per-wave length counts, by one whole wave: lane
+// l (1..15) sums its length's count over the waves, and two wave scans give the sorted-list offset
+// (a sum of the counts below l) and the first code, code_l = sum_{k<l} cnt_k << (l - k), as
+// (sum_{k<l} cnt_k << (16 - k)) >> (16 - l) -- exact: every term is a multiple of 2^(16-l).  The
+// Kraft balance left_l = 2^l - (code_l + cnt_l) is the serial recurrence left = 2 left - cnt in
+// closed form.  Also stores the number of codes no longer than the root (q0) and of all codes
+// (qn).  Returns (in every lane) 0, or ST_BAD_TABLE for an over-subscribed or (except a single
+// code) incomplete code.
 template <int W0, int NW, int R>
 DQ_AI int canon_from_counts(LdsI& L, HuffCanon& h, uint16_t* end, int32_t* q0p, int32_t* qnp) {
-  uint32_t pk[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // 16-bit lanes: no carries (<= 320 symbols)
+  const int l = tid_fresh() & 63;
+  const bool in = l >= 1 && l <= 15;
+  uint32_t pk = 0;  // 16-bit fields: no carries (<= 320 symbols)
 #pragma unroll
-  for (int w = W0; w < W0 + NW; w++)
-#pragma unroll
-    for (int j = 0; j < 8; j++) pk[j] += L.u.d.x.h.cntp[w][j];
-  int cnt[16];
-#pragma unroll
-  for (int l = 1; l <= 15; l++) cnt[l] = (int)((pk[l >> 1] >> (16 * (l & 1))) & 0xffffu);
-  int left = 1, maxl = 0, q0 = 0;
-  uint32_t code = 0, off = 0;
-  bool over = false;
-  h.first[0] = 0;
-  h.count[0] = 0;
-  h.offs[0] = 0;
-#pragma unroll
-  for (int l = 1; l <= 15; l++) {
-    const int c = cnt[l];
-    left = (left << 1) - c;
-    over = over || left < 0;
-    maxl = c ? l : maxl;
+  for (int w = W0; w < W0 + NW; w++) pk += in ? L.u.d.x.h.cntp[w][l >> 1] : 0u;
+  const int c = in ? (int)((pk >> (16 * (l & 1))) & 0xffffu) : 0;
+  const int offi = wave_incl_scan(c, l);          // codes of lengths <= l
+  const int tt = in ? c << (16 - l) : 0;
+  const int code = in ? (int)((uint32_t)(wave_incl_scan(tt, l) - tt) >> (16 - l)) : 0;
+  const int left = in ? (1 << l) - (code + c) : 0;
+  const uint64_t over = __ballot(in && left < 0);
+  const uint64_t used = __ballot(c > 0);
+  const int maxl = used ? 63 - __clzll(used) : 0;
+  const int left15 = __builtin_amdgcn_readlane(left, 15);
+  if (l < 16) {
     h.first[l] = (uint16_t)code;
     h.count[l] = (uint16_t)c;
-    h.offs[l] = (uint16_t)off;
-    if (l <= R) end[l] = (uint16_t)((code + (uint32_t)c) << (R - l));
-    off += c;
-    if (l == R) q0 = (int)off;
-    code = (code + c) << 1;
+    h.offs[l] = (uint16_t)(offi - c);
+    if (in && l <= R) end[l] = (uint16_t)((code + c) << (R - l));
   }
-  *q0p = q0;
-  *qnp = (int)off;
+  if (l == 0) {
+    *q0p = __builtin_amdgcn_readlane(offi, R);
+    *qnp = __builtin_amdgcn_readlane(offi, 15);
+  }
   if (over) return ST_BAD_TABLE;
-  if (maxl > 0 && left > 0 && maxl != 1) return ST_BAD_TABLE;  // zlib inflate_table rule
+  if (maxl > 0 && left15 > 0 && maxl != 1) return ST_BAD_TABLE;  // zlib inflate_table rule
   return 0;
 }
 
@@ -620,13 +626,13 @@ DQ_AI void build_tables(LdsI& L, int nlen, int ndist) {
                                 (((c[j >> 1] >> (16 * (j & 1) + 8)) & 0xffu) << 16);
   }
   __syncthreads();
-  if (t == 0) {
+  if (wv == 0) {  // whole waves (DPP scans)
     const int e = canon_from_counts<0, 5, LR>(L, L.u.d.hl, L.u.d.lend, &L.misc[M_LQ0], &L.misc[M_LQN]);
-    if (e) set_err(L, e);
+    if (e && lane == 0) set_err(L, e);
   }
-  if (t == 320) {
+  if (wv == 5) {
     const int e = canon_from_counts<5, 1, DR>(L, L.u.d.hd, L.u.d.dend, &L.misc[M_DQ0], &L.misc[M_DQN]);
-    if (e) set_err(L, e);
+    if (e && lane == 0) set_err(L, e);
   }
   __syncthreads();
   if (L.misc[M_ERR]) return;
