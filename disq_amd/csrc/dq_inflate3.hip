@@ -529,6 +529,15 @@ DQ_AI int wave_incl_or(int v) {
   v |= __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
   return v;
 }
+DQ_AI uint32_t wave_incl_xor(uint32_t v) {
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+  return v;
+}
 DQ_AI int wave_incl_max(int v) {  // values >= -1
   v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x111, 0xf, 0xf, false));
   v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x112, 0xf, 0xf, false));
@@ -1474,13 +1483,29 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     }
     lines_done = lines_to;
   }
+  // the CRC's constants, loaded ahead of the U tail stores and the barrier below (their latency
+  // overlaps them): this thread's two table words, its slice's shift, and for thread 0 the
+  // initial-value term and the gzip trailer
+  uint32_t ct0 = 0, ct1 = 0, cshift = 0, cinit = 0, cwant = 0;
+  if (verify_crc) {
+    ct0 = (&c_crc4[0][0])[t];
+    ct1 = (&c_crc4[0][0])[t + WG];
+    cshift = c_slice_shift[WG - 1 - t];
+    if (t == 0) {
+      cinit = crc_init[isize];  // x^(8 isize) * 0xffffffff mod P
+      const uint8_t* tr = C + cpos + csize - 8;
+      cwant = (uint32_t)tr[0] | ((uint32_t)tr[1] << 8) | ((uint32_t)tr[2] << 16) | ((uint32_t)tr[3] << 24);
+    }
+  }
+  static_assert(2 * WG == 1024, "two CRC table words per thread");
   for (int x = t; x < head; x += WG) dstU[x] = O[x];
   for (int x = head + 16 * lines_done + t; x < isize; x += WG) dstU[x] = O[x];
   TST(6);
   // ---- 7. CRC32: thread t hashes the CRC_SL-byte slice ending (511 - t) * CRC_SL bytes before isize
   if (verify_crc) {
     __syncthreads();  // the resolve scratch is dead: the CRC tables reuse it
-    for (int i = t; i < 1024; i += WG) (&L.u.crc4[0][0])[i] = (&c_crc4[0][0])[i];
+    (&L.u.crc4[0][0])[t] = ct0;
+    (&L.u.crc4[0][0])[t + WG] = ct1;
     __syncthreads();
     const int32_t e = isize - (WG - 1 - t) * CRC_SL;
     const int32_t s0 = max(0, e - CRC_SL);
@@ -1494,20 +1519,16 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
              L.u.crc4[0][v >> 24];
       }
       while (x < e) cr = L.u.crc4[0][(cr ^ O[x++]) & 0xff] ^ (cr >> 8);
-      cr = gf2_mulmod(c_slice_shift[WG - 1 - t], cr);
+      cr = gf2_mulmod(cshift, cr);
     }
-    for (int o = 32; o >= 1; o >>= 1) cr ^= __shfl_xor(cr, o, 64);
-    if (lane == 0) L.wsum[wv] = (int32_t)cr;
+    cr = wave_incl_xor(cr);  // DPP: lane 63 holds the wave's xor
+    if (lane == 63) L.wsum[wv] = (int32_t)cr;
     __syncthreads();
     if (t == 0) {
       uint32_t x = 0;
       for (int w = 0; w < WG / 64; w++) x ^= (uint32_t)L.wsum[w];
-      const uint32_t init = crc_init[isize];  // x^(8 isize) * 0xffffffff mod P
-      const uint32_t crc = (x ^ init) ^ 0xffffffffu;
-      const uint8_t* tr = C + cpos + csize - 8;
-      const uint32_t want = (uint32_t)tr[0] | ((uint32_t)tr[1] << 8) | ((uint32_t)tr[2] << 16) |
-                            ((uint32_t)tr[3] << 24);
-      if (crc != want) status[b] = ST_CRC;
+      const uint32_t crc = (x ^ cinit) ^ 0xffffffffu;
+      if (crc != cwant) status[b] = ST_CRC;
     }
   }
   TST(7);
@@ -1600,7 +1621,8 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
   if (ngrid <= 0) return;
   static const uint32_t ov = getenv("DQ_OV") ? (uint32_t)atoi(getenv("DQ_OV")) : OV_DEFAULT;
   static const uint32_t sflags =
-      (getenv("DQ_STORE") ? (uint32_t)atoi(getenv("DQ_STORE")) : 2u) |
+      (getenv("DQ_STORE") ? (uint32_t)atoi(getenv("DQ_STORE")) & 3u : 2u) |
+
       (getenv("DQ_NDEC") ? (uint32_t)(atoi(getenv("DQ_NDEC")) & 1023) << 8 : 0u) |
       (getenv("DQ_SEGBITS") ? (uint32_t)(atoi(getenv("DQ_SEGBITS")) & 1023) << 20 : 0u);
   // DQ_CFG="nb,g" (tuning experiments: 4,1 default, 2,1 or 1,4); a function-local static const is
