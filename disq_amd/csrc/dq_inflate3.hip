@@ -1622,7 +1622,6 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
   static const uint32_t ov = getenv("DQ_OV") ? (uint32_t)atoi(getenv("DQ_OV")) : OV_DEFAULT;
   static const uint32_t sflags =
       (getenv("DQ_STORE") ? (uint32_t)atoi(getenv("DQ_STORE")) & 3u : 2u) |
-
       (getenv("DQ_NDEC") ? (uint32_t)(atoi(getenv("DQ_NDEC")) & 1023) << 8 : 0u) |
       (getenv("DQ_SEGBITS") ? (uint32_t)(atoi(getenv("DQ_SEGBITS")) & 1023) << 20 : 0u);
   // DQ_CFG="nb,g" (tuning experiments: 4,1 default, 2,1 or 1,4); a function-local static const is
