@@ -21,6 +21,8 @@
 //     after a CR (fills: B0 at U0 + 4096 m; later blocks at U_b, then U_b + 1 + 4096 m).
 #include "dq_internal.h"
 
+#include <algorithm>
+
 namespace dq {
 namespace {
 
@@ -249,7 +251,24 @@ __global__ void text_plan_kernel(const Cand* __restrict__ cand, const int64_t* _
 }
 
 // Values of the listed lines: offset, length (terminator excluded, BOM stripped from line 0 when
-// flagged), hash of the value bytes, keep flag (drop '#' lines when asked).
+// flagged), hash of the value bytes, keep flag (drop '#' lines when asked).  The hash is the
+// record hash of DESIGN.md section 4 (8-byte little-endian words, zero padded, keyed by index):
+// a line of up to TV_LONG bytes is hashed by its thread from aligned dword loads (one byte-align
+// per half word); a longer line is left to text_long_hash_kernel, a wave per line.
+constexpr int64_t TV_LONG = 2048;
+__device__ inline uint32_t tv_funnel(uint32_t lo, uint32_t hi, uint32_t sh) {  // (hi:lo) >> 8 sh
+  return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+// word k of the value at byte a (len bytes), zero padded past len
+__device__ inline uint64_t tv_word(const uint32_t* __restrict__ U32, int64_t a, int64_t len, int64_t k) {
+  const int64_t wi = (a >> 2) + 2 * k;
+  const uint32_t sh = (uint32_t)(a & 3);
+  const uint32_t w0 = U32[wi], w1 = U32[wi + 1], w2 = U32[wi + 2];
+  uint64_t w = ((uint64_t)tv_funnel(w1, w2, sh) << 32) | tv_funnel(w0, w1, sh);
+  const int64_t rem = len - 8 * k;
+  if (rem < 8) w &= (1ull << (8 * rem)) - 1;
+  return w;
+}
 __global__ void text_values_kernel(const uint8_t* __restrict__ U, int64_t ulen,
                                    const int64_t* __restrict__ term, int64_t nterm,
                                    const int64_t* __restrict__ idx, int64_t n, int32_t bom,
@@ -273,16 +292,37 @@ __global__ void text_values_kernel(const uint8_t* __restrict__ U, int64_t ulen,
   vstart[t] = a;
   vlen[t] = (int32_t)len;
   keep[t] = (uint8_t)!(drop_hash && len > 0 && U[a] == '#');
+  if (len > TV_LONG) return;  // text_long_hash_kernel
+  const uint32_t* U32 = reinterpret_cast<const uint32_t*>(U);  // U: 256 bytes of slack past ulen
   uint64_t h = (uint64_t)len * DQ_K_LEN;
   const int64_t nw = (len + 7) / 8;
-  for (int64_t w = 0; w < nw; w++) {
-    uint64_t v = 0;
-    const int64_t rem = len - 8 * w;
-    const int nb = rem < 8 ? (int)rem : 8;
-    for (int b = 0; b < nb; b++) v |= (uint64_t)U[a + 8 * w + b] << (8 * b);
-    h += dq_mix64(v ^ ((uint64_t)(w + 1) * DQ_K_WORD));
-  }
+  for (int64_t w = 0; w < nw; w++) h += dq_mix64(tv_word(U32, a, len, w) ^ ((uint64_t)(w + 1) * DQ_K_WORD));
   hash[t] = dq_mix64(h);
+}
+
+// Lines longer than TV_LONG: one wave per line (a grid-stride over the lines' lengths), lane l
+// hashing words l, l + 64, ... (the word sum is order-free), summed across the wave.
+__global__ __launch_bounds__(256) void text_long_hash_kernel(const uint8_t* __restrict__ U,
+                                                             const int64_t* __restrict__ vstart,
+                                                             const int32_t* __restrict__ vlen,
+                                                             int64_t n, uint64_t* __restrict__ hash) {
+  const uint32_t* U32 = reinterpret_cast<const uint32_t*>(U);
+  const int lane = threadIdx.x & 63;
+  const int64_t nwave = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t t = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); t < n; t += nwave) {
+    const int64_t len = vlen[t];
+    if (len <= TV_LONG) continue;  // wave-uniform
+    const int64_t a = vstart[t];
+    uint64_t part = 0;
+    const int64_t nw = (len + 7) / 8;
+    for (int64_t w = lane; w < nw; w += 64) part += dq_mix64(tv_word(U32, a, len, w) ^ ((uint64_t)(w + 1) * DQ_K_WORD));
+    for (int o = 32; o >= 1; o >>= 1) {
+      const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)part, o, 64);
+      const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(part >> 32), o, 64);
+      part += ((uint64_t)hi << 32) | lo;
+    }
+    if (lane == 0) hash[t] = dq_mix64((uint64_t)len * DQ_K_LEN + part);
+  }
 }
 
 // Line values gathered into a compact byte buffer: one wave per line.
@@ -459,6 +499,9 @@ void launch_text_values(const uint8_t* U, int64_t ulen, const int64_t* term, int
   if (n <= 0) return;
   hipLaunchKernelGGL(text_values_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, U, ulen,
                      term, nterm, idx, n, bom, drop_hash, vstart, vlen, hash, keep);
+  const int64_t nwg = std::min<int64_t>((n + 3) / 4, 4096);  // 4 waves per workgroup
+  hipLaunchKernelGGL(text_long_hash_kernel, dim3((unsigned)nwg), dim3(256), 0, s, U, vstart, vlen, n,
+                     hash);
 }
 
 void launch_text_gather(const uint8_t* U, const int64_t* vstart, const int32_t* vlen,
