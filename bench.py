@@ -40,7 +40,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "decompressed BAM GB/s + reads/sec (whole node) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.29 TB/s measured copy)
-TRAFFIC_PROFILE = "r3ai_inflate_traffic_pmc.json"
+TRAFFIC_PROFILE = "r3aq_inflate_traffic_pmc.json"
 
 
 def log(*a):
@@ -394,8 +394,8 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
                 "traffic_src": traffic_src,
-                "pmc_src": "profiles/r3ai_inflate_pmc.txt (VALU busy 71 %, 56.4 % of wave cycles "
-                           "waiting, LDS bank conflicts 28.7 %)",
+                "pmc_src": "profiles/r3aq_inflate_pmc.txt (VALU busy 70 %, 56.5 % of wave cycles "
+                           "waiting, LDS bank conflicts 28.8 %)",
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_launch_ms": round(infl_avg, 3),
             },
