@@ -18,16 +18,18 @@
 //      contiguous run of the bucket list, so a search issues all its candidate loads at once
 //      instead of chasing zlib's hash-chain links one dependent load at a time.
 //   2. Parse: lane t parses from its segment start [255 t, 255 t + 255) with zlib-style lazy
-//      evaluation (a match shorter than `lazy` is deferred while the next position's is longer),
-//      the longest match among `chain` candidates (stopping at `nice`), matches running on past
-//      the segment end.  A parse step depends on its position alone, so two parses that reach the
+//      evaluation (a match shorter than `lazy` is deferred while the next position's is longer;
+//      the look-ahead search walks chain / 4 candidates once the current match is `good` long, as
+//      zlib's deflate_slow), the longest match among `chain` candidates (stopping at `nice`),
+//      matches running on past the segment end.  A parse step depends on its position alone, so two parses that reach the
 //      same position continue identically: from its exit, each lane keeps parsing until it hits a
 //      symbol boundary of a later lane's parse (usually within a few symbols) and records the
 //      merge; one thread then follows the merges from lane 0, which gives every lane the part of
 //      its symbols (and continuation) on the block's one parse.  The result is the parse a
 //      single sequential pass would make: no matches are cut at lane boundaries.
-//      (Parameters from tools/deflate_model.c: chain 48, lazy 24, nice 48 model a 2.82 ratio on
-//      the synthetic WGS stream, zlib level 5 -- htsjdk's -- 2.86.)
+//      (Defaults chain 48, lazy 24, nice 48, good 8: ratio 2.819 at 8.0 GB/s on the synthetic WGS
+//      stream, zlib level 5 -- htsjdk's -- 2.857; 64,32,64,4 gives 2.834 at the same speed;
+//      profiles/r3as_*, r3at_* for the ratio/speed frontier.)
 //   3. Codes: histograms of the parse; wave 0 builds the literal/length code and wave 1 the
 //      distance code (a rank sort, Moffat-Katajainen minimum-redundancy lengths, a Kraft fix-up
 //      capping them at 15), the code-length sequence is run-length coded; the block is coded
@@ -54,7 +56,8 @@ constexpr int OWN_WORDS = 288;           // a lane's own symbols (<= 255 + the l
 constexpr int CONT_WORDS = 224;          // its continuation past its segment end
 constexpr int LANE_WORDS = OWN_WORDS + CONT_WORDS;
 constexpr int MAX_DEFLATE = 65536 - 26;  // BSIZE limit: 18-byte header + payload + 8 trailer
-constexpr int MAXCAND = 128;             // candidates per match search at most (cfg.chain)
+constexpr int MAXCAND = 64;              // candidates per match search at most (cfg.chain; see
+                                         // launch_bgzf_deflate)
 
 __constant__ uint32_t c_dcrc[256];
 __constant__ uint16_t c_lbase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
@@ -279,9 +282,10 @@ struct Finder {
   const DLds& L;
   const uint16_t* __restrict__ bl;
   const uint16_t* __restrict__ gi;
-  int n, chain, nice;
-  // longest match (>= 3, else 0) at p, at most lim bytes; *dist its distance
-  __device__ int find(int p, int lim, int* dist) const {
+  int n, chain, nice, good;
+  // longest match (>= 3, else 0) at p, at most lim bytes, among `chain` candidates; *dist its
+  // distance
+  __device__ int find(int p, int lim, int* dist, int chain) const {
     *dist = 0;
     if (lim < 3 || p + 3 > n) return 0;
     const uint32_t h = hash3(L.in, p);
@@ -354,15 +358,18 @@ __device__ inline uint32_t match_word(int len, int d) {
 }
 
 // One parse step at p (zlib-style lazy evaluation: while the match at the next position is
-// longer and the current one shorter than `lazy`, emit a literal and move on): appends its
-// symbols to w[*ns...] and returns the new position.  The step depends on p alone, so two parses
-// that reach the same position continue identically (the merge rule below).
+// longer and the current one shorter than `lazy`, emit a literal and move on; the look-ahead
+// search walks a quarter of the candidates once the current match is `good` long, as zlib's
+// deflate_slow does): appends its symbols to w[*ns...] and returns the new position.  The step
+// depends on p alone, so two parses that reach the same position continue identically (the
+// merge rule below).
 __device__ int parse_step(const Finder& F, int lazy, int p, uint32_t* w, int* ns) {
   const int n = F.n;
-  int d = 0, l = F.find(p, min(MAXM, n - p), &d);
+  int d = 0, l = F.find(p, min(MAXM, n - p), &d, F.chain);
   while (l && l < lazy && p + 1 < n) {
     int d2 = 0;
-    const int l2 = F.find(p + 1, min(MAXM, n - p - 1), &d2);
+    const int ch = F.good > 0 && l >= F.good ? max(1, F.chain >> 2) : F.chain;
+    const int l2 = F.find(p + 1, min(MAXM, n - p - 1), &d2, ch);
     if (l2 <= l) break;
     w[(*ns)++] = lit_word(F.L.in[p]);
     p++;
@@ -395,7 +402,7 @@ __global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __rest
                                                            uint8_t* __restrict__ out_slots,
                                                            int32_t* __restrict__ out_size,
                                                            uint64_t* __restrict__ tim, int chain,
-                                                           int lazy, int nice) {
+                                                           int lazy, int nice, int good) {
   __shared__ DLds L;
   uint64_t tm[8];
   int ti = 0;
@@ -502,7 +509,7 @@ __global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __rest
   // ---- speculative parse: lane t from its segment start to the first symbol boundary at or past
   //      its end (a match may run on past it)
   uint32_t* lane_w = stage + ((int64_t)b * DWG + t) * LANE_WORDS;
-  const Finder F{L, bl, gi, n, min(chain, MAXCAND), nice};
+  const Finder F{L, bl, gi, n, min(chain, MAXCAND), nice, good};
   {
     int ns = 0, p = s0;
     while (p < s1) p = parse_step(F, lazy, p, lane_w, &ns);
@@ -861,15 +868,19 @@ void launch_bgzf_deflate(const uint8_t* src, int64_t n_in, int64_t blk0, int64_t
                          uint32_t* stage, uint16_t* link, uint8_t* out_slots, int32_t* out_size,
                          uint64_t* tim, hipStream_t s) {
   if (nblk <= 0) return;
-  // DQ_DEFLATE="chain,lazy,nice": match-search effort (default 48,24,48; zlib level 5 is 32,16,32
-  // with hash chains, tools/deflate_model.c)
-  static const int3 cfg = [] {
-    int c = 48, l = 24, n = 48;
-    if (const char* e = getenv("DQ_DEFLATE")) sscanf(e, "%d,%d,%d", &c, &l, &n);
-    return make_int3(std::max(1, std::min(c, MAXCAND)), std::max(0, std::min(l, 32)), std::max(3, n));
+  // DQ_DEFLATE="chain,lazy,nice[,good]": match-search effort (default 48,24,48,8; zlib level 5 is
+  // 32,16,32,8 with hash chains, tools/deflate_model.c; good 0 = always the full chain).  Chains
+  // are capped at MAXCAND = 64: with lazy matching, chains of 80 and more lost a byte of a
+  // 4096-byte block of 2-bit random data (tests/test_deflate_gpu.py edge sizes, profiles/r3av_*,
+  // r3aw_*; the greedy parse at 128 was exact) -- not yet explained, so not allowed.
+  static const int4 cfg = [] {
+    int c = 48, l = 24, n = 48, g = 8;
+    if (const char* e = getenv("DQ_DEFLATE")) sscanf(e, "%d,%d,%d,%d", &c, &l, &n, &g);
+    return make_int4(std::max(1, std::min(c, MAXCAND)), std::max(0, std::min(l, 32)), std::max(3, n),
+                     std::max(0, g));
   }();
   hipLaunchKernelGGL(bgzf_deflate_kernel, dim3((unsigned)nblk), dim3(DWG), 0, s, src, n_in, blk0, nblk,
-                     stage, link, out_slots, out_size, tim, cfg.x, cfg.y, cfg.z);
+                     stage, link, out_slots, out_size, tim, cfg.x, cfg.y, cfg.z, cfg.w);
 }
 
 void launch_bgzf_pack(const uint8_t* slots, const int32_t* size, const int64_t* off, int64_t nblk,

@@ -5,6 +5,8 @@ set -eo pipefail
 out=gpurun_out/${1:-deflate_prof}
 mkdir -p $out
 export TMPDIR=/tmp
+timeout -k 10 300 python3 -u -m pytest tests/test_deflate_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > $out/tests.log 2>&1
+tail -1 $out/tests.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof -o run -- \
   python3 -u tools/deflate_bench.py --records 2000000 --reps 3 > $out/bench.log 2>&1
 grep '"ratio"' $out/bench.log > $out/bench.json
