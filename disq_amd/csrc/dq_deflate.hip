@@ -27,9 +27,8 @@
 //      merge; one thread then follows the merges from lane 0, which gives every lane the part of
 //      its symbols (and continuation) on the block's one parse.  The result is the parse a
 //      single sequential pass would make: no matches are cut at lane boundaries.
-//      (Defaults chain 48, lazy 24, nice 48, good 8: ratio 2.819 at 8.0 GB/s on the synthetic WGS
-//      stream, zlib level 5 -- htsjdk's -- 2.857; 64,32,64,4 gives 2.834 at the same speed;
-//      profiles/r3as_*, r3at_* for the ratio/speed frontier.)
+//      (Defaults chain 96, lazy 32, nice 96, good 8: ratio 2.858 on the synthetic WGS stream, zlib
+//      level 5 -- htsjdk's -- 2.857; profiles/r3as_deflate_good_sweep.txt for the frontier.)
 //   3. Codes: histograms of the parse; wave 0 builds the literal/length code and wave 1 the
 //      distance code (a rank sort, Moffat-Katajainen minimum-redundancy lengths, a Kraft fix-up
 //      capping them at 15), the code-length sequence is run-length coded; the block is coded
@@ -56,8 +55,7 @@ constexpr int OWN_WORDS = 288;           // a lane's own symbols (<= 255 + the l
 constexpr int CONT_WORDS = 224;          // its continuation past its segment end
 constexpr int LANE_WORDS = OWN_WORDS + CONT_WORDS;
 constexpr int MAX_DEFLATE = 65536 - 26;  // BSIZE limit: 18-byte header + payload + 8 trailer
-constexpr int MAXCAND = 64;              // candidates per match search at most (cfg.chain; see
-                                         // launch_bgzf_deflate)
+constexpr int MAXCAND = 128;             // candidates per match search at most (cfg.chain)
 
 __constant__ uint32_t c_dcrc[256];
 __constant__ uint16_t c_lbase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
@@ -527,10 +525,20 @@ __global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __rest
     int pu = min(n, u * SEG);
     bool over = false;
     for (;;) {
-      if (u >= DWG || E >= n) {
+      if (E >= n) {
         u = DWG;
         k = 0;
         break;
+      }
+      if (u >= DWG || u * SEG >= n) {  // no later lane holds symbols: parse on to the end (these
+        if (nc > CONT_WORDS - 40) {    // empty lanes used to be skipped as "overrun", which ended
+          over = true;                 // the block one symbol short when E stopped just before n)
+          break;
+        }
+        int nn = OWN_WORDS + nc;
+        E = parse_step(F, lazy, E, lane_w, &nn);
+        nc = nn - OWN_WORDS;
+        continue;
       }
       const int nu = L.lane_nsym[u];
       const uint32_t* uw = stage + ((int64_t)b * DWG + u) * LANE_WORDS;
@@ -868,13 +876,12 @@ void launch_bgzf_deflate(const uint8_t* src, int64_t n_in, int64_t blk0, int64_t
                          uint32_t* stage, uint16_t* link, uint8_t* out_slots, int32_t* out_size,
                          uint64_t* tim, hipStream_t s) {
   if (nblk <= 0) return;
-  // DQ_DEFLATE="chain,lazy,nice[,good]": match-search effort (default 48,24,48,8; zlib level 5 is
-  // 32,16,32,8 with hash chains, tools/deflate_model.c; good 0 = always the full chain).  Chains
-  // are capped at MAXCAND = 64: with lazy matching, chains of 80 and more lost a byte of a
-  // 4096-byte block of 2-bit random data (tests/test_deflate_gpu.py edge sizes, profiles/r3av_*,
-  // r3aw_*; the greedy parse at 128 was exact) -- not yet explained, so not allowed.
+  // DQ_DEFLATE="chain,lazy,nice[,good]": match-search effort (default 96,32,96,8: htsjdk level 5's
+  // ratio on the WGS stream; 48,24,48,8 is 40 % faster at a 1.4 % lower ratio, profiles/r3as_*;
+  // zlib level 5 is 32,16,32,8 with hash chains, tools/deflate_model.c; good 0 = always the full
+  // chain)
   static const int4 cfg = [] {
-    int c = 48, l = 24, n = 48, g = 8;
+    int c = 96, l = 32, n = 96, g = 8;
     if (const char* e = getenv("DQ_DEFLATE")) sscanf(e, "%d,%d,%d,%d", &c, &l, &n, &g);
     return make_int4(std::max(1, std::min(c, MAXCAND)), std::max(0, std::min(l, 32)), std::max(3, n),
                      std::max(0, g));
