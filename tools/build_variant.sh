@@ -8,8 +8,9 @@ out=../_build/v_$name
 mkdir -p $out
 objs=()
 for f in *.hip; do
+  extra=""; [ $f = dq_inflate3.hip ] && extra="-mllvm -amdgpu-sched-strategy=max-ilp"  # as the Makefile
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function \
-    -munsafe-fp-atomics -I../../include $flags -c -o $out/${f%.hip}.o $f &
+    -munsafe-fp-atomics -I../../include $extra $flags -c -o $out/${f%.hip}.o $f &
   objs+=($out/${f%.hip}.o)
 done
 wait
