@@ -8,6 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 import threading
+import weakref
 
 import numpy as np
 
@@ -109,7 +110,7 @@ EXPORTS = ("dq_ctx_create", "dq_ctx_destroy", "dq_last_error", "dq_version", "dq
            "dq_text_open_path", "dq_text_run", "dq_text_read", "dq_text_batch_free",
            "dq_bgzf_compress", "dq_bgzf_compress_resident", "dq_bgzf_fetch",
            "dq_text_set_index", "dq_text_set_intervals", "dq_decode_file_multi",
-           "dq_set_export_arena")
+           "dq_set_export_arena", "dq_checked_report")
 
 _lib = None
 _lock = threading.Lock()
@@ -165,6 +166,7 @@ def lib():
         L.dq_debug_guess_all.argtypes = [vp, vp, C.c_int64, P(C.c_int64)]
         L.dq_batch_free.argtypes = [P(DqBatch)]
         L.dq_set_export_arena.argtypes = [vp, C.c_int64]
+        L.dq_checked_report.argtypes = [P(C.c_uint64)]
         L.dq_text_open_memory.argtypes = [vp, vp, C.c_int64]
         L.dq_text_open_path.argtypes = [vp, C.c_char_p]
         L.dq_text_run.argtypes = [vp, C.c_int32, P(DqStats)]
@@ -201,34 +203,51 @@ FIELDS = (("voffset", np.uint64), ("block_size", np.int32), ("ref_id", np.int32)
 
 
 class _BatchOwner:
-    """Frees a dq_batch once no numpy view of its arrays is left."""
+    """Frees a dq_batch once no numpy view of its arrays is left.  An arena batch's arrays live in
+    its context's pinned export arena (dq_set_export_arena): a context closed while such a batch is
+    still referenced hands its handle over (ctx_h), and the arena is freed with the last view."""
 
     def __init__(self, bp):
         self.bp = bp
+        self.ctx_h = None
 
     def __del__(self):
         try:
             lib().dq_batch_free(self.bp)
         except Exception:
             pass
+        if self.ctx_h:
+            try:
+                lib().dq_ctx_destroy(self.ctx_h)
+            except Exception:
+                pass
+            self.ctx_h = None
 
 
 _CT = {np.uint64: C.c_uint64, np.int64: C.c_int64, np.int32: C.c_int32, np.uint16: C.c_uint16,
        np.uint8: C.c_uint8}
 
 
-def batch_to_numpy(bp):
+def batch_to_numpy(bp, ctx=None):
     """The arrays of a dq_batch as numpy views of the library's memory (no copy: a batch of a
-    whole file is tens of GB); the batch is freed when the last view is gone."""
+    whole file is tens of GB); the batch is freed when the last view is gone.  The views of an
+    arena batch are read-only, and `ctx` refuses to overwrite or free its arena while any of them
+    is alive (Context._arena_guard)."""
     b = bp.contents
     owner = _BatchOwner(bp)
+    arena = bool(b.in_arena)
+    if arena and ctx is not None:
+        ctx._arena_ref = weakref.ref(owner)
 
     def view(ptr, n, dt):
         if not n or not ptr:
             return np.zeros(0, dt)
         ct = (_CT[dt] * n).from_address(C.cast(ptr, C.c_void_p).value)
         ct._owner = owner
-        return np.ctypeslib.as_array(ct)
+        a = np.ctypeslib.as_array(ct)
+        if arena:
+            a.flags.writeable = False
+        return a
     n = b.n_records
     out = {name: view(getattr(b, name), n, dt) for name, dt in FIELDS}
     out["raw"] = view(b.raw, b.raw_len, np.uint8) if (b.raw and b.raw_len) else None
@@ -255,10 +274,27 @@ class Context:
             self._h = None
             raise DqError(rc, msg)
         self._keep = None
+        self._arena_ref = None
+
+    def _arena_live(self):
+        r = self._arena_ref
+        return r() if r is not None else None
+
+    def _arena_guard(self, what):
+        """The library writes every batch of an arena context into the same pinned memory: refuse
+        a new batch (or a new arena) while the previous arena batch is still referenced."""
+        if self._arena_live() is not None:
+            raise DqError(DQ_EINVAL, f"{what}: the previous batch of this context lives in its "
+                          "export arena and is still referenced; drop it (or copy its arrays) "
+                          "before the next batch")
 
     def close(self):
         if self._h:
-            lib().dq_ctx_destroy(self._h)
+            owner = self._arena_live()
+            if owner is not None:  # views of the arena are alive: it goes with the last of them
+                owner.ctx_h = self._h
+            else:
+                lib().dq_ctx_destroy(self._h)
             self._h = None
 
     def __enter__(self):
@@ -301,6 +337,7 @@ class Context:
     def decode_chunk(self, path, vstart, vend, with_raw=True, traversal=None):
         """BamSource.getIterator (or createIndexIterator with a traversal) for one task: only the
         chunk's bytes -- or its .bai span -- are read (dq_decode_chunk[_filtered])."""
+        self._arena_guard("decode_chunk")
         bp = C.POINTER(DqBatch)()
         if traversal is None:
             check(self._h, lib().dq_decode_chunk(self._h, os.fsencode(path), vstart, vend,
@@ -309,7 +346,7 @@ class Context:
             t, keep = self._traversal(traversal)
             check(self._h, lib().dq_decode_chunk_filtered(self._h, os.fsencode(path), vstart, vend,
                                                           C.byref(t), int(with_raw), C.byref(bp)))
-        return batch_to_numpy(bp)
+        return batch_to_numpy(bp, self)
 
     def stats(self):
         st = DqStats()
@@ -487,6 +524,7 @@ class Context:
         return t, (r, s, e)
 
     def decode(self, vstart, vend, with_raw=True, traversal=None):
+        self._arena_guard("decode")
         bp = C.POINTER(DqBatch)()
         if traversal is None:
             check(self._h, lib().dq_decode(self._h, vstart, vend, int(with_raw), C.byref(bp)))
@@ -494,20 +532,22 @@ class Context:
             t, keep = self._traversal(traversal)
             check(self._h, lib().dq_decode_filtered(self._h, vstart, vend, C.byref(t),
                                                     int(with_raw), C.byref(bp)))
-        return batch_to_numpy(bp)
+        return batch_to_numpy(bp, self)
 
     def set_export_arena(self, nbytes):
         """dq_set_export_arena: later batches of this context land in `nbytes` of pinned host
         memory by DMA; an arena batch's arrays are valid until the next batch of the context
         (a streaming consumer's recycled buffers)."""
+        self._arena_guard("set_export_arena")
         check(self._h, lib().dq_set_export_arena(self._h, int(nbytes)))
 
     def read(self, with_raw=True, traversal=None):
+        self._arena_guard("read")
         bp = C.POINTER(DqBatch)()
         t, keep = self._traversal(traversal)
         check(self._h, lib().dq_read(self._h, C.byref(t) if t is not None else None,
                                      int(with_raw), C.byref(bp)))
-        return batch_to_numpy(bp)
+        return batch_to_numpy(bp, self)
 
     def run_resident(self, traversal=None):
         st = DqStats()
@@ -540,3 +580,24 @@ class Context:
         out = np.zeros(max(1, n.value), np.uint64)
         check(self._h, lib().dq_debug_guess_all(self._h, out.ctypes.data, n.value, C.byref(n)))
         return out[: n.value]
+
+
+CHECK_UNITS = ("K1/K3 kernels", "K2 inflate", "text", "deflate")
+CHECK_SITES = ("K1 candidate slot", "K2 bit reader word", "K2 image store", "K2 second-level table",
+               "K2 per-lane arrays", "K2 match bitmap", "K2 resolve next pointer",
+               "K2 resolve source", "K3 record staging", "K2 last_start")
+
+
+def checked_report():
+    """dq_checked_report of the current device: (is_checked_build, {unit: (failed checks, [sites],
+    largest excess reported)})
+    -- the device bounds-checked build (-DDQ_CHECKED)."""
+    w = (C.c_uint64 * 4)()
+    checked = lib().dq_checked_report(w) == 1
+    out = {}
+    for name, v in zip(CHECK_UNITS, w):
+        n, excess, bits = int(v) >> 32, (int(v) >> 16) & 0xffff, int(v) & 0xffff
+        if n or bits:
+            out[name] = (n, [CHECK_SITES[i] for i in range(len(CHECK_SITES)) if bits >> i & 1],
+                         excess)
+    return checked, out

@@ -3159,4 +3159,17 @@ void dq_batch_free(dq_batch* b) {
 
 void dq_free(void* p) { free(p); }
 
+int dq_checked_report(uint64_t words[4]) {
+  if (!words) return DQ_EINVAL;
+  words[0] = dq::dq_chk_take_kernels();
+  words[1] = dq::dq_chk_take_inflate();
+  words[2] = dq::dq_chk_take_text();
+  words[3] = dq::dq_chk_take_deflate();
+#ifdef DQ_CHECKED
+  return 1;
+#else
+  return 0;
+#endif
+}
+
 }  // extern "C"

@@ -25,8 +25,12 @@
 //      same position continue identically: from its exit, each lane keeps parsing until it hits a
 //      symbol boundary of a later lane's parse (usually within a few symbols) and records the
 //      merge; one thread then follows the merges from lane 0, which gives every lane the part of
-//      its symbols (and continuation) on the block's one parse.  The result is the parse a
-//      single sequential pass would make: no matches are cut at lane boundaries.
+//      its symbols (and continuation) on the block's one parse.  No matches are cut at lane
+//      boundaries.  The merged parse is valid but not always the one a single sequential pass
+//      would make: a merge can land inside a lazy step of the continuing lane (after a deferred
+//      literal whose look-ahead search walked chain / 4 candidates, where a sequential pass would
+//      start a full search), and a continuation that finds no merge within its staging is ended
+//      on the next boundary of a later lane with a shortened match.
 //      (Defaults chain 96, lazy 32, nice 96, good 8: ratio 2.858 on the synthetic WGS stream, zlib
 //      level 5 -- htsjdk's -- 2.857; profiles/r3as_deflate_good_sweep.txt for the frontier.)
 //   3. Codes: histograms of the parse; wave 0 builds the literal/length code and wave 1 the
@@ -551,7 +555,18 @@ __global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __rest
         continue;
       }
       if (nc > CONT_WORDS - 40) {  // (a step appends at most lazy + 1 <= 33 symbols)
-        over = true;
+        // no merge within the staging (e.g. one repeated byte: 258-byte matches from lane 0's
+        // positions 1 + 258 k never meet another lane's 255 u + 258 k): end exactly on lane u's
+        // boundary pu > E, with matches cut to fit and literals for the last < 3 bytes -- a valid
+        // parse that merges, where round 3 stored the whole block
+        while (E < pu && nc < CONT_WORDS) {
+          int d = 0;
+          const int l = F.find(E, min(MAXM, pu - E), &d, F.chain);
+          lane_w[OWN_WORDS + nc++] = l ? match_word(l, d) : lit_word(F.L.in[E]);
+          E += l ? l : 1;
+        }
+        if (E == pu) break;  // merged: lane u's symbols from k on
+        over = true;         // (a gap of literals longer than the staging: stored)
         break;
       }
       int nn = OWN_WORDS + nc;
@@ -879,8 +894,8 @@ void launch_bgzf_deflate(const uint8_t* src, int64_t n_in, int64_t blk0, int64_t
   // DQ_DEFLATE="chain,lazy,nice[,good]": match-search effort (default 96,32,96,8: htsjdk level 5's
   // ratio on the WGS stream; 48,24,48,8 is 40 % faster at a 1.4 % lower ratio, profiles/r3as_*;
   // zlib level 5 is 32,16,32,8 with hash chains, tools/deflate_model.c; good 0 = always the full
-  // chain)
-  static const int4 cfg = [] {
+  // chain; read at every launch, so a test can sweep settings in one process)
+  const int4 cfg = [] {
     int c = 96, l = 32, n = 96, g = 8;
     if (const char* e = getenv("DQ_DEFLATE")) sscanf(e, "%d,%d,%d,%d", &c, &l, &n, &g);
     return make_int4(std::max(1, std::min(c, MAXCAND)), std::max(0, std::min(l, 32)), std::max(3, n),
@@ -896,5 +911,7 @@ void launch_bgzf_pack(const uint8_t* slots, const int32_t* size, const int64_t* 
   hipLaunchKernelGGL(bgzf_pack_kernel, dim3((unsigned)nblk), dim3(256), 0, s, slots, size, off, nblk,
                      out);
 }
+
+DQ_CHK_UNIT(deflate)
 
 }  // namespace dq

@@ -217,7 +217,14 @@ DQ_AI void st_nt(uint4* d, uint4 v) {  // streaming store (nt): U is not re-read
 // costs 4 more SGPRs, which the kernel spills: 4 v_readlane per load.)
 struct GSrc {
   const uint32_t* __restrict__ p;
+#ifdef DQ_CHECKED
+  uint32_t lim;  // words past the member's deflate data the reader may load (refill look-ahead)
+  uint32_t tag;  // the pass (1 spec, 2 redo, 3 emit) << 12, reported with the excess
+#endif
   DQ_AI uint32_t operator[](uint32_t i) const {
+#ifdef DQ_CHECKED
+    DQ_CHKV(i < lim, CHK_K2_BITS, tag | min(i - lim + 1, 4095u));
+#endif
     return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(p) + (i << 2));
   }
 };
@@ -267,6 +274,7 @@ DQ_AI uint32_t load_desc(const LdsI& L, int a) {
 template <bool SLOW>
 DQ_AI uint32_t ll_second(const LdsI& L, uint32_t e, uint32_t bb) {
   const uint32_t sb = (e >> 4) & 7;
+  DQ_CHK(T_LSUB + (e >> 7) + ((bb >> LR) & ((1u << sb) - 1)) < (uint32_t)T_DROOT, CHK_K2_TABLE);
   if (!SLOW) return L.u.d.T[T_LSUB + (e >> 7) + ((bb >> LR) & ((1u << sb) - 1))];
   if (sb) return L.u.d.T[T_LSUB + (e >> 7) + ((bb >> LR) & ((1u << sb) - 1))];
   if (!(e & E_SLOW)) return 0u;
@@ -277,6 +285,7 @@ DQ_AI uint32_t ll_second(const LdsI& L, uint32_t e, uint32_t bb) {
 template <bool SLOW>
 DQ_AI uint32_t d_second(const LdsI& L, uint32_t e, uint32_t bb) {
   const uint32_t sb = (e >> 4) & 7;
+  DQ_CHK(T_DSUB + (e >> 7) + ((bb >> DR) & ((1u << sb) - 1)) < (uint32_t)T_END, CHK_K2_TABLE);
   if (!SLOW) return L.u.d.T[T_DSUB + (e >> 7) + ((bb >> DR) & ((1u << sb) - 1))];
   if (sb) return L.u.d.T[T_DSUB + (e >> 7) + ((bb >> DR) & ((1u << sb) - 1))];
   if (!(e & E_SLOW)) return 0u;
@@ -488,6 +497,7 @@ DQ_AI void emit_seg(const S& W, LdsI& L, uint32_t start, uint32_t target,
       return;
     }
     const bool two = !m && lit2 != 0xffffffffu && p + 1 < isize;
+    DQ_CHK(p >= 0 && sh + p + 2 < OUTCAP && (p >> 5) < 2048, CHK_K2_IMAGE);
     const uint32_t desc = (dist - 1) | ((len - 3) << 15);
     lds8* const o = (lds8*)(L.out + sh + p);
     o[0] = (uint8_t)(m ? desc : len);
@@ -975,6 +985,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       }
       const uint8_t* sp = bp + 4;
       const int32_t n = min((int32_t)len, isize - produced);
+      DQ_CHK(sh + produced + n <= OUTCAP, CHK_K2_IMAGE);
       for (int i = t; i < n; i += WG) L.out[sh + produced + i] = sp[i];
       produced += n;
       pos = q + 32 + 8 * len;
@@ -1116,8 +1127,13 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     SE = ST + nl;
     SC = SE + nl;
     if (cap >= 8) CK = reinterpret_cast<uint32_t*>(SC + nl);
+    DQ_CHK(cap < 8 || (ob >= sh + produced && ob + 4 * nl * (7 + NCK) <= OUTCAP), CHK_K2_LANES);
     const uint32_t seg = (span + nl - 1) / nl;
+#ifdef DQ_CHECKED
+    GSrc gsrc{W, (endbits >> 5) + 8, 1u << 12};
+#else
     const GSrc gsrc{W};
+#endif
     // ---- 3. speculative pass: from OV bits before the segment, counting from its first boundary
     if (t == 0) {  // published by the barrier below
       L.misc[M_RCNT] = 0;       // round 0's redo-list counter
@@ -1142,6 +1158,9 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     }
     __syncthreads();
     TST(2);
+#ifdef DQ_CHECKED
+    gsrc.tag = 2u << 12;
+#endif
     // ---- 4. rounds: lanes whose first boundary differs from the predecessor's exit re-decode
     //      from that exit (compacted onto the first threads by an LDS counter, one barrier per
     //      round besides the re-decode's); repeat until consistent
@@ -1156,6 +1175,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       int32_t* rc = &L.misc[M_RCNT + (round & 1)];
       if (need) {
         const int r = atomicAdd(rc, 1);
+        DQ_CHK(r < nl, CHK_K2_LANES);
         LS[r] = t;
         ST[r] = st;
       }
@@ -1238,6 +1258,9 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     TST(4);
     if (L.misc[M_ERR]) break;
     // ---- emit
+#ifdef DQ_CHECKED
+    gsrc.tag = 3u << 12;
+#endif
     if (t <= last && myoff < isize) {
       const uint32_t sE = t == nl - 1 ? 0xffffffffu : a + (uint32_t)(t + 1) * seg;
       if (slow) emit_seg<true>(gsrc, L, (uint32_t)myB, sE, endbits, myoff, isize, sh);
@@ -1312,6 +1335,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     for (int k = 0; k < NB; k++) {
       const int32_t g0 = b0 + k * CH + G * t;
       const int w = min(g0 >> 6, 1023);  // bytes past isize: read anything, copy = false
+      DQ_CHK(w >= 0 && w - 1 < 1024, CHK_K2_LAST);
       mw[k] = bm64[w];
       lsv[k] = w ? (int32_t)L.u.r.last_start[w - 1] : 0xffff;
     }
@@ -1350,6 +1374,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
           r = r >= D ? r - D : r;
         }
         const int32_t src = ms - D + r;
+        DQ_CHK(!copy || (src >= 0 && src < x), CHK_K2_SRC);
         const bool done = !copy || src < sbk;
         fr[e] = copy ? src : x;
         xs[e] = src;
@@ -1369,6 +1394,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
 #pragma unroll
     for (int e = 0; e < NE; e++) {
       const bool pd = (pending >> e) & 1;
+      DQ_CHK(!pd || (xs[e] - b0 >= 0 && xs[e] - b0 < BATCH), CHK_K2_NXT);
       qv[e] = (int32_t)nxt[pd ? xs[e] - b0 : (e / G) * CH + G * t + e % G];
     }
 #pragma unroll
@@ -1436,7 +1462,10 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
         uint8_t v[G];
         if (mine)
 #pragma unroll
-          for (int i = 0; i < G; i++) v[i] = O[min(frA[k * G + i], 65535)];
+          for (int i = 0; i < G; i++) {
+            DQ_CHK(g0 + i >= isize || (frA[k * G + i] >= 0 && frA[k * G + i] <= g0 + i), CHK_K2_SRC);
+            v[i] = O[min(frA[k * G + i], 65535)];
+          }
         if ((k > 0 || j > 0) && pendB) jump_round(nbs, frB, xsB, pendB);
         if (mine)
 #pragma unroll
@@ -1592,6 +1621,8 @@ struct DevTables {
 DevTables g_dev[kMaxDevices];
 
 }  // namespace
+
+DQ_CHK_UNIT(inflate)
 
 const uint32_t* inflate3_tables(int device) {
   if (device < 0 || device >= kMaxDevices) return nullptr;

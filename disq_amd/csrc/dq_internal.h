@@ -20,6 +20,54 @@ enum : int32_t {
   ST_TEXT_START = 12,     // text split: no block start in the split and none at its end
 };
 
+// ------------------------------------------------------------------ DQ_CHECKED
+// The device bounds-checked build (`make -C disq_amd/csrc checked` -> libdisq_gpu_checked.so, picked
+// up through DQ_GPU_LIB): DQ_CHK(cond, site) counts a failed check and sets bit `site` in this
+// translation unit's check words; the access itself goes ahead unchanged (the checks observe the
+// kernels, they do not alter them, and nothing traps: a trap would take the GPU down with it).
+// dq_checked_report (dq_api.hip) collects every unit's words after a run.  In the product build
+// DQ_CHK compiles to nothing.
+enum : int {
+  CHK_K1_SLOT = 0,   // K1: a candidate's slot outside its chunk's CAP slots
+  CHK_K2_BITS = 1,   // K2: the bit reader loads a word past the member's deflate data (+ slack)
+  CHK_K2_IMAGE = 2,  // K2: an emit / stored-copy store outside the LDS output image
+  CHK_K2_TABLE = 3,  // K2: a second-level table read outside its alphabet's area
+  CHK_K2_LANES = 4,  // K2: per-lane arrays / redo list outside the image tail
+  CHK_K2_BM = 5,     // K2: a match-start bitmap word outside the bitmap
+  CHK_K2_NXT = 6,    // K2: a resolve next pointer outside the batch window
+  CHK_K2_SRC = 7,    // K2: a resolve copy source outside [0, isize)
+  CHK_K3_STAGE = 8,  // K3: a record's staged bytes (or their reads) outside the LDS staging
+  CHK_K2_LAST = 9,   // K2: a last_start index outside the table
+};
+#ifdef DQ_CHECKED
+namespace {
+// failed checks, OR of their site bits, the largest excess a failed check reported (this unit)
+__device__ unsigned int g_dq_chk[3];
+}
+#define DQ_CHKV(cond, site, excess)                              \
+  do {                                                           \
+    if (__builtin_expect(!(cond), 0)) {                          \
+      atomicAdd(&g_dq_chk[0], 1u);                               \
+      atomicOr(&g_dq_chk[1], 1u << (site));                      \
+      atomicMax(&g_dq_chk[2], (unsigned int)(excess));           \
+    }                                                            \
+  } while (0)
+#define DQ_CHK(cond, site) DQ_CHKV(cond, site, 0)
+// Host: this unit's words (count << 32 | excess << 16 | site bits), reset; the current device.
+#define DQ_CHK_UNIT(name)                                                              \
+  uint64_t dq_chk_take_##name() {                                                      \
+    unsigned int w[3] = {0, 0, 0}, z[3] = {0, 0, 0};                                   \
+    if (hipMemcpyFromSymbol(w, HIP_SYMBOL(g_dq_chk), sizeof w) != hipSuccess) return ~0ull; \
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dq_chk), z, sizeof z);                        \
+    return (uint64_t)w[0] << 32 | (uint64_t)(w[2] & 0xffff) << 16 | (w[1] & 0xffff); \
+  }
+#else
+#define DQ_CHKV(cond, site, excess) ((void)0)
+#define DQ_CHK(cond, site) ((void)0)
+#define DQ_CHK_UNIT(name) \
+  uint64_t dq_chk_take_##name() { return 0; }
+#endif
+
 // ------------------------------------------------------------------ hashing
 __host__ __device__ inline uint64_t dq_mix64(uint64_t z) {
   z ^= z >> 30;
@@ -262,6 +310,12 @@ void launch_vcf_overlap(const uint8_t* U, const int64_t* vstart, const int32_t* 
 void launch_text_gather(const uint8_t* U, const int64_t* vstart, const int32_t* vlen,
                         const int64_t* kept, const int64_t* out_off, int64_t n, uint8_t* out,
                         hipStream_t s);
+
+// DQ_CHECKED: each kernel unit's check words (count << 32 | site bits), read and reset
+uint64_t dq_chk_take_kernels();
+uint64_t dq_chk_take_inflate();
+uint64_t dq_chk_take_text();
+uint64_t dq_chk_take_deflate();
 
 // ------------------------------------------------------------------ BGZF deflate (write path)
 int64_t bgzf_block_count(int64_t n);

@@ -125,6 +125,7 @@ __global__ __launch_bounds__(256) void bgzf_scan_kernel(const uint8_t* __restric
     Cand c = hits[i];
     int rank = 0;
     for (int j = 0; j < m; j++) rank += hits[j].pos < c.pos;
+    DQ_CHK(rank < CAP, CHK_K1_SLOT);
     slots[slot0 + rank] = c;
   }
   if (threadIdx.x == 0) {
@@ -437,8 +438,12 @@ __global__ void plan_blocks_kernel(const Cand* __restrict__ cand, const int64_t*
   // gives getFirstReadInPartition no positions to test, so the iterator just moves on past it;
   // one with data would be inflated by the reference (which then fails on the bytes after it,
   // or reads garbage) -- not reproduced: reported as ST_BAD_HEADER.
-  for (int hops = 0; found < 0; hops++) {
-    if (p > e || hops > 4096) return;
+  // No hop cap (the reference has none, BgzfBlockGuesser.java:78-145): every hop moves p forward
+  // (past a magic or past an empty member), and empty members inside payload all lie inside one
+  // real block (<= 65536 bytes, so <= 2341 of 28 bytes) before the chain reaches that block's
+  // successor, a real block.
+  while (found < 0) {
+    if (p > e) return;
     int64_t g = -1;
     for (;;) {
       int64_t k = lower_bound_cand(cand, nc, p);
@@ -906,6 +911,9 @@ __device__ void decode_group(const uint8_t* __restrict__ U, int64_t ulen,
     // LDS-DMA: every 16-byte piece in flight at once (a register-staged loop waits per piece)
     const uint4* src = reinterpret_cast<const uint4*>(U + base);
     const int npiece = (int)((len + 31) / 16);
+    // the staged pieces, the fixed-field words and the last hash word read stay in the staging
+    DQ_CHK(npiece * 16 <= REC_STAGE && (p - base) + 4 * 10 <= REC_STAGE &&
+               (p - base) + 8 * ((n + 7) / 8) + 4 <= REC_STAGE, CHK_K3_STAGE);
     for (int c0 = 0; c0 < npiece; c0 += REC_WAVE)
       if (c0 + lane < npiece)
         __builtin_amdgcn_global_load_lds(
@@ -1780,5 +1788,7 @@ void launch_gather_i64(const int64_t* src, const int64_t* pos, int64_t n, int64_
   hipLaunchKernelGGL(gather_i64_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, pos,
                      n, dst);
 }
+
+DQ_CHK_UNIT(kernels)
 
 }  // namespace dq

@@ -512,4 +512,6 @@ void launch_text_gather(const uint8_t* U, const int64_t* vstart, const int32_t* 
                      vlen, kept, out_off, n, out);
 }
 
+DQ_CHK_UNIT(text)
+
 }  // namespace dq

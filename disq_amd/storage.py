@@ -367,17 +367,17 @@ class HtsjdkVariantsRddStorage:
         return HtsjdkVariantsRdd(vcf_header_lines(path), VariantsRDD(parts))
 
 
-def vcf_header_lines(path: str, max_bytes: int = 64 << 20):
+def vcf_header_lines(path: str):
     """The leading '#' lines of a BGZF VCF, read from a prefix of the file: BGZF members are
     inflated from the start (on the driver, as VcfSource.getVCFCodec reads the header through
     htsjdk, D/impl/formats/vcf/VcfSource.java:60-86) only until the first line that does not start
-    with '#'.  Terminators as Hadoop's LineReader: LF, CR LF, lone CR; a UTF-8 BOM on the first
+    with '#' (or the end of the file: no byte cap, however many contig/sample lines there are).  Terminators as Hadoop's LineReader: LF, CR LF, lone CR; a UTF-8 BOM on the first
     line is dropped (LineRecordReader.skipUtfByteOrderMark)."""
     import struct
     import zlib
     lines, buf, first, read = [], b"", True, 0
     with open(path, "rb") as fh:
-        while read < max_bytes:
+        while True:
             hdr = fh.read(12)
             if len(hdr) < 12:
                 break

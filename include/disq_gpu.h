@@ -372,6 +372,13 @@ int dq_set_export_arena(dq_ctx* ctx, int64_t bytes);
 void dq_batch_free(dq_batch* b);
 void dq_free(void* p);
 
+/* Debug: the device bounds-checked build (`make -C disq_amd/csrc checked` ->
+ * libdisq_gpu_checked.so, compiled with -DDQ_CHECKED).  Writes each kernel unit's failed-check
+ * count << 32 | largest reported excess << 16 | site bits (K1/K3 kernels, K2 inflate, text,
+ * deflate: 4 words) for the current
+ * device and resets them; returns 1 in the checked build, 0 in the product build (words all 0). */
+int dq_checked_report(uint64_t words[4]);
+
 #ifdef __cplusplus
 }
 #endif

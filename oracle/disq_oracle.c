@@ -33,8 +33,11 @@
 #define R_FORMAT 13   /* htsjdk SAMFormatException / RuntimeIOException (not caught by Disq) */
 
 struct dqo_file {
-  const uint8_t* data;
-  int64_t len;
+  const uint8_t* data; /* the file's bytes [base, len) (a whole file: base 0, len = file_len) */
+  int64_t len;         /* end of the held bytes, in file coordinates */
+  int64_t base;        /* file offset of data[0] (a shard window of a larger file) */
+  int64_t file_len;    /* the whole file's length (where EOF is) */
+  int short_window;    /* a read needed bytes past a shard window that ends before EOF */
   int verify_crc;
   /* header */
   int have_header;
@@ -101,7 +104,19 @@ dqo_file* dqo_open_mem(const uint8_t* data, int64_t len, int verify_crc) {
   if (!f) return NULL;
   f->data = data;
   f->len = len;
+  f->file_len = len;
   f->verify_crc = verify_crc;
+  return f;
+}
+
+/* A shard window: bytes [base, base + len) of a file of file_len bytes (test infrastructure for
+ * the multi-GPU bench's per-rank parity: a rank holds only its byte range plus the halo).  Reads
+ * past the window's end, when it is not the file's end, set short_window instead of reading EOF. */
+dqo_file* dqo_open_window(const uint8_t* data, int64_t base, int64_t len, int64_t file_len) {
+  dqo_file* f = dqo_open_mem(data, base + len, 0);
+  if (!f) return NULL;
+  f->base = base;
+  f->file_len = file_len;
   return f;
 }
 
@@ -159,16 +174,19 @@ int64_t dqo_path_splits(int64_t len, int32_t split_size, int nio, int64_t local_
  * Any read past EOF is an IOException caught at :146-148 -> null. */
 int dqo_guess_next_bgzf(dqo_file* f, int64_t p, int64_t end, int64_t* opos, int32_t* ocsize,
                         int32_t* ousize) {
-  const uint8_t* d = f->data;
-  const int64_t L = f->len;
+  const uint8_t* d = f->data; /* indexed as d[x - B]: x in file coordinates */
+  const int64_t L = f->len, B = f->base;
 #define NEED(q, n) \
   do {             \
-    if ((q) < 0 || (q) + (n) > L) return 0; \
+    if ((q) < B || (q) + (n) > L) {                          \
+      if ((q) + (n) > L && L < f->file_len) f->short_window = 1; \
+      return 0;                                             \
+    }                                                       \
   } while (0)
   for (;;) {
     for (;;) { /* :79-92 */
       NEED(p, 4);
-      uint32_t n = (uint32_t)rd32(d + p);
+      uint32_t n = (uint32_t)rd32(d + (p - B));
       if (n == 0x04088b1fu) break;
       if ((n >> 8) == 0x00088b1fu) p += 1;
       else if ((n >> 16) == 0x8b1fu) p += 2;
@@ -178,25 +196,25 @@ int dqo_guess_next_bgzf(dqo_file* f, int64_t p, int64_t end, int64_t* opos, int3
     const int64_t p0 = p; /* :95 */
     p += 10;
     NEED(p, 2);
-    int32_t xlen = rd16(d + p);
+    int32_t xlen = rd16(d + (p - B));
     p += 2;
     const int64_t sub_end = p + xlen;
     int64_t q = p; /* stream position */
     int cancelled = 0;
     while (p < sub_end) { /* :103 */
       NEED(q, 4);
-      uint32_t id = (uint32_t)rd32(d + q);
+      uint32_t id = (uint32_t)rd32(d + (q - B));
       if (id != 0x00024342u) {
-        p += 4 + rd16(d + q + 2);
+        p += 4 + rd16(d + (q - B) + 2);
         q = p;
         continue;
       }
       NEED(q + 4, 2);
-      int32_t bsize = rd16(d + q + 4); /* :117-118 */
+      int32_t bsize = rd16(d + (q - B) + 4); /* :117-118 */
       p += 6;                          /* :121 */
       while (p < sub_end) {            /* :122-126 */
         NEED(p, 4);
-        p += 4 + rd16(d + p + 2);
+        p += 4 + rd16(d + (p - B) + 2);
       }
       if (p != sub_end) { /* :127-131 */
         cancelled = 1;
@@ -206,7 +224,7 @@ int dqo_guess_next_bgzf(dqo_file* f, int64_t p, int64_t end, int64_t* opos, int3
       NEED(p, 4);
       *opos = p0;
       *ocsize = (int32_t)(p + 4 - p0);
-      *ousize = rd32(d + p);
+      *ousize = rd32(d + (p - B));
       return 1;
     }
     (void)cancelled;
@@ -276,13 +294,21 @@ static int inflate_block(rdr* r, int64_t addr, blkbuf* b) {
   const int64_t L = r->f->len;
   b->addr = addr;
   b->valid = 1;
-  if (addr >= L) { /* headerByteCount == 0: "no empty gzip block at end" -> empty block */
+  if (addr >= r->f->file_len) { /* headerByteCount == 0: "no empty gzip block at end" -> empty block */
     b->csize = 0;
     b->len = 0;
     return 0;
   }
+  if (addr < r->f->base ||
+      (L < r->f->file_len && (L - addr < 18 || L - addr < rd16(d + (addr - r->f->base) + 16) + 1))) {
+    /* a shard window that does not hold the whole block (and does not end at EOF) */
+    r->f->short_window = 1;
+    set_err(r->f, "read outside the shard window");
+    b->valid = 0;
+    return R_IOERR;
+  }
   if (L - addr < 18) { set_err(r->f, "incorrect header size"); b->valid = 0; return R_IOERR; }
-  const uint8_t* h = d + addr;
+  const uint8_t* h = d + (addr - r->f->base);
   int32_t blen = rd16(h + 16) + 1;
   if (blen < 18 || blen > 65536) { set_err(r->f, "unexpected block length"); b->valid = 0; return R_IOERR; }
   if (L - addr < blen) { set_err(r->f, "premature end of file"); b->valid = 0; return R_IOERR; }
@@ -448,6 +474,47 @@ out:
   free(text);
   rdr_free(&r);
   return rc;
+}
+
+/* The same header from its decompressed bytes (a shard window does not hold the file's first
+ * blocks: the multi-GPU bench broadcasts the decompressed header, as the GPU shards use it). */
+int dqo_set_header(dqo_file* f, const uint8_t* u, int64_t n) {
+  int64_t p = 0;
+#define TAKE(k) do { if (p + (k) > n) { set_err(f, "short header"); return DQO_EFORMAT; } } while (0)
+  TAKE(8);
+  if (memcmp(u, "BAM\1", 4) != 0) { set_err(f, "Invalid BAM file header"); return DQO_EFORMAT; }
+  const int32_t l_text = rd32(u + 4);
+  if (l_text < 0) return DQO_EFORMAT;
+  p = 8 + (int64_t)l_text;
+  TAKE(4);
+  const int32_t nr = rd32(u + p);
+  if (nr < 0) return DQO_EFORMAT;
+  p += 4;
+  if (f->ref_name) {
+    for (int i = 0; i < f->n_ref; i++) free(f->ref_name[i]);
+    free(f->ref_name);
+    free(f->ref_len);
+  }
+  f->n_ref = nr;
+  f->ref_len = (int32_t*)calloc((size_t)nr + 1, sizeof(int32_t));
+  f->ref_name = (char**)calloc((size_t)nr + 1, sizeof(char*));
+  for (int32_t i = 0; i < nr; i++) {
+    TAKE(4);
+    const int32_t ln = rd32(u + p);
+    p += 4;
+    if (ln <= 1) { set_err(f, "missing sequence name"); return DQO_EFORMAT; }
+    TAKE(ln + 4);
+    f->ref_name[i] = (char*)calloc((size_t)ln, 1);
+    memcpy(f->ref_name[i], u + p, (size_t)ln);
+    f->ref_name[i][ln - 1] = 0;
+    p += ln;
+    f->ref_len[i] = rd32(u + p);
+    p += 4;
+  }
+#undef TAKE
+  f->first_record = 0; /* not known without the compressed header blocks (unused by a window) */
+  f->have_header = 1;
+  return DQO_OK;
 }
 
 int32_t dqo_ref_index(dqo_file* f, const char* name) {
@@ -962,6 +1029,9 @@ int64_t dqo_inflate_file(dqo_file* f, uint8_t* out, int64_t cap) {
 typedef struct {
   const uint8_t* data;
   int64_t len;
+  int64_t base, file_len;   /* a shard window (dqo_run_partitions_window); base 0 otherwise */
+  const uint8_t* header;    /* its decompressed header, or NULL: read from the file */
+  int64_t header_len;
   const int64_t* starts;
   const int64_t* ends;
   int64_t n;
@@ -970,16 +1040,18 @@ typedef struct {
   int64_t* ubytes;
   int64_t next;
   pthread_mutex_t mu;
-  int err;
+  int err, short_window;
 } job_t;
 
 static void* worker(void* arg) {
   job_t* j = (job_t*)arg;
-  dqo_file* f = dqo_open_mem(j->data, j->len, 0);
+  dqo_file* f = j->header ? dqo_open_window(j->data, j->base, j->len, j->file_len)
+                          : dqo_open_mem(j->data, j->len, 0);
   int32_t nr;
   uint64_t first;
   int32_t dummy;
-  if (dqo_read_header(f, &nr, &first, &dummy, 0) != 0) {
+  if (j->header ? dqo_set_header(f, j->header, j->header_len) != 0
+                : dqo_read_header(f, &nr, &first, &dummy, 0) != 0) {
     j->err = 1;
     dqo_close(f);
     return NULL;
@@ -1015,6 +1087,7 @@ static void* worker(void* arg) {
     j->digests[i] = dig;
     if (j->ubytes) j->ubytes[i] = ub;
   }
+  if (f->short_window) j->short_window = 1;
   free(buf);
   rdr_free(&r);
   dqo_close(f);
@@ -1036,6 +1109,30 @@ int dqo_run_partitions(const uint8_t* data, int64_t len, const int64_t* starts,
   free(th);
   pthread_mutex_destroy(&j.mu);
   return j.err ? DQO_EFORMAT : 0;
+}
+
+/* dqo_run_partitions over a shard window: bytes [base, base + len) of a file of file_len bytes
+ * whose decompressed header is `header` (the multi-GPU bench's per-rank parity: a rank's resident
+ * bytes plus its halo).  Returns DQO_ESHORT when some partition needed bytes past the window. */
+int dqo_run_partitions_window(const uint8_t* data, int64_t base, int64_t len, int64_t file_len,
+                              const uint8_t* header, int64_t header_len, const int64_t* starts,
+                              const int64_t* ends, int64_t n, int nthreads, int64_t* counts,
+                              uint64_t* digests, int64_t* ubytes) {
+  if (nthreads < 1) nthreads = 1;
+  if (!header || base < 0 || len < 0 || base + len > file_len) return DQO_EINVAL;
+  job_t j;
+  memset(&j, 0, sizeof j);
+  j.data = data; j.len = len; j.base = base; j.file_len = file_len;
+  j.header = header; j.header_len = header_len;
+  j.starts = starts; j.ends = ends; j.n = n;
+  j.counts = counts; j.digests = digests; j.ubytes = ubytes;
+  pthread_mutex_init(&j.mu, NULL);
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
+  for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, worker, &j);
+  for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+  free(th);
+  pthread_mutex_destroy(&j.mu);
+  return j.short_window ? DQO_ESHORT : j.err ? DQO_EFORMAT : 0;
 }
 
 /* ------------------------------------------------------------------ interval traversal, all

@@ -25,6 +25,7 @@ extern "C" {
 #define DQO_EFORMAT (-2)
 #define DQO_EINVAL (-3)
 #define DQO_ENOMEM (-5)
+#define DQO_ESHORT (-6) /* a shard window ended before the bytes a partition needed */
 
 /* One decoded record (a8 of SURVEY.md §8). */
 typedef struct dqo_rec {
@@ -138,6 +139,15 @@ int64_t dqo_inflate_file(dqo_file* f, uint8_t* out, int64_t cap);
 int dqo_run_partitions(const uint8_t* data, int64_t len, const int64_t* starts,
                        const int64_t* ends, int64_t n_splits, int nthreads, int64_t* counts,
                        uint64_t* digests, int64_t* ubytes);
+/* The same over a shard window: bytes [base, base + len) of a file_len-byte file, `header` its
+ * decompressed BAM header (the window lacks the file's first blocks).  DQO_ESHORT: a partition
+ * needed bytes past the window (a halo too small). */
+dqo_file* dqo_open_window(const uint8_t* data, int64_t base, int64_t len, int64_t file_len);
+int dqo_set_header(dqo_file* f, const uint8_t* u, int64_t n);
+int dqo_run_partitions_window(const uint8_t* data, int64_t base, int64_t len, int64_t file_len,
+                              const uint8_t* header, int64_t header_len, const int64_t* starts,
+                              const int64_t* ends, int64_t n, int nthreads, int64_t* counts,
+                              uint64_t* digests, int64_t* ubytes);
 /* Interval traversal of every partition on nthreads threads: per partition the records of the
  * .bai span of the optimized intervals q (sorted, disjoint; spans = 0: the whole chunk) that
  * overlap q, plus the unplaced-unmapped tail when `unplaced`; count + ordered digest. */

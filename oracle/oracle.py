@@ -111,6 +111,9 @@ def lib():
         L.dqo_run_partitions.argtypes = [C.c_void_p, C.c_int64, P(C.c_int64), P(C.c_int64),
                                          C.c_int64, C.c_int, P(C.c_int64), P(C.c_uint64),
                                          P(C.c_int64)]
+        L.dqo_run_partitions_window.argtypes = [
+            C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_void_p, C.c_int64, P(C.c_int64),
+            P(C.c_int64), C.c_int64, C.c_int, P(C.c_int64), P(C.c_uint64), P(C.c_int64)]
         L.dqo_run_partitions_traversal.argtypes = [
             C.c_void_p, C.c_int64, P(C.c_int64), P(C.c_int64), C.c_int64, C.c_int, C.c_void_p,
             C.c_int64, P(C.c_int32), P(C.c_int32), P(C.c_int32), C.c_int64, C.c_int, C.c_int,
@@ -564,6 +567,28 @@ def run_partitions(data: bytes, splits, nthreads):
     if rc != 0:
         raise OracleError("run_partitions failed")
     return cnt, dig, ub
+
+
+def run_partitions_window(window, base: int, file_len: int, header: bytes, splits, nthreads):
+    """run_partitions over a shard window: `window` holds the file's bytes [base, base + len)
+    (a rank's resident bytes + its halo), `header` the file's decompressed BAM header.  Raises
+    OracleError("window too short") when a partition needed bytes past the window."""
+    buf = np.frombuffer(window, np.uint8)
+    hb = np.frombuffer(header, np.uint8)
+    n = len(splits)
+    s = np.array([a for a, _ in splits] or [0], np.int64)
+    e = np.array([b for _, b in splits] or [0], np.int64)
+    cnt = np.zeros(max(n, 1), np.int64)
+    dig = np.zeros(max(n, 1), np.uint64)
+    ub = np.zeros(max(n, 1), np.int64)
+    rc = lib().dqo_run_partitions_window(buf.ctypes.data, base, len(buf), file_len, hb.ctypes.data,
+                                         len(hb), _p(s, C.c_int64), _p(e, C.c_int64), n, nthreads,
+                                         _p(cnt, C.c_int64), _p(dig, C.c_uint64), _p(ub, C.c_int64))
+    if rc == -6:
+        raise OracleError("window too short")
+    if rc != 0:
+        raise OracleError(f"run_partitions_window failed ({rc})")
+    return cnt[:n], dig[:n], ub[:n]
 
 
 def run_partitions_traversal(data: bytes, splits, nthreads, bai: bytes, intervals,

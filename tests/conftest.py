@@ -17,3 +17,19 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden():
     return GOLDEN
+
+
+@pytest.fixture(autouse=True)
+def _device_checks(request):
+    """Under the device bounds-checked build (DQ_GPU_LIB=.../libdisq_gpu_checked.so), a test whose
+    kernels failed a device check fails."""
+    yield
+    lib_path = os.environ.get("DQ_GPU_LIB", "")
+    if "checked" not in os.path.basename(lib_path) or request.node.get_closest_marker("gpu") is None:
+        return
+    from disq_amd import _lib
+    checked, fails = _lib.checked_report()
+    assert checked, f"{lib_path} is not a DQ_CHECKED build"
+    if fails:
+        print(f"\n[DQ_CHECKED] {request.node.nodeid}: failed device checks {fails}")
+    assert not fails, fails

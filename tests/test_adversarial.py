@@ -71,6 +71,56 @@ def test_oracle_fake_header_at_split_start(kind):
     assert plan[1][2][0] >> 16 == nxt
 
 
+def stored_member(data: bytes) -> bytes:
+    """A BGZF member holding `data` in ONE stored deflate block (payload bytes verbatim)."""
+    import struct
+    import zlib
+    assert len(data) <= 65535
+    body = bytes([1]) + struct.pack("<HH", len(data), len(data) ^ 0xffff) + data
+    hdr = b"\x1f\x8b\x08\x04\x00\x00\x00\x00\x00\xff\x06\x00BC\x02\x00"
+    member = hdr + struct.pack("<H", 18 + len(body) + 8 - 1) + body
+    return member + struct.pack("<II", zlib.crc32(data) & 0xffffffff, len(data))
+
+
+N_FAKES = 65268 // 28  # 2331 empty members: a whole stored block's payload
+
+
+def many_fakes_bam():
+    """A real (stored) BGZF block whose payload is nothing but empty BGZF members (the 28-byte EOF
+    block, 2331 times, in the qualities of a 70 kb record).  A split starting just before them makes
+    BgzfBlockSource (BgzfBlockSource.java:63-84) hop over every one of them (uSize 0) before the
+    next real block: the longest chain of guesses a BGZF file allows (real blocks are <= 64 KiB)."""
+    import struct
+    r = synth.generate(800, seed=23, level=0, nthreads=4)
+    u = B.inflate_all(r.bam)
+    off, _ = B.record_spans(u)[400]
+    ref_id, pos = struct.unpack_from("<ii", u, off + 4)
+    rec = B.make_record(ref_id, pos, b"fakes", 70000)
+    u2 = bytearray(u[:off] + rec + u[off:])
+    f0 = off + B.qual_offset(rec) + 100
+    f1 = f0 + 28 * N_FAKES
+    u2[f0:f1] = B.EOF_BLOCK * N_FAKES
+    bounds = sorted(set(list(range(0, f0, B.BLOCK_U)) + [f0, f1] +
+                        list(range(f1, len(u2), B.BLOCK_U))))
+    bounds.append(len(u2))
+    bam = b"".join(stored_member(bytes(u2[a:b])) for a, b in zip(bounds, bounds[1:])) + B.EOF_BLOCK
+    first = bam.find(B.EOF_BLOCK * 4)
+    assert first > 0 and bam[first + 28 * N_FAKES:first + 28 * N_FAKES + 4] != B.EOF_BLOCK[:4]
+    return bam, first
+
+
+def test_oracle_longest_guess_chain():
+    bam, first = many_fakes_bam()
+    ob = O.OracleBam(bam)
+    assert ob.guess_next_bgzf(first - 7, 1 << 40) == (first, 28, 0)
+    # the split's block list: every fake member (uSize 0), then the real blocks
+    blocks = ob.split_blocks(first - 7, first - 7 + 200000)
+    assert [b[2] for b in blocks[:N_FAKES]] == [0] * N_FAKES
+    assert blocks[N_FAKES][2] > 0 and blocks[N_FAKES][0] == first + 28 * N_FAKES + 8
+    parts = ob.read_partitions(first - 7)
+    assert sum(len(p) for p in parts) >= 800
+
+
 def giant_bam():
     r = synth.generate(300, seed=22, nthreads=4)
     u = B.inflate_all(r.bam)
@@ -116,6 +166,16 @@ def test_gpu_fake_header_at_split_start(kind):
     from test_gpu_parity import assert_parity
     bam, fake, _ = fake_header_bam(kind)
     for split in (fake - 7, fake, fake - 40000):
+        assert_parity(bam, split)
+
+
+@pytest.mark.gpu
+def test_gpu_longest_guess_chain():
+    """2331 guesser hops at one split start (round 3 stopped planning silently after 4096 hops;
+    the hop bound is now the file's structure, as in the reference)."""
+    from test_gpu_parity import assert_parity
+    bam, first = many_fakes_bam()
+    for split in (first - 7, first + 28 * 1000 - 3):
         assert_parity(bam, split)
 
 

@@ -93,3 +93,42 @@ def test_resident_stream_roundtrip(golden):
         z = c.bgzf_fetch(n).tobytes()
     want = O.OracleBam.from_path(os.path.join(golden, "1.bam")).inflate_all().tobytes()
     assert b"".join(members(z)) == want
+
+
+@pytest.mark.parametrize("period", [1, 3, 7, 100])
+def test_repetitive_blocks_compress(period):
+    """Long repetitive input: one repeated byte or a short pattern over whole 65280-byte
+    blocks.  Round 3 stored such blocks (a lane's continuation of 258-byte matches never met
+    another lane's symbol boundary); now the continuation is ended on a later lane's boundary and
+    the block compresses like zlib's (a few hundred bytes per block)."""
+    pat = np.random.default_rng(period).integers(0, 256, size=period, dtype=np.uint8).tobytes()
+    data = (pat * (3 * B.BLOCK_U // period + 1))[:3 * B.BLOCK_U]
+    with _lib.Context() as c:
+        z = check_roundtrip(c, data)
+    assert len(z) < 3 * 2048, len(z)  # zlib level 5: ~ 3 x 100-400 bytes
+
+
+def test_randomized_length_roundtrip_sweep():
+    """200 random lengths (0 .. 3 blocks), 2-bit and 8-bit alphabets, the default match search and
+    the longest one (chain 128, nice 258, no `good` cut): every member inflates to its input."""
+    rng = np.random.default_rng(7)
+    lens = rng.integers(0, 3 * B.BLOCK_U + 100, size=200)
+    old = os.environ.get("DQ_DEFLATE")
+    try:
+        with _lib.Context() as c:
+            for i, n in enumerate(lens):
+                os.environ["DQ_DEFLATE"] = "96,32,96,8" if i % 2 else "128,32,258,0"
+                hi = 4 if i % 4 < 2 else 256
+                data = rng.integers(0, hi, size=int(n), dtype=np.uint8).tobytes()
+                if i % 8 == 5:  # runs: long matches next to literals
+                    data = bytes(np.repeat(np.frombuffer(data[: max(1, n // 50)], np.uint8),
+                                           50)[:n]) if n else b""
+                if n == 0:
+                    assert c.bgzf_compress(data) == b""
+                else:
+                    check_roundtrip(c, data)
+    finally:
+        if old is None:
+            os.environ.pop("DQ_DEFLATE", None)
+        else:
+            os.environ["DQ_DEFLATE"] = old

@@ -564,3 +564,36 @@ def test_decode_file_multi_equals_oracle(tmp_path, ndev):
     assert m.digest == P.fold_digest(dig)
     assert m.compressed_bytes == len(r.bam)
     assert m.decompressed_bytes == len(ob.inflate_all())
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_oracle_shard_window_equals_whole_file(world):
+    """The bench's N > 1 parity oracle (oracle.run_partitions_window): each rank's owned partitions
+    read from only its window [lo_r, hi_r + halo) of the file, with the decompressed header handed
+    over (the window lacks the file's first blocks), equal the whole-file oracle's; a halo that
+    cannot hold a straddling record is an error, not a silent short read."""
+    import struct
+    import numpy as np
+    from oracle import oracle as O
+    from disq_amd import synth
+    r = synth.generate(120000, seed=17, nthreads=8, unplaced_fraction=0.01)
+    bam, L = r.bam, len(r.bam)
+    split = 512 * 1024
+    splits = O.path_splits(L, split)
+    cnt, dig, _ = O.run_partitions(bam, splits, 4)
+    u = O.OracleBam(bam).inflate_all().tobytes()
+    p = 8 + struct.unpack_from("<i", u, 4)[0]
+    nr = struct.unpack_from("<i", u, p)[0]
+    p += 4
+    for _ in range(nr):
+        p += 8 + struct.unpack_from("<i", u, p)[0]
+    header = u[:p]
+    for s in P.shard_plan(L, world, split_size=split):
+        if s.empty:
+            continue
+        win = bam[s.lo:min(L, s.hi + (4 << 20))]
+        c2, d2, _ = O.run_partitions_window(win, s.lo, L, header, splits[s.p0:s.p1], 2)
+        assert np.array_equal(c2, cnt[s.p0:s.p1]) and np.array_equal(d2, dig[s.p0:s.p1])
+        if s.hi < L - 100:
+            with pytest.raises(O.OracleError, match="too short"):
+                O.run_partitions_window(bam[s.lo:s.hi + 10], s.lo, L, header, splits[s.p0:s.p1], 2)

@@ -124,3 +124,20 @@ def test_vcf_header_lines_from_a_prefix():
     assert vcf_header_lines(os.path.join(g, "test.vcf.bgz")) == want
     hs = vcf_header_lines(os.path.join(g, "HiSeq.10000.vcf.bgz"))
     assert hs[0].startswith(b"##fileformat") and hs[-1].startswith(b"#CHROM")
+
+
+def test_vcf_header_lines_no_byte_cap(tmp_path):
+    """A header larger than any fixed prefix (a 64 MB cap truncated it silently): 80 MB
+    of '##contig' lines over ~1300 BGZF members, then one variant line."""
+    import bamutil as B
+    from disq_amd.storage import vcf_header_lines
+    n = 800_000
+    head = [b"##fileformat=VCFv4.2"] + [b"##contig=<ID=ctg%07d,length=%d,assembly=synthetic_%s>"
+                                        % (i, 1000 + i, b"x" * 40) for i in range(n)]
+    head.append(b"#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO")
+    text = b"\n".join(head) + b"\nctg0000001\t5\t.\tA\tC\t.\t.\t.\n"
+    assert len(text) > 64 << 20
+    p = tmp_path / "big_header.vcf.bgz"
+    p.write_bytes(B.bgzf(text, level=1))
+    got = vcf_header_lines(str(p))
+    assert len(got) == len(head) and got[-1] == head[-1] and got[n // 2] == head[n // 2]
