@@ -129,6 +129,7 @@ struct dq_ctx {
   int64_t ncand = 0;
   // chain + inflate
   DevBuf blk_pos, blk_cs, blk_us, uoff, status, U;
+  DevBuf tails;  // inflate: the tail kernel's descriptors (16 bytes per block)
   int n_cu = 256;
   int64_t nblk = 0, ulen = 0;
   // header
@@ -683,14 +684,19 @@ static int run_pipeline(dq_ctx* ctx) {
     if (!crc_init) RET(DQ_EDEVICE, "CRC32 table initialisation failed on this device");
     static const bool timing = getenv("DQ_TIMING") != nullptr;
     uint64_t* tim = nullptr;
-    if (timing) HIPCHK(hipMalloc(&tim, sizeof(uint64_t) * 24 * (size_t)std::max<int64_t>(1, nblk)));
+    if (timing) {
+      HIPCHK(hipMalloc(&tim, sizeof(uint64_t) * 32 * (size_t)std::max<int64_t>(1, nblk)));
+      HIPCHK(hipMemsetAsync(tim, 0, sizeof(uint64_t) * 32 * (size_t)std::max<int64_t>(1, nblk), s));
+    }
     HIPCHK(hipEventRecord(ctx->ev[5], s));
+    if ((rc = ensure_all(ctx, ctx->tails, INFLATE_TAIL_BYTES * (size_t)std::max<int64_t>(1, nblk)))) return rc;
     launch_inflate3(ctx->cbuf(), ctx->blk_pos.as<int64_t>(), ctx->blk_cs.as<int32_t>(),
                     ctx->blk_us.as<int32_t>(), ctx->uoff.as<int64_t>(), nblk, ctx->U.as<uint8_t>(),
-                    ctx->status.as<int32_t>(), ctx->o.verify_crc, crc_init, tim, s);
+                    ctx->status.as<int32_t>(), ctx->o.verify_crc, crc_init, tim, s, nullptr, 0,
+                    ctx->tails.p);
     HIPCHK(hipEventRecord(ctx->ev[6], s));
     if (timing) {
-      std::vector<uint64_t> h(24 * (size_t)nblk);
+      std::vector<uint64_t> h(32 * (size_t)nblk);
       HIPCHK(hipMemcpyAsync(h.data(), tim, 8 * h.size(), hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
       (void)hipFree(tim);
@@ -710,6 +716,14 @@ static int run_pipeline(dq_ctx* ctx) {
               "BGZF block %.3f\n", acc[16] / nb, acc[17] / nb, acc[18] / nb, acc[19] / nb, acc[21] / nb,
               (acc[0] - acc[16]) / nb, (acc[1] - acc[17]) / nb, (acc[2] - acc[18]) / nb,
               (acc[3] - acc[19]) / nb, (acc[5] - acc[21]) / nb, acc[22] / nb);
+      double ta[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int64_t i = 0; i < nblk; i++)
+        for (int k = 0; k < 8; k++) ta[k] += (double)h[24 * (size_t)nblk + 8 * (size_t)i + k];
+      if (ta[3] > 0)
+        fprintf(stderr, "[dq] tail kernel: %.0f tails (%.1f %% of blocks), cycles per tail (lane 0): "
+                "decode=%.0f (header+tables=%.0f spec=%.0f rounds=%.0f emit=%.0f) resolve_prefetch=%.0f "
+                "rows_store_crc=%.0f\n", ta[3], 100.0 * ta[3] / nb, ta[0] / ta[3], ta[4] / ta[3],
+                ta[5] / ta[3], ta[6] / ta[3], ta[7] / ta[3], ta[1] / ta[3], ta[2] / ta[3]);
     }
   }
   dbg(s, "inflate", nblk, ulen);
@@ -1709,10 +1723,11 @@ static int run_span(dq_ctx* ctx, const dq_traversal* tr, dq_stats* out) {
       HIPCHK(hipMemsetAsync(ctx->status.p, 0, sizeof(int32_t) * (size_t)(nblk + 1), s));
       const uint32_t* crc_init = inflate3_tables(ctx->o.device);
       if (!crc_init) RET(DQ_EDEVICE, "CRC32 table initialisation failed on this device");
+      if ((rc = ensure_all(ctx, ctx->tails, INFLATE_TAIL_BYTES * (size_t)nsel))) return rc;
       launch_inflate3(ctx->cbuf(), ctx->blk_pos.as<int64_t>(), ctx->blk_cs.as<int32_t>(),
                       ctx->blk_us.as<int32_t>(), ctx->uoff.as<int64_t>(), nblk, ctx->U.as<uint8_t>(),
                       ctx->status.as<int32_t>(), ctx->o.verify_crc, crc_init, nullptr, s,
-                      ctx->sel.as<int32_t>(), nsel);
+                      ctx->sel.as<int32_t>(), nsel, ctx->tails.p);
     }
     HIPCHK(hipEventRecord(ctx->ev[6], s));
     {

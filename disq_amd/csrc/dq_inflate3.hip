@@ -105,6 +105,21 @@ DQ_HD uint16_t ent_d(uint32_t d, uint32_t len) {
 
 enum : int32_t { F_EXIT = 0, F_EOB = 1, F_ERR = 2, F_END = 3 };
 
+// The tail kernel (inflate_tail_kernel): the deflate blocks of a BGZF block after its first one,
+// when they are small (htsjdk's level 5 leaves ~700 symbols, ~2.9 KB of output, after a first
+// block of 16,383 symbols).  The block kernel resolves, stores and checksums the bytes before the
+// tail and leaves this descriptor; one wave per tail does the rest.
+constexpr int TOUT = 4096;            // tail output bytes one wave holds
+constexpr int TAIL_MAX_BITS = 32768;  // tail deflate bits (64 speculative lanes of <= 512 bits)
+constexpr int TW = 4;                 // tails (waves) per tail-kernel workgroup
+constexpr int T_NCK = 4;              // checkpoints per speculative lane in the tail kernel
+struct TailDesc {
+  int32_t pos;       // bit position (from the block's aligned deflate base) of the tail's header
+  int32_t produced;  // output bytes before the tail
+  uint32_t crc_raw;  // CRC register (init 0, no final xor) of those bytes
+  int32_t flag;      // 1: the tail kernel owns the rest of this block
+};
+
 struct alignas(16) LdsI {
   uint8_t out[OUTCAP];            // output image: byte x at out[sh + x]
   alignas(8) uint32_t bm[2048];   // match-start bitmap (read as 64-bit words in resolve)
@@ -163,7 +178,11 @@ static_assert(sizeof(((LdsI*)nullptr)->scratch) >= 64 * 4, "one emit dummy word 
 static_assert(sizeof(LdsI) <= 81920, "two workgroups per CU");
 static_assert(HB_WORDS * 4 <= T_END * 2, "header staging fits the decode table");
 
+// emit's per-lane dummy words (one per lane of a wave): dead scratch during the emit
+__device__ inline uint32_t* emit_dummy(LdsI& L) { return L.scratch; }
+
 __constant__ uint32_t c_crc4[4][256];
+__constant__ uint32_t c_x2n[32];  // x^(2^k) mod P (reflected): the tail kernel's CRC shifts
 // CRC slices: 132 bytes (33 words), so the 64 lanes of a wave read 64 different LDS banks (128-byte
 // slices put every lane of a wave in the same bank: a 32-way conflict on every data read)
 constexpr int CRC_SL = 132;
@@ -177,7 +196,8 @@ enum { M_ERR = 0, M_SLOW = 1 /* an E_SLOW root entry in this deflate block's tab
        M_LASTF, M_RCNT = 28 /* and 29: redo-list counters of even / odd rounds */,
        M_DIRTY = 30 /* and 31: a re-decoded exit changed, even / odd rounds */ };
 
-__device__ __attribute__((always_inline)) inline void set_err(LdsI& L, int32_t code) { atomicCAS(&L.misc[M_ERR], 0, code); }
+template <class LT>
+__device__ __attribute__((always_inline)) inline void set_err(LT& L, int32_t code) { atomicCAS(&L.misc[M_ERR], 0, code); }
 
 // Bit reader: a 64-bit LSB-first buffer refilled 32 bits at a time from `nw`, the next input word,
 // which every refill call reloads unconditionally (one global_load_dword, almost always an L1/L2
@@ -262,7 +282,8 @@ DQ_AI uint32_t peek_bits(const uint32_t* __restrict__ W, uint32_t pos, uint32_t 
 }
 
 // 3-byte match descriptor at image byte `a` via two aligned dword reads.
-DQ_AI uint32_t load_desc(const LdsI& L, int a) {
+template <class LT>
+DQ_AI uint32_t load_desc(const LT& L, int a) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(L.out + (a & ~3));
   return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)a & 3u) & 0xffffffu;
 }
@@ -271,8 +292,8 @@ DQ_AI uint32_t load_desc(const LdsI& L, int a) {
 // entry in this deflate block's tables, M_SLOW): one read, with no nested branch -- a "no code"
 // root entry (0: only in an incomplete code, which has no long codes) reads the first entry of the
 // unused second-level area, an invalid-code sentinel (build_tables).
-template <bool SLOW>
-DQ_AI uint32_t ll_second(const LdsI& L, uint32_t e, uint32_t bb) {
+template <bool SLOW, class LT>
+DQ_AI uint32_t ll_second(const LT& L, uint32_t e, uint32_t bb) {
   const uint32_t sb = (e >> 4) & 7;
   DQ_CHK(T_LSUB + (e >> 7) + ((bb >> LR) & ((1u << sb) - 1)) < (uint32_t)T_DROOT, CHK_K2_TABLE);
   if (!SLOW) return L.u.d.T[T_LSUB + (e >> 7) + ((bb >> LR) & ((1u << sb) - 1))];
@@ -282,8 +303,8 @@ DQ_AI uint32_t ll_second(const LdsI& L, uint32_t e, uint32_t bb) {
   const int k = canon_decode(bb, L.u.d.hl, LR + 1, &l);
   return k < 0 ? 0u : L.u.d.lent[k];
 }
-template <bool SLOW>
-DQ_AI uint32_t d_second(const LdsI& L, uint32_t e, uint32_t bb) {
+template <bool SLOW, class LT>
+DQ_AI uint32_t d_second(const LT& L, uint32_t e, uint32_t bb) {
   const uint32_t sb = (e >> 4) & 7;
   DQ_CHK(T_DSUB + (e >> 7) + ((bb >> DR) & ((1u << sb) - 1)) < (uint32_t)T_END, CHK_K2_TABLE);
   if (!SLOW) return L.u.d.T[T_DSUB + (e >> 7) + ((bb >> DR) & ((1u << sb) - 1))];
@@ -306,8 +327,8 @@ DQ_AI uint32_t d_second(const LdsI& L, uint32_t e, uint32_t bb) {
 // boundary between them lies before `lim` (the next bit position at which the caller looks at
 // symbol boundaries: segment start/exit, checkpoint, end of data), both are taken at once and
 // `lit2` is the second (else 0xffffffff) -- the boundaries the caller sees are unchanged.
-template <bool SLOW, class S>
-DQ_AI bool dsym(BitR& r, const S& W, const LdsI& L, uint32_t p, uint32_t lim,
+template <bool SLOW, class S, class LT>
+DQ_AI bool dsym(BitR& r, const S& W, const LT& L, uint32_t p, uint32_t lim,
                 uint32_t& len, uint32_t& dist, uint32_t& lit2, bool& is_m) {
   br_refill(r, W);  // >= 33 bits: a litlen code + its extra bits (<= 20)
   uint32_t bb = (uint32_t)r.bb;
@@ -355,8 +376,8 @@ constexpr uint32_t CKI_DEFAULT = 48;  // checkpoint spacing in bits (>= the long
 // (offset from sB << 16 | bytes counted so far), j < nck, at ck[j * ckstride] (nullptr: none).
 // A spacing below the longest symbol only loses merges: a merge needs equal bit positions, and
 // equal positions at symbol boundaries are equal decoder states whatever the checkpoint index.
-template <bool SLOW, class S>
-DQ_AI int run_seg(const S& W, const LdsI& L, uint32_t start, uint32_t sB,
+template <bool SLOW, class S, class LT>
+DQ_AI int run_seg(const S& W, const LT& L, uint32_t start, uint32_t sB,
                   uint32_t sE, uint32_t endbits, int32_t* Bp, int32_t* Ep, int32_t* cntp,
                   uint32_t* ck, int ckstride, uint32_t CKI, int NCK) {
   BitR r;
@@ -421,8 +442,8 @@ DQ_AI int run_seg(const S& W, const LdsI& L, uint32_t start, uint32_t sB,
 // threshold the path is compared with the speculative one: the same boundary means the same
 // decoder state, so the rest of the segment is the speculative run's (exit `se` = E << 3 | flag,
 // `sc` bytes from its first boundary) and the decode stops there.
-template <bool SLOW, class S>
-DQ_AI int run_redo(const S& W, const LdsI& L, uint32_t s0, uint32_t sB,
+template <bool SLOW, class S, class LT>
+DQ_AI int run_redo(const S& W, const LT& L, uint32_t s0, uint32_t sB,
                    uint32_t sE, uint32_t endbits, const uint32_t* ck, int ckstride, int32_t se,
                    int32_t sc, int32_t* Ep, int32_t* cntp, uint32_t CKI, int NCK, int* jm = nullptr) {
   BitR r;
@@ -474,13 +495,15 @@ DQ_AI int run_redo(const S& W, const LdsI& L, uint32_t s0, uint32_t sB,
 // absolute position p; stops at isize.  Literals, literal pairs and match descriptors are written
 // by the same three byte stores: a store a symbol does not need goes to this lane's dummy word
 // (wsum / small are dead during emit), so literal and match lanes do not run separate branches.
-template <bool SLOW, class S>
-DQ_AI void emit_seg(const S& W, LdsI& L, uint32_t start, uint32_t target,
-                    uint32_t endbits, int32_t p, int32_t isize, int sh) {
+// The image and the match-start bitmap start at absolute output position ibase (0 in the block
+// kernel; the tail kernel's image holds only the bytes after the first deflate block).
+template <bool SLOW, class S, class LT>
+DQ_AI void emit_seg(const S& W, LT& L, uint32_t start, uint32_t target,
+                    uint32_t endbits, int32_t p, int32_t isize, int sh, int32_t ibase = 0) {
   typedef volatile __attribute__((address_space(3))) uint8_t lds8;
   // three ds_write_b8 (a merged unaligned b16 store stalls): volatile keeps them apart, the LDS
   // address space keeps them DS stores (a generic volatile pointer became flat stores)
-  uint32_t* const dummy32 = L.scratch + (tid_fresh() & 63);
+  uint32_t* const dummy32 = emit_dummy(L) + (tid_fresh() & 63);
   lds8* const dummy = (lds8*)dummy32;
   BitR r;
   br_init(r, W, start);
@@ -497,13 +520,14 @@ DQ_AI void emit_seg(const S& W, LdsI& L, uint32_t start, uint32_t target,
       return;
     }
     const bool two = !m && lit2 != 0xffffffffu && p + 1 < isize;
-    DQ_CHK(p >= 0 && sh + p + 2 < OUTCAP && (p >> 5) < 2048, CHK_K2_IMAGE);
+    DQ_CHK(p >= ibase && sh + p - ibase + 2 < (int)sizeof(L.out) &&
+               ((p - ibase) >> 5) < (int)(sizeof(L.bm) / 4), CHK_K2_IMAGE);
     const uint32_t desc = (dist - 1) | ((len - 3) << 15);
-    lds8* const o = (lds8*)(L.out + sh + p);
+    lds8* const o = (lds8*)(L.out + sh + (p - ibase));
     o[0] = (uint8_t)(m ? desc : len);
     *(m || two ? o + 1 : dummy) = (uint8_t)(m ? desc >> 8 : lit2);
     *(m ? o + 2 : dummy) = (uint8_t)(desc >> 16);
-    atomicOr(m ? &L.bm[p >> 5] : dummy32, 1u << (p & 31));
+    atomicOr(m ? &L.bm[(p - ibase) >> 5] : dummy32, 1u << ((p - ibase) & 31));
     p += m ? (int32_t)len : (two ? 2 : 1);
   }
 }
@@ -602,8 +626,8 @@ DQ_AI int canon_from_counts(LdsI& L, HuffCanon& h, uint16_t* end, int32_t* q0p, 
 // are consecutive in left-aligned order, so the length is 1 + the number of range ends <= r and
 // the canonical position follows from the length's first code; 0 past the short codes (a long
 // code's prefix, linked below, or no code).
-template <int R>
-DQ_AI uint16_t root_entry(const LdsI& L, const HuffCanon& h, const uint16_t* end,
+template <int R, class LT>
+DQ_AI uint16_t root_entry(const LT& L, const HuffCanon& h, const uint16_t* end,
                           const uint16_t* ent, uint32_t r) {
   int l = 1;
 #pragma unroll
@@ -611,6 +635,52 @@ DQ_AI uint16_t root_entry(const LdsI& L, const HuffCanon& h, const uint16_t* end
   if (l > R) return 0;
   const int q = (int)h.offs[l] + (int)(r >> (R - l)) - (int)h.first[l];
   return ent[q];
+}
+
+// Entry t (< 128) of the code-length code's 7-bit decode table from the 19 code-length code
+// lengths (sym << 3 | len, 0 = no code); *ok = false for an incomplete or over-subscribed code.
+DQ_AI uint16_t clt_entry(const uint8_t* clen, int t, bool* okp) {
+  uint8_t cl[19];
+#pragma unroll
+  for (int s = 0; s < 19; s++) cl[s] = clen[s];
+  // length counts packed 8 bits per length: 0-3 in pk[0], 4-7 in pk[1]
+  uint32_t pk[2] = {0u, 0u};
+#pragma unroll
+  for (int s = 0; s < 19; s++) {
+    const uint32_t inc = 1u << (8 * (cl[s] & 3));
+    pk[0] += cl[s] < 4 ? inc : 0u;
+    pk[1] += cl[s] >= 4 ? inc : 0u;
+  }
+  // the codes of lengths 1..7 occupy consecutive left-aligned ranges: the length of index
+  // rv is 1 + the number of range ends at or below it (as root_entry), its rank among that
+  // length's codes follows from the length's first code
+  int left = 1, code = 0, len = 1, first_l = 0;
+  bool ok = true;
+  const int rv = (int)bitrev((uint32_t)t, 7);
+#pragma unroll
+  for (int l = 1; l <= 7; l++) {
+    const int c = (int)((pk[l >> 2] >> (8 * (l & 3))) & 0xffu);
+    left = (left << 1) - c;
+    ok = ok && left >= 0;
+    first_l = len == l ? code : first_l;
+    code += c;
+    len += (code << (7 - l)) <= rv ? 1 : 0;  // end of the length-l range
+    code <<= 1;
+  }
+  ok = ok && left == 0;  // the code-length code must be complete
+  uint16_t ent = 0;
+  if (len <= 7) {  // the k-th symbol of length len (one pass, no divergence over lengths)
+    int k = (rv >> (7 - len)) - first_l, s2 = 0;
+#pragma unroll
+    for (int s = 0; s < 19; s++) {
+      const bool is = cl[s] == len;
+      s2 = is && k == 0 ? s : s2;
+      k -= is ? 1 : 0;
+    }
+    ent = (uint16_t)((s2 << 3) | len);
+  }
+  *okp = ok;
+  return ent;
 }
 
 // Build both decode tables from L.u.d.x.h.lens (all threads; barriers inside).
@@ -906,7 +976,8 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     const int32_t* __restrict__ blk_csize, const int32_t* __restrict__ blk_usize,
     const int64_t* __restrict__ uoff, int64_t nblk, uint8_t* __restrict__ U,
     int32_t* __restrict__ status, int32_t verify_crc, const uint32_t* __restrict__ crc_init,
-    uint64_t* __restrict__ tim, uint32_t OV, uint32_t sflags, const int32_t* __restrict__ sel) {
+    uint64_t* __restrict__ tim, uint32_t OV, uint32_t sflags, const int32_t* __restrict__ sel,
+    TailDesc* __restrict__ tails) {
   // compile-time checkpoints (the spacing/count sweep's choice, profiles/r3ij_*): the decode loops
   // fold the threshold updates and hold fewer SGPRs (spec + rounds -8 k cycles per block, r3y)
   constexpr uint32_t CKI = CKI_DEFAULT;
@@ -955,6 +1026,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   __syncthreads();
   int32_t produced = 0;
   uint32_t pos = a0;  // bit position of the next deflate block's header
+  bool deferred = false;  // the rest of the block goes to the tail kernel
   while (L.misc[M_ERR] == 0 && produced < isize) {
     const int t = tid_fresh(), lane = t & 63, wv = t >> 6;
     // ---- 1. block header: every thread reads it (the branches below are uniform, no barrier).
@@ -1011,46 +1083,8 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       __syncthreads();
       // code-length code: 7-bit table, one entry per thread (canonical decode over 19 lengths)
       if (t < 128) {
-        uint8_t cl[19];
-#pragma unroll
-        for (int s = 0; s < 19; s++) cl[s] = L.u.d.x.h.clen[s];
-        // length counts packed 8 bits per length: 0-3 in pk[0], 4-7 in pk[1]
-        uint32_t pk[2] = {0u, 0u};
-#pragma unroll
-        for (int s = 0; s < 19; s++) {
-          const uint32_t inc = 1u << (8 * (cl[s] & 3));
-          pk[0] += cl[s] < 4 ? inc : 0u;
-          pk[1] += cl[s] >= 4 ? inc : 0u;
-        }
-        // the codes of lengths 1..7 occupy consecutive left-aligned ranges: the length of index
-        // rv is 1 + the number of range ends at or below it (as root_entry), its rank among that
-        // length's codes follows from the length's first code
-        int left = 1, code = 0, len = 1, first_l = 0;
         bool ok = true;
-        const int rv = (int)bitrev((uint32_t)t, 7);
-#pragma unroll
-        for (int l = 1; l <= 7; l++) {
-          const int c = (int)((pk[l >> 2] >> (8 * (l & 3))) & 0xffu);
-          left = (left << 1) - c;
-          ok = ok && left >= 0;
-          first_l = len == l ? code : first_l;
-          code += c;
-          len += (code << (7 - l)) <= rv ? 1 : 0;  // end of the length-l range
-          code <<= 1;
-        }
-        ok = ok && left == 0;  // the code-length code must be complete
-        uint16_t ent = 0;
-        if (len <= 7) {  // the k-th symbol of length len (one pass, no divergence over lengths)
-          int k = (rv >> (7 - len)) - first_l, s2 = 0;
-#pragma unroll
-          for (int s = 0; s < 19; s++) {
-            const bool is = cl[s] == len;
-            s2 = is && k == 0 ? s : s2;
-            k -= is ? 1 : 0;
-          }
-          ent = (uint16_t)((s2 << 3) | len);
-        }
-        L.u.d.x.h.clt[t] = ent;
+        L.u.d.x.h.clt[t] = clt_entry(L.u.d.x.h.clen, t, &ok);
         if (t == 0 && !ok) set_err(L, ST_BAD_TABLE);
       }
       __syncthreads();
@@ -1277,10 +1311,29 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     }
     if (full || bfinal) break;
     pos = (uint32_t)nextpos;
+    // the rest of the BGZF block is a small deflate block (htsjdk's level 5 closes one every 16,383
+    // symbols: ~700 symbols left of a 65,498-byte block): hand it to the tail kernel, which decodes
+    // many such tails per CU, one wave each, instead of running its fixed-latency phases here with
+    // one wave busy (~23 % of this kernel's cycles for ~4 % of the symbols, round 3)
+    if (tails && isize - produced <= TOUT && endbits - pos <= (uint32_t)TAIL_MAX_BITS) {
+      deferred = true;
+      break;
+    }
   }
   __syncthreads();
   int32_t err = L.misc[M_ERR];
-  if (!err && produced != isize) err = ST_SHORT;
+  if (!err && !deferred && produced != isize) err = ST_SHORT;
+  // the bytes this workgroup resolves, stores and checksums: the whole block, or those before the
+  // deferred tail
+  const int32_t rsize = deferred ? produced : isize;
+  if (deferred && t == 0) {
+    TailDesc td;
+    td.pos = (int32_t)pos;
+    td.produced = produced;
+    td.crc_raw = 0;
+    td.flag = 1;
+    tails[blockIdx.x] = td;
+  }
   if (err) {
     if (t == 0) status[b] = err;
     return;
@@ -1311,7 +1364,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   }
   uint8_t* dstU = U + ub;
   const uint8_t* O = L.out + sh;
-  const int head = min((16 - sh) & 15, isize);  // bytes before the first 16-byte U boundary
+  const int head = min((16 - sh) & 15, rsize);  // bytes before the first 16-byte U boundary
   int32_t lines_done = 0;                       // 16-byte lines [head + 16k, +16) stored
   // chunks of CH = G * WG bytes, thread t owns bytes [G t, G t + G) of each; NB chunks per batch;
   // a byte's chain may stop at any byte before its 512-byte step (the unit of the barriers in (b))
@@ -1334,7 +1387,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
 #pragma unroll
     for (int k = 0; k < NB; k++) {
       const int32_t g0 = b0 + k * CH + G * t;
-      const int w = min(g0 >> 6, 1023);  // bytes past isize: read anything, copy = false
+      const int w = min(g0 >> 6, 1023);  // bytes past rsize: read anything, copy = false
       DQ_CHK(w >= 0 && w - 1 < 1024, CHK_K2_LAST);
       mw[k] = bm64[w];
       lsv[k] = w ? (int32_t)L.u.r.last_start[w - 1] : 0xffff;
@@ -1363,7 +1416,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
         const bool before = ms < b0;  // descriptors before the batch are overwritten: the carry
         const uint32_t desc = before ? cdesc : (ms == msv[k * G + G - 1] ? db[k] : da[k]);
         const int32_t len = (int32_t)(desc >> 15) + 3, D = (int32_t)(desc & 0x7fff) + 1;
-        const bool copy = x < isize && ms != 0xffff && (!before || ms == cms) && x < ms + len;
+        const bool copy = x < rsize && ms != 0xffff && (!before || ms == cms) && x < ms + len;
         // src = ms - D + (x - ms) mod D; x - ms <= 257: a float reciprocal + one fix-up is exact,
         // needed only by bytes past the first period of an overlapping match (skipped per wave)
         const int32_t jj = x - ms;
@@ -1419,11 +1472,11 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   first_hop(0, cms, cdesc, frA, xsA, pendA);
   // the carries into every batch, while every descriptor is intact (off the batches' critical
   // path: round 2 had wave 0 compute each one in front of the batch barrier)
-  if (t < (isize + BATCH - 1) / BATCH) {
+  if (t < (rsize + BATCH - 1) / BATCH) {
     int32_t ncms = -1;
     uint32_t ncdesc = 0;
     const int32_t x = (t + 1) * BATCH - 1;  // batch t's last byte
-    if (x + 1 < isize) {
+    if (x + 1 < rsize) {
       const uint64_t m = bm64[x >> 6];  // bit 63 of the last word: every bit is at or before x
       const int32_t ms = m ? (x | 63) - (int32_t)__clzll(m) : (int32_t)L.u.r.last_start[(x >> 6) - 1];
       if (ms != 0xffff) {
@@ -1439,10 +1492,10 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   }
   __syncthreads();
   for (int hop = 0; pendA != 0 && hop < WG + 2; hop++) jump_round(0, frA, xsA, pendA);
-  for (int32_t bs = 0; bs < isize; bs += BATCH) {
+  for (int32_t bs = 0; bs < rsize; bs += BATCH) {
     const uint64_t tb0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
     const int32_t nbs = bs + BATCH;
-    const bool more = nbs < isize;
+    const bool more = nbs < rsize;
     __syncthreads();  // every wave's jumps of batch k are done: nxt is free for batch k+1
     const int32_t ncms = more ? L.u.r.carry_ms[bs / BATCH] : -1;
     const uint32_t ncdesc = more ? L.u.r.carry_desc[bs / BATCH] : 0u;
@@ -1463,21 +1516,21 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
         if (mine)
 #pragma unroll
           for (int i = 0; i < G; i++) {
-            DQ_CHK(g0 + i >= isize || (frA[k * G + i] >= 0 && frA[k * G + i] <= g0 + i), CHK_K2_SRC);
+            DQ_CHK(g0 + i >= rsize || (frA[k * G + i] >= 0 && frA[k * G + i] <= g0 + i), CHK_K2_SRC);
             v[i] = O[min(frA[k * G + i], 65535)];
           }
         if ((k > 0 || j > 0) && pendB) jump_round(nbs, frB, xsB, pendB);
         if (mine)
 #pragma unroll
           for (int i = 0; i < G; i++)
-            if (g0 + i < isize) L.out[sh + g0 + i] = v[i];  // a literal rewrites its own value
+            if (g0 + i < rsize) L.out[sh + g0 + i] = v[i];  // a literal rewrites its own value
         __syncthreads();
       }
     }
     if (pendB) jump_round(nbs, frB, xsB, pendB);
     const uint64_t tb2 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
     // (c) store the 16-byte U lines this batch completed
-    const int32_t c1 = min(isize, nbs);
+    const int32_t c1 = min(rsize, nbs);
     const int32_t lines_to = c1 >= head ? (c1 - head) / 16 : 0;
     if (!(sflags & 1)) {
       for (int32_t k = lines_done + t; k < lines_to; k += WG) {
@@ -1503,7 +1556,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     }
   }
   if (sflags & 1) {  // the whole block at the end
-    const int32_t lines_to = isize >= head ? (isize - head) / 16 : 0;
+    const int32_t lines_to = rsize >= head ? (rsize - head) / 16 : 0;
     for (int32_t k = t; k < lines_to; k += WG) {
       const uint4 v = *reinterpret_cast<const uint4*>(O + head + 16 * k);
       uint4* d = reinterpret_cast<uint4*>(dstU + head + 16 * k);
@@ -1521,22 +1574,22 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     ct1 = (&c_crc4[0][0])[t + WG];
     cshift = c_slice_shift[WG - 1 - t];
     if (t == 0) {
-      cinit = crc_init[isize];  // x^(8 isize) * 0xffffffff mod P
+      cinit = crc_init[rsize];  // x^(8 rsize) * 0xffffffff mod P
       const uint8_t* tr = C + cpos + csize - 8;
       cwant = (uint32_t)tr[0] | ((uint32_t)tr[1] << 8) | ((uint32_t)tr[2] << 16) | ((uint32_t)tr[3] << 24);
     }
   }
   static_assert(2 * WG == 1024, "two CRC table words per thread");
   for (int x = t; x < head; x += WG) dstU[x] = O[x];
-  for (int x = head + 16 * lines_done + t; x < isize; x += WG) dstU[x] = O[x];
+  for (int x = head + 16 * lines_done + t; x < rsize; x += WG) dstU[x] = O[x];
   TST(6);
-  // ---- 7. CRC32: thread t hashes the CRC_SL-byte slice ending (511 - t) * CRC_SL bytes before isize
+  // ---- 7. CRC32: thread t hashes the CRC_SL-byte slice ending (511 - t) * CRC_SL bytes before rsize
   if (verify_crc) {
     __syncthreads();  // the resolve scratch is dead: the CRC tables reuse it
     (&L.u.crc4[0][0])[t] = ct0;
     (&L.u.crc4[0][0])[t + WG] = ct1;
     __syncthreads();
-    const int32_t e = isize - (WG - 1 - t) * CRC_SL;
+    const int32_t e = rsize - (WG - 1 - t) * CRC_SL;
     const int32_t s0 = max(0, e - CRC_SL);
     uint32_t cr = 0;
     if (e > 0) {
@@ -1556,13 +1609,588 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     if (t == 0) {
       uint32_t x = 0;
       for (int w = 0; w < WG / 64; w++) x ^= (uint32_t)L.wsum[w];
-      const uint32_t crc = (x ^ cinit) ^ 0xffffffffu;
-      if (crc != cwant) status[b] = ST_CRC;
+      if (deferred) {  // the prefix's CRC register; the tail kernel finishes the block's CRC
+        tails[blockIdx.x].crc_raw = x;
+      } else {
+        const uint32_t crc = (x ^ cinit) ^ 0xffffffffu;
+        if (crc != cwant) status[b] = ST_CRC;
+      }
     }
   }
   TST(7);
   if (TIMING && t == 0)
     for (int i = 0; i < 24; i++) tim[(int64_t)blockIdx.x * 24 + i] = tacc[i];
+}
+
+// ================================================================ the tail kernel
+// Per-wave LDS of inflate_tail_kernel (~13 KB: four tails per workgroup, three workgroups per CU).
+struct alignas(16) LdsW {
+  union {
+    struct {
+      uint16_t T[T_END];
+      HuffCanon hl, hd;
+      uint16_t lend[16], dend[16];
+      uint16_t lent[288];
+      uint16_t dent[32];
+      union {
+        uint16_t pair[1 << LR];
+        struct {
+          uint8_t lens[320];
+          uint8_t clen[20];
+          uint16_t clt[128];
+          int32_t cnt[32];  // code-length counts: litlen [0, 16), distance [16, 32)
+          int32_t run[32];  // ranks so far per length over the symbol chunks (same split)
+        } h;
+      } x;
+    } d;
+    struct {
+      uint64_t carry[TOUT / 64];  // per row, desc << 32 | (start + 1) of the match carried in
+      uint8_t g[TOUT];            // the value of every byte whose source lies before the tail
+    } r;
+    uint32_t crc[256];            // CRC: the slice-by-1 table
+  } u;
+  uint8_t out[TOUT + 32];             // the tail's output image: tail byte k at out[sh + k]
+  alignas(8) uint32_t bm[TOUT / 32];  // match-start bitmap of the tail (bit k: tail byte k)
+  uint32_t ck[T_NCK * 64];            // checkpoints [j * 64 + lane]; emit's dummy words
+  int32_t misc[8];
+  uint32_t scratch[16];               // run_seg's dummy words
+};
+static_assert(HB_WORDS * 4 <= T_END * 2, "header staging fits the decode table");
+static_assert(4 * sizeof(LdsW) <= 54 * 1024, "four tails per workgroup, three workgroups per CU");
+DQ_AI uint32_t* emit_dummy(LdsW& L) { return L.ck; }
+
+// The code-length sequence of a dynamic header, decoded by one wave: every lane walks the same
+// symbols (the walk is uniform: no broadcast needed) and lane i of a run writes its i-th length.
+// The header's words are staged in the decode table (not built yet).  Returns the bit position
+// after the header, or sets M_ERR.
+DQ_AI uint32_t read_lengths_wave(LdsW& L, uint32_t P, int nlen, int ndist, uint32_t endbits,
+                                 uint32_t hbase) {
+  const uint32_t* hb = reinterpret_cast<const uint32_t*>(L.u.d.T);
+  auto& H = L.u.d.x.h;
+  const int lane = tid_fresh() & 63;
+  const int total = nlen + ndist;
+  int have = 0, prev = -1;
+  while (have < total) {
+    if (P > endbits) {
+      set_err(L, ST_OVERREAD);
+      return P;
+    }
+    const uint32_t wi = min((P >> 5) - hbase, (uint32_t)HB_WORDS - 2);
+    const uint32_t v = (uint32_t)((((uint64_t)hb[wi + 1] << 32) | hb[wi]) >> (P & 31));
+    const uint32_t ent = H.clt[v & 127];
+    const uint32_t cl = ent & 7, sy = ent >> 3;
+    const uint32_t ex = sy == 16 ? 2u : sy == 17 ? 3u : sy == 18 ? 7u : 0u;
+    const int xv = (int)((v >> cl) & ((1u << ex) - 1));
+    const int rep = sy < 16 ? 1 : sy == 16 ? 3 + xv : sy == 17 ? 3 + xv : 11 + xv;
+    const int val = sy < 16 ? (int)sy : sy == 16 ? prev : 0;
+    if (cl == 0 || val < 0 || have + rep > total) {  // no code / a repeat with nothing before it
+      set_err(L, ST_BAD_TABLE);
+      return P;
+    }
+    P += cl + ex;
+    if (val && lane < rep) {  // lens is zero-filled
+      const int i = have + lane;
+      H.lens[i < nlen ? i : 288 + i - nlen] = (uint8_t)val;
+    }
+    prev = val;
+    have += rep;
+  }
+  return P;
+}
+
+// The decode tables by one wave: root tables as the block kernel's (entries carry the decoded
+// values), and the canonical slow path (E_SLOW) for every root prefix of a longer code -- a tail
+// decodes ~700 symbols, so the second-level tables are not worth their build.  Sets M_SLOW.
+DQ_AI void build_tables_wave(LdsW& L, int nlen, int ndist) {
+  const int lane = tid_fresh() & 63;
+  auto& H = L.u.d.x.h;
+  if (lane < 32) {
+    H.cnt[lane] = 0;
+    H.run[lane] = 0;
+  }
+  __builtin_amdgcn_wave_barrier();
+  // code-length counts of both alphabets (LDS atomics: one pass over the symbols)
+  for (int k = lane; k < 320; k += 64) {
+    const bool isl = k < 288;
+    const int len = isl ? (k < nlen ? H.lens[k] : 0) : (k - 288 < ndist ? H.lens[k] : 0);
+    if (len) atomicAdd(&H.cnt[(isl ? 0 : 16) + len], 1);
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  // canonical descriptions (lanes 1..15: litlen; 17..31: distance), as canon_from_counts
+  int e = 0;
+  {
+    const int l = lane & 15;
+    const bool in = lane < 32 && l >= 1;
+    const int c = in ? H.cnt[lane] : 0;
+    // segmented inclusive scans: the distance half (lanes 16..31) starts from zero
+    int offi = wave_incl_scan(c, lane);
+    const int tt = in ? c << (16 - l) : 0;
+    int cs = wave_incl_scan(tt, lane);
+    const int base_o = __shfl(offi, 15, 64), base_c = __shfl(cs, 15, 64);
+    if (lane >= 16) {
+      offi -= base_o;
+      cs -= base_c;
+    }
+    const int code = in ? (int)((uint32_t)(cs - tt) >> (16 - l)) : 0;
+    const int left = in ? (1 << l) - (code + c) : 0;
+    const bool isd = lane >= 16;
+    HuffCanon& h = isd ? L.u.d.hd : L.u.d.hl;
+    uint16_t* end = isd ? L.u.d.dend : L.u.d.lend;
+    const int R = isd ? DR : LR;
+    if (lane < 32) {
+      h.first[l] = (uint16_t)code;
+      h.count[l] = (uint16_t)c;
+      h.offs[l] = (uint16_t)(offi - c);
+      if (in && l <= R) end[l] = (uint16_t)((code + c) << (R - l));
+    }
+    const uint64_t over = __ballot(in && left < 0);
+    const uint64_t used = __ballot(c > 0);
+    const int left15l = __shfl(left, 15, 64), left15d = __shfl(left, 31, 64);
+    const uint64_t ul = used & 0xffffull, ud = (used >> 16) & 0xffffull;
+    const int maxll = ul ? 63 - __clzll(ul) : 0, maxld = ud ? 63 - __clzll(ud) : 0;
+    if (over) e = ST_BAD_TABLE;
+    if (maxll > 0 && left15l > 0 && maxll != 1) e = ST_BAD_TABLE;  // zlib inflate_table rule
+    if (maxld > 0 && left15d > 0 && maxld != 1) e = ST_BAD_TABLE;
+    // codes no longer than the roots, all codes (the long ones take the canonical slow path)
+    const int ql0 = __shfl(offi, LR, 64), qln = __shfl(offi, 15, 64);
+    const int qd0 = __shfl(offi, 16 + DR, 64), qdn = __shfl(offi, 31, 64);
+    if (lane == 0) L.misc[M_SLOW] = (qln > ql0 || qdn > qd0) ? 1 : 0;
+  }
+  if (e) {
+    if (lane == 0) set_err(L, e);
+    return;
+  }
+  __builtin_amdgcn_wave_barrier();
+  // ranks among equal lengths, chunk by chunk (one-hot packed counters, 8 bits per length: at most
+  // 64 per chunk), and the decoded entries at their canonical positions
+  for (int k0 = 0; k0 < 320; k0 += 64) {
+    const int k = k0 + lane;
+    const bool isl = k < 288;
+    const int sym = isl ? k : k - 288;
+    const int len = k < 320 ? (isl ? (k < nlen ? H.lens[k] : 0) : (sym < ndist ? H.lens[k] : 0)) : 0;
+    // the chunk 256..319 mixes the alphabets: count each alphabet's lanes separately
+    uint32_t c[4], cd[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      c[j] = (isl && len && (len >> 2) == j) ? 1u << (8 * (len & 3)) : 0u;
+      cd[j] = (!isl && len && (len >> 2) == j) ? 1u << (8 * (len & 3)) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      c[j] = (uint32_t)wave_incl_scan((int)c[j], lane);
+      cd[j] = (uint32_t)wave_incl_scan((int)cd[j], lane);
+    }
+    if (len) {
+      const uint32_t* cc = isl ? c : cd;
+      const uint32_t mine = (len >> 2) == 0 ? cc[0] : (len >> 2) == 1 ? cc[1] : (len >> 2) == 2 ? cc[2] : cc[3];
+      const int rank = (int)((mine >> (8 * (len & 3))) & 0xffu) - 1 + H.run[(isl ? 0 : 16) + len];
+      const HuffCanon& hh = isl ? L.u.d.hl : L.u.d.hd;
+      const int q = hh.offs[len] + rank;
+      if (isl) L.u.d.lent[q] = ent_ll((uint32_t)sym, (uint32_t)len);
+      else L.u.d.dent[q] = ent_d((uint32_t)sym, (uint32_t)len);
+    }
+    // the chunk's totals (lane 63's inclusive counters) into the running ranks
+    uint32_t tl[4], tdd[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      tl[j] = (uint32_t)__builtin_amdgcn_readlane((int)c[j], 63);
+      tdd[j] = (uint32_t)__builtin_amdgcn_readlane((int)cd[j], 63);
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane < 32) {
+      const int l = lane & 15;
+      const uint32_t q = (l >> 2) == 0 ? (lane < 16 ? tl[0] : tdd[0]) : (l >> 2) == 1 ? (lane < 16 ? tl[1] : tdd[1])
+                       : (l >> 2) == 2 ? (lane < 16 ? tl[2] : tdd[2]) : (lane < 16 ? tl[3] : tdd[3]);
+      H.run[lane] += l ? (int)((q >> (8 * (l & 3))) & 0xffu) : 0;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  // root tables: 16 litlen and 4 distance entries per lane; an index without a short code is the
+  // prefix of long codes (a complete code), decoded canonically
+  const bool lslow = L.u.d.hl.count[11] + L.u.d.hl.count[12] + L.u.d.hl.count[13] +
+                         L.u.d.hl.count[14] + L.u.d.hl.count[15] > 0;
+  const bool dslow = L.u.d.hd.count[9] + L.u.d.hd.count[10] + L.u.d.hd.count[11] + L.u.d.hd.count[12] +
+                         L.u.d.hd.count[13] + L.u.d.hd.count[14] + L.u.d.hd.count[15] > 0;
+  for (int i = lane; i < (1 << LR); i += 64) {
+    const uint16_t v = root_entry<LR>(L, L.u.d.hl, L.u.d.lend, L.u.d.lent, bitrev((uint32_t)i, LR));
+    L.u.d.T[i] = v == 0 && lslow ? E_SLOW : v;
+  }
+  for (int i = lane; i < (1 << DR); i += 64) {
+    const uint16_t v = root_entry<DR>(L, L.u.d.hd, L.u.d.dend, L.u.d.dent, bitrev((uint32_t)i, DR));
+    L.u.d.T[T_DROOT + i] = v == 0 && dslow ? E_SLOW : v;
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+// x^(8 n) mod P (reflected), from x^(2^k)
+DQ_AI uint32_t x8n_tail(uint32_t n) {
+  uint32_t p = 1u << 31;  // x^0
+  for (int k = 3; n; n >>= 1, k++)
+    if (n & 1) p = gf2_mulmod(c_x2n[k & 31], p);
+  return p;
+}
+
+// One wave per deferred tail: the deflate blocks of BGZF block b after the first `produced` bytes
+// (TailDesc), decoded as the block kernel decodes its first one -- speculative segments (at most
+// 64, one per lane), checkpoint merges, wave-local rounds instead of barrier-separated ones, the
+// emit into the tail image -- then resolved row by row (64 bytes, one per lane): a source before
+// the tail is read from U (written by the block kernel), one in an earlier row from the image, one
+// in the same row waits for its lane.  Stores the tail's bytes and finishes the block's CRC32 from
+// the prefix's CRC register.  No workgroup barrier: the waves of a workgroup are independent.
+template <bool TIMING>
+__global__ __launch_bounds__(64 * TW, 3) void inflate_tail_kernel(
+    const uint8_t* __restrict__ C, const int64_t* __restrict__ blk_pos,
+    const int32_t* __restrict__ blk_csize, const int32_t* __restrict__ blk_usize,
+    const int64_t* __restrict__ uoff, int64_t ngrid, uint8_t* __restrict__ U,
+    int32_t* __restrict__ status, int32_t verify_crc, const uint32_t* __restrict__ crc_init,
+    uint32_t OV, uint32_t sflags, const int32_t* __restrict__ sel,
+    const TailDesc* __restrict__ tails, uint64_t* __restrict__ tim) {
+  constexpr uint32_t CKI = CKI_DEFAULT;
+  __shared__ LdsW Ls[TW];
+  const int wv = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+  const int64_t gi = (int64_t)blockIdx.x * TW + wv;
+  if (gi >= ngrid) return;
+  const TailDesc td = tails[gi];
+  if (td.flag != 1) return;
+  LdsW& L = Ls[wv];
+  const uint64_t t0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
+  const int64_t b = sel ? (int64_t)sel[gi] : gi;
+  const int64_t cpos = blk_pos[b];
+  const int32_t csize = blk_csize[b];
+  const int32_t isize = blk_usize[b];
+  const int64_t ub = uoff[b];
+  const int32_t p0 = td.produced;       // tail byte k is block byte p0 + k
+  const int sh = (int)((ub + p0) & 15);  // image byte sh + k: U's 16-byte lines align with the image
+  const uint8_t* dp = C + cpos + 18;
+  const int mis = (int)(reinterpret_cast<uintptr_t>(dp) & 15);
+  const uint32_t* W = reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(dp - mis, 16));
+  const int32_t dbytes = csize - 26;
+  const uint32_t endbits = 8u * (uint32_t)mis + 8u * (uint32_t)max(dbytes, 0);
+#ifdef DQ_CHECKED
+  GSrc gsrc{W, (endbits >> 5) + 8, 4u << 12};
+#else
+  const GSrc gsrc{W};
+#endif
+  for (int i = lane; i < TOUT / 32; i += 64) L.bm[i] = 0;
+  if (lane < 8) L.misc[lane] = 0;
+  __builtin_amdgcn_wave_barrier();
+  int32_t produced = p0;
+  uint32_t pos = (uint32_t)td.pos;
+  uint64_t tph[4] = {0, 0, 0, 0};  // TIMING: header + tables, spec, rounds, emit
+  uint64_t tl = TIMING ? __builtin_amdgcn_s_memtime() : 0;
+  auto tick = [&](int k) {
+    if (TIMING) {
+      const uint64_t now = __builtin_amdgcn_s_memtime();
+      tph[k] += now - tl;
+      tl = now;
+    }
+  };
+  while (L.misc[M_ERR] == 0 && produced < isize) {
+    // ---- header (as the block kernel: every lane reads it, the branches are uniform)
+    const uint32_t clpos = pos + 17;
+    const uint32_t hbase = clpos >> 5;
+    const uint32_t h = peek_bits(W, pos, 17);
+    const int32_t bfinal = (int32_t)(h & 1), btype = (int32_t)((h >> 1) & 3);
+    const int32_t herr = pos + 3 > endbits ? ST_OVERREAD : btype == 3 ? ST_BAD_BLOCKTYPE : 0;
+    if (herr) {
+      set_err(L, herr);
+      break;
+    }
+    if (btype == 0) {  // stored block: copy
+      const uint32_t q = (pos + 3 + 7) & ~7u;
+      const uint8_t* bp = reinterpret_cast<const uint8_t*>(W) + q / 8;
+      const uint32_t len = bp[0] | ((uint32_t)bp[1] << 8), nl = bp[2] | ((uint32_t)bp[3] << 8);
+      const int32_t serr = (len ^ 0xffffu) != nl ? ST_BAD_STORED : q + 32 + 8 * len > endbits ? ST_OVERREAD : 0;
+      if (serr) {
+        set_err(L, serr);
+        break;
+      }
+      const int32_t n = min((int32_t)len, isize - produced);
+      if (produced + n - p0 > TOUT) {
+        set_err(L, ST_SHORT);
+        break;
+      }
+      for (int i = lane; i < n; i += 64) L.out[sh + produced - p0 + i] = bp[4 + i];
+      produced += n;
+      pos = q + 32 + 8 * len;
+      __builtin_amdgcn_wave_barrier();
+      if (bfinal) break;
+      continue;
+    }
+    const int nlen = btype == 1 ? 288 : (int)((h >> 3) & 31) + 257;
+    const int ndist = btype == 1 ? 32 : (int)((h >> 8) & 31) + 1;
+    if (btype == 2 && (nlen > 286 || ndist > 30)) {
+      set_err(L, ST_BAD_TABLE);
+      break;
+    }
+    uint32_t a;
+    if (btype == 1) {
+      for (int i = lane; i < 320; i += 64) L.u.d.x.h.lens[i] = fixed_len(i);
+      a = pos + 3;
+    } else {
+      const int ncode = (int)((h >> 13) & 15) + 4;
+      for (int i = lane; i < 320; i += 64) L.u.d.x.h.lens[i] = 0;
+      for (int i = lane; i < HB_WORDS; i += 64) reinterpret_cast<uint32_t*>(L.u.d.T)[i] = W[hbase + i];
+      if (lane < 19)
+        L.u.d.x.h.clen[c_clorder3[lane]] = lane < ncode ? (uint8_t)peek_bits(W, clpos + 3 * lane, 3) : 0;
+      __builtin_amdgcn_wave_barrier();
+      bool ok = true;
+      L.u.d.x.h.clt[lane] = clt_entry(L.u.d.x.h.clen, lane, &ok);
+      L.u.d.x.h.clt[lane + 64] = clt_entry(L.u.d.x.h.clen, lane + 64, &ok);
+      if (__any(!ok)) {
+        set_err(L, ST_BAD_TABLE);
+        break;
+      }
+      __builtin_amdgcn_wave_barrier();
+      a = read_lengths_wave(L, clpos + 3 * (uint32_t)ncode, nlen, ndist, endbits, hbase);
+      __builtin_amdgcn_wave_barrier();
+      if (L.misc[M_ERR]) break;
+      if (L.u.d.x.h.lens[256] == 0) {  // an EOB code is required
+        set_err(L, ST_BAD_TABLE);
+        break;
+      }
+    }
+    // ---- tables, pair table
+    build_tables_wave(L, nlen, ndist);
+    if (L.misc[M_ERR]) break;
+    for (int i = lane; i < (1 << LR); i += 64) {
+      const uint32_t e1 = L.u.d.T[i];
+      const uint32_t l1 = e1 & 15;
+      uint16_t v = 0;
+      if (l1 > 0 && !(e1 & 16) && l1 < (uint32_t)LR) {
+        const uint32_t e2 = L.u.d.T[(uint32_t)i >> l1];
+        const uint32_t l2 = e2 & 15;
+        if (l2 > 0 && !(e2 & 16) && l1 + l2 <= (uint32_t)LR) v = (uint16_t)e2;
+      }
+      L.u.d.x.pair[i] = v;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const bool slow = L.misc[M_SLOW] != 0;
+    if (a > endbits) {
+      set_err(L, ST_OVERREAD);
+      break;
+    }
+    tick(0);
+    // ---- speculative segments, one per lane (registers hold the per-lane arrays)
+    const uint32_t span = endbits - a;
+    const int nl = (int)max(1u, min(64u, span / 96u));
+    const uint32_t seg = (span + nl - 1) / nl;
+    const bool act = lane < nl;
+    const uint32_t sB = a + (uint32_t)lane * seg;
+    const uint32_t sE = lane == nl - 1 ? 0xffffffffu : sB + seg;
+    int32_t AB = -1, AE = 0, AC = 0, SE = 0, SC = 0;
+    if (act) {
+      const uint32_t start = lane == 0 ? a : (sB > a + OV ? sB - OV : a);
+      for (int j = 0; j < T_NCK; j++) L.ck[j * 64 + lane] = 0xffffffffu;
+      int32_t B = -1, E = 0, c = 0;
+      const int f = slow ? run_seg<true>(gsrc, L, start, sB, sE, endbits, &B, &E, &c, L.ck + lane, 64, CKI, T_NCK)
+                         : run_seg<false>(gsrc, L, start, sB, sE, endbits, &B, &E, &c, L.ck + lane, 64, CKI, T_NCK);
+      AB = B;
+      AE = (E << 3) | f;
+      AC = c;
+      SE = AE;
+      SC = c;
+    }
+    tick(1);
+    // ---- rounds, wave-local: a lane whose first boundary differs from its predecessor's exit
+    //      re-decodes from that exit until it meets its speculative path at a checkpoint
+#ifdef DQ_CHECKED
+    gsrc.tag = 5u << 12;
+#endif
+    for (int round = 0; round <= nl; round++) {
+      const int32_t pe = __shfl_up(AE, 1, 64);
+      const bool need = act && lane > 0 && (pe & 7) == F_EXIT && AB != (pe >> 3);
+      if (!__any(need)) break;
+      bool changed = false;
+      if (need) {
+        const uint32_t s0 = (uint32_t)(pe >> 3);
+        int32_t E = 0, c = 0;
+        const int f = slow ? run_redo<true>(gsrc, L, s0, sB, sE, endbits, L.ck + lane, 64, SE, SC, &E, &c, CKI, T_NCK)
+                           : run_redo<false>(gsrc, L, s0, sB, sE, endbits, L.ck + lane, 64, SE, SC, &E, &c, CKI, T_NCK);
+        const int32_t ae = (E << 3) | f;
+        changed = ae != AE;
+        AB = (int32_t)s0;
+        AE = ae;
+        AC = c;
+      }
+      if (!__any(changed)) break;
+    }
+    // ---- counts -> offsets (the first non-exit lane ends the deflate block)
+    const int myF = act ? (AE & 7) : F_DEAD;
+    const uint64_t nonexit = __ballot(act && myF != F_EXIT);
+    const int last = nonexit ? (int)__builtin_ctzll(nonexit) : nl - 1;
+    const int32_t cv = lane <= last ? AC : 0;
+    const int32_t incl = wave_incl_scan(cv, lane);
+    const int32_t total = __shfl(incl, 63, 64);
+    const int32_t myoff = produced + incl - cv;
+    const bool full = produced + total >= isize;
+    const int32_t fl = __shfl(myF, last, 64);
+    const int32_t nextpos = __shfl(AE >> 3, last, 64);
+    if (!full && fl != F_EOB) {
+      set_err(L, fl == F_ERR ? ST_BAD_CODE : ST_SHORT);
+      break;
+    }
+    if (min(isize, produced + total) - p0 > TOUT) {  // the block kernel checked the bound
+      set_err(L, ST_SHORT);
+      break;
+    }
+    tick(2);
+    // ---- emit into the tail image
+#ifdef DQ_CHECKED
+    gsrc.tag = 6u << 12;
+#endif
+    if (lane <= last && myoff < isize) {
+      if (slow) emit_seg<true>(gsrc, L, (uint32_t)AB, sE, endbits, myoff, isize, sh, p0);
+      else emit_seg<false>(gsrc, L, (uint32_t)AB, sE, endbits, myoff, isize, sh, p0);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    produced = min(isize, produced + total);
+    tick(3);
+    if (full || bfinal) break;
+    pos = (uint32_t)nextpos;
+  }
+  int32_t err = L.misc[M_ERR];
+  if (!err && produced != isize) err = ST_SHORT;
+  if (err) {
+    if (lane == 0) status[b] = err;
+    return;
+  }
+  const uint64_t t1 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
+  // ---- resolve the tail, row by row (64 bytes: one per lane)
+  const int32_t n = isize - p0;
+  const int nrows = (n + 63) >> 6;
+  uint8_t* const O = L.out + sh;  // tail byte k at O[k]
+  const uint64_t* bm64 = reinterpret_cast<const uint64_t*>(L.bm);
+  {  // the match carried into every row (its descriptor is overwritten once its row is resolved)
+    int run = -1;
+    for (int r0 = 0; r0 < nrows; r0 += 64) {
+      const int r = r0 + lane;
+      const uint64_t m = r < nrows ? bm64[r] : 0ull;
+      const int lastr = m ? 64 * r + 63 - (int)__clzll(m) : -1;
+      const int incl = max(wave_incl_max(lastr), run);
+      int ex = __shfl_up(incl, 1, 64);
+      if (lane == 0) ex = run;
+      uint64_t cr = 0;
+      if (r < nrows && ex >= 0) {
+        const uint32_t d = load_desc(L, sh + ex);
+        if (ex + (int32_t)(d >> 15) + 3 > 64 * r) cr = (uint64_t)d << 32 | (uint32_t)(ex + 1);
+      }
+      if (r < nrows) L.u.r.carry[r] = cr;
+      run = __shfl(incl, 63, 64);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
+  const uint8_t* Ub = U + ub + p0;  // the tail's first byte in U: sources before it are final
+  // the first hop of byte x = 64 row + lane: its owner (this row's bitmap word, else the carried
+  // match) and the copy source (< 0: a byte before the tail, in U); descriptors of this row and
+  // the next are intact until this row is resolved
+  auto hop = [&](int row, bool& copy) -> int32_t {
+    const int32_t x = 64 * row + lane;
+    const uint64_t mi = bm64[row] & (~0ull >> (63 - lane));
+    int32_t ms;
+    uint32_t desc;
+    if (mi) {
+      ms = 64 * row + 63 - (int32_t)__clzll(mi);
+      desc = load_desc(L, sh + ms);
+    } else {
+      const uint64_t cr = L.u.r.carry[row];
+      ms = (int32_t)(uint32_t)cr - 1;
+      desc = (uint32_t)(cr >> 32);
+    }
+    const int32_t len = (int32_t)(desc >> 15) + 3, D = (int32_t)(desc & 0x7fff) + 1;
+    copy = x < n && ms >= 0 && x < ms + len;
+    const int32_t jj = x - ms;
+    int32_t r = jj;
+    if (__builtin_expect(__any(copy && jj >= D), 0)) {
+      const int32_t q = (int32_t)((float)jj * __builtin_amdgcn_rcpf((float)D));
+      r = jj - q * D;
+      r = r >= D ? r - D : r;
+    }
+    return ms - D + r;
+  };
+  // pass 1: every byte whose source lies before the tail reads it from U into g (eight rows of
+  // loads in flight at a time: U is not in cache, and one row's load at a time was most of the
+  // kernel's time)
+  for (int r0 = 0; r0 < nrows; r0 += 8) {
+    int32_t sv[8];
+    bool cv[8];
+    uint8_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {  // (r0 + j < nrows is uniform)
+      bool c = false;
+      sv[j] = r0 + j < nrows ? hop(r0 + j, c) : 0;
+      cv[j] = c && sv[j] < 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) v[j] = cv[j] ? Ub[sv[j]] : (uint8_t)0;
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+      if (cv[j]) L.u.r.g[64 * (r0 + j) + lane] = v[j];
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const uint64_t t2 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
+  // pass 2: rows in order
+  for (int row = 0; row < nrows; row++) {
+    const int32_t x = 64 * row + lane;
+    bool copy;
+    const int32_t src = hop(row, copy);
+    DQ_CHK(!copy || (src >= -p0 && src < x), CHK_K2_SRC);
+    const bool local = copy && src >= 64 * row;
+    if (copy && !local) O[x] = src < 0 ? L.u.r.g[x] : O[src];
+    uint64_t pend = __ballot(local);
+    uint64_t done = ~pend;
+    while (pend) {  // same-row sources: a lane copies once its source lane's byte is final
+      const bool go = local && ((pend >> lane) & 1) && ((done >> (src & 63)) & 1);
+      if (go) O[x] = O[src];
+      const uint64_t g = __ballot(go);
+      done |= g;
+      pend &= ~g;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  // ---- store: bytes up to the first 16-byte line of U, the lines, the last bytes
+  uint8_t* dst = U + ub + p0;
+  const int head = min((16 - sh) & 15, n);
+  const int32_t lines = (n - head) / 16;
+  for (int x = lane; x < head; x += 64) dst[x] = O[x];
+  for (int32_t k = lane; k < lines; k += 64) {
+    const uint4 v = *reinterpret_cast<const uint4*>(O + head + 16 * k);
+    uint4* d = reinterpret_cast<uint4*>(dst + head + 16 * k);
+    if (sflags & 2) st_nt(d, v);
+    else *d = v;
+  }
+  for (int x = head + 16 * lines + lane; x < n; x += 64) dst[x] = O[x];
+  // ---- CRC32 of the block: the prefix's register shifted past the tail, xor the tail's
+  if (verify_crc) {
+    for (int i = lane; i < 256; i += 64) L.u.crc[i] = c_crc4[0][i];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const int32_t sl = (n + 63) >> 6;
+    const int32_t s0 = min(n, lane * sl), s1 = min(n, s0 + sl);
+    uint32_t cr = 0;
+    for (int32_t x = s0; x < s1; x++) cr = L.u.crc[(cr ^ O[x]) & 0xff] ^ (cr >> 8);
+    cr = gf2_mulmod(x8n_tail((uint32_t)(n - s1)), cr);
+    cr = (uint32_t)__shfl((int)wave_incl_xor(cr), 63, 64);
+    if (lane == 0) {
+      const uint32_t raw = gf2_mulmod(x8n_tail((uint32_t)n), td.crc_raw) ^ cr;
+      const uint32_t crc = (raw ^ crc_init[isize]) ^ 0xffffffffu;
+      const uint8_t* tr = C + cpos + csize - 8;
+      const uint32_t want = (uint32_t)tr[0] | ((uint32_t)tr[1] << 8) | ((uint32_t)tr[2] << 16) | ((uint32_t)tr[3] << 24);
+      if (crc != want) status[b] = ST_CRC;
+    }
+  }
+  if (TIMING && lane == 0) {
+    tim[gi * 8] = t1 - t0;      // decode: headers, tables, spec, rounds, emit
+    tim[gi * 8 + 1] = t2 - t1;  // resolve pass 1 (carries, U loads)
+    tim[gi * 8 + 2] = __builtin_amdgcn_s_memtime() - t2;  // rows, store, CRC
+    tim[gi * 8 + 3] = 1;
+    for (int k = 0; k < 4; k++) tim[gi * 8 + 4 + k] = tph[k];
+  }
 }
 
 uint32_t h_mul(uint32_t a, uint32_t b) {
@@ -1582,6 +2210,7 @@ uint32_t h_mul(uint32_t a, uint32_t b) {
 struct HostTables {
   uint32_t crc4[4][256];
   uint32_t slice[WG];
+  uint32_t x2n[32];  // x^(2^k) mod P
   std::vector<uint32_t> init;  // CRC of n zero bytes with initial register ~0, n = 0..65536
   HostTables() : init(65537) {
     for (uint32_t i = 0; i < 256; i++) {
@@ -1591,7 +2220,6 @@ struct HostTables {
     }
     for (int j = 1; j < 4; j++)
       for (uint32_t i = 0; i < 256; i++) crc4[j][i] = (crc4[j - 1][i] >> 8) ^ crc4[0][crc4[j - 1][i] & 0xff];
-    uint32_t x2n[32];
     uint32_t p = 1u << 30;  // x^1
     x2n[0] = p;
     for (int k = 1; k < 32; k++) x2n[k] = p = h_mul(p, p);
@@ -1634,6 +2262,7 @@ const uint32_t* inflate3_tables(int device) {
     bool ok = hipSetDevice(device) == hipSuccess;
     ok = ok && hipMemcpyToSymbol(HIP_SYMBOL(c_crc4), H.crc4, sizeof H.crc4) == hipSuccess;
     ok = ok && hipMemcpyToSymbol(HIP_SYMBOL(c_slice_shift), H.slice, sizeof H.slice) == hipSuccess;
+    ok = ok && hipMemcpyToSymbol(HIP_SYMBOL(c_x2n), H.x2n, sizeof H.x2n) == hipSuccess;
     ok = ok && hipMalloc(&D.crc_init, sizeof(uint32_t) * H.init.size()) == hipSuccess;
     ok = ok && hipMemcpy(D.crc_init, H.init.data(), sizeof(uint32_t) * H.init.size(),
                          hipMemcpyHostToDevice) == hipSuccess;
@@ -1646,7 +2275,7 @@ const uint32_t* inflate3_tables(int device) {
 void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* blk_csize,
                      const int32_t* blk_usize, const int64_t* uoff, int64_t nblk, uint8_t* U,
                      int32_t* status, int32_t verify_crc, const uint32_t* crc_init, uint64_t* tim,
-                     hipStream_t s, const int32_t* sel, int64_t nsel) {
+                     hipStream_t s, const int32_t* sel, int64_t nsel, void* tails_buf) {
   if (nblk <= 0) return;
   const int64_t ngrid = sel ? nsel : nblk;
   if (ngrid <= 0) return;
@@ -1664,10 +2293,14 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
   }();
   // DQ_LDSPAD: extra dynamic LDS per workgroup (occupancy experiments: 80000 = one workgroup per CU)
   static const unsigned ldspad = getenv("DQ_LDSPAD") ? (unsigned)atoi(getenv("DQ_LDSPAD")) : 0u;
+  // DQ_TAIL=0: no tail kernel (the block kernel decodes every deflate block itself)
+  static const bool tail_on = !getenv("DQ_TAIL") || atoi(getenv("DQ_TAIL")) != 0;
+  TailDesc* td = tail_on ? static_cast<TailDesc*>(tails_buf) : nullptr;
+  if (td) (void)hipMemsetAsync(td, 0, sizeof(TailDesc) * (size_t)ngrid, s);
 #define DQ_LAUNCH(TM, NBT, GT)                                                                  \
   hipLaunchKernelGGL((inflate_block_kernel<TM, NBT, GT>), dim3((unsigned)ngrid), dim3(WG), ldspad, s, C, \
                      blk_pos, blk_csize, blk_usize, uoff, ngrid, U, status, verify_crc, crc_init, tim, ov, \
-                     sflags, sel)
+                     sflags, sel, td)
 #define DQ_CFGS(TM)                       \
   switch (cfg) {                          \
     case 1: DQ_LAUNCH(TM, 1, 4); break;   \
@@ -1681,6 +2314,16 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
   }
 #undef DQ_CFGS
 #undef DQ_LAUNCH
+  // DQ_TIMING: the block kernel's phases in tim[0, 24 ngrid), the tail kernel's in the 4 ngrid
+  // words after them
+  if (td && tim)
+    hipLaunchKernelGGL((inflate_tail_kernel<true>), dim3((unsigned)((ngrid + TW - 1) / TW)), dim3(64 * TW), 0, s,
+                       C, blk_pos, blk_csize, blk_usize, uoff, ngrid, U, status, verify_crc, crc_init, ov,
+                       sflags, sel, td, tim + 24 * ngrid);  // 8 words per tail
+  else if (td)
+    hipLaunchKernelGGL((inflate_tail_kernel<false>), dim3((unsigned)((ngrid + TW - 1) / TW)), dim3(64 * TW), 0, s,
+                       C, blk_pos, blk_csize, blk_usize, uoff, ngrid, U, status, verify_crc, crc_init, ov,
+                       sflags, sel, td, nullptr);
 }
 
 }  // namespace dq

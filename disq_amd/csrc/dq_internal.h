@@ -137,10 +137,13 @@ void launch_exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, int64
 // live in each device's memory: inflate3_tables(device) initialises them once per device (thread
 // safe) and returns that device's table of x^(8n) * ~0 mod P, n = 0..65536 (nullptr on failure).
 const uint32_t* inflate3_tables(int device);
+// tails: 16 bytes of device scratch per launched block (the tail kernel's descriptors; nullptr:
+// the block kernel decodes every deflate block itself)
+constexpr size_t INFLATE_TAIL_BYTES = 16;
 void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* blk_csize,
                      const int32_t* blk_usize, const int64_t* uoff, int64_t nblk, uint8_t* U,
                      int32_t* status, int32_t verify_crc, const uint32_t* crc_init, uint64_t* tim,
-                     hipStream_t s, const int32_t* sel = nullptr, int64_t nsel = 0);
+                     hipStream_t s, const int32_t* sel, int64_t nsel, void* tails);
 
 // out[0] = sum of (csize - 26) over the blocks; out[1] / out[2] = uoff of the first block starting
 // after / at or after x (ulen if none); out[3] = the index of the first block starting after x.
