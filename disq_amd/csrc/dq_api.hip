@@ -685,8 +685,8 @@ static int run_pipeline(dq_ctx* ctx) {
     static const bool timing = getenv("DQ_TIMING") != nullptr;
     uint64_t* tim = nullptr;
     if (timing) {
-      HIPCHK(hipMalloc(&tim, sizeof(uint64_t) * 32 * (size_t)std::max<int64_t>(1, nblk)));
-      HIPCHK(hipMemsetAsync(tim, 0, sizeof(uint64_t) * 32 * (size_t)std::max<int64_t>(1, nblk), s));
+      HIPCHK(hipMalloc(&tim, sizeof(uint64_t) * 40 * (size_t)std::max<int64_t>(1, nblk)));
+      HIPCHK(hipMemsetAsync(tim, 0, sizeof(uint64_t) * 40 * (size_t)std::max<int64_t>(1, nblk), s));
     }
     HIPCHK(hipEventRecord(ctx->ev[5], s));
     if ((rc = ensure_all(ctx, ctx->tails, INFLATE_TAIL_BYTES * (size_t)std::max<int64_t>(1, nblk)))) return rc;
@@ -696,7 +696,7 @@ static int run_pipeline(dq_ctx* ctx) {
                     ctx->tails.p);
     HIPCHK(hipEventRecord(ctx->ev[6], s));
     if (timing) {
-      std::vector<uint64_t> h(32 * (size_t)nblk);
+      std::vector<uint64_t> h(40 * (size_t)nblk);
       HIPCHK(hipMemcpyAsync(h.data(), tim, 8 * h.size(), hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
       (void)hipFree(tim);
@@ -716,14 +716,15 @@ static int run_pipeline(dq_ctx* ctx) {
               "BGZF block %.3f\n", acc[16] / nb, acc[17] / nb, acc[18] / nb, acc[19] / nb, acc[21] / nb,
               (acc[0] - acc[16]) / nb, (acc[1] - acc[17]) / nb, (acc[2] - acc[18]) / nb,
               (acc[3] - acc[19]) / nb, (acc[5] - acc[21]) / nb, acc[22] / nb);
-      double ta[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      double ta[16] = {0};
       for (int64_t i = 0; i < nblk; i++)
-        for (int k = 0; k < 8; k++) ta[k] += (double)h[24 * (size_t)nblk + 8 * (size_t)i + k];
+        for (int k = 0; k < 16; k++) ta[k] += (double)h[24 * (size_t)nblk + 16 * (size_t)i + k];
       if (ta[3] > 0)
         fprintf(stderr, "[dq] tail kernel: %.0f tails (%.1f %% of blocks), cycles per tail (lane 0): "
-                "decode=%.0f (header+tables=%.0f spec=%.0f rounds=%.0f emit=%.0f) resolve_prefetch=%.0f "
-                "rows_store_crc=%.0f\n", ta[3], 100.0 * ta[3] / nb, ta[0] / ta[3], ta[4] / ta[3],
-                ta[5] / ta[3], ta[6] / ta[3], ta[7] / ta[3], ta[1] / ta[3], ta[2] / ta[3]);
+                "decode=%.0f (header=%.0f tables=%.0f spec=%.0f rounds=%.0f emit=%.0f) "
+                "resolve_start=%.0f rows_store_crc=%.0f\n", ta[3], 100.0 * ta[3] / nb, ta[0] / ta[3],
+                ta[4] / ta[3], ta[5] / ta[3], ta[6] / ta[3], ta[7] / ta[3], ta[8] / ta[3],
+                ta[1] / ta[3], ta[2] / ta[3]);
     }
   }
   dbg(s, "inflate", nblk, ulen);
@@ -1195,8 +1196,8 @@ static int text_run(dq_ctx* ctx, int32_t drop_hash) {
 
 // ------------------------------------------------------------------ BGZF deflate (write path)
 // htsjdk BlockCompressedOutputStream over a byte stream in HBM: blocks of 65280 bytes compressed
-// in batches (per block 512 KiB of staged symbols and 256 KiB of match-finder buckets), packed
-// into ctx->z_out.
+// in batches (per block 1 MiB of staged-symbol space, of which the parse touches about 50 KB, and
+// 6.6 KB of lane / chunk records), packed into ctx->z_out.
 static int bgzf_compress_dev(dq_ctx* ctx, const uint8_t* d_src, int64_t len, double* ms) {
   if (!deflate_tables(ctx->o.device)) RET(DQ_EDEVICE, "deflate table initialisation failed");
   hipStream_t s = ctx->s;
@@ -1204,7 +1205,7 @@ static int bgzf_compress_dev(dq_ctx* ctx, const uint8_t* d_src, int64_t len, dou
   const int64_t batch = std::min<int64_t>(std::max<int64_t>(nblk, 1), 2048);
   int rc;
   if ((rc = ensure_all(ctx, ctx->z_stage, bgzf_stage_bytes(batch)))) return rc;
-  if ((rc = ensure_all(ctx, ctx->z_link, bgzf_link_bytes(batch)))) return rc;
+  if ((rc = ensure_all(ctx, ctx->z_link, bgzf_meta_bytes(batch)))) return rc;
   if ((rc = ensure_all(ctx, ctx->z_slots, (size_t)batch * 65536))) return rc;
   if ((rc = ensure_all(ctx, ctx->z_size, 4 * (size_t)batch))) return rc;
   if ((rc = ensure_all(ctx, ctx->z_off, 8 * (size_t)batch))) return rc;
@@ -1217,22 +1218,34 @@ static int bgzf_compress_dev(dq_ctx* ctx, const uint8_t* d_src, int64_t len, dou
     const int64_t nb = std::min(batch, nblk - b0);
     static const bool timing = getenv("DQ_DEFLATE_TIMING") != nullptr;
     uint64_t* tim = nullptr;
-    if (timing) HIPCHK(hipMalloc(&tim, 8 * 8 * (size_t)nb));
-    launch_bgzf_deflate(d_src, len, b0, nb, ctx->z_stage.as<uint32_t>(), ctx->z_link.as<uint16_t>(),
+    const size_t ntim = 8 * (size_t)nb * 3;  // 2 parse workgroups + 1 code workgroup per block
+    if (timing) HIPCHK(hipMalloc(&tim, 8 * ntim));
+    launch_bgzf_deflate(d_src, len, b0, nb, ctx->z_stage.as<uint32_t>(), ctx->z_link.as<uint32_t>(),
                         ctx->z_slots.as<uint8_t>(), ctx->z_size.as<int32_t>(), tim, s);
     HIPCHK(hipGetLastError());
     if (timing) {
-      std::vector<uint64_t> h(8 * (size_t)nb);
+      std::vector<uint64_t> h(ntim);
       HIPCHK(hipMemcpyAsync(h.data(), tim, 8 * h.size(), hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
       (void)hipFree(tim);
-      double acc[8] = {0};
-      for (int64_t i = 0; i < nb; i++)
-        for (int k = 1; k < 8; k++) acc[k] += (double)(h[8 * (size_t)i + k] - h[8 * (size_t)i + k - 1]);
-      static const char* nm[8] = {"", "load", "crc+links", "parse", "huffman", "count+scan", "write", "store"};
-      fprintf(stderr, "[dq] deflate phase cycles per block:");
-      for (int k = 1; k < 8; k++) fprintf(stderr, " %s=%.0f", nm[k], acc[k] / (double)nb);
-      fprintf(stderr, "\n");
+      // parse workgroups (per chunk), then the code workgroups (per block)
+      static const char* nm[2][8] = {{"", "load", "buckets", "parse", "merge+hist", "", "", ""},
+                                     {"", "sum", "huffman", "count+scan", "write", "store", "", ""}};
+      const int64_t cnt[2] = {2 * nb, nb};
+      size_t at = 0;
+      for (int kk = 0; kk < 2; kk++) {
+        double acc[8] = {0};
+        for (int64_t i = 0; i < cnt[kk]; i++)
+          for (int k = 1; k < 8; k++) {
+            const uint64_t a = h[at + 8 * (size_t)i + k], z = h[at + 8 * (size_t)i + k - 1];
+            if (a) acc[k] += (double)(a - z);
+          }
+        at += 8 * (size_t)cnt[kk];
+        fprintf(stderr, "[dq] deflate %s cycles per workgroup:", kk ? "code" : "parse");
+        for (int k = 1; k < 8; k++)
+          if (nm[kk][k][0]) fprintf(stderr, " %s=%.0f", nm[kk][k], acc[k] / (double)cnt[kk]);
+        fprintf(stderr, "\n");
+      }
     }
     HIPCHK(hipMemcpyAsync(sz.data(), ctx->z_size.p, 4 * (size_t)nb, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));

@@ -9,38 +9,47 @@
 // kernel's own (java.util.zip.Deflater's exact bit stream is not reproduced): the output is valid
 // BGZF whose blocks inflate to exactly htsjdk's block contents.
 //
-// One 256-thread workgroup per block, the block's bytes in LDS (79 KB: 2 workgroups per CU).
+// Two kernels per batch of blocks, everything the match finder touches in LDS:
+//   bgzf_parse_kernel: one 512-thread workgroup per CHUNK, half a block (32640 bytes), holding the
+//      chunk's bytes plus up to 16 KiB before it (its window reach) and the hash-bucket lists of
+//      all those positions (3 bytes of LDS per position: 160 KB, one workgroup per CU).  A chunk's
+//      matches end inside it and reach back at most 16 KiB before its start (the 32 KiB DEFLATE
+//      window inside the first chunk): tools/deflate_model.c puts that at zlib level 5's ratio on
+//      the WGS stream and the golden BAM / VCF streams (profiles/r4_deflate_chunk_model.txt).
 //   1. Match finder: every position with a 3-byte suffix goes into one of 2048 hash buckets, in
 //      ascending order inside its bucket (counts by LDS atomics, bucket starts by a scan, then an
-//      ordered scatter in stripes of 256 positions: the lanes of a wave with equal hashes are
-//      found by one ballot per hash bit, and the four waves take their bucket cursors in turn).
-//      A position's candidates are the entries before it in its bucket, most recent first: a
-//      contiguous run of the bucket list, so a search issues all its candidate loads at once
-//      instead of chasing zlib's hash-chain links one dependent load at a time.
-//   2. Parse: lane t parses from its segment start [255 t, 255 t + 255) with zlib-style lazy
-//      evaluation (a match shorter than `lazy` is deferred while the next position's is longer;
-//      the look-ahead search walks chain / 4 candidates once the current match is `good` long, as
-//      zlib's deflate_slow), the longest match among `chain` candidates (stopping at `nice`),
-//      matches running on past the segment end.  A parse step depends on its position alone, so two parses that reach the
-//      same position continue identically: from its exit, each lane keeps parsing until it hits a
-//      symbol boundary of a later lane's parse (usually within a few symbols) and records the
-//      merge; one thread then follows the merges from lane 0, which gives every lane the part of
-//      its symbols (and continuation) on the block's one parse.  No matches are cut at lane
-//      boundaries.  The merged parse is valid but not always the one a single sequential pass
-//      would make: a merge can land inside a lazy step of the continuing lane (after a deferred
-//      literal whose look-ahead search walked chain / 4 candidates, where a sequential pass would
-//      start a full search), and a continuation that finds no merge within its staging is ended
+//      ordered scatter with no barriers: wave w owns the buckets h >> 8 == w and walks every
+//      position in order, the lanes of a 64-position step with equal hashes ranked by one ballot
+//      per hash bit).  A position's candidates are the entries before it in its bucket, most
+//      recent first (its own slot is found by a 16-way search of the bucket): a contiguous run of
+//      the list, so a search issues a batch of candidate loads at once instead of chasing zlib's
+//      hash-chain links one dependent load at a time.
+//   2. Parse: lane t parses from its 64-byte segment start with zlib-style lazy evaluation (a
+//      match shorter than `lazy` is deferred while the next position's is longer; the look-ahead
+//      search walks chain / 4 candidates once the current match is `good` long, as zlib's
+//      deflate_slow), the longest match among `chain` candidates (stopping at `nice`), matches
+//      running on past the segment end.  A parse step depends on its position alone, so two
+//      parses that reach the same position continue identically: from its exit, each lane keeps
+//      parsing until it hits a symbol boundary of a later lane's parse (usually within a few
+//      symbols) and records the merge; pointer jumping over the merges from lane 0 marks the lanes
+//      on the chunk's one parse and the symbol each starts from.  The merged parse is valid but
+//      not always the one a single sequential pass would make: a merge can land inside a lazy
+//      step of the continuing lane (after a deferred literal whose look-ahead search walked
+//      chain / 4 candidates), and a continuation that finds no merge within its staging is ended
 //      on the next boundary of a later lane with a shortened match.
-//      (Defaults chain 96, lazy 32, nice 96, good 8: ratio 2.858 on the synthetic WGS stream, zlib
-//      level 5 -- htsjdk's -- 2.857; profiles/r3as_deflate_good_sweep.txt for the frontier.)
-//   3. Codes: histograms of the parse; wave 0 builds the literal/length code and wave 1 the
-//      distance code (a rank sort, Moffat-Katajainen minimum-redundancy lengths, a Kraft fix-up
-//      capping them at 15), the code-length sequence is run-length coded; the block is coded
-//      dynamic (BTYPE 10) or fixed (01), whichever is shorter.
-//   4. Emit: each lane's bit count gives its offset by an exclusive scan; every lane OR-s its bits
-//      into the LDS image of the block (the input is dead by then).  A block whose code would not
-//      fit BSIZE (or whose parse overflowed its staging) is stored (BTYPE 00).
+//      Symbols are staged per lane in HBM (one word each); the chunk's literal/length and distance
+//      histograms over its parse, its CRC and a word per lane (first symbol, counts) go with them.
+//   bgzf_code_kernel: one 256-thread workgroup per block (73 KB of LDS, two per CU).
+//   3. Codes: the two chunks' histograms summed; wave 0 builds the literal/length code and wave 1
+//      the distance code (a rank sort, Moffat-Katajainen minimum-redundancy lengths, a Kraft
+//      fix-up capping them at 15), the code-length sequence is run-length coded; the block is
+//      coded dynamic (BTYPE 10) or fixed (01), whichever is shorter -- one DEFLATE block per
+//      member, as zlib writes a 64 KiB input.
+//   4. Emit: each lane's bit count gives its offset by an exclusive scan; every thread OR-s its
+//      four lanes' bits into the LDS image of the block.  A block whose code would not fit BSIZE
+//      (or whose parse overflowed its staging) is stored (BTYPE 00).
 // CRC32: per-lane table CRC over the segment, combined with x^(8 n) mod P multipliers.
+// (Defaults chain 96, lazy 32, nice 96, good 8.)
 #include "dq_internal.h"
 
 #include <algorithm>
@@ -49,17 +58,32 @@
 namespace dq {
 namespace {
 
-constexpr int DWG = 256;                 // threads per block
 constexpr int BLK_U = 65280;             // htsjdk DEFAULT_UNCOMPRESSED_BLOCK_SIZE
-constexpr int SEG = BLK_U / DWG;         // 255 bytes per lane
-constexpr int HBITS = 11;                // hash buckets (LDS counts / offsets: 8 KB)
+constexpr int NCH = 2;                   // chunks per block
+constexpr int CH = BLK_U / NCH;          // 32640 bytes per chunk
+constexpr int PSEG = 64;                 // bytes per parsing lane
+constexpr int PL = CH / PSEG;            // 510 lanes per chunk
+constexpr int PWG = 512;                 // threads per chunk workgroup
+constexpr int XW = 16384;                // window reach before the chunk start
+constexpr int NPMAX = CH + XW;           // bytes (positions) a chunk workgroup holds
+constexpr int HBITS = 11;                // hash buckets
 constexpr int MAXM = 258;
 constexpr int WIN = 32768;               // DEFLATE window
-constexpr int OWN_WORDS = 288;           // a lane's own symbols (<= 255 + the last step's <= 32 deferrals)
-constexpr int CONT_WORDS = 224;          // its continuation past its segment end
+constexpr int OWN_WORDS = 100;           // a lane's own symbols (<= 64 + the last step's <= 33)
+constexpr int CONT_WORDS = 156;          // its continuation past its segment end
 constexpr int LANE_WORDS = OWN_WORDS + CONT_WORDS;
 constexpr int MAX_DEFLATE = 65536 - 26;  // BSIZE limit: 18-byte header + payload + 8 trailer
 constexpr int MAXCAND = 128;             // candidates per match search at most (cfg.chain)
+constexpr int CWG = 256;                 // threads of the code kernel
+constexpr int NLANE = NCH * PL;          // 1020 lanes per block; code thread i owns lanes 4i..4i+3
+// per block in `meta`: a word per lane (NCH x PWG), then NCH chunk records of CI_WORDS
+constexpr int CI_WORDS = 320;
+enum { CI_LL = 0, CI_D = 286, CI_CRC = 316, CI_OVER = 317, CI_BYTES = 318 };
+constexpr int META_WORDS = NCH * (PWG + CI_WORDS);
+// lane word: first own symbol | own symbols << 8 | continuation symbols << 16 | reached << 24
+constexpr uint32_t LM_REACHED = 1u << 24;
+static_assert(PL * PSEG == CH && PL <= PWG && NLANE <= 4 * CWG, "lane layout");
+static_assert(OWN_WORDS < 256 && CONT_WORDS < 256, "lane word fields");
 
 __constant__ uint32_t c_dcrc[256];
 __constant__ uint16_t c_lbase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
@@ -116,19 +140,7 @@ __device__ inline void fixed_ll(int sym, uint32_t& code, int& len) {
   else { len = 8; code = rev(0xC0 + sym - 280, 8); }
 }
 
-struct alignas(16) DLds {
-  uint8_t in[65536 + 16];     // the block's bytes; later the deflate image (<= 65510 bytes)
-  uint32_t crc_t[256];
-  uint32_t lane_bits[DWG];    // the parse's exit of each lane; later its bit count, bit offset
-  uint32_t lane_crc[DWG];
-  uint32_t lane_mrg[DWG];     // continuation: merge lane | symbol index << 9 | count << 18 | over << 27
-  uint32_t lane_eff[DWG];     // effective symbols: own start | continuation count << 9 | EFF_* flags
-  uint16_t lane_nsym[DWG];    // own symbols
-  int32_t head[1 << HBITS];   // bucket counts -> ends; then histograms, code tables (H_* below)
-  int32_t misc[8];
-};
-constexpr uint32_t EFF_REACHED = 1u << 18, EFF_EOB = 1u << 19;
-// word offsets inside DLds::head once the buckets are dead
+// word offsets of the code tables in the code kernel's table area
 enum { H_LL = 0, H_D = 288, H_CL = 320, C_LL = 352, C_D = 640, C_CL = 672, H_TOK = 704,
        H_SORT = 864, H_W = 1152, H_LEN = 1440, H_LEN_D = 1728, H_LEN_CL = 1760, H_SORT_D = 1792,
        H_W_D = 1824, H_CNT = 1856, H_CNT_D = 1890, H_BL = 1924, H_END = 1956 };
@@ -254,12 +266,14 @@ struct ImgOut {  // LSB-first bits OR-ed into the LDS image from bit position p 
     acc |= (uint64_t)v << n;
     n += len;
     if (n >= 32) {
+      DQ_CHK(w < 65536 / 4, CHK_Z_IMAGE);
       atomicOr(&img[w++], (uint32_t)acc);
       acc >>= 32;
       n -= 32;
     }
   }
   __device__ void flush() {
+    DQ_CHK(n <= 0 || w < 65536 / 4, CHK_Z_IMAGE);
     if (n > 0) atomicOr(&img[w], (uint32_t)acc);
   }
 };
@@ -275,82 +289,6 @@ __device__ inline int sym_bytes(uint32_t w) {  // uncompressed bytes of a staged
 }
 __device__ inline uint64_t lanes_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
 
-// Match finder over the block's hash buckets: bl holds every position with a >= 3-byte suffix,
-// grouped by bucket (hash3) and ascending inside a bucket; gi[p] is p's index in bl; the bucket of
-// hash h ends at head[h] (it starts where bucket h - 1 ends).  The candidates of p are the
-// entries before gi[p] in its bucket, most recent first -- consecutive words of bl, so all of a
-// search's candidate loads are in flight together (no pointer chasing as in zlib's hash chains).
-struct Finder {
-  const DLds& L;
-  const uint16_t* __restrict__ bl;
-  const uint16_t* __restrict__ gi;
-  int n, chain, nice, good;
-  // longest match (>= 3, else 0) at p, at most lim bytes, among `chain` candidates; *dist its
-  // distance
-  __device__ int find(int p, int lim, int* dist, int chain) const {
-    *dist = 0;
-    if (lim < 3 || p + 3 > n) return 0;
-    const uint32_t h = hash3(L.in, p);
-    const int g = gi[p];
-    const int lo = max(h ? L.head[h - 1] : 0, g - chain);
-    const uint32_t p4 = ld4(L.in, p);
-    int best = 0, bd = 0;
-    const int cap = min(lim, nice);
-    for (int i0 = g - 1; i0 >= lo && best < cap; i0 -= 8) {
-      // a batch of 8 candidates: their positions (global) and first / scan-end words (LDS) are
-      // all loaded before any is tested, so the batch costs about one load latency of each kind
-      int q8[8];
-#pragma unroll
-      for (int k = 0; k < 8; k++) q8[k] = i0 - k >= lo ? (int)bl[i0 - k] : -1;
-      // only a candidate that also matches the byte at `best` can win: the 4 bytes ending there
-      // are tested first (zlib's scan_end test), with the best length at the batch start
-      const bool use_e = best >= 3;
-      const int be = use_e ? best - 3 : 0;
-      const uint32_t pe = ld4(L.in, p + be);
-      uint32_t x8[8], e8[8];
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const int q = q8[k] >= 0 ? q8[k] : p;
-        x8[k] = ld4(L.in, q) ^ p4;
-        e8[k] = ld4(L.in, q + be) ^ pe;
-      }
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const int q = q8[k];
-        if (q < 0 || p - q > WIN) break;
-        if ((x8[k] & 0xffffffu) || (use_e && e8[k])) continue;  // a hash collision / no match at best
-        // compared up to `cap` only: the first candidate that reaches it ends the search (the
-        // same choice as comparing every candidate in full), and only that one is extended on
-        uint32_t x = x8[k];
-        int l = 0;
-        while (x == 0 && l + 4 < cap) {
-          l += 4;
-          x = ld4(L.in, q + l) ^ ld4(L.in, p + l);
-        }
-        l = x ? l + (int)(__builtin_ctz(x) >> 3) : l + 4;
-        l = min(l, cap);
-        if (l > best) {
-          best = l;
-          bd = p - q;
-        }
-        if (best >= cap) break;
-      }
-    }
-    if (best >= cap && cap < lim) {  // the winner, extended to the end of its match
-      const int q = p - bd;
-      int l = cap;
-      uint32_t x = 0;
-      while (x == 0 && l < lim) {
-        x = ld4(L.in, q + l) ^ ld4(L.in, p + l);
-        l += x ? (int)(__builtin_ctz(x) >> 3) : 4;
-      }
-      best = min(l, lim);
-    }
-    *dist = bd;
-    return best >= 3 ? best : 0;
-  }
-};
-
 __device__ inline uint32_t lit_word(uint32_t b) { return b; }
 __device__ inline uint32_t match_word(int len, int d) {
   int sym, nx, xv, ds, dnx, dxv;
@@ -359,99 +297,215 @@ __device__ inline uint32_t match_word(int len, int d) {
   return (uint32_t)sym | ((uint32_t)xv << 9) | ((uint32_t)ds << 14) | ((uint32_t)dxv << 19);
 }
 
-// One parse step at p (zlib-style lazy evaluation: while the match at the next position is
+
+struct alignas(16) PLds {
+  uint8_t in[NPMAX + 16];     // bytes [r0, ce) of the block (+ zero pad for the 4-byte compares)
+  uint16_t bl[NPMAX];         // positions grouped by hash bucket, ascending inside a bucket
+  int32_t head[1 << HBITS];   // bucket counts -> cursors -> ends; later the chunk's histograms
+  uint32_t crc_t[256];
+  uint32_t lane_exit[PWG];    // the parse's exit of each lane; later jump pointers, first symbols
+  uint32_t lane_mrg[PWG];     // continuation: merge lane | symbol << 10 | count << 17 | over << 25
+  uint32_t lane_mark[PWG];    // on the chunk's parse
+  uint16_t lane_nsym[PWG];    // own symbols
+  uint32_t wred[16];
+  int32_t misc[8];
+};
+static_assert(sizeof(PLds) <= 160 * 1024, "one chunk workgroup per CU");
+
+// Match finder over the chunk's hash buckets: bl holds every local position x with a 3-byte
+// suffix (x + 3 <= np), grouped by bucket (hash3) and ascending inside a bucket; the bucket of
+// hash h ends at head[h] (it starts where bucket h - 1 ends).  The candidates of x are the entries
+// before x's own slot in its bucket, most recent first -- consecutive words of bl, so all of a
+// search's candidate loads are in flight together.
+struct Finder {
+  const PLds& L;
+  int np, chain, nice, good;
+  // the slot of x in the ascending list bl[lo, hi), which holds it: 16-way search
+  __device__ int slot(int lo, int hi, int x) const {
+    int a = lo, b = hi;
+    while (b - a > 16) {
+      const int st = (b - a) >> 4;
+      int m = 0;
+#pragma unroll
+      for (int k = 1; k < 16; k++) m += (int)L.bl[a + k * st] <= x;
+      const int na = a + m * st;
+      b = m == 15 ? b : na + st;
+      a = na;
+    }
+    int c = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) c += a + k < b && (int)L.bl[a + k] < x;
+    return a + c;
+  }
+  // longest match (>= 3, else 0) at x, at most lim bytes, among `chain` candidates; *dist its
+  // distance
+  __device__ int find(int x, int lim, int* dist, int chain) const {
+    *dist = 0;
+    if (lim < 3 || x + 3 > np) return 0;
+    const uint32_t h = hash3(L.in, x);
+    const int blo = h ? L.head[h - 1] : 0;
+    const int g = slot(blo, L.head[h], x);
+    const int lo = max(blo, g - chain);
+    const uint32_t p4 = ld4(L.in, x);
+    int best = 0, bd = 0;
+    const int cap = min(lim, nice);
+    for (int i0 = g - 1; i0 >= lo && best < cap; i0 -= 8) {
+      // a batch of 8 candidates: their positions and first / scan-end words are all loaded
+      // before any is tested, so the batch costs about one LDS latency of each kind
+      int q8[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) q8[k] = i0 - k >= lo ? (int)L.bl[i0 - k] : -1;
+      // only a candidate that also matches the byte at `best` can win: the 4 bytes ending there
+      // are tested first (zlib's scan_end test), with the best length at the batch start
+      const bool use_e = best >= 3;
+      const int be = use_e ? best - 3 : 0;
+      const uint32_t pe = ld4(L.in, x + be);
+      uint32_t x8[8], e8[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int q = q8[k] >= 0 ? q8[k] : x;
+        x8[k] = ld4(L.in, q) ^ p4;
+        e8[k] = ld4(L.in, q + be) ^ pe;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int q = q8[k];
+        if (q < 0 || x - q > WIN) break;
+        if ((x8[k] & 0xffffffu) || (use_e && e8[k])) continue;  // a hash collision / no match at best
+        // compared up to `cap` only: the first candidate that reaches it ends the search (the
+        // same choice as comparing every candidate in full), and only that one is extended on
+        uint32_t y = x8[k];
+        int l = 0;
+        while (y == 0 && l + 4 < cap) {
+          l += 4;
+          y = ld4(L.in, q + l) ^ ld4(L.in, x + l);
+        }
+        l = y ? l + (int)(__builtin_ctz(y) >> 3) : l + 4;
+        l = min(l, cap);
+        if (l > best) {
+          best = l;
+          bd = x - q;
+        }
+        if (best >= cap) break;
+      }
+    }
+    if (best >= cap && cap < lim) {  // the winner, extended to the end of its match
+      const int q = x - bd;
+      int l = cap;
+      uint32_t y = 0;
+      while (y == 0 && l < lim) {
+        y = ld4(L.in, q + l) ^ ld4(L.in, x + l);
+        l += y ? (int)(__builtin_ctz(y) >> 3) : 4;
+      }
+      best = min(l, lim);
+    }
+    *dist = bd;
+    return best >= 3 ? best : 0;
+  }
+};
+
+// One parse step at x (zlib-style lazy evaluation: while the match at the next position is
 // longer and the current one shorter than `lazy`, emit a literal and move on; the look-ahead
 // search walks a quarter of the candidates once the current match is `good` long, as zlib's
 // deflate_slow does): appends its symbols to w[*ns...] and returns the new position.  The step
-// depends on p alone, so two parses that reach the same position continue identically (the
-// merge rule below).
-__device__ int parse_step(const Finder& F, int lazy, int p, uint32_t* w, int* ns) {
-  const int n = F.n;
-  int d = 0, l = F.find(p, min(MAXM, n - p), &d, F.chain);
-  while (l && l < lazy && p + 1 < n) {
+// depends on x alone, so two parses that reach the same position continue identically (the
+// merge rule below).  Matches end at the chunk end np.
+__device__ int parse_step(const Finder& F, int lazy, int x, uint32_t* w, int* ns, int cap) {
+  const int n = F.np;
+  int d = 0, l = F.find(x, min(MAXM, n - x), &d, F.chain);
+  while (l && l < lazy && x + 1 < n) {
     int d2 = 0;
     const int ch = F.good > 0 && l >= F.good ? max(1, F.chain >> 2) : F.chain;
-    const int l2 = F.find(p + 1, min(MAXM, n - p - 1), &d2, ch);
+    const int l2 = F.find(x + 1, min(MAXM, n - x - 1), &d2, ch);
     if (l2 <= l) break;
-    w[(*ns)++] = lit_word(F.L.in[p]);
-    p++;
+    DQ_CHK(*ns < cap, CHK_Z_STAGE);
+    w[(*ns)++] = lit_word(F.L.in[x]);
+    x++;
     l = l2;
     d = d2;
   }
+  DQ_CHK(*ns < cap, CHK_Z_STAGE);
   if (l) {
     w[(*ns)++] = match_word(l, d);
-    return p + l;
+    return x + l;
   }
-  w[(*ns)++] = lit_word(F.L.in[p]);
-  return p + 1;
+  w[(*ns)++] = lit_word(F.L.in[x]);
+  return x + 1;
 }
 
-// Runs f(word) over lane t's effective symbols: its own from the merge index, then its
-// continuation, when the parse reaches it (EFF_REACHED).
-template <class Fn>
-__device__ inline void for_each_sym(const DLds& L, const uint32_t* lane_w, int t, Fn f) {
-  const uint32_t e = L.lane_eff[t];
-  if (!(e & EFF_REACHED)) return;
-  const int k0 = (int)(e & 511), nc = (int)((e >> 9) & 511), ns = L.lane_nsym[t];
-  for (int k = k0; k < ns; k++) f(lane_w[k]);
-  for (int k = 0; k < nc; k++) f(lane_w[OWN_WORDS + k]);
+// The merge fields of lane_mrg
+__device__ inline uint32_t mrg_word(int u, int k, int nc, bool over) {
+  return (uint32_t)u | (uint32_t)k << 10 | (uint32_t)nc << 17 | (over ? 1u << 25 : 0u);
 }
+__device__ inline int mrg_lane(uint32_t m) { return (int)(m & 1023); }
+__device__ inline int mrg_sym(uint32_t m) { return (int)((m >> 10) & 127); }
+__device__ inline int mrg_cont(uint32_t m) { return (int)((m >> 17) & 255); }
+__device__ inline bool mrg_over(uint32_t m) { return (m >> 25) & 1u; }
 
-__global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __restrict__ src,
-                                                           int64_t n_in, int64_t blk0,
-                                                           int64_t nblk, uint32_t* __restrict__ stage,
-                                                           uint16_t* __restrict__ link,
-                                                           uint8_t* __restrict__ out_slots,
-                                                           int32_t* __restrict__ out_size,
-                                                           uint64_t* __restrict__ tim, int chain,
-                                                           int lazy, int nice, int good) {
-  __shared__ DLds L;
-  uint64_t tm[8];
-  int ti = 0;
-#define DTS()                                                            \
-  do {                                                                   \
+#define DTS()                                                                      \
+  do {                                                                             \
     if (tim && threadIdx.x == 0 && ti < 8) tm[ti++] = __builtin_amdgcn_s_memtime(); \
   } while (0)
+
+__global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restrict__ src,
+                                                         int64_t n_in, int64_t blk0, int64_t nblk,
+                                                         uint32_t* __restrict__ stage,
+                                                         uint32_t* __restrict__ meta,
+                                                         uint64_t* __restrict__ tim, int chain,
+                                                         int lazy, int nice, int good) {
+  __shared__ PLds L;
+  uint64_t tm[8];
+  int ti = 0;
   DTS();
-  const int64_t b = (int64_t)blockIdx.x;  // block within this launch
+  const int64_t b = (int64_t)blockIdx.x / NCH;  // block within this launch
   if (b >= nblk) return;
+  const int c = (int)(blockIdx.x % NCH);
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int64_t base = (blk0 + b) * (int64_t)BLK_U;
   const int n = (int)min<int64_t>(BLK_U, n_in - base);
-  // load (16-byte loads where aligned)
-  for (int i = t; i < 256; i += DWG) L.crc_t[i] = c_dcrc[i];
-  for (int i = t; i < (1 << HBITS); i += DWG) L.head[i] = 0;
+  const int cs = c * CH;
+  uint32_t* lm = meta + b * META_WORDS + c * PWG;
+  int32_t* ci = reinterpret_cast<int32_t*>(meta + b * META_WORDS + NCH * PWG + c * CI_WORDS);
+  if (cs >= n) {  // an empty chunk (the last block is short)
+    lm[t] = 0;
+    for (int i = t; i < CI_WORDS; i += PWG) ci[i] = 0;
+    if (tim && t == 0)
+      for (int k = 0; k < 8; k++) tim[blockIdx.x * 8 + k] = 0;
+    return;
+  }
+  const int ce = min(n, cs + CH);
+  const int r0 = max(0, cs - XW);
+  const int np = ce - r0;       // bytes held: local positions [0, np)
+  const int xs = cs - r0;       // the chunk's first local position
+  const int npos = max(0, np - 2);
+  const int nlc = (np - xs + PSEG - 1) / PSEG;  // lanes holding bytes
+  // ---- load (16-byte loads where aligned)
+  for (int i = t; i < 256; i += PWG) L.crc_t[i] = c_dcrc[i];
+  for (int i = t; i < (1 << HBITS); i += PWG) L.head[i] = 0;
   if (t < 8) L.misc[t] = 0;
   {
-    const uint8_t* s = src + base;
+    const uint8_t* s = src + base + r0;
     const int head = (int)((16 - (reinterpret_cast<uintptr_t>(s) & 15)) & 15);
-    const int h = min(head, n);
-    for (int i = t; i < h; i += DWG) L.in[i] = s[i];
-    const int nv = (n - h) / 16;
-    for (int i = t; i < nv; i += DWG) {
+    const int h = min(head, np);
+    for (int i = t; i < h; i += PWG) L.in[i] = s[i];
+    const int nv = (np - h) / 16;
+    for (int i = t; i < nv; i += PWG) {
       const uint4 v = *reinterpret_cast<const uint4*>(s + h + 16 * i);
       uint8_t* d = L.in + h + 16 * i;
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int k = 0; k < 16; k++) d[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
     }
-    for (int i = h + 16 * nv + t; i < n; i += DWG) L.in[i] = s[i];
-    if (t < 16) L.in[n + t] = 0;  // the 4-byte compares read up to 3 bytes past the end
+    for (int i = h + 16 * nv + t; i < np; i += PWG) L.in[i] = s[i];
+    if (t < 16) L.in[np + t] = 0;  // the 4-byte compares read up to 3 bytes past the end
   }
   __syncthreads();
   DTS();
-  const int s0 = min(n, t * SEG), s1 = min(n, s0 + SEG);
-  // ---- CRC32 of the segment (raw register, init 0)
-  {
-    uint32_t c = 0;
-    for (int i = s0; i < s1; i++) c = L.crc_t[(c ^ L.in[i]) & 0xff] ^ (c >> 8);
-    L.lane_crc[t] = gf2_mul(x8n((uint32_t)(n - s1)), c);
-  }
-  // ---- hash buckets of every position with a 3-byte suffix: counts, then bucket ends by a scan
-  for (int p = t; p + 3 <= n; p += DWG) atomicAdd(&L.head[hash3(L.in, p)], 1);
+  // ---- hash buckets of every position with a 3-byte suffix: counts, then cursors by a scan
+  for (int x = t; x < npos; x += PWG) atomicAdd(&L.head[hash3(L.in, x)], 1);
   __syncthreads();
-  {  // exclusive scan of the 2048 counts: 8 per thread
-    constexpr int PER = (1 << HBITS) / DWG;
+  {  // exclusive scan of the 2048 counts: 4 per thread
+    constexpr int PER = (1 << HBITS) / PWG;
     int v[PER], sum = 0;
 #pragma unroll
     for (int k = 0; k < PER; k++) {
@@ -463,150 +517,224 @@ __global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __rest
       const int y = __shfl_up(inc, d, 64);
       if (lane >= d) inc += y;
     }
-    if (lane == 63) L.lane_mrg[wv] = (uint32_t)inc;
+    if (lane == 63) L.wred[wv] = (uint32_t)inc;
     __syncthreads();
     int off = inc - sum;
-    for (int w = 0; w < wv; w++) off += (int)L.lane_mrg[w];
+    for (int w = 0; w < wv; w++) off += (int)L.wred[w];
 #pragma unroll
     for (int k = 0; k < PER; k++) {
-      L.head[PER * t + k] = off;  // the bucket's cursor: its start, advanced by the scatter
+      L.head[PER * t + k] = off;
       off += v[k];
     }
   }
   __syncthreads();
-  // ---- ordered scatter: positions in stripes of 256, ascending inside each bucket.  Inside a
-  //      wave the lanes with equal hashes are found by one ballot per hash bit; the four waves of
-  //      a stripe take their cursors in turn (one barrier each).  Afterwards head[h] is the end
-  //      of bucket h.
-  uint16_t* bl = link + b * (2 * 65536);
-  uint16_t* gi = bl + 65536;
-  for (int r = 0; r * DWG < n; r++) {
-    const int p = r * DWG + t;
-    const bool valid = p + 3 <= n;
-    const uint32_t h = valid ? hash3(L.in, p) : 0u;
-    uint64_t m = __ballot(valid);
+  // ---- ordered scatter, no barriers: wave wv owns the buckets h >> 8 == wv and walks every
+  //      position in order; the lanes of a step with equal hashes are ranked by one ballot per
+  //      hash bit, the group's last lane advances the cursor.  Afterwards head[h] is the end of
+  //      bucket h.
+  for (int x0 = 0; x0 < npos; x0 += 64) {
+    const int x = x0 + lane;
+    const uint32_t h = x < npos ? hash3(L.in, x) : 0u;
+    const bool mine = x < npos && (int)(h >> 8) == wv;
+    uint64_t m = __ballot(mine);
+    if (!m) continue;
 #pragma unroll
-    for (int k = 0; k < HBITS; k++) {
+    for (int k = 0; k < 8; k++) {
       const bool bit = (h >> k) & 1u;
       const uint64_t bk = __ballot(bit);
       m &= bit ? bk : ~bk;
     }
-    const uint64_t bel = m & lanes_below(lane);
-    int rank = 0;
-    for (int w = 0; w < DWG / 64; w++) {
-      if (wv == w && valid) {
-        rank = L.head[h] + __popcll(bel);
-        if (lane == 63 || !(m >> (lane + 1))) L.head[h] = rank + 1;  // the group's last lane
-      }
-      __syncthreads();
+    if (mine) {
+      const int rank = L.head[h] + __popcll(m & lanes_below(lane));
+      if (lane == 63 || !(m >> (lane + 1))) L.head[h] = rank + 1;  // the group's last lane
+      DQ_CHK(rank < npos, CHK_Z_BL);
+      L.bl[rank] = (uint16_t)x;
     }
-    if (valid) {
-      bl[rank] = (uint16_t)p;
-      gi[p] = (uint16_t)rank;
-    }
+  }
+  __syncthreads();
+  DTS();
+  // ---- CRC32 of the lane's segment (raw register, init 0), moved to the chunk end, XOR-ed
+  const int s0 = min(np, xs + PSEG * t), s1 = min(np, s0 + PSEG);
+  {
+    uint32_t cr = 0;
+    for (int i = s0; i < s1; i++) cr = L.crc_t[(cr ^ L.in[i]) & 0xff] ^ (cr >> 8);
+    if (s1 > s0) cr = gf2_mul(x8n((uint32_t)(np - s1)), cr);
+    for (int o = 32; o >= 1; o >>= 1) cr ^= __shfl_xor(cr, o, 64);
+    if (lane == 0) L.wred[8 + wv] = cr;
+  }
+  // ---- speculative parse: lane t from its segment start to the first symbol boundary at or past
+  //      its end (a match may run on past it)
+  uint32_t* const lanes_w = stage + (b * NCH + c) * (int64_t)PWG * LANE_WORDS;
+  uint32_t* const lane_w = lanes_w + (int64_t)t * LANE_WORDS;
+  const Finder F{L, np, min(chain, MAXCAND), nice, good};
+  {
+    int ns = 0, x = s0;
+    while (x < s1) x = parse_step(F, lazy, x, lane_w, &ns, OWN_WORDS);
+    L.lane_nsym[t] = (uint16_t)ns;
+    L.lane_exit[t] = (uint32_t)x;
   }
   __threadfence_block();
   __syncthreads();
   DTS();
-  // ---- speculative parse: lane t from its segment start to the first symbol boundary at or past
-  //      its end (a match may run on past it)
-  uint32_t* lane_w = stage + ((int64_t)b * DWG + t) * LANE_WORDS;
-  const Finder F{L, bl, gi, n, min(chain, MAXCAND), nice, good};
-  {
-    int ns = 0, p = s0;
-    while (p < s1) p = parse_step(F, lazy, p, lane_w, &ns);
-    L.lane_nsym[t] = (uint16_t)ns;
-    L.lane_bits[t] = (uint32_t)p;  // exit
-    L.lane_eff[t] = 0;
-  }
-  __threadfence_block();
-  __syncthreads();
   // ---- continuation: from its exit, lane t parses on until it reaches a symbol boundary of a
   //      later lane's speculative parse (the same position continues identically), skipping
   //      lanes whose whole parse it overruns
-  {
-    int E = (int)L.lane_bits[t], u = t + 1, k = 0, nc = 0;
-    int pu = min(n, u * SEG);
+  if (t < nlc) {
+    int E = (int)L.lane_exit[t], u = t + 1, k = 0, nc = 0;
+    int pu = min(np, xs + PSEG * u);
     bool over = false;
+    uint32_t* const cw = lane_w + OWN_WORDS;
     for (;;) {
-      if (E >= n) {
-        u = DWG;
+      if (E >= np) {  // the chunk's end
+        u = PWG;
         k = 0;
         break;
       }
-      if (u >= DWG || u * SEG >= n) {  // no later lane holds symbols: parse on to the end (these
-        if (nc > CONT_WORDS - 40) {    // empty lanes used to be skipped as "overrun", which ended
-          over = true;                 // the block one symbol short when E stopped just before n)
+      if (u >= nlc) {  // no later lane holds symbols: parse on to the chunk end
+        if (nc > CONT_WORDS - 40) {
+          over = true;
           break;
         }
-        int nn = OWN_WORDS + nc;
-        E = parse_step(F, lazy, E, lane_w, &nn);
-        nc = nn - OWN_WORDS;
+        E = parse_step(F, lazy, E, cw, &nc, CONT_WORDS);
         continue;
       }
       const int nu = L.lane_nsym[u];
-      const uint32_t* uw = stage + ((int64_t)b * DWG + u) * LANE_WORDS;
+      const uint32_t* uw = lanes_w + (int64_t)u * LANE_WORDS;
       while (k < nu && pu < E) pu += sym_bytes(uw[k++]);
       if (pu == E) break;  // merged: lane u's symbols from k on
       if (k == nu) {       // lane u's whole parse lies before E
         u++;
         k = 0;
-        pu = min(n, u * SEG);
+        pu = min(np, xs + PSEG * u);
         continue;
       }
       if (nc > CONT_WORDS - 40) {  // (a step appends at most lazy + 1 <= 33 symbols)
-        // no merge within the staging (e.g. one repeated byte: 258-byte matches from lane 0's
-        // positions 1 + 258 k never meet another lane's 255 u + 258 k): end exactly on lane u's
-        // boundary pu > E, with matches cut to fit and literals for the last < 3 bytes -- a valid
-        // parse that merges, where round 3 stored the whole block
+        // no merge within the staging (e.g. one repeated byte: 258-byte matches from lane t's
+        // positions never meet lane u's): end exactly on lane u's boundary pu > E, with matches
+        // cut to fit and literals for the last < 3 bytes -- a valid parse that merges
         while (E < pu && nc < CONT_WORDS) {
           int d = 0;
           const int l = F.find(E, min(MAXM, pu - E), &d, F.chain);
-          lane_w[OWN_WORDS + nc++] = l ? match_word(l, d) : lit_word(F.L.in[E]);
+          cw[nc++] = l ? match_word(l, d) : lit_word(L.in[E]);
           E += l ? l : 1;
         }
         if (E == pu) break;  // merged: lane u's symbols from k on
         over = true;         // (a gap of literals longer than the staging: stored)
         break;
       }
-      int nn = OWN_WORDS + nc;
-      E = parse_step(F, lazy, E, lane_w, &nn);
-      nc = nn - OWN_WORDS;
+      E = parse_step(F, lazy, E, cw, &nc, CONT_WORDS);
     }
-    L.lane_mrg[t] = (uint32_t)u | ((uint32_t)k << 9) | ((uint32_t)nc << 18) | (over ? 1u << 27 : 0u);
+    L.lane_mrg[t] = mrg_word(over ? PWG : u, k, nc, over);
   }
-  __threadfence_block();
+  // ---- the chunk's parse: lane 0, then the lane each continuation merged into.  Pointer
+  //      jumping: after round r every lane within 2^(r+1) - 1 merges of lane 0 is marked.
+  uint32_t* const jmp = L.lane_exit;  // the exits are dead
+  L.lane_mark[t] = t == 0;
   __syncthreads();
-  // ---- the parse of the block: lane 0, then the lane each continuation merged into
+  if (t < nlc) jmp[t] = (uint32_t)mrg_lane(L.lane_mrg[t]);
+  __syncthreads();
+  for (int r = 0; (1 << r) < nlc; r++) {
+    const uint32_t j = t < nlc ? jmp[t] : (uint32_t)PWG;
+    if (j < (uint32_t)PWG && L.lane_mark[t]) L.lane_mark[j] = 1;
+    const uint32_t jj = j < (uint32_t)PWG ? jmp[j] : (uint32_t)PWG;
+    __syncthreads();
+    if (t < nlc) jmp[t] = jj;
+    __syncthreads();
+  }
+  const bool reached = t < nlc && L.lane_mark[t];
+  const uint32_t mw = t < nlc ? L.lane_mrg[t] : 0u;
+  // the first symbol of each lane on the parse: set by the lane that merged into it
+  if (t == 0) jmp[0] = 0;
+  __syncthreads();
+  if (reached && mrg_lane(mw) < PWG) jmp[mrg_lane(mw)] = (uint32_t)mrg_sym(mw);
+  if (reached && mrg_over(mw)) L.misc[7] = 1;
+  int32_t* const H = L.head;  // the buckets are dead from here
+  for (int i = t; i < CI_D + 32; i += PWG) H[i] = 0;
+  __syncthreads();
+  const int k0 = reached ? (int)jmp[t] : 0;
+  const int ns = L.lane_nsym[t], nc = mrg_cont(mw);
+  lm[t] = reached ? (uint32_t)k0 | (uint32_t)ns << 8 | (uint32_t)nc << 16 | LM_REACHED : 0u;
+  // histograms of the chunk's parse
+  if (reached) {
+    auto hist = [&](uint32_t x) {
+      const uint32_t ll = sym_ll(x);
+      atomicAdd(&H[CI_LL + ll], 1);
+      if (ll > 256) atomicAdd(&H[CI_D + sym_d(x)], 1);
+    };
+    for (int k = k0; k < ns; k++) hist(lane_w[k]);
+    for (int k = 0; k < nc; k++) hist(lane_w[OWN_WORDS + k]);
+  }
+  __syncthreads();
+  for (int i = t; i < CI_CRC; i += PWG) ci[i] = H[i];
   if (t == 0) {
-    int cur = 0, k0 = 0;
-    for (int it = 0; it <= DWG; it++) {
-      const uint32_t m = L.lane_mrg[cur];
-      if ((m >> 27) & 1u) {
-        L.misc[7] = 2;  // a continuation overflowed: the block is stored
-        break;
-      }
-      const int u = (int)(m & 511), k = (int)((m >> 9) & 511);
-      L.lane_eff[cur] = (uint32_t)k0 | (m & (511u << 18)) >> 9 | EFF_REACHED | (u >= DWG ? EFF_EOB : 0u);
-      if (u >= DWG) break;
-      cur = u;
-      k0 = k;
-    }
+    uint32_t cr = 0;
+    for (int w = 0; w < PWG / 64; w++) cr ^= L.wred[8 + w];
+    ci[CI_CRC] = (int32_t)cr;
+    ci[CI_OVER] = L.misc[7];
+    ci[CI_BYTES] = ce - cs;
   }
-  int32_t* H = L.head;  // the buckets are dead from here
+  DTS();
+  if (tim && t == 0)
+    for (int k = 0; k < 8; k++) tim[blockIdx.x * 8 + k] = k < ti ? tm[k] - tm[0] : 0;
+}
+
+struct alignas(16) CLds {
+  uint8_t img[65536 + 16];  // the deflate image (<= 65510 bytes)
+  int32_t head[H_END];      // histograms and code tables (H_* offsets)
+  uint32_t wsum[16];
+  int32_t misc[8];
+};
+
+// the words of lane word m's symbols on the block's parse: own from the first, then continuation
+template <class Fn>
+__device__ inline void for_each_sym(uint32_t m, const uint32_t* __restrict__ w, Fn f) {
+  if (!(m & LM_REACHED)) return;
+  const int k0 = (int)(m & 255), ns = (int)((m >> 8) & 255), nc = (int)((m >> 16) & 255);
+  for (int k = k0; k < ns; k++) f(w[k]);
+  for (int k = 0; k < nc; k++) f(w[OWN_WORDS + k]);
+}
+
+__global__ __launch_bounds__(CWG) void bgzf_code_kernel(const uint8_t* __restrict__ src,
+                                                        int64_t n_in, int64_t blk0, int64_t nblk,
+                                                        const uint32_t* __restrict__ stage,
+                                                        const uint32_t* __restrict__ meta,
+                                                        uint8_t* __restrict__ out_slots,
+                                                        int32_t* __restrict__ out_size,
+                                                        uint64_t* __restrict__ tim) {
+  __shared__ CLds L;
+  uint64_t tm[8];
+  int ti = 0;
+  DTS();
+  const int64_t b = (int64_t)blockIdx.x;
+  if (b >= nblk) return;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t base = (blk0 + b) * (int64_t)BLK_U;
+  const int n = (int)min<int64_t>(BLK_U, n_in - base);
+  const uint32_t* lm = meta + b * META_WORDS;
+  const int32_t* ci = reinterpret_cast<const int32_t*>(meta + b * META_WORDS + NCH * PWG);
+  int32_t* H = L.head;
+  for (int i = t; i < H_CL + 32; i += CWG) H[i] = 0;
   __syncthreads();
-  for (int i = t; i < H_CL + 32; i += DWG) H[i] = 0;
+  for (int s = t; s < CI_CRC; s += CWG) {
+    int v = 0;
+#pragma unroll
+    for (int c = 0; c < NCH; c++) v += ci[c * CI_WORDS + s];
+    H[s < CI_D ? H_LL + s : H_D + (s - CI_D)] = v;
+  }
   __syncthreads();
-  // histograms of the effective symbols
-  for_each_sym(L, lane_w, t, [&](uint32_t x) {
-    const uint32_t ll = sym_ll(x);
-    atomicAdd(&H[H_LL + ll], 1);
-    if (ll > 256) atomicAdd(&H[H_D + sym_d(x)], 1);
-  });
-  if (L.lane_eff[t] & EFF_EOB) atomicAdd(&H[H_LL + 256], 1);
-  const bool over = L.misc[7] == 2;
-  __threadfence_block();
+  if (t == 0) {
+    H[H_LL + 256] += 1;  // end of block
+    int over = 0;
+    uint32_t cr = 0;
+    for (int c = 0; c < NCH; c++) {  // raw(A B) = raw(A) x^(8 |B|) + raw(B)
+      over |= ci[c * CI_WORDS + CI_OVER];
+      cr = gf2_mul(x8n((uint32_t)ci[c * CI_WORDS + CI_BYTES]), cr) ^ (uint32_t)ci[c * CI_WORDS + CI_CRC];
+    }
+    L.misc[1] = (int32_t)(cr ^ gf2_mul(x8n((uint32_t)n), 0xffffffffu) ^ 0xffffffffu);
+    L.misc[7] = over;
+  }
   __syncthreads();
+  const bool over = L.misc[7] != 0;
   DTS();
   // ---- dynamic Huffman codes: wave 0 the literal/length alphabet, wave 1 the distances
   if (wv == 0) build_lengths(H + H_LL, 286, 15, H + H_SORT, H + H_W, H + H_LEN, H + H_CNT, lane);
@@ -663,76 +791,79 @@ __global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __rest
   }
   __syncthreads();
   DTS();
-  // ---- bits per lane under the dynamic and the fixed code
+  // ---- bits of this thread's four lanes under the dynamic and the fixed code
+  uint32_t lw[4];
+  const uint32_t* wp[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int g = 4 * t + j, c = g / PL, u = g - c * PL;
+    lw[j] = g < NLANE ? lm[c * PWG + u] : 0u;
+    wp[j] = stage + ((b * NCH + c) * PWG + u) * (int64_t)LANE_WORDS;
+  }
+  const bool has_eob = 4 * t + 3 == NLANE - 1;  // the block's last lane ends with end-of-block
+  uint32_t vd[4], vf[4];
   {
     const uint32_t* cll = reinterpret_cast<const uint32_t*>(H + C_LL);
     const uint32_t* cd = reinterpret_cast<const uint32_t*>(H + C_D);
-    uint32_t bdyn = 0, bfix = 0;
-    for_each_sym(L, lane_w, t, [&](uint32_t x) {
-      const int ll = (int)sym_ll(x);
-      int extra = 0;
-      if (ll > 256) {
-        const int d = (int)sym_d(x);
-        extra = lextra_bits(ll) + dextra_bits(d);
-        bdyn += cd[d] >> 16;
-        bfix += 5;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      uint32_t bdyn = 0, bfix = 0;
+      for_each_sym(lw[j], wp[j], [&](uint32_t x) {
+        const int ll = (int)sym_ll(x);
+        int extra = 0;
+        if (ll > 256) {
+          const int d = (int)sym_d(x);
+          extra = lextra_bits(ll) + dextra_bits(d);
+          bdyn += cd[d] >> 16;
+          bfix += 5;
+        }
+        bdyn += (cll[ll] >> 16) + extra;
+        bfix += fixed_len_of(ll) + extra;
+      });
+      if (j == 3 && has_eob) {
+        bdyn += cll[256] >> 16;
+        bfix += 7;
       }
-      bdyn += (cll[ll] >> 16) + extra;
-      bfix += fixed_len_of(ll) + extra;
-    });
-    if (L.lane_eff[t] & EFF_EOB) {
-      bdyn += cll[256] >> 16;
-      bfix += 7;
+      vd[j] = bdyn;
+      vf[j] = bfix;
     }
-    L.lane_bits[t] = bdyn;
-    // fixed totals: the sort scratch is dead
-    reinterpret_cast<uint32_t*>(H + H_SORT)[t] = bfix;
+  }
+  // ---- choose dynamic or fixed; exclusive scan of the chosen lane bit counts
+  uint32_t dsum = vd[0] + vd[1] + vd[2] + vd[3], fsum = vf[0] + vf[1] + vf[2] + vf[3];
+  for (int o = 32; o >= 1; o >>= 1) {
+    dsum += __shfl_xor(dsum, o, 64);
+    fsum += __shfl_xor(fsum, o, 64);
+  }
+  if (lane == 0) {
+    L.wsum[wv] = dsum;
+    L.wsum[4 + wv] = fsum;
   }
   __syncthreads();
-  // ---- choose dynamic or fixed; exclusive scan of the chosen lane bit counts; CRC fold
-  if (t < 64) {
-    uint32_t dsum = 0, fsum = 0;
+  dsum = L.wsum[0] + L.wsum[1] + L.wsum[2] + L.wsum[3];
+  fsum = L.wsum[4] + L.wsum[5] + L.wsum[6] + L.wsum[7];
+  const bool dyn = (uint32_t)L.misc[6] + dsum < 3u + fsum;
+  const uint32_t hdr_bits = dyn ? (uint32_t)L.misc[6] : 3u;
+  uint32_t v[4], sm = 0;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      dsum += L.lane_bits[4 * t + k];
-      fsum += reinterpret_cast<uint32_t*>(H + H_SORT)[4 * t + k];
-    }
-    for (int o = 32; o >= 1; o >>= 1) {
-      dsum += __shfl_xor(dsum, o, 64);
-      fsum += __shfl_xor(fsum, o, 64);
-    }
-    const bool dyn = (uint32_t)L.misc[6] + dsum < 3u + fsum;
-    uint32_t v[4], sm = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      v[k] = dyn ? L.lane_bits[4 * t + k] : reinterpret_cast<uint32_t*>(H + H_SORT)[4 * t + k];
-      sm += v[k];
-    }
-    uint32_t inc = sm;
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(inc, d, 64);
-      if (t >= d) inc += y;
-    }
-    const uint32_t hdr_bits = dyn ? (uint32_t)L.misc[6] : 3u;
-    uint32_t off = hdr_bits + inc - sm;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      L.lane_bits[4 * t + k] = off;  // now: bit offset of lane 4t+k
-      off += v[k];
-    }
-    if (t == 63) L.misc[0] = (int32_t)(hdr_bits + inc);  // total bits
-    if (t == 0) L.misc[7] = dyn ? 1 : 0;
-    uint32_t c = L.lane_crc[4 * t] ^ L.lane_crc[4 * t + 1] ^ L.lane_crc[4 * t + 2] ^ L.lane_crc[4 * t + 3];
-    for (int o = 32; o >= 1; o >>= 1) c ^= __shfl_xor(c, o, 64);
-    if (t == 0) L.misc[1] = (int32_t)(c ^ gf2_mul(x8n((uint32_t)n), 0xffffffffu) ^ 0xffffffffu);
+  for (int j = 0; j < 4; j++) {
+    v[j] = dyn ? vd[j] : vf[j];
+    sm += v[j];
   }
+  uint32_t inc = sm;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += y;
+  }
+  if (lane == 63) L.wsum[8 + wv] = inc;
   __syncthreads();
+  uint32_t off = hdr_bits + inc - sm;
+  for (int w = 0; w < wv; w++) off += L.wsum[8 + w];
+  const uint32_t total_bits = hdr_bits + L.wsum[8] + L.wsum[9] + L.wsum[10] + L.wsum[11];
   DTS();
-  const bool dyn = L.misc[7] != 0;
   if (!dyn) {  // the fixed code into the code tables
     uint32_t* cll = reinterpret_cast<uint32_t*>(H + C_LL);
     uint32_t* cd = reinterpret_cast<uint32_t*>(H + C_D);
-    for (int sy = t; sy < 286; sy += DWG) {
+    for (int sy = t; sy < 286; sy += CWG) {
       uint32_t code;
       int cl;
       fixed_ll(sy, code, cl);
@@ -740,7 +871,6 @@ __global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __rest
     }
     if (t < 30) cd[t] = rev((uint32_t)t, 5) | (5u << 16);
   }
-  const uint32_t total_bits = (uint32_t)L.misc[0];
   const int dbytes = (int)((total_bits + 7) / 8);
   uint8_t* o = out_slots + b * 65536;
   const uint32_t crc = (uint32_t)L.misc[1];
@@ -748,9 +878,9 @@ __global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __rest
   const bool stored = over || dbytes > min(MAX_DEFLATE, n + 5);
   int payload;
   if (!stored) {
-    // ---- the header, then every lane's symbols, OR-ed into the LDS image (the input is dead)
-    uint32_t* img = reinterpret_cast<uint32_t*>(L.in);
-    for (int i = t; i < (int)(sizeof(L.in) / 4); i += DWG) img[i] = 0;
+    // ---- the header, then every lane's symbols, OR-ed into the LDS image
+    uint32_t* img = reinterpret_cast<uint32_t*>(L.img);
+    for (int i = t; i < (int)(sizeof(L.img) / 4); i += CWG) img[i] = 0;
     __syncthreads();
     if (t == 0) {
       ImgOut io(img, 0);
@@ -778,29 +908,32 @@ __global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __rest
     {
       const uint32_t* cll = reinterpret_cast<const uint32_t*>(H + C_LL);
       const uint32_t* cd = reinterpret_cast<const uint32_t*>(H + C_D);
-      ImgOut io(img, L.lane_bits[t]);
-      for_each_sym(L, lane_w, t, [&](uint32_t x) {
-        const int ll = (int)sym_ll(x);
-        io.put(cll[ll] & 0xffff, (int)(cll[ll] >> 16));
-        if (ll > 256) {
-          const int lx = lextra_bits(ll);
-          if (lx) io.put(sym_lx(x), lx);
-          const int d = (int)sym_d(x);
-          io.put(cd[d] & 0xffff, (int)(cd[d] >> 16));
-          const int dx = dextra_bits(d);
-          if (dx) io.put(sym_dx(x), dx);
-        }
-      });
-      if (L.lane_eff[t] & EFF_EOB) io.put(cll[256] & 0xffff, (int)(cll[256] >> 16));
+      ImgOut io(img, off);
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        for_each_sym(lw[j], wp[j], [&](uint32_t x) {
+          const int ll = (int)sym_ll(x);
+          io.put(cll[ll] & 0xffff, (int)(cll[ll] >> 16));
+          if (ll > 256) {
+            const int lx = lextra_bits(ll);
+            if (lx) io.put(sym_lx(x), lx);
+            const int d = (int)sym_d(x);
+            io.put(cd[d] & 0xffff, (int)(cd[d] >> 16));
+            const int dx = dextra_bits(d);
+            if (dx) io.put(sym_dx(x), dx);
+          }
+        });
+      }
+      if (has_eob) io.put(cll[256] & 0xffff, (int)(cll[256] >> 16));
       io.flush();
     }
     __syncthreads();
     DTS();
     payload = dbytes;
-    // stored 16 bytes at a time after the 18-byte header: o + 18 is 2 mod 16, so bytes
-    for (int i = t; i < payload; i += DWG) o[18 + i] = L.in[i];
+    // o + 18 is 2 mod 16: bytes
+    for (int i = t; i < payload; i += CWG) o[18 + i] = L.img[i];
   } else {
-    // stored block: BFINAL 1, BTYPE 00, LEN, NLEN, the bytes (from global: LDS image may be dirty)
+    // stored block: BFINAL 1, BTYPE 00, LEN, NLEN, the bytes
     payload = n + 5;
     if (t == 0) {
       o[18] = 1;
@@ -809,7 +942,7 @@ __global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __rest
       o[21] = (uint8_t)~n;
       o[22] = (uint8_t)(~n >> 8);
     }
-    for (int i = t; i < n; i += DWG) o[23 + i] = src[base + i];
+    for (int i = t; i < n; i += CWG) o[23 + i] = src[base + i];
   }
   if (t == 0) {
     const int bsize = 18 + payload + 8 - 1;
@@ -824,8 +957,8 @@ __global__ __launch_bounds__(DWG) void bgzf_deflate_kernel(const uint8_t* __rest
   DTS();
   if (tim && t == 0)
     for (int k = 0; k < 8; k++) tim[b * 8 + k] = k < ti ? tm[k] - tm[0] : 0;
-#undef DTS
 }
+#undef DTS
 
 // Packs the fixed-stride block slots into one contiguous BGZF stream: one workgroup per block.
 __global__ __launch_bounds__(256) void bgzf_pack_kernel(const uint8_t* __restrict__ slots,
@@ -849,8 +982,8 @@ DefTables g_def[64];
 }  // namespace
 
 int64_t bgzf_block_count(int64_t n) { return n <= 0 ? 0 : (n + BLK_U - 1) / BLK_U; }
-size_t bgzf_stage_bytes(int64_t nblk) { return (size_t)nblk * DWG * LANE_WORDS * 4; }
-size_t bgzf_link_bytes(int64_t nblk) { return (size_t)nblk * 2 * 65536 * sizeof(uint16_t); }
+size_t bgzf_stage_bytes(int64_t nblk) { return (size_t)nblk * NCH * PWG * LANE_WORDS * 4; }
+size_t bgzf_meta_bytes(int64_t nblk) { return (size_t)nblk * META_WORDS * 4; }
 
 bool deflate_tables(int device) {
   if (device < 0 || device >= 64) return false;
@@ -888,21 +1021,23 @@ bool deflate_tables(int device) {
 }
 
 void launch_bgzf_deflate(const uint8_t* src, int64_t n_in, int64_t blk0, int64_t nblk,
-                         uint32_t* stage, uint16_t* link, uint8_t* out_slots, int32_t* out_size,
+                         uint32_t* stage, uint32_t* meta, uint8_t* out_slots, int32_t* out_size,
                          uint64_t* tim, hipStream_t s) {
   if (nblk <= 0) return;
   // DQ_DEFLATE="chain,lazy,nice[,good]": match-search effort (default 96,32,96,8: htsjdk level 5's
-  // ratio on the WGS stream; 48,24,48,8 is 40 % faster at a 1.4 % lower ratio, profiles/r3as_*;
-  // zlib level 5 is 32,16,32,8 with hash chains, tools/deflate_model.c; good 0 = always the full
-  // chain; read at every launch, so a test can sweep settings in one process)
-  const int4 cfg = [] {
-    int c = 96, l = 32, n = 96, g = 8;
-    if (const char* e = getenv("DQ_DEFLATE")) sscanf(e, "%d,%d,%d,%d", &c, &l, &n, &g);
-    return make_int4(std::max(1, std::min(c, MAXCAND)), std::max(0, std::min(l, 32)), std::max(3, n),
-                     std::max(0, g));
-  }();
-  hipLaunchKernelGGL(bgzf_deflate_kernel, dim3((unsigned)nblk), dim3(DWG), 0, s, src, n_in, blk0, nblk,
-                     stage, link, out_slots, out_size, tim, cfg.x, cfg.y, cfg.z, cfg.w);
+  // ratio on the WGS stream; zlib level 5 is 32,16,32,8 with hash chains, tools/deflate_model.c;
+  // good 0 = always the full chain; read at every launch, so a test can sweep settings in one
+  // process)
+  int cc = 96, cl = 32, cn = 96, cg = 8;
+  if (const char* e = getenv("DQ_DEFLATE")) sscanf(e, "%d,%d,%d,%d", &cc, &cl, &cn, &cg);
+  cc = std::max(1, std::min(cc, MAXCAND));
+  cl = std::max(0, std::min(cl, 32));
+  cn = std::max(3, cn);
+  cg = std::max(0, cg);
+  hipLaunchKernelGGL(bgzf_parse_kernel, dim3((unsigned)(nblk * NCH)), dim3(PWG), 0, s, src, n_in, blk0,
+                     nblk, stage, meta, tim, cc, cl, cn, cg);
+  hipLaunchKernelGGL(bgzf_code_kernel, dim3((unsigned)nblk), dim3(CWG), 0, s, src, n_in, blk0, nblk,
+                     stage, meta, out_slots, out_size, tim ? tim + nblk * NCH * 8 : nullptr);
 }
 
 void launch_bgzf_pack(const uint8_t* slots, const int32_t* size, const int64_t* off, int64_t nblk,

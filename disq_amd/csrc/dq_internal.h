@@ -38,6 +38,9 @@ enum : int {
   CHK_K2_SRC = 7,    // K2: a resolve copy source outside [0, isize)
   CHK_K3_STAGE = 8,  // K3: a record's staged bytes (or their reads) outside the LDS staging
   CHK_K2_LAST = 9,   // K2: a last_start index outside the table
+  CHK_Z_BL = 10,     // deflate: a bucket-list slot outside the chunk's position list
+  CHK_Z_STAGE = 11,  // deflate: a staged symbol word outside its lane's staging
+  CHK_Z_IMAGE = 12,  // deflate: an emitted word outside the LDS deflate image
 };
 #ifdef DQ_CHECKED
 namespace {
@@ -323,11 +326,13 @@ uint64_t dq_chk_take_deflate();
 // ------------------------------------------------------------------ BGZF deflate (write path)
 int64_t bgzf_block_count(int64_t n);
 size_t bgzf_stage_bytes(int64_t nblk);
-size_t bgzf_link_bytes(int64_t nblk);
+size_t bgzf_meta_bytes(int64_t nblk);
 bool deflate_tables(int device);
-// Blocks [blk0, blk0 + nblk) of src[0, n_in) (65280 bytes each) into fixed 64 KiB slots.
+// Blocks [blk0, blk0 + nblk) of src[0, n_in) (65280 bytes each) into fixed 64 KiB slots: the
+// chunk parse kernel, then the code/emit kernel.  tim (DQ_DEFLATE_TIMING): 8 words per parse
+// workgroup (2 per block), then 8 per block for the code kernel.
 void launch_bgzf_deflate(const uint8_t* src, int64_t n_in, int64_t blk0, int64_t nblk,
-                         uint32_t* stage, uint16_t* link, uint8_t* out_slots, int32_t* out_size,
+                         uint32_t* stage, uint32_t* meta, uint8_t* out_slots, int32_t* out_size,
                          uint64_t* tim, hipStream_t s);
 void launch_bgzf_pack(const uint8_t* slots, const int32_t* size, const int64_t* off, int64_t nblk,
                       uint8_t* out, hipStream_t s);

@@ -49,7 +49,9 @@ def test_edge_sizes():
     rng = np.random.default_rng(1)
     with _lib.Context() as c:
         assert c.bgzf_compress(b"") == b""
-        for n in (1, 2, 3, 257, 4096, B.BLOCK_U - 1, B.BLOCK_U, B.BLOCK_U + 1, 3 * B.BLOCK_U + 17):
+        # (32640: the parse kernel's chunk -- half a block -- whose matches end inside it)
+        for n in (1, 2, 3, 257, 4096, 32639, 32640, 32641, 32642, 32643, 32700, B.BLOCK_U - 1,
+                  B.BLOCK_U, B.BLOCK_U + 1, B.BLOCK_U + 32642, 3 * B.BLOCK_U + 17):
             check_roundtrip(c, rng.integers(0, 4, size=n, dtype=np.uint8).tobytes())
 
 
@@ -66,6 +68,30 @@ def test_bam_stream_ratio_and_roundtrip():
     with _lib.Context() as c:
         z = check_roundtrip(c, u)
     assert len(z) < 0.6 * len(u)  # LZ77 + fixed Huffman on BAM records
+
+
+def zlib5_bgzf_size(data):
+    """htsjdk's BGZF size at its default level 5: a raw deflate member per 65280-byte block."""
+    total = 0
+    for i in range(0, len(data), B.BLOCK_U):
+        z = zlib.compressobj(5, zlib.DEFLATED, -15)
+        total += len(z.compress(data[i:i + B.BLOCK_U]) + z.flush()) + 26
+    return total
+
+
+@pytest.mark.parametrize("name", ["1.bam", "hiseq_part-r-00000.bam", "HiSeq.10000.vcf.bgz", "wgs"])
+def test_ratio_at_zlib_level5(golden, name):
+    """The chunked LDS parse (two 32640-byte chunks per block, 16 KiB reach before a chunk) keeps
+    htsjdk's level-5 ratio on the golden BAM / VCF streams and the synthetic WGS stream
+    (tools/deflate_model.c, profiles/r4_deflate_chunk_model.txt): at most 0.5 % larger."""
+    if name == "wgs":
+        u = B.inflate_all(synth.generate(60000, seed=5, nthreads=8).bam)
+    else:
+        u = B.inflate_all(open(os.path.join(golden, name), "rb").read())
+    with _lib.Context() as c:
+        z = check_roundtrip(c, u)
+    ref = zlib5_bgzf_size(u)
+    assert len(z) <= 1.005 * ref, (len(z), ref, len(u) / len(z), len(u) / ref)
 
 
 def test_bamsink_assembly_reads_back(tmp_path, golden):

@@ -22,6 +22,8 @@ typedef struct {
   int lazy;       // zlib-style lazy evaluation: defer a match shorter than this
   int nice;       // stop the chain walk at a match this long
   int lazy_once;  // look one position ahead only (else defer while the next match is longer)
+  int half;       // chunk size: each chunk parses on its own (its matches end inside it), with
+  int xw;         // candidates from xw bytes before the chunk start on (0 = no chunks)
 } Cfg;
 
 static int lcode(int len) {  // length symbol
@@ -144,12 +146,13 @@ static int match_len(const uint8_t* b, int p, int q, int lim) {
 static int find(const Cfg* c, const uint8_t* b, int n, int p, int lim, const int* link, int* dist) {
   int best = 0, bd = 0;
   if (lim < 3) return 0;
+  const int qmin = c->half ? (p / c->half) * c->half - c->xw : 0;
   for (int d = 1; d <= c->shortd && d <= p; d++) {
     int l = match_len(b, p, p - d, lim);
     if (l > best) { best = l; bd = d; }
   }
   int q = link[p];
-  for (int k = 0; k < c->chain && q >= 0 && p - q <= WIN; k++) {
+  for (int k = 0; k < c->chain && q >= qmin && p - q <= WIN; k++) {
     if (p - q > c->shortd) {
       int l = match_len(b, p, q, lim);
       if (l > best) { best = l; bd = p - q; }
@@ -201,6 +204,11 @@ static long block_bits(const Cfg* c, const uint8_t* b, int n, int* link, int* he
     if (p < s0) p = s0;  // (never: the previous lane ended at or past s0)
     if (!c->cross) p = s0;
     int end = c->cross ? n : s1;
+    if (c->half) {  // a chunk's parse ends at the chunk end
+      const int ce = (s0 / c->half + 1) * c->half;
+      if (end > ce) end = ce;
+      if (s1 > ce) s1 = ce;
+    }
     while (p < s1) {
       int lim = end - p < MAXM ? end - p : MAXM;
       int d = 0, l = find(c, b, n, p, lim, link, &d);
@@ -258,6 +266,15 @@ int main(int argc, char** argv) {
       {"seg255 cross, exact h12 chain32 lazy16 nice32 short0", 255, 1, 0, 32, 12, 0, 16, 32, 0},
       {"seg255 nocross, exact h12 chain32 lazy16 nice32", 255, 0, 8, 32, 12, 0, 16, 32, 0},
       {"one parse, exact h15 chain32 lazy16 nice32 (zlib 5 like)", 0, 0, 0, 32, 15, 0, 16, 32, 0},
+      {"gpu r3: seg255 cross h11 chain96 lazy32 nice96", 255, 1, 0, 96, 11, 0, 32, 96, 0},
+      {"chunks: halves C=32640 X=16K", 255, 1, 0, 96, 11, 0, 32, 96, 0, 32640, 16384},
+      {"chunks: halves C=32640 X=16K seg64 (bgzf_parse_kernel)", 64, 1, 0, 96, 11, 0, 32, 96, 0, 32640, 16384},
+      {"chunks: quarters C=16320 X=7.5K", 255, 1, 0, 96, 11, 0, 32, 96, 0, 16320, 7680},
+      {"chunks: quarters C=16320 X=4K", 255, 1, 0, 96, 11, 0, 32, 96, 0, 16320, 4096},
+      {"chunks: eighths C=8160 X=8K", 255, 1, 0, 96, 11, 0, 32, 96, 0, 8160, 8192},
+      {"chunks: eighths C=8160 X=16K", 255, 1, 0, 96, 11, 0, 32, 96, 0, 8160, 16384},
+      {"chunks: quarters C=16320 X=7.5K seg64", 64, 1, 0, 96, 11, 0, 32, 96, 0, 16320, 7680},
+      {"chunks: quarters C=16320 X=7.5K chain128", 255, 1, 0, 128, 11, 0, 32, 128, 0, 16320, 7680},
   };
   int nc = sizeof cfgs / sizeof cfgs[0];
   long nb = (n + BLK - 1) / BLK;

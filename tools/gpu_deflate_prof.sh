@@ -13,7 +13,7 @@ grep '"ratio"' $out/bench.log > $out/bench.json
 find $out/prof -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} $out/kernel_stats.csv
 head -6 $out/kernel_stats.csv | cut -c1-160
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex deflate --output-format csv -d $out/$c -o run -- \
+  timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex "bgzf_(parse|code)" --output-format csv -d $out/$c -o run -- \
     python3 -u tools/deflate_bench.py --records 2000000 --reps 1 > $out/$c.log 2>&1
 done
 python3 - $out <<'PY'
