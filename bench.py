@@ -424,7 +424,8 @@ def shard_parity(rs, shard, offsets, rank, file_len, header, split_size, ctx, di
                  threads):
     """N > 1 parity, untimed, on every rank: the oracle (run_partitions_window) over exactly the
     bytes the rank decoded -- its resident range from its first split plus the halo it received
-    over RCCL in the timed steps, copied back from HBM -- with the broadcast header, for the
+    over RCCL in the timed steps, copied back from HBM a group of partitions at a time -- with
+    the broadcast header, for the
     partitions it owns (one chunk per partition, AbstractBinarySamSource.java:61-73); per-partition
     record count + ordered digest compared with the GPU's descriptors of the last timed step.
     The verdicts are all-gathered: every rank's line field is the same."""
@@ -434,17 +435,42 @@ def shard_parity(rs, shard, offsets, rank, file_len, header, split_size, ctx, di
     t0 = time.perf_counter()
     ok, nparts, nrec, short = 1, 0, 0, 0
     if not shard.empty:
-        skip = shard.lo - offsets[rank]
-        win = rs.buf[skip:rs.n_own + rs.nrecv].cpu().numpy()
+        # in groups of about 1 GB of partitions, so a rank's host copy stays small (8 ranks x a
+        # 12.5 GB shard at once would be 100 GB of host memory); each group's window runs from its
+        # first split start to its last split end + 4 MiB (x4 while the oracle finds it short)
+        have = rs.n_own + rs.nrecv  # bytes of rs.buf, from offsets[rank]
         splits = O.path_splits(file_len, split_size)[shard.p0:shard.p1]
         gcnt, gdig = ctx.partition_digests()
+        ocnt, odig = [], []
+        i = 0
         try:
-            ocnt, odig, _ = O.run_partitions_window(win, shard.lo, file_len, header, splits, threads)
+            while i < len(splits):
+                j = i + 1
+                while j < len(splits) and splits[j][1] - splits[i][0] <= (1 << 30):
+                    j += 1
+                lo, extra = splits[i][0], 4 << 20
+                while True:
+                    a = lo - offsets[rank]
+                    b = min(have, splits[j - 1][1] - offsets[rank] + extra)
+                    win = rs.buf[a:b].cpu().numpy()
+                    try:
+                        c, d, _ = O.run_partitions_window(win, lo, file_len, header, splits[i:j],
+                                                          threads)
+                        break
+                    except O.OracleError as e:
+                        if "short" not in str(e) or b >= have:
+                            raise
+                        extra *= 4
+                    finally:
+                        del win
+                ocnt.append(c)
+                odig.append(d)
+                i = j
+            ocnt, odig = np.concatenate(ocnt), np.concatenate(odig)
             ok = int(np.array_equal(gcnt, ocnt) and np.array_equal(gdig, odig))
             nparts, nrec = len(ocnt), int(ocnt.sum())
         except O.OracleError:
             ok, short = 0, 1
-        del win
     row = torch.tensor([ok, nparts, nrec, short, int(1e3 * (time.perf_counter() - t0))],
                        dtype=torch.int64, device=cdev)
     if dist is not None:

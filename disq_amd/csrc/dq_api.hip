@@ -76,6 +76,10 @@ struct dq_ctx {
   dq_opts o{};
   hipStream_t s = nullptr;
   hipEvent_t ev[8] = {};
+  // DQ_EXPORT_STREAMS=2: the export's device-to-pinned copies alternate between s and this second
+  // stream (a second DMA engine); created on first use
+  hipStream_t sx = nullptr;
+  hipEvent_t ev_x[2] = {};
   std::string err;
   // resident file (or byte-range shard of one: DESIGN.md §8)
   int64_t flen = 0;
@@ -1229,7 +1233,7 @@ static int bgzf_compress_dev(dq_ctx* ctx, const uint8_t* d_src, int64_t len, dou
       HIPCHK(hipStreamSynchronize(s));
       (void)hipFree(tim);
       // parse workgroups (per chunk), then the code workgroups (per block)
-      static const char* nm[2][8] = {{"", "load", "buckets", "parse", "merge+hist", "", "", ""},
+      static const char* nm[2][8] = {{"", "load", "counts", "scan", "scatter", "parse", "continue", "merge+hist"},
                                      {"", "sum", "huffman", "count+scan", "write", "store", "", ""}};
       const int64_t cnt[2] = {2 * nb, nb};
       size_t at = 0;
@@ -1484,13 +1488,32 @@ static int make_batch(dq_ctx* ctx, const std::vector<std::pair<int64_t, int64_t>
       !b->next_pos || !b->tlen || !b->flag || !b->bin || !b->n_cigar || !b->mapq ||
       !b->l_read_name || !b->hash || !b->raw_offset)
     return fail(DQ_ENOMEM);
+  // pinned destination: one DMA per array (with DQ_EXPORT_STREAMS=2 the arrays, and the halves of
+  // the raw bytes, alternate between two streams so two DMA engines run); heap: through the staging
+  // buffers
+  static const bool two = [] {
+    const char* e = getenv("DQ_EXPORT_STREAMS");
+    return e && atoi(e) == 2;
+  }();
+  const bool split = in_arena && two && n > 0;
+  if (split) {
+    if (!ctx->sx) {
+      XCHK(hipStreamCreateWithFlags(&ctx->sx, hipStreamNonBlocking));
+      for (auto& e : ctx->ev_x) XCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    // everything the copies read was produced on s
+    XCHK(hipEventRecord(ctx->ev_x[0], s));
+    XCHK(hipStreamWaitEvent(ctx->sx, ctx->ev_x[0], 0));
+  }
+  int turn = 0;
+  auto dma = [&](void* dst, const void* src, size_t bytes) -> int {
+    hipStream_t q = split && (turn++ & 1) ? ctx->sx : s;
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, q));
+    return 0;
+  };
   if (n > 0) {
-    // pinned destination: one DMA per array; heap: through the staging buffers
     auto d2h = [&](const void* src, size_t bytes, void* dst) -> int {
-      if (in_arena) {
-        HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
-        return 0;
-      }
+      if (in_arena) return dma(dst, src, bytes);
       return d2h_large(ctx, dst, src, bytes);
     };
     auto fld = [&](const void* dbase, size_t esz, void* dst) {
@@ -1509,18 +1532,33 @@ static int make_batch(dq_ctx* ctx, const std::vector<std::pair<int64_t, int64_t>
   if (with_raw && n > 0) {
     b->raw = (uint8_t*)halloc((size_t)std::max<int64_t>(1, raw_len));
     if (!b->raw) return fail(DQ_ENOMEM);
+    // the raw bytes: in halves over the two streams when split
+    auto raw_d2h = [&](const uint8_t* src) -> int {
+      const size_t len = (size_t)raw_len;
+      if (!in_arena) return d2h_large(ctx, b->raw, src, len);
+      if (!split || len < (8u << 20)) return dma(b->raw, src, len);
+      const size_t h = (len / 2 + 63) & ~(size_t)63;
+      int r = dma(b->raw, src, h);
+      return r ? r : dma(b->raw + h, src + h, len - h);
+    };
     if (direct) {  // consecutive chain records are contiguous in U
       int64_t lo = 0;
       XCHK(hipMemcpy(&lo, ctx->rec_lin.as<int64_t>() + first, 8, hipMemcpyDeviceToHost));
-      if (in_arena) XCHK(hipMemcpyAsync(b->raw, ctx->U.as<uint8_t>() + lo, (size_t)raw_len, hipMemcpyDeviceToHost, s));
-      else if ((rc = d2h_large(ctx, b->raw, ctx->U.as<uint8_t>() + lo, (size_t)raw_len))) return fail(rc);
+      if ((rc = raw_d2h(ctx->U.as<uint8_t>() + lo))) return fail(rc);
     } else {
       if ((rc = ensure_all(ctx, ctx->x_raw, (size_t)raw_len))) return fail(rc);
       launch_gather_raw(ctx->U.as<uint8_t>(), ctx->rec_lin.as<int64_t>(), ctx->f_bs.as<int32_t>(),
                         d_idx, 0, n, ctx->x_boff.as<int64_t>(), ctx->x_raw.as<uint8_t>(), s);
-      if (in_arena) XCHK(hipMemcpyAsync(b->raw, ctx->x_raw.p, (size_t)raw_len, hipMemcpyDeviceToHost, s));
-      else if ((rc = d2h_large(ctx, b->raw, ctx->x_raw.p, (size_t)raw_len))) return fail(rc);
+      if (split) {  // the second stream waits for the gather too
+        XCHK(hipEventRecord(ctx->ev_x[0], s));
+        XCHK(hipStreamWaitEvent(ctx->sx, ctx->ev_x[0], 0));
+      }
+      if ((rc = raw_d2h(ctx->x_raw.as<uint8_t>()))) return fail(rc);
     }
+  }
+  if (split) {  // s completes after the second stream's copies
+    XCHK(hipEventRecord(ctx->ev_x[1], ctx->sx));
+    XCHK(hipStreamWaitEvent(s, ctx->ev_x[1], 0));
   }
   b->n_partitions = np;
   b->part_offset = (int64_t*)malloc(sizeof(int64_t) * (size_t)(np + 1));
@@ -2252,6 +2290,10 @@ void dq_ctx_destroy(dq_ctx* ctx) {
     if (ctx->pin[k]) (void)hipHostFree(ctx->pin[k]);
   }
   if (ctx->arena) (void)hipHostFree(ctx->arena);
+  if (ctx->sx) (void)hipStreamSynchronize(ctx->sx);
+  for (auto& e : ctx->ev_x)
+    if (e) (void)hipEventDestroy(e);
+  if (ctx->sx) (void)hipStreamDestroy(ctx->sx);
   if (ctx->s) (void)hipStreamDestroy(ctx->s);
   delete ctx;
 }

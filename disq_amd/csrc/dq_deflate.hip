@@ -11,19 +11,20 @@
 //
 // Two kernels per batch of blocks, everything the match finder touches in LDS:
 //   bgzf_parse_kernel: one 512-thread workgroup per CHUNK, half a block (32640 bytes), holding the
-//      chunk's bytes plus up to 16 KiB before it (its window reach) and the hash-bucket lists of
+//      chunk's bytes plus up to 15000 bytes before it (its window reach) and the hash-bucket lists of
 //      all those positions (3 bytes of LDS per position: 160 KB, one workgroup per CU).  A chunk's
-//      matches end inside it and reach back at most 16 KiB before its start (the 32 KiB DEFLATE
+//      matches end inside it and reach back at most 15000 bytes before its start (the 32 KiB DEFLATE
 //      window inside the first chunk): tools/deflate_model.c puts that at zlib level 5's ratio on
 //      the WGS stream and the golden BAM / VCF streams (profiles/r4_deflate_chunk_model.txt).
-//   1. Match finder: every position with a 3-byte suffix goes into one of 2048 hash buckets, in
-//      ascending order inside its bucket (counts by LDS atomics, bucket starts by a scan, then an
-//      ordered scatter with no barriers: wave w owns the buckets h >> 8 == w and walks every
-//      position in order, the lanes of a 64-position step with equal hashes ranked by one ballot
-//      per hash bit).  A position's candidates are the entries before it in its bucket, most
-//      recent first (its own slot is found by a 16-way search of the bucket): a contiguous run of
-//      the list, so a search issues a batch of candidate loads at once instead of chasing zlib's
-//      hash-chain links one dependent load at a time.
+//   1. Match finder: every position with a 4-byte suffix goes into one of 2048 hash buckets of its
+//      first 4 bytes (a 4-byte key keeps 3-byte candidates, which rarely pay for their distance,
+//      out of the chain), ascending inside its bucket: counts by LDS atomics, bucket starts by a
+//      scan, then four waves scatter four position ranges in order with their own cursors (the
+//      lanes of a 64-position step with equal hashes ranked by one ballot per hash bit): no
+//      barrier, no position hashed twice.  A position's candidates are the entries before it in
+//      its bucket, most recent first (its own slot is found by a 16-way search of the bucket): a
+//      contiguous run of the list, so a search loads 8 candidates and their first 16 bytes at
+//      once instead of chasing zlib's hash-chain links one dependent load at a time.
 //   2. Parse: lane t parses from its 64-byte segment start with zlib-style lazy evaluation (a
 //      match shorter than `lazy` is deferred while the next position's is longer; the look-ahead
 //      search walks chain / 4 candidates once the current match is `good` long, as zlib's
@@ -49,7 +50,7 @@
 //      four lanes' bits into the LDS image of the block.  A block whose code would not fit BSIZE
 //      (or whose parse overflowed its staging) is stored (BTYPE 00).
 // CRC32: per-lane table CRC over the segment, combined with x^(8 n) mod P multipliers.
-// (Defaults chain 96, lazy 32, nice 96, good 8.)
+// (Defaults chain 32, lazy 16, nice 32, good 8: zlib level 5's.)
 #include "dq_internal.h"
 
 #include <algorithm>
@@ -64,7 +65,7 @@ constexpr int CH = BLK_U / NCH;          // 32640 bytes per chunk
 constexpr int PSEG = 64;                 // bytes per parsing lane
 constexpr int PL = CH / PSEG;            // 510 lanes per chunk
 constexpr int PWG = 512;                 // threads per chunk workgroup
-constexpr int XW = 16384;                // window reach before the chunk start
+constexpr int XW = 15000;                // window reach before the chunk start
 constexpr int NPMAX = CH + XW;           // bytes (positions) a chunk workgroup holds
 constexpr int HBITS = 11;                // hash buckets
 constexpr int MAXM = 258;
@@ -241,11 +242,34 @@ __device__ void canon_codes(const int32_t* len, int m, uint32_t* code, int32_t* 
   }
 }
 
-// 4 bytes at an arbitrary LDS offset x from two aligned words
+#ifndef DQ_LDS_UNALIGNED
+#define DQ_LDS_UNALIGNED 1
+#endif
+#if DQ_LDS_UNALIGNED
+// 4 / 8 bytes at an arbitrary LDS offset x: one unaligned ds_read_b32 / ds_read_b64
+__device__ inline uint32_t ld4(const uint8_t* in, int x) {
+  uint32_t v;
+  __builtin_memcpy(&v, in + x, 4);
+  return v;
+}
+__device__ inline uint64_t ld8(const uint8_t* in, int x) {
+  uint64_t v;
+  __builtin_memcpy(&v, in + x, 8);
+  return v;
+}
+#else
+// 4 / 8 bytes at an arbitrary LDS offset x from aligned words and byte shifts
 __device__ inline uint32_t ld4(const uint8_t* in, int x) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(in + (x & ~3));
-  return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(x & 3));  // byte shift
+  return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(x & 3));
 }
+__device__ inline uint64_t ld8(const uint8_t* in, int x) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(in + (x & ~3));
+  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], sh = (uint32_t)(x & 3);
+  return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sh) |
+         (uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32;
+}
+#endif
 
 // Staged symbol word: litlen symbol | length extra << 9 | distance symbol << 14 | distance extra << 19
 __device__ inline uint32_t sym_ll(uint32_t w) { return w & 511; }
@@ -278,9 +302,12 @@ struct ImgOut {  // LSB-first bits OR-ed into the LDS image from bit position p 
   }
 };
 
-__device__ inline uint32_t hash3(const uint8_t* in, int p) {
-  const uint32_t v = (uint32_t)in[p] | ((uint32_t)in[p + 1] << 8) | ((uint32_t)in[p + 2] << 16);
-  return (v * 2654435761u) >> (32 - HBITS);
+// bucket hash of the 4 bytes at p: candidates share 4 bytes (rarely 3 or fewer, on a collision).
+// A 4-byte key keeps 3-byte matches (which rarely pay for their distance) out of the chain, so
+// the same chain reaches more useful candidates: ratio 2.93 at chain 32 against 2.86 at chain 96
+// with a 3-byte key on the WGS stream (tools/deflate_model.c, profiles/r4_deflate_chunk_model.txt)
+__device__ inline uint32_t hash4(const uint8_t* in, int p) {
+  return (ld4(in, p) * 2654435761u) >> (32 - HBITS);
 }
 
 __device__ inline int sym_bytes(uint32_t w) {  // uncompressed bytes of a staged symbol
@@ -298,22 +325,35 @@ __device__ inline uint32_t match_word(int len, int d) {
 }
 
 
+constexpr int SCAT_WAVES = 4;  // waves of the bucket scatter: one position range each
 struct alignas(16) PLds {
-  uint8_t in[NPMAX + 16];     // bytes [r0, ce) of the block (+ zero pad for the 4-byte compares)
+  uint8_t in[NPMAX + 16];     // bytes [r0, ce) of the block (+ zero pad for the 4/8-byte compares)
   uint16_t bl[NPMAX];         // positions grouped by hash bucket, ascending inside a bucket
-  int32_t head[1 << HBITS];   // bucket counts -> cursors -> ends; later the chunk's histograms
-  uint32_t crc_t[256];
-  uint32_t lane_exit[PWG];    // the parse's exit of each lane; later jump pointers, first symbols
-  uint32_t lane_mrg[PWG];     // continuation: merge lane | symbol << 10 | count << 17 | over << 25
-  uint32_t lane_mark[PWG];    // on the chunk's parse
-  uint16_t lane_nsym[PWG];    // own symbols
+  int32_t head[1 << HBITS];   // bucket counts -> starts (wave 0's cursors) -> ends; later the
+                              // chunk's histograms
+  union {
+    struct {
+      uint32_t crc_t[256];
+      uint32_t lane_exit[PWG];  // the parse's exit of each lane; later jump pointers, first symbols
+      uint32_t lane_mrg[PWG];   // continuation: merge lane | symbol << 10 | count << 17 | over << 25
+      uint32_t lane_mark[PWG];  // on the chunk's parse
+      uint16_t lane_nsym[PWG];  // own symbols
+      uint32_t sbits[CH / 32];  // symbol starts of the lanes' own parses inside their segments (a
+                                // deferred literal past the segment end is left out): each lane's
+                                // 64-bit word holds its own starts only
+    };
+    // the bucket build (before any of the above is live): the counts of scatter waves 0..2's
+    // position ranges, two 16-bit counts per word, then those waves' successors' cursors
+    uint32_t cnt[SCAT_WAVES - 1][1 << (HBITS - 1)];
+  };
   uint32_t wred[16];
   int32_t misc[8];
 };
 static_assert(sizeof(PLds) <= 160 * 1024, "one chunk workgroup per CU");
+static_assert(PSEG == 64, "a lane's symbol starts are one 64-bit word of sbits");
 
-// Match finder over the chunk's hash buckets: bl holds every local position x with a 3-byte
-// suffix (x + 3 <= np), grouped by bucket (hash3) and ascending inside a bucket; the bucket of
+// Match finder over the chunk's hash buckets: bl holds every local position x with a 4-byte
+// suffix (x + 4 <= np), grouped by bucket (hash4) and ascending inside a bucket; the bucket of
 // hash h ends at head[h] (it starts where bucket h - 1 ends).  The candidates of x are the entries
 // before x's own slot in its bucket, most recent first -- consecutive words of bl, so all of a
 // search's candidate loads are in flight together.
@@ -341,61 +381,79 @@ struct Finder {
   // distance
   __device__ int find(int x, int lim, int* dist, int chain) const {
     *dist = 0;
-    if (lim < 3 || x + 3 > np) return 0;
-    const uint32_t h = hash3(L.in, x);
+    if (lim < 3 || x + 4 > np) return 0;
+    const uint32_t h = hash4(L.in, x);
     const int blo = h ? L.head[h - 1] : 0;
     const int g = slot(blo, L.head[h], x);
     const int lo = max(blo, g - chain);
-    const uint32_t p4 = ld4(L.in, x);
+    // the first 16 bytes at x, once; each batch compares its 8 candidates' first 16 bytes with
+    // 16 loads issued together (lengths < 16, most of them, need no further round trip)
+    const uint64_t pa = ld8(L.in, x), pb = ld8(L.in, x + 8);
     int best = 0, bd = 0;
     const int cap = min(lim, nice);
-    for (int i0 = g - 1; i0 >= lo && best < cap; i0 -= 8) {
-      // a batch of 8 candidates: their positions and first / scan-end words are all loaded
-      // before any is tested, so the batch costs about one LDS latency of each kind
+    bool more = true;
+    for (int i0 = g - 1; i0 >= lo && more; i0 -= 8) {
       int q8[8];
-#pragma unroll
-      for (int k = 0; k < 8; k++) q8[k] = i0 - k >= lo ? (int)L.bl[i0 - k] : -1;
-      // only a candidate that also matches the byte at `best` can win: the 4 bytes ending there
-      // are tested first (zlib's scan_end test), with the best length at the batch start
-      const bool use_e = best >= 3;
-      const int be = use_e ? best - 3 : 0;
-      const uint32_t pe = ld4(L.in, x + be);
-      uint32_t x8[8], e8[8];
+      uint64_t ya[8], yb[8];
+#if DQ_LDS_UNALIGNED
+      // entries i0 - 7 .. i0 in one 16-byte read (below lo, or before bl itself: masked)
+      uint4 qq;
+      __builtin_memcpy(&qq, &L.bl[i0 - 7], 16);
+      const uint32_t qw[4] = {qq.x, qq.y, qq.z, qq.w};
+#endif
 #pragma unroll
       for (int k = 0; k < 8; k++) {
+#if DQ_LDS_UNALIGNED
+        q8[k] = i0 - k >= lo ? (int)((qw[(7 - k) >> 1] >> (16 * ((7 - k) & 1))) & 0xffffu) : -1;
+#else
+        q8[k] = i0 - k >= lo ? (int)L.bl[i0 - k] : -1;
+#endif
         const int q = q8[k] >= 0 ? q8[k] : x;
-        x8[k] = ld4(L.in, q) ^ p4;
-        e8[k] = ld4(L.in, q + be) ^ pe;
+        ya[k] = ld8(L.in, q) ^ pa;
+        yb[k] = ld8(L.in, q + 8) ^ pb;
       }
 #pragma unroll
       for (int k = 0; k < 8; k++) {
         const int q = q8[k];
-        if (q < 0 || x - q > WIN) break;
-        if ((x8[k] & 0xffffffu) || (use_e && e8[k])) continue;  // a hash collision / no match at best
-        // compared up to `cap` only: the first candidate that reaches it ends the search (the
-        // same choice as comparing every candidate in full), and only that one is extended on
-        uint32_t y = x8[k];
-        int l = 0;
-        while (y == 0 && l + 4 < cap) {
-          l += 4;
-          y = ld4(L.in, q + l) ^ ld4(L.in, x + l);
+        if (q < 0 || x - q > WIN) {  // past the window (candidates are most recent first)
+          more = false;
+          break;
         }
-        l = y ? l + (int)(__builtin_ctz(y) >> 3) : l + 4;
+        int l = ya[k] ? (int)(__builtin_ctzll(ya[k]) >> 3)
+                      : yb[k] ? 8 + (int)(__builtin_ctzll(yb[k]) >> 3) : 16;
+        // (rare) 16 bytes equal: on up to cap, unless the 4 bytes ending at `best` differ (then
+        // it cannot beat best: zlib's scan_end test)
+        if (l == 16 && l < cap && (best <= 16 || ld4(L.in, q + best - 3) == ld4(L.in, x + best - 3))) {
+          while (l < cap) {
+            const uint64_t y = ld8(L.in, q + l) ^ ld8(L.in, x + l);
+            if (y) {
+              l += (int)(__builtin_ctzll(y) >> 3);
+              break;
+            }
+            l += 8;
+          }
+        }
         l = min(l, cap);
         if (l > best) {
           best = l;
           bd = x - q;
         }
-        if (best >= cap) break;
+        if (best >= cap) {  // the first candidate to reach cap wins
+          more = false;
+          break;
+        }
       }
     }
     if (best >= cap && cap < lim) {  // the winner, extended to the end of its match
       const int q = x - bd;
       int l = cap;
-      uint32_t y = 0;
-      while (y == 0 && l < lim) {
-        y = ld4(L.in, q + l) ^ ld4(L.in, x + l);
-        l += y ? (int)(__builtin_ctz(y) >> 3) : 4;
+      while (l < lim) {
+        const uint64_t y = ld8(L.in, q + l) ^ ld8(L.in, x + l);
+        if (y) {
+          l += (int)(__builtin_ctzll(y) >> 3);
+          break;
+        }
+        l += 8;
       }
       best = min(l, lim);
     }
@@ -410,8 +468,12 @@ struct Finder {
 // deflate_slow does): appends its symbols to w[*ns...] and returns the new position.  The step
 // depends on x alone, so two parses that reach the same position continue identically (the
 // merge rule below).  Matches end at the chunk end np.
-__device__ int parse_step(const Finder& F, int lazy, int x, uint32_t* w, int* ns, int cap) {
+__device__ int parse_step(const Finder& F, int lazy, int x, uint32_t* w, int* ns, int cap,
+                          uint64_t* starts = nullptr, int sbase = 0) {
   const int n = F.np;
+  auto mark = [&](int p) {  // (a deferred literal can start past the segment: not recorded)
+    if (starts && p - sbase < 64) *starts |= 1ull << (p - sbase);
+  };
   int d = 0, l = F.find(x, min(MAXM, n - x), &d, F.chain);
   while (l && l < lazy && x + 1 < n) {
     int d2 = 0;
@@ -419,12 +481,14 @@ __device__ int parse_step(const Finder& F, int lazy, int x, uint32_t* w, int* ns
     const int l2 = F.find(x + 1, min(MAXM, n - x - 1), &d2, ch);
     if (l2 <= l) break;
     DQ_CHK(*ns < cap, CHK_Z_STAGE);
+    mark(x);
     w[(*ns)++] = lit_word(F.L.in[x]);
     x++;
     l = l2;
     d = d2;
   }
   DQ_CHK(*ns < cap, CHK_Z_STAGE);
+  mark(x);
   if (l) {
     w[(*ns)++] = match_word(l, d);
     return x + l;
@@ -477,11 +541,11 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
   const int r0 = max(0, cs - XW);
   const int np = ce - r0;       // bytes held: local positions [0, np)
   const int xs = cs - r0;       // the chunk's first local position
-  const int npos = max(0, np - 2);
+  const int npos = max(0, np - 3);  // positions with a 4-byte suffix
   const int nlc = (np - xs + PSEG - 1) / PSEG;  // lanes holding bytes
   // ---- load (16-byte loads where aligned)
-  for (int i = t; i < 256; i += PWG) L.crc_t[i] = c_dcrc[i];
   for (int i = t; i < (1 << HBITS); i += PWG) L.head[i] = 0;
+  for (int i = t; i < (SCAT_WAVES - 1) << (HBITS - 1); i += PWG) (&L.cnt[0][0])[i] = 0;
   if (t < 8) L.misc[t] = 0;
   {
     const uint8_t* s = src + base + r0;
@@ -501,9 +565,21 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
   }
   __syncthreads();
   DTS();
-  // ---- hash buckets of every position with a 3-byte suffix: counts, then cursors by a scan
-  for (int x = t; x < npos; x += PWG) atomicAdd(&L.head[hash3(L.in, x)], 1);
+  // ---- hash buckets of every position with a 4-byte suffix.  Counts per bucket, and per bucket
+  //      for each of the first three of four position ranges; bucket starts by a scan; each
+  //      range's cursors = start + the earlier ranges' counts.  Then four waves scatter their
+  //      ranges in order (the lanes of a 64-position step with equal hashes ranked by one ballot
+  //      per hash bit, the group's last lane advancing the cursor): ascending inside each bucket,
+  //      no barrier, no position hashed twice.
+  const int rng = ((npos + SCAT_WAVES - 1) / SCAT_WAVES + 63) & ~63;  // positions per range
+  for (int x = t; x < npos; x += PWG) {
+    const uint32_t h = hash4(L.in, x);
+    atomicAdd(&L.head[h], 1);
+    const int r = x / rng;
+    if (r < SCAT_WAVES - 1) atomicAdd(&L.cnt[r][h >> 1], 1u << (16 * (h & 1)));
+  }
   __syncthreads();
+  DTS();
   {  // exclusive scan of the 2048 counts: 4 per thread
     constexpr int PER = (1 << HBITS) / PWG;
     int v[PER], sum = 0;
@@ -521,36 +597,54 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
     __syncthreads();
     int off = inc - sum;
     for (int w = 0; w < wv; w++) off += (int)L.wred[w];
+    uint16_t* const c16 = reinterpret_cast<uint16_t*>(&L.cnt[0][0]);
 #pragma unroll
     for (int k = 0; k < PER; k++) {
-      L.head[PER * t + k] = off;
+      const int h = PER * t + k;
+      L.head[h] = off;  // range 0's cursor
+      int c = off;
+#pragma unroll
+      for (int r = 0; r < SCAT_WAVES - 1; r++) {  // range r + 1's cursor, over range r's count
+        c += c16[(r << HBITS) + h];
+        c16[(r << HBITS) + h] = (uint16_t)c;
+      }
       off += v[k];
     }
   }
   __syncthreads();
-  // ---- ordered scatter, no barriers: wave wv owns the buckets h >> 8 == wv and walks every
-  //      position in order; the lanes of a step with equal hashes are ranked by one ballot per
-  //      hash bit, the group's last lane advances the cursor.  Afterwards head[h] is the end of
-  //      bucket h.
-  for (int x0 = 0; x0 < npos; x0 += 64) {
-    const int x = x0 + lane;
-    const uint32_t h = x < npos ? hash3(L.in, x) : 0u;
-    const bool mine = x < npos && (int)(h >> 8) == wv;
-    uint64_t m = __ballot(mine);
-    if (!m) continue;
+  DTS();
+  if (wv < SCAT_WAVES) {
+    uint16_t* const cur16 = wv ? reinterpret_cast<uint16_t*>(&L.cnt[wv - 1][0]) : nullptr;
+    const int xe = min(npos, (wv + 1) * rng);
+    for (int x0 = wv * rng; x0 < xe; x0 += 64) {
+      const int x = x0 + lane;
+      const bool valid = x < xe;
+      const uint32_t h = valid ? hash4(L.in, x) : 0u;
+      uint64_t m = __ballot(valid);
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const bool bit = (h >> k) & 1u;
-      const uint64_t bk = __ballot(bit);
-      m &= bit ? bk : ~bk;
-    }
-    if (mine) {
-      const int rank = L.head[h] + __popcll(m & lanes_below(lane));
-      if (lane == 63 || !(m >> (lane + 1))) L.head[h] = rank + 1;  // the group's last lane
-      DQ_CHK(rank < npos, CHK_Z_BL);
-      L.bl[rank] = (uint16_t)x;
+      for (int k = 0; k < HBITS; k++) {
+        const bool bit = (h >> k) & 1u;
+        const uint64_t bk = __ballot(bit);
+        m &= bit ? bk : ~bk;
+      }
+      if (valid) {
+        const int cur = wv ? (int)cur16[h] : L.head[h];
+        const int rank = cur + __popcll(m & lanes_below(lane));
+        if (lane == 63 || !(m >> (lane + 1))) {  // the group's last lane
+          if (wv) cur16[h] = (uint16_t)(rank + 1);
+          else L.head[h] = rank + 1;
+        }
+        DQ_CHK(rank < npos, CHK_Z_BL);
+        L.bl[rank] = (uint16_t)x;
+      }
     }
   }
+  __syncthreads();
+  {  // bucket ends: the last range's cursors
+    const uint16_t* const c16 = reinterpret_cast<const uint16_t*>(&L.cnt[SCAT_WAVES - 2][0]);
+    for (int h = t; h < (1 << HBITS); h += PWG) L.head[h] = c16[h];
+  }
+  for (int i = t; i < 256; i += PWG) L.crc_t[i] = c_dcrc[i];  // (over the dead counts)
   __syncthreads();
   DTS();
   // ---- CRC32 of the lane's segment (raw register, init 0), moved to the chunk end, XOR-ed
@@ -569,9 +663,14 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
   const Finder F{L, np, min(chain, MAXCAND), nice, good};
   {
     int ns = 0, x = s0;
-    while (x < s1) x = parse_step(F, lazy, x, lane_w, &ns, OWN_WORDS);
+    uint64_t st = 0;
+    while (x < s1) x = parse_step(F, lazy, x, lane_w, &ns, OWN_WORDS, &st, s0);
     L.lane_nsym[t] = (uint16_t)ns;
     L.lane_exit[t] = (uint32_t)x;
+    if (t < PL) {
+      L.sbits[2 * t] = (uint32_t)st;
+      L.sbits[2 * t + 1] = (uint32_t)(st >> 32);
+    }
   }
   __threadfence_block();
   __syncthreads();
@@ -581,7 +680,6 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
   //      lanes whose whole parse it overruns
   if (t < nlc) {
     int E = (int)L.lane_exit[t], u = t + 1, k = 0, nc = 0;
-    int pu = min(np, xs + PSEG * u);
     bool over = false;
     uint32_t* const cw = lane_w + OWN_WORDS;
     for (;;) {
@@ -598,34 +696,45 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
         E = parse_step(F, lazy, E, cw, &nc, CONT_WORDS);
         continue;
       }
-      const int nu = L.lane_nsym[u];
-      const uint32_t* uw = lanes_w + (int64_t)u * LANE_WORDS;
-      while (k < nu && pu < E) pu += sym_bytes(uw[k++]);
-      if (pu == E) break;  // merged: lane u's symbols from k on
-      if (k == nu) {       // lane u's whole parse lies before E
+      // lane u's symbol starts (its segment [su, su + 64)) and its exit; E >= su
+      const int su = xs + PSEG * u, eu = (int)L.lane_exit[u];
+      if (E > eu) {  // lane u's whole parse lies before E
         u++;
-        k = 0;
-        pu = min(np, xs + PSEG * u);
         continue;
+      }
+      if (E == eu) {  // merged: lane u's continuation
+        k = L.lane_nsym[u];
+        break;
+      }
+      const uint64_t ub = (uint64_t)L.sbits[2 * u] | (uint64_t)L.sbits[2 * u + 1] << 32;
+      if (E < su + PSEG && ((ub >> (E - su)) & 1)) {  // merged: lane u's symbols from k on
+        k = __popcll(ub & ((1ull << (E - su)) - 1));
+        break;
       }
       if (nc > CONT_WORDS - 40) {  // (a step appends at most lazy + 1 <= 33 symbols)
         // no merge within the staging (e.g. one repeated byte: 258-byte matches from lane t's
-        // positions never meet lane u's): end exactly on lane u's boundary pu > E, with matches
-        // cut to fit and literals for the last < 3 bytes -- a valid parse that merges
+        // positions never meet lane u's): end exactly on lane u's next boundary pu > E, with
+        // matches cut to fit and literals for the last < 3 bytes -- a valid parse that merges
+        const uint64_t after = E - su + 1 < 64 ? ub >> (E - su + 1) : 0ull;
+        const int pu = E < su + PSEG && after ? E + 1 + (int)__builtin_ctzll(after) : eu;
         while (E < pu && nc < CONT_WORDS) {
           int d = 0;
           const int l = F.find(E, min(MAXM, pu - E), &d, F.chain);
           cw[nc++] = l ? match_word(l, d) : lit_word(L.in[E]);
           E += l ? l : 1;
         }
-        if (E == pu) break;  // merged: lane u's symbols from k on
-        over = true;         // (a gap of literals longer than the staging: stored)
+        if (E != pu) {  // (a gap of literals longer than the staging: stored)
+          over = true;
+          break;
+        }
+        k = pu == eu ? (int)L.lane_nsym[u] : __popcll(ub & ((1ull << (pu - su)) - 1));
         break;
       }
       E = parse_step(F, lazy, E, cw, &nc, CONT_WORDS);
     }
     L.lane_mrg[t] = mrg_word(over ? PWG : u, k, nc, over);
   }
+  DTS();
   // ---- the chunk's parse: lane 0, then the lane each continuation merged into.  Pointer
   //      jumping: after round r every lane within 2^(r+1) - 1 merges of lane 0 is marked.
   uint32_t* const jmp = L.lane_exit;  // the exits are dead
@@ -1024,11 +1133,11 @@ void launch_bgzf_deflate(const uint8_t* src, int64_t n_in, int64_t blk0, int64_t
                          uint32_t* stage, uint32_t* meta, uint8_t* out_slots, int32_t* out_size,
                          uint64_t* tim, hipStream_t s) {
   if (nblk <= 0) return;
-  // DQ_DEFLATE="chain,lazy,nice[,good]": match-search effort (default 96,32,96,8: htsjdk level 5's
-  // ratio on the WGS stream; zlib level 5 is 32,16,32,8 with hash chains, tools/deflate_model.c;
-  // good 0 = always the full chain; read at every launch, so a test can sweep settings in one
-  // process)
-  int cc = 96, cl = 32, cn = 96, cg = 8;
+  // DQ_DEFLATE="chain,lazy,nice[,good]": match-search effort (default 32,16,32,8: zlib level 5's
+  // own settings; with the 4-byte bucket key that is ratio 2.92 on the WGS stream against htsjdk's
+  // 2.857, profiles/r4m_deflate_sweep.txt; good 0 = always the full chain; read at every launch, so
+  // a test can sweep settings in one process)
+  int cc = 32, cl = 16, cn = 32, cg = 8;
   if (const char* e = getenv("DQ_DEFLATE")) sscanf(e, "%d,%d,%d,%d", &cc, &cl, &cn, &cg);
   cc = std::max(1, std::min(cc, MAXCAND));
   cl = std::max(0, std::min(cl, 32));

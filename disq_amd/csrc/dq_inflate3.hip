@@ -63,10 +63,7 @@ constexpr int WG = 512;           // threads per workgroup
 constexpr int NDEC = 512;         // speculative decode lanes (<= WG)
 constexpr uint32_t OV_DEFAULT = 96;  // speculative warm-up bits before each segment
 constexpr int OUTCAP = 65536 + 24;  // + alignment shift (<= 15) + descriptor overhang; bm 8-aligned
-constexpr int RES_NXT = 2048;
-#ifndef DQ_SPLITJUMP
-#define DQ_SPLITJUMP 1  // resolve steps: the next batch's pointer stores after the step's byte store
-#endif        // resolve batch bytes (NB * G * WG) at most
+constexpr int RES_NXT = 2048;        // resolve batch bytes (NB * G * WG) at most
 
 // 16-bit decode table layout: [litlen root | litlen subtables | dist root | dist subtables]
 constexpr int LR = 10, DR = 8;            // root bits
@@ -1375,7 +1372,6 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   constexpr int BATCH = NB * CH;
   constexpr int NE = NB * G;
   static_assert(BATCH <= RES_NXT, "the batch's next-pointers fit the resolve scratch");
-  static_assert(NB * G <= 15, "the step's lgkmcnt wait leaves NE pointer stores outstanding");
   uint16_t* nxt = L.u.r.nxt;
   // (a) sources of batch `b0`.  First hop, every byte: its owner (one 64-bit bitmap word, one
   //     last_start) and the owner's descriptor give the copy source (G <= 4 bytes have at most
@@ -1466,30 +1462,6 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       nxt[(e / G) * CH + G * t + e % G] = (uint16_t)q;
     }
   };
-  // The same round split around a step's byte store (the steps below): the pointer reads are issued
-  // with the step's, the pointer stores after the step's byte store, so the step's barrier waits
-  // for the byte store only (LDS operations of a wave complete in order)
-  auto jump_read = [&](int32_t b0, const int32_t* xs, uint32_t pending, int32_t* qv) {
-#pragma unroll
-    for (int e = 0; e < NE; e++) {
-      const bool pd = (pending >> e) & 1;
-      DQ_CHK(!pd || (xs[e] - b0 >= 0 && xs[e] - b0 < BATCH), CHK_K2_NXT);
-      qv[e] = (int32_t)nxt[pd ? xs[e] - b0 : (e / G) * CH + G * t + e % G];
-    }
-  };
-  auto jump_finish = [&](int32_t b0, int32_t* fr, int32_t* xs, uint32_t& pending, const int32_t* qv) {
-#pragma unroll
-    for (int e = 0; e < NE; e++) {
-      const bool pd = (pending >> e) & 1;
-      const int32_t p = xs[e], q = qv[e];
-      const int32_t sbk = b0 + (e / G) * CH + ((G * t) & ~511);
-      const bool fin = pd && (q == p || q < sbk);
-      fr[e] = fin ? q : fr[e];
-      xs[e] = pd && !fin ? q : p;
-      pending &= fin ? ~(1u << e) : ~0u;
-      nxt[(e / G) * CH + G * t + e % G] = (uint16_t)q;
-    }
-  };
   // Software pipeline over batches: while batch k's ordered steps (b) run, batch k+1 takes its
   // first hop (its descriptors are intact until its own steps) and one jump round after each
   // step barrier (nxt holds batch k+1 only: batch k's sources are final in registers by then).
@@ -1547,36 +1519,12 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
             DQ_CHK(g0 + i >= rsize || (frA[k * G + i] >= 0 && frA[k * G + i] <= g0 + i), CHK_K2_SRC);
             v[i] = O[min(frA[k * G + i], 65535)];
           }
-#if DQ_SPLITJUMP
-        // the next batch's jump round (every lane of a wave that has a pending entry runs it, the
-        // others re-store their own pointers): reads now, stores after this step's byte store
-        const bool jmp = (k > 0 || j > 0) && __any(pendB != 0);
-        int32_t qv[NE];
-        if (jmp) jump_read(nbs, xsB, pendB, qv);
-        if (mine)
-#pragma unroll
-          for (int i = 0; i < G; i++)
-            if (g0 + i < rsize) L.out[sh + g0 + i] = v[i];  // a literal rewrites its own value
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        if (jmp) {
-          jump_finish(nbs, frB, xsB, pendB, qv);
-          // the byte stores (issued before the NE pointer stores) are complete; the pointer
-          // stores need not be -- a jump round tolerates reading an older pointer
-          __builtin_amdgcn_s_waitcnt(0xC07F | (NE << 8));
-        } else {
-          __builtin_amdgcn_s_waitcnt(0xC07F);
-        }
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        __builtin_amdgcn_s_barrier();
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-#else
         if ((k > 0 || j > 0) && pendB) jump_round(nbs, frB, xsB, pendB);
         if (mine)
 #pragma unroll
           for (int i = 0; i < G; i++)
             if (g0 + i < rsize) L.out[sh + g0 + i] = v[i];  // a literal rewrites its own value
         __syncthreads();
-#endif
       }
     }
     if (pendB) jump_round(nbs, frB, xsB, pendB);

@@ -81,7 +81,7 @@ def zlib5_bgzf_size(data):
 
 @pytest.mark.parametrize("name", ["1.bam", "hiseq_part-r-00000.bam", "HiSeq.10000.vcf.bgz", "wgs"])
 def test_ratio_at_zlib_level5(golden, name):
-    """The chunked LDS parse (two 32640-byte chunks per block, 16 KiB reach before a chunk) keeps
+    """The chunked LDS parse (two 32640-byte chunks per block, 15000 bytes of reach before a chunk, a 4-byte bucket key) keeps
     htsjdk's level-5 ratio on the golden BAM / VCF streams and the synthetic WGS stream
     (tools/deflate_model.c, profiles/r4_deflate_chunk_model.txt): at most 0.5 % larger."""
     if name == "wgs":

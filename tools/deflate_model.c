@@ -24,6 +24,8 @@ typedef struct {
   int lazy_once;  // look one position ahead only (else defer while the next match is longer)
   int half;       // chunk size: each chunk parses on its own (its matches end inside it), with
   int xw;         // candidates from xw bytes before the chunk start on (0 = no chunks)
+  int hchunk;     // one dynamic Huffman block per chunk (else one per BGZF block)
+  int h4;         // bucket positions by a hash of 4 bytes (so matches are >= 4 bytes)
 } Cfg;
 
 static int lcode(int len) {  // length symbol
@@ -145,7 +147,7 @@ static int match_len(const uint8_t* b, int p, int q, int lim) {
 // best match at p among the tried candidates; returns len (0 if < 3), *dist
 static int find(const Cfg* c, const uint8_t* b, int n, int p, int lim, const int* link, int* dist) {
   int best = 0, bd = 0;
-  if (lim < 3) return 0;
+  if (lim < 3 + (c->h4 ? 1 : 0)) return 0;
   const int qmin = c->half ? (p / c->half) * c->half - c->xw : 0;
   for (int d = 1; d <= c->shortd && d <= p; d++) {
     int l = match_len(b, p, p - d, lim);
@@ -187,8 +189,8 @@ static long block_bits(const Cfg* c, const uint8_t* b, int n, int* link, int* he
   } else {
     for (int p = 0; p < n; p++) {
       link[p] = -1;
-      if (p + 3 <= n) {
-        uint32_t v = b[p] | b[p + 1] << 8 | b[p + 2] << 16;
+      if (p + 3 + (c->h4 ? 1 : 0) <= n) {
+        uint32_t v = b[p] | b[p + 1] << 8 | b[p + 2] << 16 | (c->h4 ? (uint32_t)b[p + 3] << 24 : 0u);
         uint32_t h = (v * 2654435761u) >> (32 - c->hbits);
         link[p] = head[h];
         head[h] = p;
@@ -223,23 +225,35 @@ static long block_bits(const Cfg* c, const uint8_t* b, int n, int* link, int* he
       else { sy[ns++] = (Sym){b[p], 0, 0}; p++; }
     }
   }
-  long fl[286] = {0}, fd[30] = {0};
-  long extra = 0;
-  for (int i = 0; i < ns; i++) {
-    if (sy[i].len) {
-      int s = lcode(sy[i].len), d = dcode(sy[i].dist);
-      fl[s]++; fd[d]++;
-      extra += lextra(s) + dextra(d);
-    } else fl[sy[i].lit]++;
+  // Huffman blocks: the whole parse, or one per chunk (symbols split where their bytes start)
+  long total = 0;
+  int s0 = 0, pos = 0;
+  for (int b = 0; ; b++) {
+    const int bend = c->hchunk && c->half ? (b + 1) * c->half : n;
+    int s1 = s0, p1 = pos;
+    while (s1 < ns && p1 < bend) { p1 += sy[s1].len ? sy[s1].len : 1; s1++; }
+    long fl[286] = {0}, fd[30] = {0};
+    long extra = 0;
+    for (int i = s0; i < s1; i++) {
+      if (sy[i].len) {
+        int s = lcode(sy[i].len), d = dcode(sy[i].dist);
+        fl[s]++; fd[d]++;
+        extra += lextra(s) + dextra(d);
+      } else fl[sy[i].lit]++;
+    }
+    fl[256]++;
+    int ll[286], dl[30];
+    huff(fl, 286, ll);
+    huff(fd, 30, dl);
+    long bits = extra;
+    for (int i = 0; i < 286; i++) bits += fl[i] * ll[i];
+    for (int i = 0; i < 30; i++) bits += fd[i] * dl[i];
+    total += bits + header_bits(ll, dl);
+    s0 = s1;
+    pos = p1;
+    if (s0 >= ns) break;
   }
-  fl[256]++;
-  int ll[286], dl[30];
-  huff(fl, 286, ll);
-  huff(fd, 30, dl);
-  long bits = extra;
-  for (int i = 0; i < 286; i++) bits += fl[i] * ll[i];
-  for (int i = 0; i < 30; i++) bits += fd[i] * dl[i];
-  return bits + header_bits(ll, dl);
+  return total;
 }
 
 int main(int argc, char** argv) {
@@ -267,14 +281,15 @@ int main(int argc, char** argv) {
       {"seg255 nocross, exact h12 chain32 lazy16 nice32", 255, 0, 8, 32, 12, 0, 16, 32, 0},
       {"one parse, exact h15 chain32 lazy16 nice32 (zlib 5 like)", 0, 0, 0, 32, 15, 0, 16, 32, 0},
       {"gpu r3: seg255 cross h11 chain96 lazy32 nice96", 255, 1, 0, 96, 11, 0, 32, 96, 0},
-      {"chunks: halves C=32640 X=16K", 255, 1, 0, 96, 11, 0, 32, 96, 0, 32640, 16384},
-      {"chunks: halves C=32640 X=16K seg64 (bgzf_parse_kernel)", 64, 1, 0, 96, 11, 0, 32, 96, 0, 32640, 16384},
-      {"chunks: quarters C=16320 X=7.5K", 255, 1, 0, 96, 11, 0, 32, 96, 0, 16320, 7680},
-      {"chunks: quarters C=16320 X=4K", 255, 1, 0, 96, 11, 0, 32, 96, 0, 16320, 4096},
-      {"chunks: eighths C=8160 X=8K", 255, 1, 0, 96, 11, 0, 32, 96, 0, 8160, 8192},
-      {"chunks: eighths C=8160 X=16K", 255, 1, 0, 96, 11, 0, 32, 96, 0, 8160, 16384},
-      {"chunks: quarters C=16320 X=7.5K seg64", 64, 1, 0, 96, 11, 0, 32, 96, 0, 16320, 7680},
-      {"chunks: quarters C=16320 X=7.5K chain128", 255, 1, 0, 128, 11, 0, 32, 128, 0, 16320, 7680},
+      {"chunks: halves C=32640 X=15K seg64 (bgzf_parse_kernel)", 64, 1, 0, 96, 11, 0, 32, 96, 0, 32640, 15000, 0},
+      {"  4-byte hash, 96/32/96", 64, 1, 0, 96, 11, 0, 32, 96, 0, 32640, 15000, 0, 1},
+      {"  4-byte hash, 32/16/32", 64, 1, 0, 32, 11, 0, 16, 32, 0, 32640, 15000, 0, 1},
+      {"  4-byte hash, 24/16/32", 64, 1, 0, 24, 11, 0, 16, 32, 0, 32640, 15000, 0, 1},
+      {"  4-byte hash, 16/16/32", 64, 1, 0, 16, 11, 0, 16, 32, 0, 32640, 15000, 0, 1},
+      {"  4-byte hash, 16/8/16", 64, 1, 0, 16, 11, 0, 8, 16, 0, 32640, 15000, 0, 1},
+      {"  4-byte hash, 12/8/16", 64, 1, 0, 12, 11, 0, 8, 16, 0, 32640, 15000, 0, 1},
+      {"  4-byte hash, 8/8/16", 64, 1, 0, 8, 11, 0, 8, 16, 0, 32640, 15000, 0, 1},
+      {"  4-byte hash, 8/4/16", 64, 1, 0, 8, 11, 0, 4, 16, 0, 32640, 15000, 0, 1},
   };
   int nc = sizeof cfgs / sizeof cfgs[0];
   long nb = (n + BLK - 1) / BLK;

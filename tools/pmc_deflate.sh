@@ -1,0 +1,25 @@
+#!/bin/bash
+# Dev tool: PMC counter passes over the deflate kernels (bgzf_parse_kernel, bgzf_code_kernel), one
+# rocprofv3 run per pass, over tools/deflate_bench.py.  usage: tools/pmc_deflate.sh OUTDIR [NRECORDS]
+set -e
+out=${1:-gpurun_out/pmc_deflate}; n=${2:-500000}
+export TMPDIR=/tmp
+mkdir -p "$out"
+i=0
+for pass in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
+            "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" \
+            "SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM_WR SQ_LDS_UNALIGNED_STALL SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM SQ_INST_CYCLES_VMEM_WR" \
+            "FETCH_SIZE GRBM_GUI_ACTIVE GRBM_COUNT" "WRITE_SIZE"; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --pmc $pass --kernel-include-regex "bgzf_(parse|code)" --output-format csv -d $out/p$i -o run -- python3 -u tools/deflate_bench.py --records $n --reps 1 > $out/p$i.log 2>&1
+done
+python3 - "$out" <<'PY'
+import csv, glob, sys, collections
+out = sys.argv[1]
+agg = collections.defaultdict(float); nd = collections.Counter()
+for f in glob.glob(out + "/p*/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        k = ("parse" if "parse" in r['Kernel_Name'] else "code", r['Counter_Name'])
+        agg[k] += float(r['Counter_Value']); nd[k] += 1
+for k in sorted(agg): print(f"{k[0]:6s} {k[1]:28s} {agg[k]:.4g}  (dispatch-rows {nd[k]})")
+PY
