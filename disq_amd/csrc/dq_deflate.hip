@@ -361,7 +361,7 @@ struct Finder {
   const PLds& L;
   int np, chain, nice, good;
   // the slot of x in the ascending list bl[lo, hi), which holds it: 16-way search
-  __device__ int slot(int lo, int hi, int x) const {
+  __device__ __attribute__((always_inline)) int slot(int lo, int hi, int x) const {
     int a = lo, b = hi;
     while (b - a > 16) {
       const int st = (b - a) >> 4;
@@ -377,124 +377,174 @@ struct Finder {
     for (int k = 0; k < 16; k++) c += a + k < b && (int)L.bl[a + k] < x;
     return a + c;
   }
-  // longest match (>= 3, else 0) at x, at most lim bytes, among `chain` candidates; *dist its
-  // distance
-  __device__ int find(int x, int lim, int* dist, int chain) const {
-    *dist = 0;
-    if (lim < 3 || x + 4 > np) return 0;
+  // A match search in progress: batches of 8 candidates, resumable, so the lanes of a wave run
+  // one batch per step of the parse loop whichever search each is in (a lane whose search ends
+  // early starts its next one instead of idling while the wave's longest search finishes).
+  struct Search {
+    int x, lim, i0, lo, best, bd, cap;
+    uint64_t pa, pb;  // the first 16 bytes at x
+    bool more;        // batches left
+  };
+  __device__ __attribute__((always_inline)) void begin(Search& S, int x, int lim, int ch) const {
+    S.x = x;
+    S.lim = lim;
+    S.best = 0;
+    S.bd = 0;
+    S.cap = min(lim, nice);
+    S.more = false;
+    if (lim < 3 || x + 4 > np) return;
     const uint32_t h = hash4(L.in, x);
     const int blo = h ? L.head[h - 1] : 0;
     const int g = slot(blo, L.head[h], x);
-    const int lo = max(blo, g - chain);
-    // the first 16 bytes at x, once; each batch compares its 8 candidates' first 16 bytes with
-    // 16 loads issued together (lengths < 16, most of them, need no further round trip)
-    const uint64_t pa = ld8(L.in, x), pb = ld8(L.in, x + 8);
-    int best = 0, bd = 0;
-    const int cap = min(lim, nice);
+    S.lo = max(blo, g - ch);
+    S.i0 = g - 1;
+    S.more = S.i0 >= S.lo;
+    S.pa = ld8(L.in, x);
+    S.pb = ld8(L.in, x + 8);
+  }
+  // one batch: 8 candidates' positions in one 16-byte read and their first 16 bytes with 16 loads
+  // issued together (lengths < 16, most of them, need no further round trip)
+  __device__ __attribute__((always_inline)) void batch(Search& S) const {
+    const int x = S.x, i0 = S.i0, lo = S.lo, cap = S.cap;
+    int best = S.best, bd = S.bd;
     bool more = true;
-    for (int i0 = g - 1; i0 >= lo && more; i0 -= 8) {
-      int q8[8];
-      uint64_t ya[8], yb[8];
+    int q8[8];
+    uint64_t ya[8], yb[8];
 #if DQ_LDS_UNALIGNED
-      // entries i0 - 7 .. i0 in one 16-byte read (below lo, or before bl itself: masked)
-      uint4 qq;
-      __builtin_memcpy(&qq, &L.bl[i0 - 7], 16);
-      const uint32_t qw[4] = {qq.x, qq.y, qq.z, qq.w};
+    // entries i0 - 7 .. i0 (below lo, or before bl itself: masked)
+    uint4 qq;
+    __builtin_memcpy(&qq, &L.bl[i0 - 7], 16);
+    const uint32_t qw[4] = {qq.x, qq.y, qq.z, qq.w};
 #endif
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
+    for (int k = 0; k < 8; k++) {
 #if DQ_LDS_UNALIGNED
-        q8[k] = i0 - k >= lo ? (int)((qw[(7 - k) >> 1] >> (16 * ((7 - k) & 1))) & 0xffffu) : -1;
+      q8[k] = i0 - k >= lo ? (int)((qw[(7 - k) >> 1] >> (16 * ((7 - k) & 1))) & 0xffffu) : -1;
 #else
-        q8[k] = i0 - k >= lo ? (int)L.bl[i0 - k] : -1;
+      q8[k] = i0 - k >= lo ? (int)L.bl[i0 - k] : -1;
 #endif
-        const int q = q8[k] >= 0 ? q8[k] : x;
-        ya[k] = ld8(L.in, q) ^ pa;
-        yb[k] = ld8(L.in, q + 8) ^ pb;
-      }
+      const int q = q8[k] >= 0 ? q8[k] : x;
+      ya[k] = ld8(L.in, q) ^ S.pa;
+      yb[k] = ld8(L.in, q + 8) ^ S.pb;
+    }
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const int q = q8[k];
-        if (q < 0 || x - q > WIN) {  // past the window (candidates are most recent first)
-          more = false;
-          break;
-        }
-        int l = ya[k] ? (int)(__builtin_ctzll(ya[k]) >> 3)
-                      : yb[k] ? 8 + (int)(__builtin_ctzll(yb[k]) >> 3) : 16;
-        // (rare) 16 bytes equal: on up to cap, unless the 4 bytes ending at `best` differ (then
-        // it cannot beat best: zlib's scan_end test)
-        if (l == 16 && l < cap && (best <= 16 || ld4(L.in, q + best - 3) == ld4(L.in, x + best - 3))) {
-          while (l < cap) {
-            const uint64_t y = ld8(L.in, q + l) ^ ld8(L.in, x + l);
-            if (y) {
-              l += (int)(__builtin_ctzll(y) >> 3);
-              break;
-            }
-            l += 8;
+    for (int k = 0; k < 8; k++) {
+      const int q = q8[k];
+      if (q < 0 || x - q > WIN) {  // past the window (candidates are most recent first)
+        more = false;
+        break;
+      }
+      int l = ya[k] ? (int)(__builtin_ctzll(ya[k]) >> 3)
+                    : yb[k] ? 8 + (int)(__builtin_ctzll(yb[k]) >> 3) : 16;
+      // (rare) 16 bytes equal: on up to cap, unless the 4 bytes ending at `best` differ (then it
+      // cannot beat best: zlib's scan_end test)
+      if (l == 16 && l < cap && (best <= 16 || ld4(L.in, q + best - 3) == ld4(L.in, x + best - 3))) {
+        while (l < cap) {
+          const uint64_t y = ld8(L.in, q + l) ^ ld8(L.in, x + l);
+          if (y) {
+            l += (int)(__builtin_ctzll(y) >> 3);
+            break;
           }
+          l += 8;
         }
-        l = min(l, cap);
-        if (l > best) {
-          best = l;
-          bd = x - q;
-        }
-        if (best >= cap) {  // the first candidate to reach cap wins
-          more = false;
-          break;
-        }
+      }
+      l = min(l, cap);
+      if (l > best) {
+        best = l;
+        bd = x - q;
+      }
+      if (best >= cap) {  // the first candidate to reach cap wins
+        more = false;
+        break;
       }
     }
-    if (best >= cap && cap < lim) {  // the winner, extended to the end of its match
-      const int q = x - bd;
-      int l = cap;
-      while (l < lim) {
-        const uint64_t y = ld8(L.in, q + l) ^ ld8(L.in, x + l);
+    S.best = best;
+    S.bd = bd;
+    S.i0 = i0 - 8;
+    S.more = more && S.i0 >= lo;
+  }
+  // the search's match (>= 3, else 0), the winner extended to the end of its match; *dist
+  __device__ __attribute__((always_inline)) int finish(const Search& S, int* dist) const {
+    int best = S.best;
+    if (best >= S.cap && S.cap < S.lim) {
+      const int q = S.x - S.bd;
+      int l = S.cap;
+      while (l < S.lim) {
+        const uint64_t y = ld8(L.in, q + l) ^ ld8(L.in, S.x + l);
         if (y) {
           l += (int)(__builtin_ctzll(y) >> 3);
           break;
         }
         l += 8;
       }
-      best = min(l, lim);
+      best = min(l, S.lim);
     }
-    *dist = bd;
+    *dist = S.bd;
     return best >= 3 ? best : 0;
+  }
+  // longest match (>= 3, else 0) at x, at most lim bytes, among `ch` candidates; *dist its
+  // distance (the search run to its end at once)
+  __device__ int find(int x, int lim, int* dist, int ch) const {
+    Search S;
+    begin(S, x, lim, ch);
+    while (S.more) batch(S);
+    return finish(S, dist);
   }
 };
 
-// One parse step at x (zlib-style lazy evaluation: while the match at the next position is
-// longer and the current one shorter than `lazy`, emit a literal and move on; the look-ahead
-// search walks a quarter of the candidates once the current match is `good` long, as zlib's
-// deflate_slow does): appends its symbols to w[*ns...] and returns the new position.  The step
-// depends on x alone, so two parses that reach the same position continue identically (the
-// merge rule below).  Matches end at the chunk end np.
-__device__ int parse_step(const Finder& F, int lazy, int x, uint32_t* w, int* ns, int cap,
-                          uint64_t* starts = nullptr, int sbase = 0) {
+// The lane parse loop: zlib-style lazy evaluation (while the match at the next position is longer
+// and the current one shorter than `lazy`, emit a literal and move on; the look-ahead search walks
+// a quarter of the candidates once the current match is `good` long, as zlib's deflate_slow
+// does), as a per-lane state machine: each pass of the loop runs one batch of each lane's current
+// search, or ends it and takes the parse decision, so the wave's lanes stay busy however their
+// search lengths differ (round 4: one lane in five was active per instruction with the searches
+// run to their ends inside each parse step).  A step depends on its position alone, so two parses
+// that reach the same position continue identically (the merge rule below).  Matches end at the
+// chunk end np.  emit(word, position) stores a symbol; step_done(x) is called when a step ends at
+// x and returns whether the lane parses on.
+template <class Emit, class Done>
+__device__ __attribute__((always_inline)) inline void parse_lanes(const Finder& F, int lazy, int x, bool act, Emit emit, Done step_done) {
   const int n = F.np;
-  auto mark = [&](int p) {  // (a deferred literal can start past the segment: not recorded)
-    if (starts && p - sbase < 64) *starts |= 1ull << (p - sbase);
-  };
-  int d = 0, l = F.find(x, min(MAXM, n - x), &d, F.chain);
-  while (l && l < lazy && x + 1 < n) {
-    int d2 = 0;
-    const int ch = F.good > 0 && l >= F.good ? max(1, F.chain >> 2) : F.chain;
-    const int l2 = F.find(x + 1, min(MAXM, n - x - 1), &d2, ch);
-    if (l2 <= l) break;
-    DQ_CHK(*ns < cap, CHK_Z_STAGE);
-    mark(x);
-    w[(*ns)++] = lit_word(F.L.in[x]);
-    x++;
-    l = l2;
-    d = d2;
+  Finder::Search S;
+  int l = 0, d = 0;
+  bool lz = false;  // the current search is the look-ahead at x + 1
+  if (act) F.begin(S, x, min(MAXM, n - x), F.chain);
+  while (__any(act)) {
+    if (act && S.more) F.batch(S);
+    if (act && !S.more) {  // the search ended: the parse decision
+      int d2 = 0;
+      const int r = F.finish(S, &d2);
+      bool next = false;  // emit the pending symbol at x and end the step
+      if (!lz) {
+        l = r;
+        d = d2;
+        if (l && l < lazy && x + 1 < n) {
+          lz = true;
+          F.begin(S, x + 1, min(MAXM, n - x - 1), F.good > 0 && l >= F.good ? max(1, F.chain >> 2) : F.chain);
+        } else {
+          next = true;
+        }
+      } else if (r <= l) {
+        next = true;
+      } else {  // a longer match one on: a literal, and look one further
+        emit(lit_word(F.L.in[x]), x);
+        x++;
+        l = r;
+        d = d2;
+        if (l < lazy && x + 1 < n)
+          F.begin(S, x + 1, min(MAXM, n - x - 1), F.good > 0 && l >= F.good ? max(1, F.chain >> 2) : F.chain);
+        else
+          next = true;
+      }
+      if (next) {
+        emit(l ? match_word(l, d) : lit_word(F.L.in[x]), x);
+        x += l ? l : 1;
+        lz = false;
+        act = step_done(x);
+        if (act) F.begin(S, x, min(MAXM, n - x), F.chain);
+      }
+    }
   }
-  DQ_CHK(*ns < cap, CHK_Z_STAGE);
-  mark(x);
-  if (l) {
-    w[(*ns)++] = match_word(l, d);
-    return x + l;
-  }
-  w[(*ns)++] = lit_word(F.L.in[x]);
-  return x + 1;
 }
 
 // The merge fields of lane_mrg
@@ -662,11 +712,22 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
   uint32_t* const lane_w = lanes_w + (int64_t)t * LANE_WORDS;
   const Finder F{L, np, min(chain, MAXCAND), nice, good};
   {
-    int ns = 0, x = s0;
-    uint64_t st = 0;
-    while (x < s1) x = parse_step(F, lazy, x, lane_w, &ns, OWN_WORDS, &st, s0);
+    int ns = 0;
+    uint64_t st = 0;  // symbol starts in the segment (a deferred literal past its end: left out)
+    int ex = s0;
+    parse_lanes(
+        F, lazy, s0, s0 < s1,
+        [&](uint32_t w, int p) __attribute__((always_inline)) {
+          DQ_CHK(ns < OWN_WORDS, CHK_Z_STAGE);
+          if (p - s0 < 64) st |= 1ull << (p - s0);
+          lane_w[ns++] = w;
+        },
+        [&](int x) __attribute__((always_inline)) {
+          ex = x;
+          return x < s1;
+        });
     L.lane_nsym[t] = (uint16_t)ns;
-    L.lane_exit[t] = (uint32_t)x;
+    L.lane_exit[t] = (uint32_t)ex;
     if (t < PL) {
       L.sbits[2 * t] = (uint32_t)st;
       L.sbits[2 * t + 1] = (uint32_t)(st >> 32);
@@ -678,61 +739,73 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
   // ---- continuation: from its exit, lane t parses on until it reaches a symbol boundary of a
   //      later lane's speculative parse (the same position continues identically), skipping
   //      lanes whose whole parse it overruns
-  if (t < nlc) {
-    int E = (int)L.lane_exit[t], u = t + 1, k = 0, nc = 0;
+  {
+    int E = t < nlc ? (int)L.lane_exit[t] : np, u = t + 1, k = 0, nc = 0;
     bool over = false;
     uint32_t* const cw = lane_w + OWN_WORDS;
-    for (;;) {
-      if (E >= np) {  // the chunk's end
-        u = PWG;
-        k = 0;
-        break;
-      }
-      if (u >= nlc) {  // no later lane holds symbols: parse on to the chunk end
-        if (nc > CONT_WORDS - 40) {
-          over = true;
-          break;
+    // the merge test at E: false when the lane stops here (merged, the chunk's end, overflowed),
+    // true when it parses another step
+    auto check = [&](int Ex) __attribute__((always_inline)) -> bool {
+      E = Ex;
+      for (;;) {
+        if (E >= np) {  // the chunk's end
+          u = PWG;
+          k = 0;
+          return false;
         }
-        E = parse_step(F, lazy, E, cw, &nc, CONT_WORDS);
-        continue;
-      }
-      // lane u's symbol starts (its segment [su, su + 64)) and its exit; E >= su
-      const int su = xs + PSEG * u, eu = (int)L.lane_exit[u];
-      if (E > eu) {  // lane u's whole parse lies before E
-        u++;
-        continue;
-      }
-      if (E == eu) {  // merged: lane u's continuation
-        k = L.lane_nsym[u];
-        break;
-      }
-      const uint64_t ub = (uint64_t)L.sbits[2 * u] | (uint64_t)L.sbits[2 * u + 1] << 32;
-      if (E < su + PSEG && ((ub >> (E - su)) & 1)) {  // merged: lane u's symbols from k on
-        k = __popcll(ub & ((1ull << (E - su)) - 1));
-        break;
-      }
-      if (nc > CONT_WORDS - 40) {  // (a step appends at most lazy + 1 <= 33 symbols)
-        // no merge within the staging (e.g. one repeated byte: 258-byte matches from lane t's
-        // positions never meet lane u's): end exactly on lane u's next boundary pu > E, with
-        // matches cut to fit and literals for the last < 3 bytes -- a valid parse that merges
-        const uint64_t after = E - su + 1 < 64 ? ub >> (E - su + 1) : 0ull;
-        const int pu = E < su + PSEG && after ? E + 1 + (int)__builtin_ctzll(after) : eu;
-        while (E < pu && nc < CONT_WORDS) {
-          int d = 0;
-          const int l = F.find(E, min(MAXM, pu - E), &d, F.chain);
-          cw[nc++] = l ? match_word(l, d) : lit_word(L.in[E]);
-          E += l ? l : 1;
+        if (u >= nlc) {  // no later lane holds symbols: parse on to the chunk end
+          if (nc > CONT_WORDS - 40) {
+            over = true;
+            return false;
+          }
+          return true;
         }
-        if (E != pu) {  // (a gap of literals longer than the staging: stored)
-          over = true;
-          break;
+        // lane u's symbol starts (its segment [su, su + 64)) and its exit; E >= su
+        const int su = xs + PSEG * u, eu = (int)L.lane_exit[u];
+        if (E > eu) {  // lane u's whole parse lies before E
+          u++;
+          continue;
         }
-        k = pu == eu ? (int)L.lane_nsym[u] : __popcll(ub & ((1ull << (pu - su)) - 1));
-        break;
+        if (E == eu) {  // merged: lane u's continuation
+          k = L.lane_nsym[u];
+          return false;
+        }
+        const uint64_t ub = (uint64_t)L.sbits[2 * u] | (uint64_t)L.sbits[2 * u + 1] << 32;
+        if (E < su + PSEG && ((ub >> (E - su)) & 1)) {  // merged: lane u's symbols from k on
+          k = __popcll(ub & ((1ull << (E - su)) - 1));
+          return false;
+        }
+        if (nc > CONT_WORDS - 40) {  // (a step appends at most lazy + 1 <= 33 symbols)
+          // no merge within the staging (e.g. one repeated byte: 258-byte matches from lane t's
+          // positions never meet lane u's): end exactly on lane u's next boundary pu > E, with
+          // matches cut to fit and literals for the last < 3 bytes -- a valid parse that merges
+          const uint64_t after = E - su + 1 < 64 ? ub >> (E - su + 1) : 0ull;
+          const int pu = E < su + PSEG && after ? E + 1 + (int)__builtin_ctzll(after) : eu;
+          while (E < pu && nc < CONT_WORDS) {
+            int d = 0;
+            const int l = F.find(E, min(MAXM, pu - E), &d, F.chain);
+            cw[nc++] = l ? match_word(l, d) : lit_word(L.in[E]);
+            E += l ? l : 1;
+          }
+          if (E != pu) {  // (a gap of literals longer than the staging: stored)
+            over = true;
+            return false;
+          }
+          k = pu == eu ? (int)L.lane_nsym[u] : __popcll(ub & ((1ull << (pu - su)) - 1));
+          return false;
+        }
+        return true;
       }
-      E = parse_step(F, lazy, E, cw, &nc, CONT_WORDS);
-    }
-    L.lane_mrg[t] = mrg_word(over ? PWG : u, k, nc, over);
+    };
+    const bool go = t < nlc && check(E);
+    parse_lanes(
+        F, lazy, E, go,
+        [&](uint32_t w, int) __attribute__((always_inline)) {
+          DQ_CHK(nc < CONT_WORDS, CHK_Z_STAGE);
+          cw[nc++] = w;
+        },
+        check);
+    if (t < nlc) L.lane_mrg[t] = mrg_word(over ? PWG : u, k, nc, over);
   }
   DTS();
   // ---- the chunk's parse: lane 0, then the lane each continuation merged into.  Pointer

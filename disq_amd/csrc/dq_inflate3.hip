@@ -1147,13 +1147,12 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     // 20-29 set the minimum segment bits)
     const uint32_t maxl = (sflags >> 8) & 1023u, minseg = (sflags >> 20) & 1023u;
     int nl = (int)max(1u, min(maxl ? maxl : (uint32_t)NDEC, span / (minseg ? minseg : 128u)));
-    if (cap >= 8) {
-      nl = min(nl, cap);
-      AB = reinterpret_cast<int32_t*>(L.out + ob);
-    } else {  // a short image tail: at most 8 lanes, no checkpoints
-      nl = min(nl, 8);
-      AB = L.small;
-    }
+    nl = cap >= 8 ? min(nl, cap) : min(nl, 8);  // a short image tail: at most 8 lanes, no checkpoints
+    // segments of ceil(span / nl) bits; lanes whose segment would start past the data end (up to
+    // nl - seg bits of rounding: their warm-up read words past the member) are not started
+    const uint32_t seg = (span + nl - 1) / nl;
+    if (seg) nl = (int)((span + seg - 1) / seg);
+    AB = cap >= 8 ? reinterpret_cast<int32_t*>(L.out + ob) : L.small;
     AE = AB + nl;
     AC = AE + nl;
     LS = AC + nl;
@@ -1162,7 +1161,6 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     SC = SE + nl;
     if (cap >= 8) CK = reinterpret_cast<uint32_t*>(SC + nl);
     DQ_CHK(cap < 8 || (ob >= sh + produced && ob + 4 * nl * (7 + NCK) <= OUTCAP), CHK_K2_LANES);
-    const uint32_t seg = (span + nl - 1) / nl;
 #ifdef DQ_CHECKED
     GSrc gsrc{W, (endbits >> 5) + 8, 1u << 12};
 #else
