@@ -40,7 +40,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "decompressed BAM GB/s + reads/sec (whole node) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.29 TB/s measured copy)
-TRAFFIC_PROFILE = "r3aq_inflate_traffic_pmc.json"
+TRAFFIC_PROFILE = "r4u_inflate_traffic_pmc.json"
 
 
 def log(*a):
@@ -396,15 +396,15 @@ def main():
                 "bound": "hbm",
                 "limiter": "VALU issue + LDS/barrier latency of the serial Huffman decode "
                            "(DESIGN.md section 3), far below the HBM roof",
-                "kernel": "inflate_block_kernel",
+                "kernel": "inflate_block_kernel + inflate_tail_kernel (one K2 launch)",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
                 "traffic_src": traffic_src,
-                "pmc_src": "profiles/r3aq_inflate_pmc.txt (VALU busy 70 %, 56.5 % of wave cycles "
-                           "waiting, LDS bank conflicts 28.8 %)",
+                "pmc_src": "profiles/r4u_inflate_pmc.txt (SQ counters of both K2 kernels, this build)",
+                "trace_src": "profiles/r4u_rocprof_summary.txt (rocprofv3 kernel trace of this bench command)",
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_launch_ms": round(infl_avg, 3),
             },

@@ -309,6 +309,12 @@ struct ImgOut {  // LSB-first bits OR-ed into the LDS image from bit position p 
 __device__ inline uint32_t hash4(const uint8_t* in, int p) {
   return (ld4(in, p) * 2654435761u) >> (32 - HBITS);
 }
+// the same from aligned words (faster for a pass over every position: consecutive lanes' words
+// coincide)
+__device__ inline uint32_t hash4a(const uint8_t* in, int p) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(in + (p & ~3));
+  return (__builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(p & 3)) * 2654435761u) >> (32 - HBITS);
+}
 
 __device__ inline int sym_bytes(uint32_t w) {  // uncompressed bytes of a staged symbol
   const uint32_t ll = sym_ll(w);
@@ -372,9 +378,14 @@ struct Finder {
       b = m == 15 ? b : na + st;
       a = na;
     }
+    // the last <= 16 entries in two 16-byte reads
+    uint4 v0, v1;
+    __builtin_memcpy(&v0, &L.bl[a], 16);
+    __builtin_memcpy(&v1, &L.bl[a + 8], 16);
+    const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
     int c = 0;
 #pragma unroll
-    for (int k = 0; k < 16; k++) c += a + k < b && (int)L.bl[a + k] < x;
+    for (int k = 0; k < 16; k++) c += a + k < b && (int)((w[k >> 1] >> (16 * (k & 1))) & 0xffffu) < x;
     return a + c;
   }
   // A match search in progress: batches of 8 candidates, resumable, so the lanes of a wave run
@@ -484,7 +495,7 @@ struct Finder {
   }
   // longest match (>= 3, else 0) at x, at most lim bytes, among `ch` candidates; *dist its
   // distance (the search run to its end at once)
-  __device__ int find(int x, int lim, int* dist, int ch) const {
+  __device__ __attribute__((always_inline)) int find(int x, int lim, int* dist, int ch) const {
     Search S;
     begin(S, x, lim, ch);
     while (S.more) batch(S);
@@ -623,7 +634,7 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
   //      no barrier, no position hashed twice.
   const int rng = ((npos + SCAT_WAVES - 1) / SCAT_WAVES + 63) & ~63;  // positions per range
   for (int x = t; x < npos; x += PWG) {
-    const uint32_t h = hash4(L.in, x);
+    const uint32_t h = hash4a(L.in, x);
     atomicAdd(&L.head[h], 1);
     const int r = x / rng;
     if (r < SCAT_WAVES - 1) atomicAdd(&L.cnt[r][h >> 1], 1u << (16 * (h & 1)));
@@ -669,7 +680,7 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
     for (int x0 = wv * rng; x0 < xe; x0 += 64) {
       const int x = x0 + lane;
       const bool valid = x < xe;
-      const uint32_t h = valid ? hash4(L.in, x) : 0u;
+      const uint32_t h = valid ? hash4a(L.in, x) : 0u;
       uint64_t m = __ballot(valid);
 #pragma unroll
       for (int k = 0; k < HBITS; k++) {
@@ -807,6 +818,7 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
         check);
     if (t < nlc) L.lane_mrg[t] = mrg_word(over ? PWG : u, k, nc, over);
   }
+  if (tim) __syncthreads();  // (timing: the continuation stamp after every wave's)
   DTS();
   // ---- the chunk's parse: lane 0, then the lane each continuation merged into.  Pointer
   //      jumping: after round r every lane within 2^(r+1) - 1 merges of lane 0 is marked.

@@ -14,6 +14,11 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device)")
 
 
+def pytest_report_header(config):
+    lib = os.environ.get("DQ_GPU_LIB")
+    return f"DQ_GPU_LIB={lib}" if lib else None
+
+
 @pytest.fixture(scope="session")
 def golden():
     return GOLDEN
