@@ -1200,13 +1200,13 @@ static int text_run(dq_ctx* ctx, int32_t drop_hash) {
 
 // ------------------------------------------------------------------ BGZF deflate (write path)
 // htsjdk BlockCompressedOutputStream over a byte stream in HBM: blocks of 65280 bytes compressed
-// in batches (per block 1 MiB of staged-symbol space, of which the parse touches about 50 KB, and
-// 6.6 KB of lane / chunk records), packed into ctx->z_out.
+// in batches of 1024 (per block 1.8 MiB of staged-symbol space, of which the parse touches about
+// 60 KB, and 10.7 KB of segment / chunk records), packed into ctx->z_out.
 static int bgzf_compress_dev(dq_ctx* ctx, const uint8_t* d_src, int64_t len, double* ms) {
   if (!deflate_tables(ctx->o.device)) RET(DQ_EDEVICE, "deflate table initialisation failed");
   hipStream_t s = ctx->s;
   const int64_t nblk = bgzf_block_count(len);
-  const int64_t batch = std::min<int64_t>(std::max<int64_t>(nblk, 1), 2048);
+  const int64_t batch = std::min<int64_t>(std::max<int64_t>(nblk, 1), 1024);
   int rc;
   if ((rc = ensure_all(ctx, ctx->z_stage, bgzf_stage_bytes(batch)))) return rc;
   if ((rc = ensure_all(ctx, ctx->z_link, bgzf_meta_bytes(batch)))) return rc;

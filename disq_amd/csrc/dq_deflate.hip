@@ -62,28 +62,30 @@ namespace {
 constexpr int BLK_U = 65280;             // htsjdk DEFAULT_UNCOMPRESSED_BLOCK_SIZE
 constexpr int NCH = 2;                   // chunks per block
 constexpr int CH = BLK_U / NCH;          // 32640 bytes per chunk
-constexpr int PSEG = 64;                 // bytes per parsing lane
-constexpr int PL = CH / PSEG;            // 510 lanes per chunk
+constexpr int PSEG = 32;                 // bytes per parse segment
+constexpr int PL = CH / PSEG;            // 1020 segments per chunk
+constexpr int MSEG = 1024;               // segment slots per chunk (staging, lane words)
 constexpr int PWG = 512;                 // threads per chunk workgroup
-constexpr int XW = 15000;                // window reach before the chunk start
+constexpr int XW = 13600;                // window reach before the chunk start
 constexpr int NPMAX = CH + XW;           // bytes (positions) a chunk workgroup holds
 constexpr int HBITS = 11;                // hash buckets
 constexpr int MAXM = 258;
 constexpr int WIN = 32768;               // DEFLATE window
-constexpr int OWN_WORDS = 100;           // a lane's own symbols (<= 64 + the last step's <= 33)
-constexpr int CONT_WORDS = 156;          // its continuation past its segment end
+constexpr int OWN_WORDS = 68;            // a segment's own symbols (<= 32 + the last step's <= 33)
+constexpr int CONT_WORDS = 156;          // its continuation past its end
 constexpr int LANE_WORDS = OWN_WORDS + CONT_WORDS;
 constexpr int MAX_DEFLATE = 65536 - 26;  // BSIZE limit: 18-byte header + payload + 8 trailer
 constexpr int MAXCAND = 128;             // candidates per match search at most (cfg.chain)
 constexpr int CWG = 256;                 // threads of the code kernel
-constexpr int NLANE = NCH * PL;          // 1020 lanes per block; code thread i owns lanes 4i..4i+3
-// per block in `meta`: a word per lane (NCH x PWG), then NCH chunk records of CI_WORDS
+constexpr int NLANE = NCH * PL;          // 2040 segments per block; code thread i owns 8i..8i+7
+constexpr int CSEG = 8;                  // segments per code thread
+// per block in `meta`: a word per segment (NCH x MSEG), then NCH chunk records of CI_WORDS
 constexpr int CI_WORDS = 320;
 enum { CI_LL = 0, CI_D = 286, CI_CRC = 316, CI_OVER = 317, CI_BYTES = 318 };
-constexpr int META_WORDS = NCH * (PWG + CI_WORDS);
-// lane word: first own symbol | own symbols << 8 | continuation symbols << 16 | reached << 24
+constexpr int META_WORDS = NCH * (MSEG + CI_WORDS);
+// segment word: first own symbol | own symbols << 8 | continuation symbols << 16 | reached << 24
 constexpr uint32_t LM_REACHED = 1u << 24;
-static_assert(PL * PSEG == CH && PL <= PWG && NLANE <= 4 * CWG, "lane layout");
+static_assert(PL * PSEG == CH && PL <= MSEG && NLANE <= CSEG * CWG, "segment layout");
 static_assert(OWN_WORDS < 256 && CONT_WORDS < 256, "lane word fields");
 
 __constant__ uint32_t c_dcrc[256];
@@ -167,6 +169,7 @@ __device__ void build_lengths(const int32_t* f, int m, int maxlen, int32_t* sort
     const int fs = f[s];
     if (fs <= 0) continue;
     int r = 0;
+#pragma unroll 8
     for (int k = 0; k < m; k++) {
       const int fk = f[k];
       r += fk > 0 && (fk < fs || (fk == fs && k < s));
@@ -225,20 +228,38 @@ __device__ void build_lengths(const int32_t* f, int m, int maxlen, int32_t* sort
     for (int c = cnt[l]; c > 0; c--) len[sorted[--j]] = l;
 }
 
-// Canonical codes (RFC 1951 3.2.2), bit-reversed for the LSB-first stream: code | len << 16.
-// bl: 32 LDS words of scratch (length counts, then next codes).
-__device__ void canon_codes(const int32_t* len, int m, uint32_t* code, int32_t* bl) {
-  for (int l = 0; l < 32; l++) bl[l] = 0;
-  for (int s = 0; s < m; s++) bl[len[s]]++;
-  bl[0] = 0;
-  uint32_t c = 0;
-  for (int l = 1; l < 16; l++) {
-    c = (c + (uint32_t)bl[l - 1]) << 1;
-    bl[16 + l] = (int32_t)c;
+// Canonical codes (RFC 1951 3.2.2), bit-reversed for the LSB-first stream: code | len << 16, by one
+// wave: length counts by ballots, a symbol's code = its length's first code + its rank among the
+// symbols of that length before it (ballots again), no serial loop over symbols.
+__device__ void canon_codes_wave(const int32_t* len, int m, uint32_t* code, int lane) {
+  int cnt[16];
+#pragma unroll
+  for (int l = 0; l < 16; l++) cnt[l] = 0;
+  for (int s0 = 0; s0 < m; s0 += 64) {
+    const int l = s0 + lane < m ? len[s0 + lane] : 0;
+#pragma unroll
+    for (int L = 1; L < 16; L++) cnt[L] += __popcll(__ballot(l == L));
   }
-  for (int s = 0; s < m; s++) {
-    const int l = len[s];
-    code[s] = l ? (rev((uint32_t)bl[16 + l]++, l) | ((uint32_t)l << 16)) : 0u;
+  uint32_t next[16];
+  uint32_t c = 0;
+  next[0] = 0;
+#pragma unroll
+  for (int L = 1; L < 16; L++) {
+    c = (c + (uint32_t)(L > 1 ? cnt[L - 1] : 0)) << 1;
+    next[L] = c;
+  }
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (int s0 = 0; s0 < m; s0 += 64) {
+    const int s = s0 + lane;
+    const int l = s < m ? len[s] : 0;
+    uint32_t mine = 0;
+#pragma unroll
+    for (int L = 1; L < 16; L++) {
+      const uint64_t b = __ballot(l == L);
+      if (l == L) mine = next[L] + (uint32_t)__popcll(b & below);
+      next[L] += (uint32_t)__popcll(b);
+    }
+    if (s < m) code[s] = l ? (rev(mine, l) | ((uint32_t)l << 16)) : 0u;
   }
 }
 
@@ -246,7 +267,8 @@ __device__ void canon_codes(const int32_t* len, int m, uint32_t* code, int32_t* 
 #define DQ_LDS_UNALIGNED 1
 #endif
 #if DQ_LDS_UNALIGNED
-// 4 / 8 bytes at an arbitrary LDS offset x: one unaligned ds_read_b32 / ds_read_b64
+// 4 / 8 bytes at an arbitrary LDS offset x: one unaligned ds_read_b32 / ds_read_b64 (measured
+// faster than aligned words + byte shifts, profiles/r4m_deflate_sweep.txt)
 __device__ inline uint32_t ld4(const uint8_t* in, int x) {
   uint32_t v;
   __builtin_memcpy(&v, in + x, 4);
@@ -340,23 +362,23 @@ struct alignas(16) PLds {
   union {
     struct {
       uint32_t crc_t[256];
-      uint32_t lane_exit[PWG];  // the parse's exit of each lane; later jump pointers, first symbols
-      uint32_t lane_mrg[PWG];   // continuation: merge lane | symbol << 10 | count << 17 | over << 25
-      uint32_t lane_mark[PWG];  // on the chunk's parse
-      uint16_t lane_nsym[PWG];  // own symbols
-      uint32_t sbits[CH / 32];  // symbol starts of the lanes' own parses inside their segments (a
-                                // deferred literal past the segment end is left out): each lane's
-                                // 64-bit word holds its own starts only
+      uint32_t seg_exit[MSEG];  // the parse's exit of each segment; later jump pointers, first symbols
+      uint32_t seg_mrg[MSEG];   // continuation: merge segment | symbol << 11 | count << 18 | over << 26
+      uint8_t seg_mark[MSEG];   // on the chunk's parse
+      uint8_t seg_nsym[MSEG];   // own symbols
+      uint32_t sbits[PL];       // symbol starts of each segment's own parse inside it (a deferred
+                                // literal past the segment end is left out): one word each
     };
     // the bucket build (before any of the above is live): the counts of scatter waves 0..2's
     // position ranges, two 16-bit counts per word, then those waves' successors' cursors
     uint32_t cnt[SCAT_WAVES - 1][1 << (HBITS - 1)];
   };
+  int32_t hist[CI_CRC];       // literal/length and distance histograms of every symbol parsed
   uint32_t wred[16];
   int32_t misc[8];
 };
 static_assert(sizeof(PLds) <= 160 * 1024, "one chunk workgroup per CU");
-static_assert(PSEG == 64, "a lane's symbol starts are one 64-bit word of sbits");
+static_assert(PSEG == 32, "a segment's symbol starts are one word of sbits");
 
 // Match finder over the chunk's hash buckets: bl holds every local position x with a 4-byte
 // suffix (x + 4 <= np), grouped by bucket (hash4) and ascending inside a bucket; the bucket of
@@ -508,24 +530,38 @@ struct Finder {
 // a quarter of the candidates once the current match is `good` long, as zlib's deflate_slow
 // does), as a per-lane state machine: each pass of the loop runs one batch of each lane's current
 // search, or ends it and takes the parse decision, so the wave's lanes stay busy however their
-// search lengths differ (round 4: one lane in five was active per instruction with the searches
-// run to their ends inside each parse step).  A step depends on its position alone, so two parses
-// that reach the same position continue identically (the merge rule below).  Matches end at the
-// chunk end np.  emit(word, position) stores a symbol; step_done(x) is called when a step ends at
-// x and returns whether the lane parses on.
-template <class Emit, class Done>
-__device__ __attribute__((always_inline)) inline void parse_lanes(const Finder& F, int lazy, int x, bool act, Emit emit, Done step_done) {
+// search lengths differ (round 4: one lane in five was active per VALU instruction with the
+// searches run to their ends inside each parse step).  A step depends on its position alone, so
+// two parses that reach the same position continue identically (the merge rule below).  Matches
+// end at the chunk end np.  emit(word, position) stores a symbol; between steps next(x) says what
+// the lane does after a step that ended at x (or first, at its start): the position of its next
+// step, NX_WAIT (ask again in the next pass) or NX_STOP.
+enum { NX_WAIT = -1, NX_STOP = -2 };
+template <class Emit, class Next>
+__device__ __attribute__((always_inline)) inline void parse_lanes(const Finder& F, int lazy, int x0,
+                                                                  Emit emit, Next next) {
   const int n = F.np;
   Finder::Search S;
-  int l = 0, d = 0;
-  bool lz = false;  // the current search is the look-ahead at x + 1
-  if (act) F.begin(S, x, min(MAXM, n - x), F.chain);
-  while (__any(act)) {
-    if (act && S.more) F.batch(S);
-    if (act && !S.more) {  // the search ended: the parse decision
+  int x = x0, l = 0, d = 0;
+  bool lz = false;    // the current search is the look-ahead at x + 1
+  bool busy = false;  // a step is in progress
+  bool done = false;
+  while (__any(!done)) {
+    if (!done && !busy) {  // between steps: stop, wait, or begin the next step's search
+      const int r = next(x);
+      done = r == NX_STOP;
+      if (r >= 0) {
+        x = r;
+        busy = true;
+        lz = false;
+        F.begin(S, x, min(MAXM, n - x), F.chain);
+      }
+    }
+    if (busy && S.more) F.batch(S);
+    if (busy && !S.more) {  // the search ended: the parse decision
       int d2 = 0;
       const int r = F.finish(S, &d2);
-      bool next = false;  // emit the pending symbol at x and end the step
+      bool end = false;  // emit the pending symbol at x and end the step
       if (!lz) {
         l = r;
         d = d2;
@@ -533,10 +569,10 @@ __device__ __attribute__((always_inline)) inline void parse_lanes(const Finder& 
           lz = true;
           F.begin(S, x + 1, min(MAXM, n - x - 1), F.good > 0 && l >= F.good ? max(1, F.chain >> 2) : F.chain);
         } else {
-          next = true;
+          end = true;
         }
       } else if (r <= l) {
-        next = true;
+        end = true;
       } else {  // a longer match one on: a literal, and look one further
         emit(lit_word(F.L.in[x]), x);
         x++;
@@ -545,27 +581,60 @@ __device__ __attribute__((always_inline)) inline void parse_lanes(const Finder& 
         if (l < lazy && x + 1 < n)
           F.begin(S, x + 1, min(MAXM, n - x - 1), F.good > 0 && l >= F.good ? max(1, F.chain >> 2) : F.chain);
         else
-          next = true;
+          end = true;
       }
-      if (next) {
+      if (end) {
         emit(l ? match_word(l, d) : lit_word(F.L.in[x]), x);
         x += l ? l : 1;
-        lz = false;
-        act = step_done(x);
-        if (act) F.begin(S, x, min(MAXM, n - x), F.chain);
+        busy = false;
+        const int r2 = next(x);  // the next step at once (no pass in between)
+        done = r2 == NX_STOP;
+        if (r2 >= 0) {
+          x = r2;
+          busy = true;
+          lz = false;
+          F.begin(S, x, min(MAXM, n - x), F.chain);
+        }
       }
     }
   }
 }
 
-// The merge fields of lane_mrg
+// The merge fields of seg_mrg (merge segment MSEG = the chunk's end)
 __device__ inline uint32_t mrg_word(int u, int k, int nc, bool over) {
-  return (uint32_t)u | (uint32_t)k << 10 | (uint32_t)nc << 17 | (over ? 1u << 25 : 0u);
+  return (uint32_t)u | (uint32_t)k << 11 | (uint32_t)nc << 18 | (over ? 1u << 26 : 0u);
 }
-__device__ inline int mrg_lane(uint32_t m) { return (int)(m & 1023); }
-__device__ inline int mrg_sym(uint32_t m) { return (int)((m >> 10) & 127); }
-__device__ inline int mrg_cont(uint32_t m) { return (int)((m >> 17) & 255); }
-__device__ inline bool mrg_over(uint32_t m) { return (m >> 25) & 1u; }
+__device__ inline int mrg_lane(uint32_t m) { return (int)(m & 2047); }
+__device__ inline int mrg_sym(uint32_t m) { return (int)((m >> 11) & 127); }
+__device__ inline int mrg_cont(uint32_t m) { return (int)((m >> 18) & 255); }
+__device__ inline bool mrg_over(uint32_t m) { return (m >> 26) & 1u; }
+
+// Stage words buffered four at a time, one 16-byte store per four symbols: single 4-byte stores
+// from 64 lanes into 64 different lines were written back as partial lines (the parse kernel wrote
+// 6x the staged bytes, profiles/r4r_deflate_pmc.txt).  `base` is 16-byte aligned.
+struct WBuf {
+  uint32_t* base;
+  uint32_t p0, p1, p2, p3;
+  __device__ __attribute__((always_inline)) void put(int n, uint32_t w) {  // word n (n = count so far)
+    const int k = n & 3;
+    p0 = k == 0 ? w : p0;
+    p1 = k == 1 ? w : p1;
+    p2 = k == 2 ? w : p2;
+    p3 = k == 3 ? w : p3;
+    if (k == 3) *reinterpret_cast<uint4*>(base + (n - 3)) = make_uint4(p0, p1, p2, p3);
+  }
+  __device__ __attribute__((always_inline)) void flush(int n) {  // the last n & 3 words
+    const int k = n & 3, a = n - k;
+    if (k > 0) base[a] = p0;
+    if (k > 1) base[a + 1] = p1;
+    if (k > 2) base[a + 2] = p2;
+  }
+};
+__device__ __attribute__((always_inline)) inline void hist_add(int32_t* H, uint32_t x, int v) {
+  const uint32_t ll = sym_ll(x);
+  atomicAdd(&H[CI_LL + ll], v);
+  if (ll > 256) atomicAdd(&H[CI_D + sym_d(x)], v);
+}
 
 #define DTS()                                                                      \
   do {                                                                             \
@@ -589,10 +658,10 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
   const int64_t base = (blk0 + b) * (int64_t)BLK_U;
   const int n = (int)min<int64_t>(BLK_U, n_in - base);
   const int cs = c * CH;
-  uint32_t* lm = meta + b * META_WORDS + c * PWG;
-  int32_t* ci = reinterpret_cast<int32_t*>(meta + b * META_WORDS + NCH * PWG + c * CI_WORDS);
+  uint32_t* lm = meta + b * META_WORDS + c * MSEG;
+  int32_t* ci = reinterpret_cast<int32_t*>(meta + b * META_WORDS + NCH * MSEG + c * CI_WORDS);
   if (cs >= n) {  // an empty chunk (the last block is short)
-    lm[t] = 0;
+    for (int i = t; i < MSEG; i += PWG) lm[i] = 0;
     for (int i = t; i < CI_WORDS; i += PWG) ci[i] = 0;
     if (tim && t == 0)
       for (int k = 0; k < 8; k++) tim[blockIdx.x * 8 + k] = 0;
@@ -603,11 +672,12 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
   const int np = ce - r0;       // bytes held: local positions [0, np)
   const int xs = cs - r0;       // the chunk's first local position
   const int npos = max(0, np - 3);  // positions with a 4-byte suffix
-  const int nlc = (np - xs + PSEG - 1) / PSEG;  // lanes holding bytes
+  const int nlc = (np - xs + PSEG - 1) / PSEG;  // segments holding bytes
   // ---- load (16-byte loads where aligned)
   for (int i = t; i < (1 << HBITS); i += PWG) L.head[i] = 0;
   for (int i = t; i < (SCAT_WAVES - 1) << (HBITS - 1); i += PWG) (&L.cnt[0][0])[i] = 0;
   if (t < 8) L.misc[t] = 0;
+  for (int i = t; i < CI_CRC; i += PWG) L.hist[i] = 0;
   {
     const uint8_t* s = src + base + r0;
     const int head = (int)((16 - (reinterpret_cast<uintptr_t>(s) & 15)) & 15);
@@ -708,158 +778,219 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
   for (int i = t; i < 256; i += PWG) L.crc_t[i] = c_dcrc[i];  // (over the dead counts)
   __syncthreads();
   DTS();
-  // ---- CRC32 of the lane's segment (raw register, init 0), moved to the chunk end, XOR-ed
-  const int s0 = min(np, xs + PSEG * t), s1 = min(np, s0 + PSEG);
+  // ---- CRC32 of 64 bytes per thread (raw register, init 0), moved to the chunk end, XOR-ed
   {
+    const int c0 = min(np, xs + 64 * t), c1 = min(np, c0 + 64);
     uint32_t cr = 0;
-    for (int i = s0; i < s1; i++) cr = L.crc_t[(cr ^ L.in[i]) & 0xff] ^ (cr >> 8);
-    if (s1 > s0) cr = gf2_mul(x8n((uint32_t)(np - s1)), cr);
+    for (int i = c0; i < c1; i++) cr = L.crc_t[(cr ^ L.in[i]) & 0xff] ^ (cr >> 8);
+    if (c1 > c0) cr = gf2_mul(x8n((uint32_t)(np - c1)), cr);
     for (int o = 32; o >= 1; o >>= 1) cr ^= __shfl_xor(cr, o, 64);
     if (lane == 0) L.wred[8 + wv] = cr;
   }
-  // ---- speculative parse: lane t from its segment start to the first symbol boundary at or past
-  //      its end (a match may run on past it)
-  uint32_t* const lanes_w = stage + (b * NCH + c) * (int64_t)PWG * LANE_WORDS;
-  uint32_t* const lane_w = lanes_w + (int64_t)t * LANE_WORDS;
+  // ---- speculative parses: segment j (32 bytes) from its start to the first symbol boundary at
+  //      or past its end (a match may run on past it).  The segments are handed out by an LDS
+  //      counter (thread t takes segment t, then the next unclaimed one), so a lane whose
+  //      segments parse quickly takes more of them instead of idling until the wave's slowest
+  //      lane is done.
+  uint32_t* const segs_w = stage + (b * NCH + c) * (int64_t)MSEG * LANE_WORDS;
   const Finder F{L, np, min(chain, MAXCAND), nice, good};
   {
-    int ns = 0;
-    uint64_t st = 0;  // symbol starts in the segment (a deferred literal past its end: left out)
-    int ex = s0;
+    int j = t < nlc ? t : nlc;
+    int s0 = xs + PSEG * j, s1 = min(np, s0 + PSEG), ns = 0;
+    uint32_t st = 0;  // symbol starts in the segment (a deferred literal past its end: left out)
+    WBuf wb{segs_w + (int64_t)j * LANE_WORDS, 0, 0, 0, 0};
     parse_lanes(
-        F, lazy, s0, s0 < s1,
+        F, lazy, s0,
         [&](uint32_t w, int p) __attribute__((always_inline)) {
           DQ_CHK(ns < OWN_WORDS, CHK_Z_STAGE);
-          if (p - s0 < 64) st |= 1ull << (p - s0);
-          lane_w[ns++] = w;
+          if (p - s0 < PSEG) st |= 1u << (p - s0);
+          hist_add(L.hist, w, 1);
+          wb.put(ns++, w);
         },
-        [&](int x) __attribute__((always_inline)) {
-          ex = x;
-          return x < s1;
+        [&](int x) __attribute__((always_inline)) -> int {
+          if (j >= nlc) return NX_STOP;
+          if (x < s1) return x;
+          wb.flush(ns);
+          L.seg_nsym[j] = (uint8_t)ns;
+          L.seg_exit[j] = (uint32_t)x;
+          L.sbits[j] = st;
+          j = PWG + atomicAdd(&L.misc[0], 1);  // the next unclaimed segment
+          if (j >= nlc) return NX_STOP;
+          s0 = xs + PSEG * j;
+          s1 = min(np, s0 + PSEG);
+          ns = 0;
+          st = 0;
+          wb.base = segs_w + (int64_t)j * LANE_WORDS;
+          return s0;
         });
-    L.lane_nsym[t] = (uint16_t)ns;
-    L.lane_exit[t] = (uint32_t)ex;
-    if (t < PL) {
-      L.sbits[2 * t] = (uint32_t)st;
-      L.sbits[2 * t + 1] = (uint32_t)(st >> 32);
-    }
   }
   __threadfence_block();
   __syncthreads();
   DTS();
-  // ---- continuation: from its exit, lane t parses on until it reaches a symbol boundary of a
-  //      later lane's speculative parse (the same position continues identically), skipping
-  //      lanes whose whole parse it overruns
+  // ---- continuations, handed out the same way: from its exit, segment j's parse goes on until it
+  //      reaches a symbol boundary of a later segment's speculative parse (the same position
+  //      continues identically), skipping segments whose whole parse it overruns
   {
-    int E = t < nlc ? (int)L.lane_exit[t] : np, u = t + 1, k = 0, nc = 0;
+    int j = t < nlc ? t : nlc;
+    int u = 0, k = 0, nc = 0;
     bool over = false;
-    uint32_t* const cw = lane_w + OWN_WORDS;
-    // the merge test at E: false when the lane stops here (merged, the chunk's end, overflowed),
-    // true when it parses another step
-    auto check = [&](int Ex) __attribute__((always_inline)) -> bool {
-      E = Ex;
+    WBuf wb{nullptr, 0, 0, 0, 0};
+    // the merge test at E: NX_STOP (merged, the chunk's end, overflowed) or E (parse a step)
+    auto check = [&](int E) __attribute__((always_inline)) -> int {
       for (;;) {
         if (E >= np) {  // the chunk's end
-          u = PWG;
+          u = MSEG;
           k = 0;
-          return false;
+          return NX_STOP;
         }
-        if (u >= nlc) {  // no later lane holds symbols: parse on to the chunk end
+        if (u >= nlc) {  // no later segment holds symbols: parse on to the chunk end
           if (nc > CONT_WORDS - 40) {
             over = true;
-            return false;
+            return NX_STOP;
           }
-          return true;
+          return E;
         }
-        // lane u's symbol starts (its segment [su, su + 64)) and its exit; E >= su
-        const int su = xs + PSEG * u, eu = (int)L.lane_exit[u];
-        if (E > eu) {  // lane u's whole parse lies before E
+        // segment u's symbol starts ([su, su + 32)) and its exit; E >= su
+        const int su = xs + PSEG * u, eu = (int)L.seg_exit[u];
+        if (E > eu) {  // segment u's whole parse lies before E
           u++;
           continue;
         }
-        if (E == eu) {  // merged: lane u's continuation
-          k = L.lane_nsym[u];
-          return false;
+        if (E == eu) {  // merged: segment u's continuation
+          k = L.seg_nsym[u];
+          return NX_STOP;
         }
-        const uint64_t ub = (uint64_t)L.sbits[2 * u] | (uint64_t)L.sbits[2 * u + 1] << 32;
-        if (E < su + PSEG && ((ub >> (E - su)) & 1)) {  // merged: lane u's symbols from k on
-          k = __popcll(ub & ((1ull << (E - su)) - 1));
-          return false;
+        const uint32_t ub = L.sbits[u];
+        if (E < su + PSEG && ((ub >> (E - su)) & 1)) {  // merged: segment u's symbols from k on
+          k = __popc(ub & ((1u << (E - su)) - 1));
+          return NX_STOP;
         }
         if (nc > CONT_WORDS - 40) {  // (a step appends at most lazy + 1 <= 33 symbols)
-          // no merge within the staging (e.g. one repeated byte: 258-byte matches from lane t's
-          // positions never meet lane u's): end exactly on lane u's next boundary pu > E, with
-          // matches cut to fit and literals for the last < 3 bytes -- a valid parse that merges
-          const uint64_t after = E - su + 1 < 64 ? ub >> (E - su + 1) : 0ull;
-          const int pu = E < su + PSEG && after ? E + 1 + (int)__builtin_ctzll(after) : eu;
+          // no merge within the staging (e.g. one repeated byte: 258-byte matches from this
+          // parse's positions never meet segment u's): end exactly on segment u's next boundary
+          // pu > E, with matches cut to fit and literals for the last < 3 bytes -- a valid parse
+          // that merges
+          const uint32_t after = E - su + 1 < PSEG ? ub >> (E - su + 1) : 0u;
+          const int pu = E < su + PSEG && after ? E + 1 + (int)__builtin_ctz(after) : eu;
           while (E < pu && nc < CONT_WORDS) {
             int d = 0;
             const int l = F.find(E, min(MAXM, pu - E), &d, F.chain);
-            cw[nc++] = l ? match_word(l, d) : lit_word(L.in[E]);
+            const uint32_t w = l ? match_word(l, d) : lit_word(L.in[E]);
+            hist_add(L.hist, w, 1);
+            wb.put(nc++, w);
             E += l ? l : 1;
           }
           if (E != pu) {  // (a gap of literals longer than the staging: stored)
             over = true;
-            return false;
+            return NX_STOP;
           }
-          k = pu == eu ? (int)L.lane_nsym[u] : __popcll(ub & ((1ull << (pu - su)) - 1));
-          return false;
+          k = pu == eu ? (int)L.seg_nsym[u] : __popc(ub & ((1u << (pu - su)) - 1));
+          return NX_STOP;
         }
-        return true;
+        return E;
       }
     };
-    const bool go = t < nlc && check(E);
+    // segment j's continuation from its exit: the position of its first step, or NX_STOP when it
+    // ended at once (its merge word written)
+    auto start = [&]() __attribute__((always_inline)) -> int {
+      u = j + 1;
+      k = 0;
+      nc = 0;
+      over = false;
+      wb.base = segs_w + (int64_t)j * LANE_WORDS + OWN_WORDS;
+      return check((int)L.seg_exit[j]);
+    };
+    int x0 = NX_STOP;
+    while (j < nlc) {  // the first segment with a step to parse
+      x0 = start();
+      if (x0 >= 0) break;
+      wb.flush(nc);
+      L.seg_mrg[j] = mrg_word(over ? MSEG : u, k, nc, over);
+      j = PWG + atomicAdd(&L.misc[1], 1);
+    }
     parse_lanes(
-        F, lazy, E, go,
+        F, lazy, x0 >= 0 ? x0 : 0,
         [&](uint32_t w, int) __attribute__((always_inline)) {
           DQ_CHK(nc < CONT_WORDS, CHK_Z_STAGE);
-          cw[nc++] = w;
+          hist_add(L.hist, w, 1);
+          wb.put(nc++, w);
         },
-        check);
-    if (t < nlc) L.lane_mrg[t] = mrg_word(over ? PWG : u, k, nc, over);
+        [&](int x) __attribute__((always_inline)) -> int {
+          if (j >= nlc) return NX_STOP;
+          int r = check(x);
+          while (r < 0) {  // this continuation ended: the next unclaimed segment's
+            wb.flush(nc);
+            L.seg_mrg[j] = mrg_word(over ? MSEG : u, k, nc, over);
+            j = PWG + atomicAdd(&L.misc[1], 1);
+            if (j >= nlc) return NX_STOP;
+            r = start();
+          }
+          return r;
+        });
   }
+  __threadfence_block();  // staged words are read below by other threads than their writers
   if (tim) __syncthreads();  // (timing: the continuation stamp after every wave's)
   DTS();
-  // ---- the chunk's parse: lane 0, then the lane each continuation merged into.  Pointer
-  //      jumping: after round r every lane within 2^(r+1) - 1 merges of lane 0 is marked.
-  uint32_t* const jmp = L.lane_exit;  // the exits are dead
-  L.lane_mark[t] = t == 0;
+  // ---- the chunk's parse: segment 0, then the segment each continuation merged into.  Pointer
+  //      jumping: after round r every segment within 2^(r+1) - 1 merges of segment 0 is marked.
   __syncthreads();
-  if (t < nlc) jmp[t] = (uint32_t)mrg_lane(L.lane_mrg[t]);
+  uint32_t* const jmp = L.seg_exit;  // the exits are dead
+  for (int i = t; i < nlc; i += PWG) {
+    L.seg_mark[i] = i == 0;
+    jmp[i] = (uint32_t)mrg_lane(L.seg_mrg[i]);
+  }
   __syncthreads();
   for (int r = 0; (1 << r) < nlc; r++) {
-    const uint32_t j = t < nlc ? jmp[t] : (uint32_t)PWG;
-    if (j < (uint32_t)PWG && L.lane_mark[t]) L.lane_mark[j] = 1;
-    const uint32_t jj = j < (uint32_t)PWG ? jmp[j] : (uint32_t)PWG;
+    uint32_t jj[2] = {MSEG, MSEG};
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      const int i = t + q * PWG;
+      const uint32_t g = i < nlc ? jmp[i] : (uint32_t)MSEG;
+      if (g < (uint32_t)MSEG && L.seg_mark[i]) L.seg_mark[g] = 1;
+      jj[q] = g < (uint32_t)MSEG ? jmp[g] : (uint32_t)MSEG;
+    }
     __syncthreads();
-    if (t < nlc) jmp[t] = jj;
+#pragma unroll
+    for (int q = 0; q < 2; q++)
+      if (t + q * PWG < nlc) jmp[t + q * PWG] = jj[q];
     __syncthreads();
   }
-  const bool reached = t < nlc && L.lane_mark[t];
-  const uint32_t mw = t < nlc ? L.lane_mrg[t] : 0u;
-  // the first symbol of each lane on the parse: set by the lane that merged into it
+  // the first symbol of each segment on the parse: set by the segment that merged into it
+  bool rch[2];
+  uint32_t mw[2];
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const int i = t + q * PWG;
+    rch[q] = i < nlc && L.seg_mark[i];
+    mw[q] = i < nlc ? L.seg_mrg[i] : 0u;
+  }
+  __syncthreads();
   if (t == 0) jmp[0] = 0;
-  __syncthreads();
-  if (reached && mrg_lane(mw) < PWG) jmp[mrg_lane(mw)] = (uint32_t)mrg_sym(mw);
-  if (reached && mrg_over(mw)) L.misc[7] = 1;
-  int32_t* const H = L.head;  // the buckets are dead from here
-  for (int i = t; i < CI_D + 32; i += PWG) H[i] = 0;
-  __syncthreads();
-  const int k0 = reached ? (int)jmp[t] : 0;
-  const int ns = L.lane_nsym[t], nc = mrg_cont(mw);
-  lm[t] = reached ? (uint32_t)k0 | (uint32_t)ns << 8 | (uint32_t)nc << 16 | LM_REACHED : 0u;
-  // histograms of the chunk's parse
-  if (reached) {
-    auto hist = [&](uint32_t x) {
-      const uint32_t ll = sym_ll(x);
-      atomicAdd(&H[CI_LL + ll], 1);
-      if (ll > 256) atomicAdd(&H[CI_D + sym_d(x)], 1);
-    };
-    for (int k = k0; k < ns; k++) hist(lane_w[k]);
-    for (int k = 0; k < nc; k++) hist(lane_w[OWN_WORDS + k]);
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    if (rch[q] && mrg_lane(mw[q]) < MSEG) jmp[mrg_lane(mw[q])] = (uint32_t)mrg_sym(mw[q]);
+    if (rch[q] && mrg_over(mw[q])) L.misc[7] = 1;
   }
   __syncthreads();
-  for (int i = t; i < CI_CRC; i += PWG) ci[i] = H[i];
+  // the segment words; the histograms counted every symbol parsed: those not on the chunk's parse
+  // (a reached segment's symbols before its first one, every symbol of a segment not reached) are
+  // taken off again -- a few per chunk
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const int i = t + q * PWG;
+    if (i >= MSEG) continue;
+    const int k0 = rch[q] ? (int)jmp[i] : 0;
+    const int ns = i < nlc ? (int)L.seg_nsym[i] : 0, nc = mrg_cont(mw[q]);
+    lm[i] = rch[q] ? (uint32_t)k0 | (uint32_t)ns << 8 | (uint32_t)nc << 16 | LM_REACHED : 0u;
+    if (i < nlc) {
+      const uint32_t* w = segs_w + (int64_t)i * LANE_WORDS;
+      const int ko = rch[q] ? k0 : ns, kc = rch[q] ? 0 : nc;
+      for (int k = 0; k < ko; k++) hist_add(L.hist, w[k], -1);
+      for (int k = 0; k < kc; k++) hist_add(L.hist, w[OWN_WORDS + k], -1);
+    }
+  }
+  __syncthreads();
+  for (int i = t; i < CI_CRC; i += PWG) ci[i] = L.hist[i];
   if (t == 0) {
     uint32_t cr = 0;
     for (int w = 0; w < PWG / 64; w++) cr ^= L.wred[8 + w];
@@ -884,9 +1015,23 @@ template <class Fn>
 __device__ inline void for_each_sym(uint32_t m, const uint32_t* __restrict__ w, Fn f) {
   if (!(m & LM_REACHED)) return;
   const int k0 = (int)(m & 255), ns = (int)((m >> 8) & 255), nc = (int)((m >> 16) & 255);
-  for (int k = k0; k < ns; k++) f(w[k]);
-  for (int k = 0; k < nc; k++) f(w[OWN_WORDS + k]);
+  // 16-byte loads (the own and continuation areas start 16-byte aligned)
+  for (int k = k0 & ~3; k < ns; k += 4) {
+    const uint4 v = *reinterpret_cast<const uint4*>(w + k);
+    if (k >= k0) f(v.x);
+    if (k + 1 >= k0 && k + 1 < ns) f(v.y);
+    if (k + 2 >= k0 && k + 2 < ns) f(v.z);
+    if (k + 3 < ns) f(v.w);
+  }
+  for (int k = 0; k < nc; k += 4) {
+    const uint4 v = *reinterpret_cast<const uint4*>(w + OWN_WORDS + k);
+    f(v.x);
+    if (k + 1 < nc) f(v.y);
+    if (k + 2 < nc) f(v.z);
+    if (k + 3 < nc) f(v.w);
+  }
 }
+static_assert(OWN_WORDS % 4 == 0 && LANE_WORDS % 4 == 0, "16-byte aligned stage areas");
 
 __global__ __launch_bounds__(CWG) void bgzf_code_kernel(const uint8_t* __restrict__ src,
                                                         int64_t n_in, int64_t blk0, int64_t nblk,
@@ -905,7 +1050,7 @@ __global__ __launch_bounds__(CWG) void bgzf_code_kernel(const uint8_t* __restric
   const int64_t base = (blk0 + b) * (int64_t)BLK_U;
   const int n = (int)min<int64_t>(BLK_U, n_in - base);
   const uint32_t* lm = meta + b * META_WORDS;
-  const int32_t* ci = reinterpret_cast<const int32_t*>(meta + b * META_WORDS + NCH * PWG);
+  const int32_t* ci = reinterpret_cast<const int32_t*>(meta + b * META_WORDS + NCH * MSEG);
   int32_t* H = L.head;
   for (int i = t; i < H_CL + 32; i += CWG) H[i] = 0;
   __syncthreads();
@@ -934,9 +1079,10 @@ __global__ __launch_bounds__(CWG) void bgzf_code_kernel(const uint8_t* __restric
   if (wv == 0) build_lengths(H + H_LL, 286, 15, H + H_SORT, H + H_W, H + H_LEN, H + H_CNT, lane);
   if (wv == 1) build_lengths(H + H_D, 30, 15, H + H_SORT_D, H + H_W_D, H + H_LEN_D, H + H_CNT_D, lane);
   __syncthreads();
-  if (t == 0) {
-    canon_codes(H + H_LEN, 286, reinterpret_cast<uint32_t*>(H + C_LL), H + H_BL);
-    canon_codes(H + H_LEN_D, 30, reinterpret_cast<uint32_t*>(H + C_D), H + H_BL);
+  // codes by waves 0 and 1 while wave 2's first lane run-length codes the code lengths
+  if (wv == 0) canon_codes_wave(H + H_LEN, 286, reinterpret_cast<uint32_t*>(H + C_LL), lane);
+  if (wv == 1) canon_codes_wave(H + H_LEN_D, 30, reinterpret_cast<uint32_t*>(H + C_D), lane);
+  if (t == 128) {
     // code-length sequence, run-length coded (16: repeat 3-6, 17: 3-10 zeros, 18: 11-138 zeros)
     int nlit = 286, ndist = 30;
     while (nlit > 257 && H[H_LEN + nlit - 1] == 0) nlit--;
@@ -970,60 +1116,61 @@ __global__ __launch_bounds__(CWG) void bgzf_code_kernel(const uint8_t* __restric
   __syncthreads();
   if (wv == 0) build_lengths(H + H_CL, 19, 7, H + H_SORT, H + H_W, H + H_LEN_CL, H + H_CNT, lane);
   __syncthreads();
-  if (t == 0) {
-    canon_codes(H + H_LEN_CL, 19, reinterpret_cast<uint32_t*>(H + C_CL), H + H_BL);
+  if (wv == 0) {
+    canon_codes_wave(H + H_LEN_CL, 19, reinterpret_cast<uint32_t*>(H + C_CL), lane);
     int ncl = 19;
     while (ncl > 4 && H[H_LEN_CL + c_clord[ncl - 1]] == 0) ncl--;
-    L.misc[5] = ncl;
+    // dynamic header bits: the tokens' code lengths and extra bits, summed over the wave
     const uint16_t* tok = reinterpret_cast<const uint16_t*>(H + H_TOK);
-    uint32_t hb = 3 + 5 + 5 + 4 + 3 * (uint32_t)ncl;
-    for (int k = 0; k < L.misc[4]; k++) {
+    uint32_t hb = 0;
+    for (int k = lane; k < L.misc[4]; k += 64) {
       const int sy = tok[k] & 31;
       hb += (uint32_t)H[H_LEN_CL + sy] + (sy == 16 ? 2 : sy == 17 ? 3 : sy == 18 ? 7 : 0);
     }
-    L.misc[6] = (int32_t)hb;  // dynamic header bits
+    for (int o = 32; o >= 1; o >>= 1) hb += __shfl_xor(hb, o, 64);
+    if (lane == 0) {
+      L.misc[5] = ncl;
+      L.misc[6] = (int32_t)(hb + 3 + 5 + 5 + 4 + 3 * (uint32_t)ncl);
+    }
   }
   __syncthreads();
   DTS();
-  // ---- bits of this thread's four lanes under the dynamic and the fixed code
-  uint32_t lw[4];
-  const uint32_t* wp[4];
+  // ---- bits of this thread's eight segments under the dynamic and the fixed code
+  uint32_t lw[CSEG];
+  const uint32_t* wp[CSEG];
 #pragma unroll
-  for (int j = 0; j < 4; j++) {
-    const int g = 4 * t + j, c = g / PL, u = g - c * PL;
-    lw[j] = g < NLANE ? lm[c * PWG + u] : 0u;
-    wp[j] = stage + ((b * NCH + c) * PWG + u) * (int64_t)LANE_WORDS;
+  for (int j = 0; j < CSEG; j++) {
+    const int g = CSEG * t + j, c = g / PL, u = g - c * PL;
+    lw[j] = g < NLANE ? lm[c * MSEG + u] : 0u;
+    wp[j] = stage + ((b * NCH + c) * MSEG + u) * (int64_t)LANE_WORDS;
   }
-  const bool has_eob = 4 * t + 3 == NLANE - 1;  // the block's last lane ends with end-of-block
-  uint32_t vd[4], vf[4];
+  const bool has_eob = CSEG * t + CSEG - 1 == NLANE - 1;  // the block's last segment ends with EOB
+  uint32_t vd = 0, vf = 0;
   {
     const uint32_t* cll = reinterpret_cast<const uint32_t*>(H + C_LL);
     const uint32_t* cd = reinterpret_cast<const uint32_t*>(H + C_D);
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-      uint32_t bdyn = 0, bfix = 0;
+    for (int j = 0; j < CSEG; j++) {
       for_each_sym(lw[j], wp[j], [&](uint32_t x) {
         const int ll = (int)sym_ll(x);
         int extra = 0;
         if (ll > 256) {
           const int d = (int)sym_d(x);
           extra = lextra_bits(ll) + dextra_bits(d);
-          bdyn += cd[d] >> 16;
-          bfix += 5;
+          vd += cd[d] >> 16;
+          vf += 5;
         }
-        bdyn += (cll[ll] >> 16) + extra;
-        bfix += fixed_len_of(ll) + extra;
+        vd += (cll[ll] >> 16) + extra;
+        vf += fixed_len_of(ll) + extra;
       });
-      if (j == 3 && has_eob) {
-        bdyn += cll[256] >> 16;
-        bfix += 7;
-      }
-      vd[j] = bdyn;
-      vf[j] = bfix;
+    }
+    if (has_eob) {
+      vd += cll[256] >> 16;
+      vf += 7;
     }
   }
-  // ---- choose dynamic or fixed; exclusive scan of the chosen lane bit counts
-  uint32_t dsum = vd[0] + vd[1] + vd[2] + vd[3], fsum = vf[0] + vf[1] + vf[2] + vf[3];
+  // ---- choose dynamic or fixed; exclusive scan of the threads' chosen bit counts
+  uint32_t dsum = vd, fsum = vf;
   for (int o = 32; o >= 1; o >>= 1) {
     dsum += __shfl_xor(dsum, o, 64);
     fsum += __shfl_xor(fsum, o, 64);
@@ -1037,12 +1184,7 @@ __global__ __launch_bounds__(CWG) void bgzf_code_kernel(const uint8_t* __restric
   fsum = L.wsum[4] + L.wsum[5] + L.wsum[6] + L.wsum[7];
   const bool dyn = (uint32_t)L.misc[6] + dsum < 3u + fsum;
   const uint32_t hdr_bits = dyn ? (uint32_t)L.misc[6] : 3u;
-  uint32_t v[4], sm = 0;
-#pragma unroll
-  for (int j = 0; j < 4; j++) {
-    v[j] = dyn ? vd[j] : vf[j];
-    sm += v[j];
-  }
+  const uint32_t sm = dyn ? vd : vf;
   uint32_t inc = sm;
   for (int d = 1; d < 64; d <<= 1) {
     const uint32_t y = __shfl_up(inc, d, 64);
@@ -1104,7 +1246,7 @@ __global__ __launch_bounds__(CWG) void bgzf_code_kernel(const uint8_t* __restric
       const uint32_t* cd = reinterpret_cast<const uint32_t*>(H + C_D);
       ImgOut io(img, off);
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
+      for (int j = 0; j < CSEG; j++) {
         for_each_sym(lw[j], wp[j], [&](uint32_t x) {
           const int ll = (int)sym_ll(x);
           io.put(cll[ll] & 0xffff, (int)(cll[ll] >> 16));
@@ -1176,7 +1318,7 @@ DefTables g_def[64];
 }  // namespace
 
 int64_t bgzf_block_count(int64_t n) { return n <= 0 ? 0 : (n + BLK_U - 1) / BLK_U; }
-size_t bgzf_stage_bytes(int64_t nblk) { return (size_t)nblk * NCH * PWG * LANE_WORDS * 4; }
+size_t bgzf_stage_bytes(int64_t nblk) { return (size_t)nblk * NCH * MSEG * LANE_WORDS * 4; }
 size_t bgzf_meta_bytes(int64_t nblk) { return (size_t)nblk * META_WORDS * 4; }
 
 bool deflate_tables(int device) {
