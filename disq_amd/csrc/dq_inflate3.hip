@@ -1825,8 +1825,10 @@ DQ_AI void build_tables_wave(LdsW& L, int nlen, int ndist) {
       cd[j] = (uint32_t)wave_incl_scan((int)cd[j], lane);
     }
     if (len) {
-      const uint32_t* cc = isl ? c : cd;
-      const uint32_t mine = (len >> 2) == 0 ? cc[0] : (len >> 2) == 1 ? cc[1] : (len >> 2) == 2 ? cc[2] : cc[3];
+      // (selected register by register: a pointer to either array put both in scratch)
+      const uint32_t m0 = isl ? c[0] : cd[0], m1 = isl ? c[1] : cd[1], m2 = isl ? c[2] : cd[2],
+                     m3 = isl ? c[3] : cd[3];
+      const uint32_t mine = (len >> 2) == 0 ? m0 : (len >> 2) == 1 ? m1 : (len >> 2) == 2 ? m2 : m3;
       const int rank = (int)((mine >> (8 * (len & 3))) & 0xffu) - 1 + H.run[(isl ? 0 : 16) + len];
       const HuffCanon& hh = isl ? L.u.d.hl : L.u.d.hd;
       const int q = hh.offs[len] + rank;

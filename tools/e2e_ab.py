@@ -61,7 +61,7 @@ def run(path, window_gb, depth, reps, arena_factor):
                 dg[p0 + i] = int(x)
         secs = res["seconds"]
         print(json.dumps({
-            "rep": rep, "mmap": os.environ.get("DQ_MMAP", "1"), "window_gb": window_gb,
+            "rep": rep, "mmap": os.environ.get("DQ_MMAP", "0"), "window_gb": window_gb,
             "depth": depth, "seconds": round(secs, 3),
             "decompressed_gbs": round(res["owned_bytes"] / secs / 1e9, 2),
             "file_gbs": round(flen / secs / 1e9, 2),
