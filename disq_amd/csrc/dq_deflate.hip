@@ -266,6 +266,9 @@ __device__ void canon_codes_wave(const int32_t* len, int m, uint32_t* code, int 
 #ifndef DQ_LDS_UNALIGNED
 #define DQ_LDS_UNALIGNED 1
 #endif
+#ifndef DQ_BATCH_REDUCE
+#define DQ_BATCH_REDUCE 1  // a candidate batch without a branch per candidate (else the loop)
+#endif
 #if DQ_LDS_UNALIGNED
 // 4 / 8 bytes at an arbitrary LDS offset x: one unaligned ds_read_b32 / ds_read_b64 (measured
 // faster than aligned words + byte shifts, profiles/r4m_deflate_sweep.txt)
@@ -460,6 +463,40 @@ struct Finder {
       ya[k] = ld8(L.in, q) ^ S.pa;
       yb[k] = ld8(L.in, q + 8) ^ S.pb;
     }
+#if DQ_BATCH_REDUCE
+    // the 8 lengths without a branch per candidate, the winner by one max over keys
+    // length << 19 | (7 - k) << 16 | distance: the longest, the most recent among equals -- the
+    // candidate the sequential loop below would pick, with the same stop at cap
+    uint32_t key = 0;
+    bool stop = false;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int q = q8[k];
+      const bool valid = q >= 0 && x - q <= WIN;
+      stop |= !valid;  // the bucket's list or the window ended (candidates: most recent first)
+      int l = ya[k] ? (int)(__builtin_ctzll(ya[k]) >> 3)
+                    : yb[k] ? 8 + (int)(__builtin_ctzll(yb[k]) >> 3) : 16;
+      // (rare) 16 bytes equal: on up to cap, unless the 4 bytes ending at the batch's best differ
+      if (valid && l == 16 && l < cap && (best <= 16 || ld4(L.in, q + best - 3) == ld4(L.in, x + best - 3))) {
+        while (l < cap) {
+          const uint64_t y = ld8(L.in, q + l) ^ ld8(L.in, x + l);
+          if (y) {
+            l += (int)(__builtin_ctzll(y) >> 3);
+            break;
+          }
+          l += 8;
+        }
+      }
+      l = valid ? min(l, cap) : 0;
+      key = max(key, (uint32_t)l << 19 | (uint32_t)(7 - k) << 16 | (uint32_t)(valid ? x - q : 0));
+    }
+    const int lb = (int)(key >> 19);
+    if (lb > best) {
+      best = lb;
+      bd = (int)(key & 0xffffu);
+    }
+    more = !stop && best < cap;
+#else
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       const int q = q8[k];
@@ -491,6 +528,7 @@ struct Finder {
         break;
       }
     }
+#endif
     S.best = best;
     S.bd = bd;
     S.i0 = i0 - 8;
