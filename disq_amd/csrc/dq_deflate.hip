@@ -826,17 +826,39 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
     if (lane == 0) L.wred[8 + wv] = cr;
   }
   // ---- speculative parses: segment j (32 bytes) from its start to the first symbol boundary at
-  //      or past its end (a match may run on past it).  The segments are handed out by an LDS
-  //      counter (thread t takes segment t, then the next unclaimed one), so a lane whose
-  //      segments parse quickly takes more of them instead of idling until the wave's slowest
-  //      lane is done.
+  //      or past its end (a match may run on past it).  Thread t starts on segment 2t; a lane that
+  //      ends an even segment claims the odd one after it and parses straight on into it (from
+  //      where it stands: that segment's parse starts where its predecessor's ended, so the
+  //      predecessor needs no continuation); the odd segments nobody flowed into are handed out by
+  //      an LDS counter, so a lane whose segments parse quickly takes more of them instead of
+  //      idling until the wave's slowest lane is done.
   uint32_t* const segs_w = stage + (b * NCH + c) * (int64_t)MSEG * LANE_WORDS;
   const Finder F{L, np, min(chain, MAXCAND), nice, good};
+  for (int i = t; i < MSEG; i += PWG) L.seg_mrg[i] = 0;  // odd segments' claim flags
+  __syncthreads();
   {
-    int j = t < nlc ? t : nlc;
-    int s0 = xs + PSEG * j, s1 = min(np, s0 + PSEG), ns = 0;
+    int j = 2 * t, s0 = 0, s1 = 0, ns = 0;
     uint32_t st = 0;  // symbol starts in the segment (a deferred literal past its end: left out)
-    WBuf wb{segs_w + (int64_t)j * LANE_WORDS, 0, 0, 0, 0};
+    WBuf wb{nullptr, 0, 0, 0, 0};
+    auto take = [&](int jj) __attribute__((always_inline)) {
+      j = jj;
+      s0 = xs + PSEG * j;
+      s1 = min(np, s0 + PSEG);
+      ns = 0;
+      st = 0;
+      wb.base = segs_w + (int64_t)j * LANE_WORDS;
+    };
+    // the next odd segment from the counter that no lane has flowed into (nlc: none left)
+    auto pull = [&]() __attribute__((always_inline)) -> int {
+      for (;;) {
+        const int q = 2 * atomicAdd(&L.misc[0], 1) + 1;
+        if (q >= nlc) return nlc;
+        if (atomicCAS(&L.seg_mrg[q], 0u, 1u) == 0u) return q;
+      }
+    };
+    const int j0 = 2 * t < nlc ? 2 * t : pull();
+    if (j0 < nlc) take(j0);
+    else j = nlc;
     parse_lanes(
         F, lazy, s0,
         [&](uint32_t w, int p) __attribute__((always_inline)) {
@@ -846,20 +868,24 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
           wb.put(ns++, w);
         },
         [&](int x) __attribute__((always_inline)) -> int {
-          if (j >= nlc) return NX_STOP;
-          if (x < s1) return x;
-          wb.flush(ns);
-          L.seg_nsym[j] = (uint8_t)ns;
-          L.seg_exit[j] = (uint32_t)x;
-          L.sbits[j] = st;
-          j = PWG + atomicAdd(&L.misc[0], 1);  // the next unclaimed segment
-          if (j >= nlc) return NX_STOP;
-          s0 = xs + PSEG * j;
-          s1 = min(np, s0 + PSEG);
-          ns = 0;
-          st = 0;
-          wb.base = segs_w + (int64_t)j * LANE_WORDS;
-          return s0;
+          while (j < nlc && x >= s1) {  // segment j is parsed: publish it
+            wb.flush(ns);
+            L.seg_nsym[j] = (uint8_t)ns;
+            L.seg_exit[j] = (uint32_t)x;
+            L.sbits[j] = st;
+            if (!(j & 1) && j + 1 < nlc && atomicCAS(&L.seg_mrg[j + 1], 0u, 1u) == 0u) {
+              take(j + 1);  // flow on into the odd segment after it, from x
+              continue;     // (x may lie past it too: then it is published empty)
+            }
+            const int q = pull();
+            if (q >= nlc) {
+              j = nlc;
+              break;
+            }
+            take(q);
+            return s0;
+          }
+          return j < nlc ? x : NX_STOP;
         });
   }
   __threadfence_block();

@@ -20,7 +20,9 @@ def hash3(b, x):
 
 
 class Chunk:
-    def __init__(self, blk, cs, ch, xw, pseg, nlanes, chain, lazy, nice, good, own, cont):
+    def __init__(self, blk, cs, ch, xw, pseg, nlanes, chain, lazy, nice, good, own, cont, rng=None,
+                 flow=0.0):
+        self.rng, self.flow = rng, flow
         ce = min(len(blk), cs + ch)
         self.r0 = max(0, cs - xw)
         self.inb = bytes(blk[self.r0:ce]) + bytes(16)
@@ -103,11 +105,17 @@ class Chunk:
     def run(self):
         np_, xs, P = self.np, self.xs, self.pseg
         nlc = (np_ - xs + P - 1) // P
-        own, ex = [], []
+        own, ex, begin = [], [], []
         for t in range(nlc):
             s0 = min(np_, xs + P * t)
             s1 = min(np_, s0 + P)
-            w, x = [], s0
+            # an odd segment is flowed into from its even predecessor's exit (the kernel's usual
+            # case) or, when the predecessor's lane was late, started at its own start
+            x = s0
+            if t % 2 == 1 and self.rng.random() < self.flow:
+                x = ex[t - 1]
+            begin.append(x)
+            w = []
             while x < s1:
                 x = self.step(x, w, self.own)
             own.append(w)
@@ -115,7 +123,7 @@ class Chunk:
         # symbol starts of each lane's own parse (the kernel's sbits words)
         starts = []
         for t in range(nlc):
-            s0, sb, x = xs + P * t, set(), xs + P * t
+            s0, sb, x = xs + P * t, set(), begin[t]
             for sy in own[t]:
                 if x < s0 + P:  # a deferred literal past the segment end is not recorded
                     sb.add(x)
@@ -208,6 +216,7 @@ def main():
     ap.add_argument("--blocks", type=int, default=20)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cont", type=int, default=104, help="continuation staging (forced merges past cont - 40)")
+    ap.add_argument("--flow", type=float, default=0.8, help="share of odd segments flowed into")
     a = ap.parse_args()
     rng = random.Random(a.seed)
     CH, NCH, XW, PSEG = 2040, 2, 1024, 8
@@ -231,7 +240,8 @@ def main():
         for c in range(NCH):
             if c * CH >= n:
                 continue
-            ck = Chunk(blk, c * CH, CH, XW, PSEG, CH // PSEG, *cfg, own=8 + 33 + 3, cont=a.cont)
+            ck = Chunk(blk, c * CH, CH, XW, PSEG, CH // PSEG, *cfg, own=8 + 33 + 3, cont=a.cont,
+                       rng=rng, flow=a.flow)
             syms, forced = ck.run()
             tot_forced += forced
             decode(syms, out)
