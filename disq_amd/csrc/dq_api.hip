@@ -1222,7 +1222,7 @@ static int bgzf_compress_dev(dq_ctx* ctx, const uint8_t* d_src, int64_t len, dou
     const int64_t nb = std::min(batch, nblk - b0);
     static const bool timing = getenv("DQ_DEFLATE_TIMING") != nullptr;
     uint64_t* tim = nullptr;
-    const size_t ntim = 8 * (size_t)nb * 3;  // 2 parse workgroups + 1 code workgroup per block
+    const size_t ntim = 8 * (size_t)nb * 4;  // 2 parse workgroups + 1 Huffman + 1 code per block
     if (timing) HIPCHK(hipMalloc(&tim, 8 * ntim));
     launch_bgzf_deflate(d_src, len, b0, nb, ctx->z_stage.as<uint32_t>(), ctx->z_link.as<uint32_t>(),
                         ctx->z_slots.as<uint8_t>(), ctx->z_size.as<int32_t>(), tim, s);
@@ -1233,11 +1233,13 @@ static int bgzf_compress_dev(dq_ctx* ctx, const uint8_t* d_src, int64_t len, dou
       HIPCHK(hipStreamSynchronize(s));
       (void)hipFree(tim);
       // parse workgroups (per chunk), then the code workgroups (per block)
-      static const char* nm[2][8] = {{"", "load", "counts", "scan", "scatter", "parse", "continue", "merge+hist"},
-                                     {"", "sum", "huffman", "count+scan", "write", "store", "", ""}};
-      const int64_t cnt[2] = {2 * nb, nb};
+      static const char* nm[3][8] = {{"", "load", "counts", "scan", "scatter", "parse", "continue", "merge+hist"},
+                                     {"", "sum", "lengths", "codes+rle", "cl_code", "", "", ""},
+                                     {"", "load", "count+scan", "write", "store", "", "", ""}};
+      static const char* kn[3] = {"parse", "huffman", "code"};
+      const int64_t cnt[3] = {2 * nb, nb, nb};
       size_t at = 0;
-      for (int kk = 0; kk < 2; kk++) {
+      for (int kk = 0; kk < 3; kk++) {
         double acc[8] = {0};
         for (int64_t i = 0; i < cnt[kk]; i++)
           for (int k = 1; k < 8; k++) {
@@ -1245,7 +1247,7 @@ static int bgzf_compress_dev(dq_ctx* ctx, const uint8_t* d_src, int64_t len, dou
             if (a) acc[k] += (double)(a - z);
           }
         at += 8 * (size_t)cnt[kk];
-        fprintf(stderr, "[dq] deflate %s cycles per workgroup:", kk ? "code" : "parse");
+        fprintf(stderr, "[dq] deflate %s cycles per workgroup:", kn[kk]);
         for (int k = 1; k < 8; k++)
           if (nm[kk][k][0]) fprintf(stderr, " %s=%.0f", nm[kk][k], acc[k] / (double)cnt[kk]);
         fprintf(stderr, "\n");

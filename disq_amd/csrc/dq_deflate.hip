@@ -74,6 +74,7 @@ constexpr int WIN = 32768;               // DEFLATE window
 constexpr int OWN_WORDS = 68;            // a segment's own symbols (<= 32 + the last step's <= 33)
 constexpr int CONT_WORDS = 156;          // its continuation past its end
 constexpr int LANE_WORDS = OWN_WORDS + CONT_WORDS;
+constexpr int FMERGE = CONT_WORDS - 40;  // continuation symbols before a forced merge (default)
 constexpr int MAX_DEFLATE = 65536 - 26;  // BSIZE limit: 18-byte header + payload + 8 trailer
 constexpr int MAXCAND = 128;             // candidates per match search at most (cfg.chain)
 constexpr int CWG = 256;                 // threads of the code kernel
@@ -82,7 +83,10 @@ constexpr int CSEG = 8;                  // segments per code thread
 // per block in `meta`: a word per segment (NCH x MSEG), then NCH chunk records of CI_WORDS
 constexpr int CI_WORDS = 320;
 enum { CI_LL = 0, CI_D = 286, CI_CRC = 316, CI_OVER = 317, CI_BYTES = 318 };
-constexpr int META_WORDS = NCH * (MSEG + CI_WORDS);
+// then the block's code tables (bgzf_huff_kernel -> bgzf_code_kernel): literal/length, distance
+// and code-length codes, the code-length code's lengths, the run-length tokens (2 per word), misc
+enum { TB_LL = 0, TB_D = 286, TB_CL = 316, TB_LENCL = 335, TB_TOK = 354, TB_MISC = 512, TB_WORDS = 520 };
+constexpr int META_WORDS = NCH * (MSEG + CI_WORDS) + TB_WORDS;
 // segment word: first own symbol | own symbols << 8 | continuation symbols << 16 | reached << 24
 constexpr uint32_t LM_REACHED = 1u << 24;
 static_assert(PL * PSEG == CH && PL <= MSEG && NLANE <= CSEG * CWG, "segment layout");
@@ -684,7 +688,7 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
                                                          uint32_t* __restrict__ stage,
                                                          uint32_t* __restrict__ meta,
                                                          uint64_t* __restrict__ tim, int chain,
-                                                         int lazy, int nice, int good) {
+                                                         int lazy, int nice, int good, int fmerge) {
   __shared__ PLds L;
   uint64_t tm[8];
   int ti = 0;
@@ -929,8 +933,8 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
           k = __popc(ub & ((1u << (E - su)) - 1));
           return NX_STOP;
         }
-        if (nc > CONT_WORDS - 40) {  // (a step appends at most lazy + 1 <= 33 symbols)
-          // no merge within the staging (e.g. one repeated byte: 258-byte matches from this
+        if (nc > fmerge) {  // (a step appends at most lazy + 1 <= 33 symbols: fmerge <= CONT - 40)
+          // no merge within `fmerge` symbols (e.g. one repeated byte: 258-byte matches from this
           // parse's positions never meet segment u's): end exactly on segment u's next boundary
           // pu > E, with matches cut to fit and literals for the last < 3 bytes -- a valid parse
           // that merges
@@ -1097,14 +1101,20 @@ __device__ inline void for_each_sym(uint32_t m, const uint32_t* __restrict__ w, 
 }
 static_assert(OWN_WORDS % 4 == 0 && LANE_WORDS % 4 == 0, "16-byte aligned stage areas");
 
-__global__ __launch_bounds__(CWG) void bgzf_code_kernel(const uint8_t* __restrict__ src,
-                                                        int64_t n_in, int64_t blk0, int64_t nblk,
-                                                        const uint32_t* __restrict__ stage,
-                                                        const uint32_t* __restrict__ meta,
-                                                        uint8_t* __restrict__ out_slots,
-                                                        int32_t* __restrict__ out_size,
+// Huffman codes of one block per 128-thread workgroup (7.9 KB of LDS, many per CU, so the
+// latency-bound serial parts -- the Moffat-Katajainen pass, the run-length coding -- of many blocks
+// overlap): the two chunks' histograms summed, wave 0 the literal/length code and wave 1 the
+// distance code, the code-length code; the tables and header tokens go to the block's record for
+// bgzf_code_kernel.
+constexpr int HWG = 128;
+struct alignas(16) HLds {
+  int32_t head[H_END];
+  int32_t misc[8];
+};
+__global__ __launch_bounds__(HWG) void bgzf_huff_kernel(int64_t n_in, int64_t blk0, int64_t nblk,
+                                                        uint32_t* __restrict__ meta,
                                                         uint64_t* __restrict__ tim) {
-  __shared__ CLds L;
+  __shared__ HLds L;
   uint64_t tm[8];
   int ti = 0;
   DTS();
@@ -1113,12 +1123,12 @@ __global__ __launch_bounds__(CWG) void bgzf_code_kernel(const uint8_t* __restric
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int64_t base = (blk0 + b) * (int64_t)BLK_U;
   const int n = (int)min<int64_t>(BLK_U, n_in - base);
-  const uint32_t* lm = meta + b * META_WORDS;
   const int32_t* ci = reinterpret_cast<const int32_t*>(meta + b * META_WORDS + NCH * MSEG);
+  uint32_t* tb = meta + b * META_WORDS + NCH * (MSEG + CI_WORDS);
   int32_t* H = L.head;
-  for (int i = t; i < H_CL + 32; i += CWG) H[i] = 0;
+  for (int i = t; i < H_CL + 32; i += HWG) H[i] = 0;
   __syncthreads();
-  for (int s = t; s < CI_CRC; s += CWG) {
+  for (int s = t; s < CI_CRC; s += HWG) {
     int v = 0;
 #pragma unroll
     for (int c = 0; c < NCH; c++) v += ci[c * CI_WORDS + s];
@@ -1137,16 +1147,16 @@ __global__ __launch_bounds__(CWG) void bgzf_code_kernel(const uint8_t* __restric
     L.misc[7] = over;
   }
   __syncthreads();
-  const bool over = L.misc[7] != 0;
   DTS();
   // ---- dynamic Huffman codes: wave 0 the literal/length alphabet, wave 1 the distances
   if (wv == 0) build_lengths(H + H_LL, 286, 15, H + H_SORT, H + H_W, H + H_LEN, H + H_CNT, lane);
   if (wv == 1) build_lengths(H + H_D, 30, 15, H + H_SORT_D, H + H_W_D, H + H_LEN_D, H + H_CNT_D, lane);
   __syncthreads();
-  // codes by waves 0 and 1 while wave 2's first lane run-length codes the code lengths
+  DTS();
+  // codes by waves 0 and 1; wave 1's first lane then run-length codes the code lengths
   if (wv == 0) canon_codes_wave(H + H_LEN, 286, reinterpret_cast<uint32_t*>(H + C_LL), lane);
   if (wv == 1) canon_codes_wave(H + H_LEN_D, 30, reinterpret_cast<uint32_t*>(H + C_D), lane);
-  if (t == 128) {
+  if (t == 64) {  // (wave 1, after its distance codes)
     // code-length sequence, run-length coded (16: repeat 3-6, 17: 3-10 zeros, 18: 11-138 zeros)
     int nlit = 286, ndist = 30;
     while (nlit > 257 && H[H_LEN + nlit - 1] == 0) nlit--;
@@ -1178,6 +1188,7 @@ __global__ __launch_bounds__(CWG) void bgzf_code_kernel(const uint8_t* __restric
     L.misc[4] = nt;
   }
   __syncthreads();
+  DTS();
   if (wv == 0) build_lengths(H + H_CL, 19, 7, H + H_SORT, H + H_W, H + H_LEN_CL, H + H_CNT, lane);
   __syncthreads();
   if (wv == 0) {
@@ -1198,6 +1209,50 @@ __global__ __launch_bounds__(CWG) void bgzf_code_kernel(const uint8_t* __restric
     }
   }
   __syncthreads();
+  DTS();
+  // the record
+  for (int i = t; i < 286; i += HWG) tb[TB_LL + i] = (uint32_t)H[C_LL + i];
+  for (int i = t; i < 30; i += HWG) tb[TB_D + i] = (uint32_t)H[C_D + i];
+  for (int i = t; i < 19; i += HWG) {
+    tb[TB_CL + i] = (uint32_t)H[C_CL + i];
+    tb[TB_LENCL + i] = (uint32_t)H[H_LEN_CL + i];
+  }
+  for (int i = t; i < TB_MISC - TB_TOK; i += HWG) tb[TB_TOK + i] = (uint32_t)H[H_TOK + i];
+  if (t < 8) tb[TB_MISC + t] = (uint32_t)L.misc[t];
+  if (tim && t == 0)
+    for (int k = 0; k < 8; k++) tim[b * 8 + k] = k < ti ? tm[k] - tm[0] : 0;
+}
+
+__global__ __launch_bounds__(CWG) void bgzf_code_kernel(const uint8_t* __restrict__ src,
+                                                        int64_t n_in, int64_t blk0, int64_t nblk,
+                                                        const uint32_t* __restrict__ stage,
+                                                        const uint32_t* __restrict__ meta,
+                                                        uint8_t* __restrict__ out_slots,
+                                                        int32_t* __restrict__ out_size,
+                                                        uint64_t* __restrict__ tim) {
+  __shared__ CLds L;
+  uint64_t tm[8];
+  int ti = 0;
+  DTS();
+  const int64_t b = (int64_t)blockIdx.x;
+  if (b >= nblk) return;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t base = (blk0 + b) * (int64_t)BLK_U;
+  const int n = (int)min<int64_t>(BLK_U, n_in - base);
+  const uint32_t* lm = meta + b * META_WORDS;
+  int32_t* H = L.head;
+  // the block's code tables from bgzf_huff_kernel
+  const uint32_t* tb = meta + b * META_WORDS + NCH * (MSEG + CI_WORDS);
+  for (int i = t; i < 286; i += CWG) H[C_LL + i] = (int32_t)tb[TB_LL + i];
+  for (int i = t; i < 30; i += CWG) H[C_D + i] = (int32_t)tb[TB_D + i];
+  for (int i = t; i < 19; i += CWG) {
+    H[C_CL + i] = (int32_t)tb[TB_CL + i];
+    H[H_LEN_CL + i] = (int32_t)tb[TB_LENCL + i];
+  }
+  for (int i = t; i < TB_MISC - TB_TOK; i += CWG) H[H_TOK + i] = (int32_t)tb[TB_TOK + i];
+  if (t < 8) L.misc[t] = (int32_t)tb[TB_MISC + t];
+  __syncthreads();
+  const bool over = L.misc[7] != 0;
   DTS();
   // ---- bits of this thread's eight segments under the dynamic and the fixed code
   uint32_t lw[CSEG];
@@ -1428,16 +1483,19 @@ void launch_bgzf_deflate(const uint8_t* src, int64_t n_in, int64_t blk0, int64_t
   // own settings; with the 4-byte bucket key that is ratio 2.92 on the WGS stream against htsjdk's
   // 2.857, profiles/r4m_deflate_sweep.txt; good 0 = always the full chain; read at every launch, so
   // a test can sweep settings in one process)
-  int cc = 32, cl = 16, cn = 32, cg = 8;
-  if (const char* e = getenv("DQ_DEFLATE")) sscanf(e, "%d,%d,%d,%d", &cc, &cl, &cn, &cg);
+  int cc = 32, cl = 16, cn = 32, cg = 8, cf = FMERGE;
+  if (const char* e = getenv("DQ_DEFLATE")) sscanf(e, "%d,%d,%d,%d,%d", &cc, &cl, &cn, &cg, &cf);
+  cf = std::max(0, std::min(cf, CONT_WORDS - 40));
   cc = std::max(1, std::min(cc, MAXCAND));
   cl = std::max(0, std::min(cl, 32));
   cn = std::max(3, cn);
   cg = std::max(0, cg);
   hipLaunchKernelGGL(bgzf_parse_kernel, dim3((unsigned)(nblk * NCH)), dim3(PWG), 0, s, src, n_in, blk0,
-                     nblk, stage, meta, tim, cc, cl, cn, cg);
+                     nblk, stage, meta, tim, cc, cl, cn, cg, cf);
+  hipLaunchKernelGGL(bgzf_huff_kernel, dim3((unsigned)nblk), dim3(HWG), 0, s, n_in, blk0, nblk, meta,
+                     tim ? tim + nblk * NCH * 8 : nullptr);
   hipLaunchKernelGGL(bgzf_code_kernel, dim3((unsigned)nblk), dim3(CWG), 0, s, src, n_in, blk0, nblk,
-                     stage, meta, out_slots, out_size, tim ? tim + nblk * NCH * 8 : nullptr);
+                     stage, meta, out_slots, out_size, tim ? tim + nblk * (NCH + 1) * 8 : nullptr);
 }
 
 void launch_bgzf_pack(const uint8_t* slots, const int32_t* size, const int64_t* off, int64_t nblk,

@@ -12,7 +12,7 @@ tail -1 $out/deflate_tests.log
 for v in "$@"; do
   echo "== $v"
   DQ_GPU_LIB=$PWD/disq_amd/_build/$v DQ_DEFLATE_TIMING=1 timeout -k 10 120 python3 -u tools/deflate_bench.py --records 2000000 --reps 1 > $out/timing_$v.log 2>&1
-  grep "cycles" $out/timing_$v.log | tail -2
+  grep "cycles" $out/timing_$v.log | tail -3
   DQ_GPU_LIB=$PWD/disq_amd/_build/$v timeout -k 10 120 python3 -u tools/deflate_bench.py --records 2000000 --reps 3 > $out/bench_$v.log 2>&1
   grep '"ratio"' $out/bench_$v.log
 done
