@@ -1200,24 +1200,30 @@ static int text_run(dq_ctx* ctx, int32_t drop_hash) {
 
 // ------------------------------------------------------------------ BGZF deflate (write path)
 // htsjdk BlockCompressedOutputStream over a byte stream in HBM: blocks of 65280 bytes compressed
-// in batches of 1024 (per block 1.8 MiB of staged-symbol space, of which the parse touches about
-// 60 KB, and 10.7 KB of segment / chunk records), packed into ctx->z_out.
+// in batches of DQ_DEFLATE_BATCH blocks (default 4096: per block 1.8 MiB of staged-symbol space, of
+// which the parse touches about 60 KB, and 10.7 KB of segment / chunk records), packed into
+// ctx->z_out at offsets scanned on the device: no host round trip between batches.
 static int bgzf_compress_dev(dq_ctx* ctx, const uint8_t* d_src, int64_t len, double* ms) {
   if (!deflate_tables(ctx->o.device)) RET(DQ_EDEVICE, "deflate table initialisation failed");
   hipStream_t s = ctx->s;
   const int64_t nblk = bgzf_block_count(len);
-  const int64_t batch = std::min<int64_t>(std::max<int64_t>(nblk, 1), 1024);
+  static const int64_t max_batch = [] {
+    const char* e = getenv("DQ_DEFLATE_BATCH");
+    return e && atoll(e) > 0 ? (int64_t)atoll(e) : (int64_t)4096;
+  }();
+  // (the batches evenly sized: the last one no shorter than the others)
+  const int64_t nbat = std::max<int64_t>(1, (nblk + max_batch - 1) / max_batch);
+  const int64_t batch = std::max<int64_t>(1, (nblk + nbat - 1) / nbat);
   int rc;
   if ((rc = ensure_all(ctx, ctx->z_stage, bgzf_stage_bytes(batch)))) return rc;
   if ((rc = ensure_all(ctx, ctx->z_link, bgzf_meta_bytes(batch)))) return rc;
   if ((rc = ensure_all(ctx, ctx->z_slots, (size_t)batch * 65536))) return rc;
   if ((rc = ensure_all(ctx, ctx->z_size, 4 * (size_t)batch))) return rc;
-  if ((rc = ensure_all(ctx, ctx->z_off, 8 * (size_t)batch))) return rc;
+  if ((rc = ensure_all(ctx, ctx->z_off, 8 * (size_t)batch + 8))) return rc;  // + the running total
   if ((rc = ensure_all(ctx, ctx->z_out, (size_t)std::max<int64_t>(nblk, 1) * 65536))) return rc;
+  int64_t* d_total = ctx->z_off.as<int64_t>() + batch;
   HIPCHK(hipEventRecord(ctx->ev[0], s));
-  std::vector<int32_t> sz((size_t)batch);
-  std::vector<int64_t> off((size_t)batch);
-  int64_t total = 0;
+  HIPCHK(hipMemsetAsync(d_total, 0, 8, s));
   for (int64_t b0 = 0; b0 < nblk; b0 += batch) {
     const int64_t nb = std::min(batch, nblk - b0);
     static const bool timing = getenv("DQ_DEFLATE_TIMING") != nullptr;
@@ -1253,17 +1259,13 @@ static int bgzf_compress_dev(dq_ctx* ctx, const uint8_t* d_src, int64_t len, dou
         fprintf(stderr, "\n");
       }
     }
-    HIPCHK(hipMemcpyAsync(sz.data(), ctx->z_size.p, 4 * (size_t)nb, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    for (int64_t i = 0; i < nb; i++) {
-      off[(size_t)i] = total;
-      total += sz[(size_t)i];
-    }
-    HIPCHK(hipMemcpyAsync(ctx->z_off.p, off.data(), 8 * (size_t)nb, hipMemcpyHostToDevice, s));
-    launch_bgzf_pack(ctx->z_slots.as<uint8_t>(), ctx->z_size.as<int32_t>(), ctx->z_off.as<int64_t>(), nb,
-                     ctx->z_out.as<uint8_t>(), s);
+    launch_bgzf_pack(ctx->z_slots.as<uint8_t>(), ctx->z_size.as<int32_t>(), ctx->z_off.as<int64_t>(),
+                     d_total, nb, ctx->z_out.as<uint8_t>(), s);
+    HIPCHK(hipGetLastError());
   }
   HIPCHK(hipEventRecord(ctx->ev[1], s));
+  int64_t total = 0;
+  HIPCHK(hipMemcpyAsync(&total, d_total, 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   ctx->z_len = total;
   if (ms) *ms = ev_ms(ctx->ev[0], ctx->ev[1]);

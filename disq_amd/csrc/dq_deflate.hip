@@ -9,11 +9,11 @@
 // kernel's own (java.util.zip.Deflater's exact bit stream is not reproduced): the output is valid
 // BGZF whose blocks inflate to exactly htsjdk's block contents.
 //
-// Two kernels per batch of blocks, everything the match finder touches in LDS:
+// Three kernels per batch of blocks, everything the match finder touches in LDS:
 //   bgzf_parse_kernel: one 512-thread workgroup per CHUNK, half a block (32640 bytes), holding the
-//      chunk's bytes plus up to 15000 bytes before it (its window reach) and the hash-bucket lists of
+//      chunk's bytes plus up to 13600 bytes before it (its window reach) and the hash-bucket lists of
 //      all those positions (3 bytes of LDS per position: 160 KB, one workgroup per CU).  A chunk's
-//      matches end inside it and reach back at most 15000 bytes before its start (the 32 KiB DEFLATE
+//      matches end inside it and reach back at most 13600 bytes before its start (the 32 KiB DEFLATE
 //      window inside the first chunk): tools/deflate_model.c puts that at zlib level 5's ratio on
 //      the WGS stream and the golden BAM / VCF streams (profiles/r4_deflate_chunk_model.txt).
 //   1. Match finder: every position with a 4-byte suffix goes into one of 2048 hash buckets of its
@@ -25,30 +25,33 @@
 //      its bucket, most recent first (its own slot is found by a 16-way search of the bucket): a
 //      contiguous run of the list, so a search loads 8 candidates and their first 16 bytes at
 //      once instead of chasing zlib's hash-chain links one dependent load at a time.
-//   2. Parse: lane t parses from its 64-byte segment start with zlib-style lazy evaluation (a
-//      match shorter than `lazy` is deferred while the next position's is longer; the look-ahead
-//      search walks chain / 4 candidates once the current match is `good` long, as zlib's
-//      deflate_slow), the longest match among `chain` candidates (stopping at `nice`), matches
-//      running on past the segment end.  A parse step depends on its position alone, so two
-//      parses that reach the same position continue identically: from its exit, each lane keeps
-//      parsing until it hits a symbol boundary of a later lane's parse (usually within a few
-//      symbols) and records the merge; pointer jumping over the merges from lane 0 marks the lanes
-//      on the chunk's one parse and the symbol each starts from.  The merged parse is valid but
-//      not always the one a single sequential pass would make: a merge can land inside a lazy
-//      step of the continuing lane (after a deferred literal whose look-ahead search walked
-//      chain / 4 candidates), and a continuation that finds no merge within its staging is ended
-//      on the next boundary of a later lane with a shortened match.
-//      Symbols are staged per lane in HBM (one word each); the chunk's literal/length and distance
-//      histograms over its parse, its CRC and a word per lane (first symbol, counts) go with them.
-//   bgzf_code_kernel: one 256-thread workgroup per block (73 KB of LDS, two per CU).
+//   2. Parse: the chunk is cut into 32-byte segments; thread t parses segment 2t from its start
+//      with zlib-style lazy evaluation (a match shorter than `lazy` is deferred while the next
+//      position's is longer; the look-ahead search walks chain / 4 candidates once the current
+//      match is `good` long, as zlib's deflate_slow), the longest match among `chain` candidates
+//      (stopping at `nice`), and flows on into segment 2t + 1 unless a thread that finished early
+//      claimed it first.  A parse step depends on its position alone, so two parses that reach the
+//      same position continue identically: from its exit, each segment's parse is continued until
+//      it hits a symbol boundary of a later segment's parse (usually within a few symbols) and the
+//      merge is recorded; after `fmerge` continuation symbols without one (default 2) it is ended
+//      on the next boundary of the later segment with a shortened match.  Pointer jumping over the
+//      merges from segment 0 marks the segments on the chunk's one parse and the symbol each
+//      starts from.  The merged parse is valid but not always the one a single sequential pass
+//      would make (0.3% larger on the WGS stream; within 0.5% of zlib level 5 on every golden
+//      stream, tests/test_deflate_gpu.py).  Symbols are staged per segment in HBM (one word
+//      each); the chunk's literal/length and distance histograms over its parse, its CRC and a
+//      word per segment (first symbol, counts) go with them.
+//   bgzf_huff_kernel: one 128-thread workgroup per block (7.9 KB of LDS, many per CU).
 //   3. Codes: the two chunks' histograms summed; wave 0 builds the literal/length code and wave 1
 //      the distance code (a rank sort, Moffat-Katajainen minimum-redundancy lengths, a Kraft
-//      fix-up capping them at 15), the code-length sequence is run-length coded; the block is
-//      coded dynamic (BTYPE 10) or fixed (01), whichever is shorter -- one DEFLATE block per
-//      member, as zlib writes a 64 KiB input.
-//   4. Emit: each lane's bit count gives its offset by an exclusive scan; every thread OR-s its
-//      four lanes' bits into the LDS image of the block.  A block whose code would not fit BSIZE
-//      (or whose parse overflowed its staging) is stored (BTYPE 00).
+//      fix-up capping them at 15), the code-length sequence is run-length coded; the tables go to
+//      the block's record.
+//   bgzf_code_kernel: one 256-thread workgroup per block (73 KB of LDS, two per CU).
+//   4. Emit: the block is coded dynamic (BTYPE 10) or fixed (01), whichever is shorter -- one
+//      DEFLATE block per member, as zlib writes a 64 KiB input; each thread's bit count gives its
+//      offset by an exclusive scan; every thread OR-s its eight segments' bits into the LDS image
+//      of the block.  A block whose code would not fit BSIZE (or whose parse overflowed its
+//      staging) is stored (BTYPE 00).
 // CRC32: per-lane table CRC over the segment, combined with x^(8 n) mod P multipliers.
 // (Defaults chain 32, lazy 16, nice 32, good 8: zlib level 5's.)
 #include "dq_internal.h"
@@ -74,7 +77,7 @@ constexpr int WIN = 32768;               // DEFLATE window
 constexpr int OWN_WORDS = 68;            // a segment's own symbols (<= 32 + the last step's <= 33)
 constexpr int CONT_WORDS = 156;          // its continuation past its end
 constexpr int LANE_WORDS = OWN_WORDS + CONT_WORDS;
-constexpr int FMERGE = CONT_WORDS - 40;  // continuation symbols before a forced merge (default)
+constexpr int FMERGE = 2;  // continuation symbols before a forced merge (default; profiles/r4aj_*)
 constexpr int MAX_DEFLATE = 65536 - 26;  // BSIZE limit: 18-byte header + payload + 8 trailer
 constexpr int MAXCAND = 128;             // candidates per match search at most (cfg.chain)
 constexpr int CWG = 256;                 // threads of the code kernel
@@ -1428,6 +1431,37 @@ __global__ __launch_bounds__(256) void bgzf_pack_kernel(const uint8_t* __restric
   for (int i = threadIdx.x; i < n; i += 256) d[i] = s[i];
 }
 
+// The blocks' offsets in the packed stream: an exclusive scan of their sizes on top of the running
+// total at off[nblk] (one workgroup; the batch's total is added to it), so the batches need no host
+// round trip.
+__global__ __launch_bounds__(1024) void bgzf_offsets_kernel(const int32_t* __restrict__ size,
+                                                            int64_t nblk, int64_t* __restrict__ off,
+                                                            int64_t* __restrict__ total) {
+  __shared__ int64_t wsum[16];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  int64_t carry = *total;
+  for (int64_t b0 = 0; b0 < nblk; b0 += 1024) {
+    const int64_t i = b0 + t;
+    const int64_t v = i < nblk ? size[i] : 0;
+    int64_t inc = v;
+    for (int d = 1; d < 64; d <<= 1) {
+      const int64_t y = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += y;
+    }
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    int64_t pre = carry, all = carry;
+    for (int w = 0; w < 16; w++) {
+      pre += w < wv ? wsum[w] : 0;
+      all += wsum[w];
+    }
+    if (i < nblk) off[i] = pre + inc - v;
+    carry = all;
+    __syncthreads();
+  }
+  if (t == 0) *total = carry;
+}
+
 struct DefTables {
   std::once_flag once;
   bool ok = false;
@@ -1479,10 +1513,12 @@ void launch_bgzf_deflate(const uint8_t* src, int64_t n_in, int64_t blk0, int64_t
                          uint32_t* stage, uint32_t* meta, uint8_t* out_slots, int32_t* out_size,
                          uint64_t* tim, hipStream_t s) {
   if (nblk <= 0) return;
-  // DQ_DEFLATE="chain,lazy,nice[,good]": match-search effort (default 32,16,32,8: zlib level 5's
-  // own settings; with the 4-byte bucket key that is ratio 2.92 on the WGS stream against htsjdk's
-  // 2.857, profiles/r4m_deflate_sweep.txt; good 0 = always the full chain; read at every launch, so
-  // a test can sweep settings in one process)
+  // DQ_DEFLATE="chain,lazy,nice[,good[,fmerge]]": match-search effort (default 32,16,32,8: zlib
+  // level 5's own settings; with the 4-byte bucket key that is ratio 2.92 on the WGS stream against
+  // htsjdk's 2.857, profiles/r4m_deflate_sweep.txt; good 0 = always the full chain) and the
+  // continuation symbols before a forced merge (default 2: ratio 2.919 against 2.924 at 116, 7%
+  // faster, profiles/r4aj_deflate_fmerge.txt); read at every launch, so a test can sweep settings
+  // in one process
   int cc = 32, cl = 16, cn = 32, cg = 8, cf = FMERGE;
   if (const char* e = getenv("DQ_DEFLATE")) sscanf(e, "%d,%d,%d,%d,%d", &cc, &cl, &cn, &cg, &cf);
   cf = std::max(0, std::min(cf, CONT_WORDS - 40));
@@ -1498,9 +1534,10 @@ void launch_bgzf_deflate(const uint8_t* src, int64_t n_in, int64_t blk0, int64_t
                      stage, meta, out_slots, out_size, tim ? tim + nblk * (NCH + 1) * 8 : nullptr);
 }
 
-void launch_bgzf_pack(const uint8_t* slots, const int32_t* size, const int64_t* off, int64_t nblk,
-                      uint8_t* out, hipStream_t s) {
+void launch_bgzf_pack(const uint8_t* slots, const int32_t* size, int64_t* off, int64_t* total,
+                      int64_t nblk, uint8_t* out, hipStream_t s) {
   if (nblk <= 0) return;
+  hipLaunchKernelGGL(bgzf_offsets_kernel, dim3(1), dim3(1024), 0, s, size, nblk, off, total);
   hipLaunchKernelGGL(bgzf_pack_kernel, dim3((unsigned)nblk), dim3(256), 0, s, slots, size, off, nblk,
                      out);
 }

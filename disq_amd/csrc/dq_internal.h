@@ -334,7 +334,9 @@ bool deflate_tables(int device);
 void launch_bgzf_deflate(const uint8_t* src, int64_t n_in, int64_t blk0, int64_t nblk,
                          uint32_t* stage, uint32_t* meta, uint8_t* out_slots, int32_t* out_size,
                          uint64_t* tim, hipStream_t s);
-void launch_bgzf_pack(const uint8_t* slots, const int32_t* size, const int64_t* off, int64_t nblk,
-                      uint8_t* out, hipStream_t s);
+// Packs the slots at offsets scanned on the device from the sizes on top of *total (the stream's
+// length so far, updated).
+void launch_bgzf_pack(const uint8_t* slots, const int32_t* size, int64_t* off, int64_t* total,
+                      int64_t nblk, uint8_t* out, hipStream_t s);
 
 }  // namespace dq
