@@ -1200,16 +1200,17 @@ static int text_run(dq_ctx* ctx, int32_t drop_hash) {
 
 // ------------------------------------------------------------------ BGZF deflate (write path)
 // htsjdk BlockCompressedOutputStream over a byte stream in HBM: blocks of 65280 bytes compressed
-// in batches of DQ_DEFLATE_BATCH blocks (default 4096: per block 1.8 MiB of staged-symbol space, of
-// which the parse touches about 60 KB, and 10.7 KB of segment / chunk records), packed into
-// ctx->z_out at offsets scanned on the device: no host round trip between batches.
+// in batches of DQ_DEFLATE_BATCH blocks (default 16384, about 1 GB of input: per block 384 KB of
+// staged-match space -- a dense area and an overflow pool per chunk, of which the parse fills about
+// 10 KB -- and 35 KB of segment / chunk records), packed into ctx->z_out at offsets scanned on the
+// device: no host round trip between batches.
 static int bgzf_compress_dev(dq_ctx* ctx, const uint8_t* d_src, int64_t len, double* ms) {
   if (!deflate_tables(ctx->o.device)) RET(DQ_EDEVICE, "deflate table initialisation failed");
   hipStream_t s = ctx->s;
   const int64_t nblk = bgzf_block_count(len);
   static const int64_t max_batch = [] {
     const char* e = getenv("DQ_DEFLATE_BATCH");
-    return e && atoll(e) > 0 ? (int64_t)atoll(e) : (int64_t)4096;
+    return e && atoll(e) > 0 ? (int64_t)atoll(e) : (int64_t)16384;
   }();
   // (the batches evenly sized: the last one no shorter than the others)
   const int64_t nbat = std::max<int64_t>(1, (nblk + max_batch - 1) / max_batch);
@@ -1217,7 +1218,7 @@ static int bgzf_compress_dev(dq_ctx* ctx, const uint8_t* d_src, int64_t len, dou
   int rc;
   if ((rc = ensure_all(ctx, ctx->z_stage, bgzf_stage_bytes(batch)))) return rc;
   if ((rc = ensure_all(ctx, ctx->z_link, bgzf_meta_bytes(batch)))) return rc;
-  if ((rc = ensure_all(ctx, ctx->z_slots, (size_t)batch * 65536))) return rc;
+  if ((rc = ensure_all(ctx, ctx->z_slots, bgzf_slot_bytes(batch)))) return rc;
   if ((rc = ensure_all(ctx, ctx->z_size, 4 * (size_t)batch))) return rc;
   if ((rc = ensure_all(ctx, ctx->z_off, 8 * (size_t)batch + 8))) return rc;  // + the running total
   if ((rc = ensure_all(ctx, ctx->z_out, (size_t)std::max<int64_t>(nblk, 1) * 65536))) return rc;

@@ -74,30 +74,52 @@ constexpr int NPMAX = CH + XW;           // bytes (positions) a chunk workgroup 
 constexpr int HBITS = 11;                // hash buckets
 constexpr int MAXM = 258;
 constexpr int WIN = 32768;               // DEFLATE window
-constexpr int OWN_WORDS = 68;            // a segment's own symbols (<= 32 + the last step's <= 33)
-constexpr int CONT_WORDS = 156;          // its continuation past its end
-constexpr int LANE_WORDS = OWN_WORDS + CONT_WORDS;
+// Staged matches (literals are the input bytes between them: the code kernel reads those
+// itself): a word each, gap of literals before it | (length - 3) << 9 | (distance - 1) << 17.  Up
+// to MB_INL matches of a segment's own parse (or of its continuation) go to the chunk's dense
+// area at an offset taken from an LDS counter when the part ends; a part with more goes whole to
+// the chunk's overflow pool (OWN_CAP or CONT_CAP words taken from another counter when its ninth
+// match comes; a pathological chunk that exhausts the pool has its block stored).
+constexpr int MB_INL = 8;
+constexpr int CONT_WORDS = 156;          // continuation symbols at most
+constexpr int OWN_CAP = 16;              // own matches (a 32-byte segment's, + one past its end)
+constexpr int CONT_CAP = 160;            // continuation matches (<= CONT_WORDS)
+constexpr int DENSE_WORDS = 2 * MSEG * MB_INL;  // per chunk
+#ifndef DQ_POOL_WORDS
+#define DQ_POOL_WORDS 32768  // (a build with a small pool exercises the exhaustion path)
+#endif
+constexpr int POOL_WORDS = DQ_POOL_WORDS;       // per chunk
+constexpr int64_t STAGE_CH_WORDS = DENSE_WORDS + POOL_WORDS;  // per chunk
 constexpr int FMERGE = 2;  // continuation symbols before a forced merge (default; profiles/r4aj_*)
 constexpr int MAX_DEFLATE = 65536 - 26;  // BSIZE limit: 18-byte header + payload + 8 trailer
+// a block's output slot: the member's 18-byte header at SLOT_HDR, the deflate payload 16-byte
+// aligned at SLOT_HDR + 18, the trailer after it
+constexpr int SLOT = 65600, SLOT_HDR = 14, SLOT_PAY = SLOT_HDR + 18;
+static_assert(SLOT_PAY % 16 == 0 && SLOT_PAY + MAX_DEFLATE + 4 + 8 <= SLOT && SLOT % 16 == 0, "slot layout");
 constexpr int MAXCAND = 128;             // candidates per match search at most (cfg.chain)
-constexpr int CWG = 256;                 // threads of the code kernel
-constexpr int NLANE = NCH * PL;          // 2040 segments per block; code thread i owns 8i..8i+7
-constexpr int CSEG = 8;                  // segments per code thread
+constexpr int CWG = 1024;                // threads of the code kernel
+constexpr int NLANE = NCH * PL;          // 2040 segments per block; code thread i owns 2i, 2i + 1
+constexpr int CSEG = 2;                  // segments per code thread
 // per block in `meta`: a word per segment (NCH x MSEG), then NCH chunk records of CI_WORDS
 constexpr int CI_WORDS = 320;
 enum { CI_LL = 0, CI_D = 286, CI_CRC = 316, CI_OVER = 317, CI_BYTES = 318 };
 // then the block's code tables (bgzf_huff_kernel -> bgzf_code_kernel): literal/length, distance
 // and code-length codes, the code-length code's lengths, the run-length tokens (2 per word), misc
 enum { TB_LL = 0, TB_D = 286, TB_CL = 316, TB_LENCL = 335, TB_TOK = 354, TB_MISC = 512, TB_WORDS = 520 };
-constexpr int META_WORDS = NCH * (MSEG + CI_WORDS) + TB_WORDS;
-// segment word: first own symbol | own symbols << 8 | continuation symbols << 16 | reached << 24
-constexpr uint32_t LM_REACHED = 1u << 24;
+// per block in `meta`: four words per segment (NCH x MSEG each), then NCH chunk records of
+// CI_WORDS, then the table record.  Segment words (positions chunk-local):
+//   SW_RANGE: first | end << 16 of its bytes on the chunk's parse (SW_NONE: not on it)
+//   SW_OWN:   own parse start | own parse exit << 16
+//   SW_OWNM, SW_CONTM: the own / continuation matches, dense offset | count << 16 | overflow << 24
+enum { SW_RANGE = 0, SW_OWN = 1, SW_OWNM = 2, SW_CONTM = 3 };
+constexpr uint32_t SW_NONE = 0xffffffffu;
+constexpr int CI_OFF = 4 * NCH * MSEG;
+constexpr int TB_OFF = CI_OFF + NCH * CI_WORDS;
+constexpr int META_WORDS = TB_OFF + TB_WORDS;
 static_assert(PL * PSEG == CH && PL <= MSEG && NLANE <= CSEG * CWG, "segment layout");
-static_assert(OWN_WORDS < 256 && CONT_WORDS < 256, "lane word fields");
+static_assert(CONT_WORDS < 256 && DENSE_WORDS <= 65536, "segment word fields");
 
 __constant__ uint32_t c_dcrc[256];
-__constant__ uint16_t c_lbase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
-                                     35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
 __constant__ uint32_t c_x2n[32];  // x^(2^k) mod P (reflected)
 
 __device__ inline uint32_t gf2_mul(uint32_t a, uint32_t b) {  // reflected, poly 0xEDB88320
@@ -303,13 +325,6 @@ __device__ inline uint64_t ld8(const uint8_t* in, int x) {
 }
 #endif
 
-// Staged symbol word: litlen symbol | length extra << 9 | distance symbol << 14 | distance extra << 19
-__device__ inline uint32_t sym_ll(uint32_t w) { return w & 511; }
-__device__ inline uint32_t sym_lx(uint32_t w) { return (w >> 9) & 31; }
-__device__ inline uint32_t sym_d(uint32_t w) { return (w >> 14) & 31; }
-__device__ inline uint32_t sym_dx(uint32_t w) { return w >> 19; }
-__device__ inline int lextra_bits(int s) { return (s < 265 || s == 285) ? 0 : (s - 261) >> 2; }
-__device__ inline int dextra_bits(int d) { return d < 4 ? 0 : (d - 2) >> 1; }
 __device__ inline int fixed_len_of(int s) { return s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8; }
 
 struct ImgOut {  // LSB-first bits OR-ed into the LDS image from bit position p on
@@ -323,7 +338,8 @@ struct ImgOut {  // LSB-first bits OR-ed into the LDS image from bit position p 
     n += len;
     if (n >= 32) {
       DQ_CHK(w < 65536 / 4, CHK_Z_IMAGE);
-      atomicOr(&img[w++], (uint32_t)acc);
+      atomicOr(&img[w], (uint32_t)acc);
+      w++;
       acc >>= 32;
       n -= 32;
     }
@@ -348,19 +364,14 @@ __device__ inline uint32_t hash4a(const uint8_t* in, int p) {
   return (__builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(p & 3)) * 2654435761u) >> (32 - HBITS);
 }
 
-__device__ inline int sym_bytes(uint32_t w) {  // uncompressed bytes of a staged symbol
-  const uint32_t ll = sym_ll(w);
-  return ll < 256 ? 1 : (int)c_lbase[ll - 257] + (int)sym_lx(w);
-}
 __device__ inline uint64_t lanes_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
 
-__device__ inline uint32_t lit_word(uint32_t b) { return b; }
-__device__ inline uint32_t match_word(int len, int d) {
-  int sym, nx, xv, ds, dnx, dxv;
-  len_code(len, sym, nx, xv);
-  dist_code(d, ds, dnx, dxv);
-  return (uint32_t)sym | ((uint32_t)xv << 9) | ((uint32_t)ds << 14) | ((uint32_t)dxv << 19);
+__device__ inline uint32_t mword(int gap, int len, int d) {
+  return (uint32_t)gap | (uint32_t)(len - 3) << 9 | (uint32_t)(d - 1) << 17;
 }
+__device__ inline int mw_gap(uint32_t w) { return (int)(w & 511); }
+__device__ inline int mw_len(uint32_t w) { return (int)((w >> 9) & 255) + 3; }
+__device__ inline int mw_dist(uint32_t w) { return (int)(w >> 17) + 1; }
 
 
 constexpr int SCAT_WAVES = 4;  // waves of the bucket scatter: one position range each
@@ -375,7 +386,6 @@ struct alignas(16) PLds {
       uint32_t seg_exit[MSEG];  // the parse's exit of each segment; later jump pointers, first symbols
       uint32_t seg_mrg[MSEG];   // continuation: merge segment | symbol << 11 | count << 18 | over << 26
       uint8_t seg_mark[MSEG];   // on the chunk's parse
-      uint8_t seg_nsym[MSEG];   // own symbols
       uint32_t sbits[PL];       // symbol starts of each segment's own parse inside it (a deferred
                                 // literal past the segment end is left out): one word each
     };
@@ -578,9 +588,10 @@ struct Finder {
 // search lengths differ (round 4: one lane in five was active per VALU instruction with the
 // searches run to their ends inside each parse step).  A step depends on its position alone, so
 // two parses that reach the same position continue identically (the merge rule below).  Matches
-// end at the chunk end np.  emit(word, position) stores a symbol; between steps next(x) says what
-// the lane does after a step that ended at x (or first, at its start): the position of its next
-// step, NX_WAIT (ask again in the next pass) or NX_STOP.
+// end at the chunk end np.  emit(length, distance, position) takes a symbol (length 0: the
+// literal at position); between steps next(x) says what the lane does after a step that ended at
+// x (or first, at its start): the position of its next step, NX_WAIT (ask again in the next pass)
+// or NX_STOP.
 enum { NX_WAIT = -1, NX_STOP = -2 };
 template <class Emit, class Next>
 __device__ __attribute__((always_inline)) inline void parse_lanes(const Finder& F, int lazy, int x0,
@@ -619,7 +630,7 @@ __device__ __attribute__((always_inline)) inline void parse_lanes(const Finder& 
       } else if (r <= l) {
         end = true;
       } else {  // a longer match one on: a literal, and look one further
-        emit(lit_word(F.L.in[x]), x);
+        emit(0, 0, x);
         x++;
         l = r;
         d = d2;
@@ -629,7 +640,7 @@ __device__ __attribute__((always_inline)) inline void parse_lanes(const Finder& 
           end = true;
       }
       if (end) {
-        emit(l ? match_word(l, d) : lit_word(F.L.in[x]), x);
+        emit(l, d, x);
         x += l ? l : 1;
         busy = false;
         const int r2 = next(x);  // the next step at once (no pass in between)
@@ -645,40 +656,112 @@ __device__ __attribute__((always_inline)) inline void parse_lanes(const Finder& 
   }
 }
 
-// The merge fields of seg_mrg (merge segment MSEG = the chunk's end)
-__device__ inline uint32_t mrg_word(int u, int k, int nc, bool over) {
-  return (uint32_t)u | (uint32_t)k << 11 | (uint32_t)nc << 18 | (over ? 1u << 26 : 0u);
+// The merge fields of seg_mrg: the segment merged into (MSEG = the chunk's end) | the merge
+// position's offset from that segment's start << 11 | overflowed << 20
+__device__ inline uint32_t mrg_word(int u, int off, bool over) {
+  return (uint32_t)u | (uint32_t)off << 11 | (over ? 1u << 20 : 0u);
 }
 __device__ inline int mrg_lane(uint32_t m) { return (int)(m & 2047); }
-__device__ inline int mrg_sym(uint32_t m) { return (int)((m >> 11) & 127); }
-__device__ inline int mrg_cont(uint32_t m) { return (int)((m >> 18) & 255); }
-__device__ inline bool mrg_over(uint32_t m) { return (m >> 26) & 1u; }
+__device__ inline int mrg_off(uint32_t m) { return (int)((m >> 11) & 511); }
+__device__ inline bool mrg_over(uint32_t m) { return (m >> 20) & 1u; }
 
-// Stage words buffered four at a time, one 16-byte store per four symbols: single 4-byte stores
-// from 64 lanes into 64 different lines were written back as partial lines (the parse kernel wrote
-// 6x the staged bytes, profiles/r4r_deflate_pmc.txt).  `base` is 16-byte aligned.
-struct WBuf {
-  uint32_t* base;
-  uint32_t p0, p1, p2, p3;
-  __device__ __attribute__((always_inline)) void put(int n, uint32_t w) {  // word n (n = count so far)
-    const int k = n & 3;
-    p0 = k == 0 ? w : p0;
-    p1 = k == 1 ? w : p1;
-    p2 = k == 2 ? w : p2;
-    p3 = k == 3 ? w : p3;
-    if (k == 3) *reinterpret_cast<uint4*>(base + (n - 3)) = make_uint4(p0, p1, p2, p3);
+// A part's (own parse's or continuation's) match words: the first MB_INL in registers; when the
+// part ends they go to the chunk's dense area at an offset from an LDS counter (the dense area is
+// packed: the code kernel reads a line per few segments instead of a line per segment part).  A
+// part with more is written whole to a `cap`-word area of the overflow pool instead.
+struct MBuf {
+  uint32_t* pool;
+  int* pctr;   // the pool's LDS counter
+  int* over;   // the chunk's "store the block" flag
+  int cap, po;
+  uint32_t p0, p1, p2, p3, p4, p5, p6, p7;
+  int n;
+  __device__ __attribute__((always_inline)) void put(uint32_t w) {
+    p0 = n == 0 ? w : p0;
+    p1 = n == 1 ? w : p1;
+    p2 = n == 2 ? w : p2;
+    p3 = n == 3 ? w : p3;
+    p4 = n == 4 ? w : p4;
+    p5 = n == 5 ? w : p5;
+    p6 = n == 6 ? w : p6;
+    p7 = n == 7 ? w : p7;
+    if (n >= MB_INL) {
+      if (n == MB_INL) {
+        po = atomicAdd(pctr, cap);
+        if (po + cap <= POOL_WORDS) {
+          *reinterpret_cast<uint4*>(pool + po) = make_uint4(p0, p1, p2, p3);
+          *reinterpret_cast<uint4*>(pool + po + 4) = make_uint4(p4, p5, p6, p7);
+        } else {
+          po = -1;
+          *over = 1;
+        }
+      }
+      if (po >= 0) pool[po + n] = w;
+    }
+    n++;
   }
-  __device__ __attribute__((always_inline)) void flush(int n) {  // the last n & 3 words
-    const int k = n & 3, a = n - k;
-    if (k > 0) base[a] = p0;
-    if (k > 1) base[a + 1] = p1;
-    if (k > 2) base[a + 2] = p2;
+  // the part's segment word (SW_OWNM / SW_CONTM): offset | count << 16 | in the pool << 24 (no
+  // matches when the pool ran out: the block is stored)
+  __device__ __attribute__((always_inline)) uint32_t publish(uint32_t* dense, int* ctr) {
+    if (n > MB_INL) return po >= 0 ? (uint32_t)po | (uint32_t)n << 16 | 1u << 24 : 0u;
+    const int o = n ? atomicAdd(ctr, n) : 0;
+    uint32_t* d = dense + o;
+    if (n > 0) d[0] = p0;
+    if (n > 1) d[1] = p1;
+    if (n > 2) d[2] = p2;
+    if (n > 3) d[3] = p3;
+    if (n > 4) d[4] = p4;
+    if (n > 5) d[5] = p5;
+    if (n > 6) d[6] = p6;
+    if (n > 7) d[7] = p7;
+    return (uint32_t)o | (uint32_t)n << 16;
   }
 };
-__device__ __attribute__((always_inline)) inline void hist_add(int32_t* H, uint32_t x, int v) {
-  const uint32_t ll = sym_ll(x);
-  atomicAdd(&H[CI_LL + ll], v);
-  if (ll > 256) atomicAdd(&H[CI_D + sym_d(x)], v);
+// the match words a segment word points at
+__device__ inline const uint32_t* part_words(const uint32_t* dense, uint32_t m) {
+  return dense + ((m >> 24) ? DENSE_WORDS : 0) + (m & 0xffff);
+}
+
+// The bytes of a segment on the chunk's parse, [first, end) of SW_RANGE, as literals and matches:
+// its own parse's symbols from `first` on, then its continuation's.  lit(byte) for a literal (the
+// chunk's bytes at `in`, LDS, read four at a time), mat(length, distance) for a match; `own` /
+// `cont` its parts' match words.
+template <class Lit, class Mat>
+__device__ __attribute__((always_inline)) inline void walk_segment(const uint8_t* in, uint32_t range, uint32_t ownw,
+                                                                    const uint32_t* __restrict__ own, int nown,
+                                                                    const uint32_t* __restrict__ cont, int ncont,
+                                                                    Lit lit, Mat mat) {
+  auto lits = [&](int a, int e) __attribute__((always_inline)) {
+    for (; a < e; a += 4) {
+      const uint32_t v = ld4(in, a);
+      lit(v & 255u);
+      if (a + 1 < e) lit((v >> 8) & 255u);
+      if (a + 2 < e) lit((v >> 16) & 255u);
+      if (a + 3 < e) lit(v >> 24);
+    }
+  };
+  const int first = (int)(range & 0xffff), end = (int)(range >> 16);
+  const int eo = (int)(ownw >> 16);
+  int pos = (int)(ownw & 0xffff);
+  for (int k = 0; k < nown; k++) {
+    const uint32_t w = own[k];
+    const int ms = pos + mw_gap(w), ml = mw_len(w);
+    if (ms >= first) {  // (a match before `first` ends at or before it: a boundary)
+      lits(max(pos, first), ms);
+      mat(ml, mw_dist(w));
+    }
+    pos = ms + ml;
+  }
+  lits(max(pos, first), eo);
+  pos = eo;
+  for (int k = 0; k < ncont; k++) {
+    const uint32_t w = cont[k];
+    const int ms = pos + mw_gap(w);
+    lits(pos, ms);
+    mat(mw_len(w), mw_dist(w));
+    pos = ms + mw_len(w);
+  }
+  lits(pos, end);
 }
 
 #define DTS()                                                                      \
@@ -703,10 +786,11 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
   const int64_t base = (blk0 + b) * (int64_t)BLK_U;
   const int n = (int)min<int64_t>(BLK_U, n_in - base);
   const int cs = c * CH;
-  uint32_t* lm = meta + b * META_WORDS + c * MSEG;
-  int32_t* ci = reinterpret_cast<int32_t*>(meta + b * META_WORDS + NCH * MSEG + c * CI_WORDS);
+  // this chunk's segment words: sw[k * NCH * MSEG + i] = word k of segment i
+  uint32_t* sw = meta + b * META_WORDS + c * MSEG;
+  int32_t* ci = reinterpret_cast<int32_t*>(meta + b * META_WORDS + CI_OFF + c * CI_WORDS);
   if (cs >= n) {  // an empty chunk (the last block is short)
-    for (int i = t; i < MSEG; i += PWG) lm[i] = 0;
+    for (int i = t; i < MSEG; i += PWG) sw[SW_RANGE * NCH * MSEG + i] = SW_NONE;
     for (int i = t; i < CI_WORDS; i += PWG) ci[i] = 0;
     if (tim && t == 0)
       for (int k = 0; k < 8; k++) tim[blockIdx.x * 8 + k] = 0;
@@ -839,21 +923,23 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
   //      predecessor needs no continuation); the odd segments nobody flowed into are handed out by
   //      an LDS counter, so a lane whose segments parse quickly takes more of them instead of
   //      idling until the wave's slowest lane is done.
-  uint32_t* const segs_w = stage + (b * NCH + c) * (int64_t)MSEG * LANE_WORDS;
+  uint32_t* const dense = stage + (b * NCH + c) * STAGE_CH_WORDS;
+  uint32_t* const pool = dense + DENSE_WORDS;
   const Finder F{L, np, min(chain, MAXCAND), nice, good};
   for (int i = t; i < MSEG; i += PWG) L.seg_mrg[i] = 0;  // odd segments' claim flags
   __syncthreads();
   {
-    int j = 2 * t, s0 = 0, s1 = 0, ns = 0;
+    int j = 2 * t, s0 = 0, s1 = 0, x0 = 0, pe = 0;
     uint32_t st = 0;  // symbol starts in the segment (a deferred literal past its end: left out)
-    WBuf wb{nullptr, 0, 0, 0, 0};
-    auto take = [&](int jj) __attribute__((always_inline)) {
+    MBuf mb{pool, &L.misc[3], &L.misc[7], OWN_CAP, 0};
+    auto take = [&](int jj, int x) __attribute__((always_inline)) {
       j = jj;
       s0 = xs + PSEG * j;
       s1 = min(np, s0 + PSEG);
-      ns = 0;
+      x0 = x;
+      pe = x;
       st = 0;
-      wb.base = segs_w + (int64_t)j * LANE_WORDS;
+      mb.n = 0;
     };
     // the next odd segment from the counter that no lane has flowed into (nlc: none left)
     auto pull = [&]() __attribute__((always_inline)) -> int {
@@ -864,32 +950,34 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
       }
     };
     const int j0 = 2 * t < nlc ? 2 * t : pull();
-    if (j0 < nlc) take(j0);
+    if (j0 < nlc) take(j0, xs + PSEG * j0);
     else j = nlc;
     parse_lanes(
         F, lazy, s0,
-        [&](uint32_t w, int p) __attribute__((always_inline)) {
-          DQ_CHK(ns < OWN_WORDS, CHK_Z_STAGE);
+        [&](int l, int d, int p) __attribute__((always_inline)) {
           if (p - s0 < PSEG) st |= 1u << (p - s0);
-          hist_add(L.hist, w, 1);
-          wb.put(ns++, w);
+          if (l) {
+            DQ_CHK(mb.n < OWN_CAP && p - pe < 512, CHK_Z_STAGE);
+            mb.put(mword(p - pe, l, d));
+            pe = p + l;
+          }
         },
         [&](int x) __attribute__((always_inline)) -> int {
           while (j < nlc && x >= s1) {  // segment j is parsed: publish it
-            wb.flush(ns);
-            L.seg_nsym[j] = (uint8_t)ns;
+            sw[SW_OWNM * NCH * MSEG + j] = mb.publish(dense, &L.misc[2]);
+            sw[SW_OWN * NCH * MSEG + j] = (uint32_t)x0 | (uint32_t)x << 16;
             L.seg_exit[j] = (uint32_t)x;
             L.sbits[j] = st;
             if (!(j & 1) && j + 1 < nlc && atomicCAS(&L.seg_mrg[j + 1], 0u, 1u) == 0u) {
-              take(j + 1);  // flow on into the odd segment after it, from x
-              continue;     // (x may lie past it too: then it is published empty)
+              take(j + 1, x);  // flow on into the odd segment after it, from x
+              continue;        // (x may lie past it too: then it is published empty)
             }
             const int q = pull();
             if (q >= nlc) {
               j = nlc;
               break;
             }
-            take(q);
+            take(q, xs + PSEG * q);
             return s0;
           }
           return j < nlc ? x : NX_STOP;
@@ -903,15 +991,14 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
   //      continues identically), skipping segments whose whole parse it overruns
   {
     int j = t < nlc ? t : nlc;
-    int u = 0, k = 0, nc = 0;
+    int u = 0, pm = 0, nc = 0, pe = 0;  // merge segment, merge position, symbols, last match end
     bool over = false;
-    WBuf wb{nullptr, 0, 0, 0, 0};
+    MBuf mb{pool, &L.misc[3], &L.misc[7], CONT_CAP, 0};
     // the merge test at E: NX_STOP (merged, the chunk's end, overflowed) or E (parse a step)
     auto check = [&](int E) __attribute__((always_inline)) -> int {
       for (;;) {
         if (E >= np) {  // the chunk's end
           u = MSEG;
-          k = 0;
           return NX_STOP;
         }
         if (u >= nlc) {  // no later segment holds symbols: parse on to the chunk end
@@ -927,13 +1014,9 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
           u++;
           continue;
         }
-        if (E == eu) {  // merged: segment u's continuation
-          k = L.seg_nsym[u];
-          return NX_STOP;
-        }
         const uint32_t ub = L.sbits[u];
-        if (E < su + PSEG && ((ub >> (E - su)) & 1)) {  // merged: segment u's symbols from k on
-          k = __popc(ub & ((1u << (E - su)) - 1));
+        if (E == eu || (E < su + PSEG && ((ub >> (E - su)) & 1))) {  // merged: u's symbols from E on
+          pm = E - su;
           return NX_STOP;
         }
         if (nc > fmerge) {  // (a step appends at most lazy + 1 <= 33 symbols: fmerge <= CONT - 40)
@@ -946,16 +1029,18 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
           while (E < pu && nc < CONT_WORDS) {
             int d = 0;
             const int l = F.find(E, min(MAXM, pu - E), &d, F.chain);
-            const uint32_t w = l ? match_word(l, d) : lit_word(L.in[E]);
-            hist_add(L.hist, w, 1);
-            wb.put(nc++, w);
+            nc++;
+            if (l) {
+              mb.put(mword(E - pe, l, d));
+              pe = E + l;
+            }
             E += l ? l : 1;
           }
           if (E != pu) {  // (a gap of literals longer than the staging: stored)
             over = true;
             return NX_STOP;
           }
-          k = pu == eu ? (int)L.seg_nsym[u] : __popc(ub & ((1u << (pu - su)) - 1));
+          pm = pu - su;
           return NX_STOP;
         }
         return E;
@@ -965,33 +1050,40 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
     // ended at once (its merge word written)
     auto start = [&]() __attribute__((always_inline)) -> int {
       u = j + 1;
-      k = 0;
+      pm = 0;
       nc = 0;
       over = false;
-      wb.base = segs_w + (int64_t)j * LANE_WORDS + OWN_WORDS;
-      return check((int)L.seg_exit[j]);
+      pe = (int)L.seg_exit[j];
+      mb.n = 0;
+      return check(pe);
+    };
+    auto finish = [&]() __attribute__((always_inline)) {
+      DQ_CHK(over || u == MSEG || pm < 512, CHK_Z_STAGE);
+      sw[SW_CONTM * NCH * MSEG + j] = mb.publish(dense, &L.misc[2]);
+      L.seg_mrg[j] = mrg_word(over ? MSEG : u, over || u == MSEG ? 0 : pm, over);
     };
     int x0 = NX_STOP;
     while (j < nlc) {  // the first segment with a step to parse
       x0 = start();
       if (x0 >= 0) break;
-      wb.flush(nc);
-      L.seg_mrg[j] = mrg_word(over ? MSEG : u, k, nc, over);
+      finish();
       j = PWG + atomicAdd(&L.misc[1], 1);
     }
     parse_lanes(
         F, lazy, x0 >= 0 ? x0 : 0,
-        [&](uint32_t w, int) __attribute__((always_inline)) {
-          DQ_CHK(nc < CONT_WORDS, CHK_Z_STAGE);
-          hist_add(L.hist, w, 1);
-          wb.put(nc++, w);
+        [&](int l, int d, int p) __attribute__((always_inline)) {
+          DQ_CHK(nc < CONT_WORDS && p - pe < 512, CHK_Z_STAGE);
+          nc++;
+          if (l) {
+            mb.put(mword(p - pe, l, d));
+            pe = p + l;
+          }
         },
         [&](int x) __attribute__((always_inline)) -> int {
           if (j >= nlc) return NX_STOP;
           int r = check(x);
           while (r < 0) {  // this continuation ended: the next unclaimed segment's
-            wb.flush(nc);
-            L.seg_mrg[j] = mrg_word(over ? MSEG : u, k, nc, over);
+            finish();
             j = PWG + atomicAdd(&L.misc[1], 1);
             if (j >= nlc) return NX_STOP;
             r = start();
@@ -1026,7 +1118,7 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
       if (t + q * PWG < nlc) jmp[t + q * PWG] = jj[q];
     __syncthreads();
   }
-  // the first symbol of each segment on the parse: set by the segment that merged into it
+  // the first position of each segment on the parse: set by the segment that merged into it
   bool rch[2];
   uint32_t mw[2];
 #pragma unroll
@@ -1036,29 +1128,42 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
     mw[q] = i < nlc ? L.seg_mrg[i] : 0u;
   }
   __syncthreads();
-  if (t == 0) jmp[0] = 0;
+  if (t == 0) jmp[0] = (uint32_t)xs;
 #pragma unroll
   for (int q = 0; q < 2; q++) {
-    if (rch[q] && mrg_lane(mw[q]) < MSEG) jmp[mrg_lane(mw[q])] = (uint32_t)mrg_sym(mw[q]);
+    const int g = mrg_lane(mw[q]);
+    if (rch[q] && g < MSEG) jmp[g] = (uint32_t)(xs + PSEG * g + mrg_off(mw[q]));
     if (rch[q] && mrg_over(mw[q])) L.misc[7] = 1;
   }
   __syncthreads();
-  // the segment words; the histograms counted every symbol parsed: those not on the chunk's parse
-  // (a reached segment's symbols before its first one, every symbol of a segment not reached) are
-  // taken off again -- a few per chunk
+  // each segment's range on the parse, and the histograms of the parse's symbols: its literals'
+  // bytes and its matches, walked as the code kernel walks them
 #pragma unroll
   for (int q = 0; q < 2; q++) {
     const int i = t + q * PWG;
     if (i >= MSEG) continue;
-    const int k0 = rch[q] ? (int)jmp[i] : 0;
-    const int ns = i < nlc ? (int)L.seg_nsym[i] : 0, nc = mrg_cont(mw[q]);
-    lm[i] = rch[q] ? (uint32_t)k0 | (uint32_t)ns << 8 | (uint32_t)nc << 16 | LM_REACHED : 0u;
-    if (i < nlc) {
-      const uint32_t* w = segs_w + (int64_t)i * LANE_WORDS;
-      const int ko = rch[q] ? k0 : ns, kc = rch[q] ? 0 : nc;
-      for (int k = 0; k < ko; k++) hist_add(L.hist, w[k], -1);
-      for (int k = 0; k < kc; k++) hist_add(L.hist, w[OWN_WORDS + k], -1);
+    if (!rch[q]) {
+      sw[SW_RANGE * NCH * MSEG + i] = SW_NONE;
+      continue;
     }
+    const int g = mrg_lane(mw[q]);
+    const int end = g < MSEG ? xs + PSEG * g + mrg_off(mw[q]) : np;
+    const uint32_t range = jmp[i] | (uint32_t)end << 16;
+    sw[SW_RANGE * NCH * MSEG + i] = range;
+    const uint32_t ow = sw[SW_OWN * NCH * MSEG + i], om = sw[SW_OWNM * NCH * MSEG + i],
+                   cm = sw[SW_CONTM * NCH * MSEG + i];
+    const uint32_t* own = part_words(dense, om);
+    const uint32_t* cont = part_words(dense, cm);
+    walk_segment(
+        L.in, range, ow, own, (int)((om >> 16) & 255), cont, (int)((cm >> 16) & 255),
+        [&](uint32_t by) __attribute__((always_inline)) { atomicAdd(&L.hist[CI_LL + by], 1); },
+        [&](int ml, int md) __attribute__((always_inline)) {
+          int sy, nx, xv;
+          len_code(ml, sy, nx, xv);
+          atomicAdd(&L.hist[CI_LL + sy], 1);
+          dist_code(md, sy, nx, xv);
+          atomicAdd(&L.hist[CI_D + sy], 1);
+        });
   }
   __syncthreads();
   for (int i = t; i < CI_CRC; i += PWG) ci[i] = L.hist[i];
@@ -1075,34 +1180,16 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
 }
 
 struct alignas(16) CLds {
-  uint8_t img[65536 + 16];  // the deflate image (<= 65510 bytes)
+  uint8_t src[BLK_U + 16];  // the block's bytes (the literals)
+  uint8_t img[65536];       // the deflate image (<= 65510 bytes)
   int32_t head[H_END];      // histograms and code tables (H_* offsets)
-  uint32_t wsum[16];
+  uint32_t wsum[3 * (CWG / 64)];
   int32_t misc[8];
 };
 
-// the words of lane word m's symbols on the block's parse: own from the first, then continuation
-template <class Fn>
-__device__ inline void for_each_sym(uint32_t m, const uint32_t* __restrict__ w, Fn f) {
-  if (!(m & LM_REACHED)) return;
-  const int k0 = (int)(m & 255), ns = (int)((m >> 8) & 255), nc = (int)((m >> 16) & 255);
-  // 16-byte loads (the own and continuation areas start 16-byte aligned)
-  for (int k = k0 & ~3; k < ns; k += 4) {
-    const uint4 v = *reinterpret_cast<const uint4*>(w + k);
-    if (k >= k0) f(v.x);
-    if (k + 1 >= k0 && k + 1 < ns) f(v.y);
-    if (k + 2 >= k0 && k + 2 < ns) f(v.z);
-    if (k + 3 < ns) f(v.w);
-  }
-  for (int k = 0; k < nc; k += 4) {
-    const uint4 v = *reinterpret_cast<const uint4*>(w + OWN_WORDS + k);
-    f(v.x);
-    if (k + 1 < nc) f(v.y);
-    if (k + 2 < nc) f(v.z);
-    if (k + 3 < nc) f(v.w);
-  }
-}
-static_assert(OWN_WORDS % 4 == 0 && LANE_WORDS % 4 == 0, "16-byte aligned stage areas");
+static_assert(OWN_CAP % 4 == 0 && CONT_CAP % 4 == 0 && CONT_CAP >= CONT_WORDS && STAGE_CH_WORDS % 4 == 0 &&
+                  DENSE_WORDS % 4 == 0 && POOL_WORDS <= 65536,
+              "16-byte aligned overflow areas");
 
 // Huffman codes of one block per 128-thread workgroup (7.9 KB of LDS, many per CU, so the
 // latency-bound serial parts -- the Moffat-Katajainen pass, the run-length coding -- of many blocks
@@ -1126,8 +1213,8 @@ __global__ __launch_bounds__(HWG) void bgzf_huff_kernel(int64_t n_in, int64_t bl
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int64_t base = (blk0 + b) * (int64_t)BLK_U;
   const int n = (int)min<int64_t>(BLK_U, n_in - base);
-  const int32_t* ci = reinterpret_cast<const int32_t*>(meta + b * META_WORDS + NCH * MSEG);
-  uint32_t* tb = meta + b * META_WORDS + NCH * (MSEG + CI_WORDS);
+  const int32_t* ci = reinterpret_cast<const int32_t*>(meta + b * META_WORDS + CI_OFF);
+  uint32_t* tb = meta + b * META_WORDS + TB_OFF;
   int32_t* H = L.head;
   for (int i = t; i < H_CL + 32; i += HWG) H[i] = 0;
   __syncthreads();
@@ -1242,10 +1329,10 @@ __global__ __launch_bounds__(CWG) void bgzf_code_kernel(const uint8_t* __restric
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int64_t base = (blk0 + b) * (int64_t)BLK_U;
   const int n = (int)min<int64_t>(BLK_U, n_in - base);
-  const uint32_t* lm = meta + b * META_WORDS;
+  const uint32_t* swb = meta + b * META_WORDS;
   int32_t* H = L.head;
   // the block's code tables from bgzf_huff_kernel
-  const uint32_t* tb = meta + b * META_WORDS + NCH * (MSEG + CI_WORDS);
+  const uint32_t* tb = meta + b * META_WORDS + TB_OFF;
   for (int i = t; i < 286; i += CWG) H[C_LL + i] = (int32_t)tb[TB_LL + i];
   for (int i = t; i < 30; i += CWG) H[C_D + i] = (int32_t)tb[TB_D + i];
   for (int i = t; i < 19; i += CWG) {
@@ -1254,38 +1341,62 @@ __global__ __launch_bounds__(CWG) void bgzf_code_kernel(const uint8_t* __restric
   }
   for (int i = t; i < TB_MISC - TB_TOK; i += CWG) H[H_TOK + i] = (int32_t)tb[TB_TOK + i];
   if (t < 8) L.misc[t] = (int32_t)tb[TB_MISC + t];
+  {  // the block's bytes (16-byte loads where aligned)
+    const uint8_t* sb = src + base;
+    const int h = min(n, (int)((16 - (reinterpret_cast<uintptr_t>(sb) & 15)) & 15));
+    for (int i = t; i < h; i += CWG) L.src[i] = sb[i];
+    const int nv = (n - h) / 16;
+    if (h == 0) {  // (the usual case: the stream 16-byte aligned)
+      for (int i = t; i < nv; i += CWG)
+        reinterpret_cast<uint4*>(L.src)[i] = *reinterpret_cast<const uint4*>(sb + 16 * i);
+    } else {
+      for (int i = t; i < nv; i += CWG) {
+        const uint4 v = *reinterpret_cast<const uint4*>(sb + h + 16 * i);
+        uint8_t* d = L.src + h + 16 * i;
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 16; k++) d[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+      }
+    }
+    for (int i = h + 16 * nv + t; i < n; i += CWG) L.src[i] = sb[i];
+  }
   __syncthreads();
   const bool over = L.misc[7] != 0;
   DTS();
   // ---- bits of this thread's eight segments under the dynamic and the fixed code
-  uint32_t lw[CSEG];
-  const uint32_t* wp[CSEG];
-#pragma unroll
-  for (int j = 0; j < CSEG; j++) {
-    const int g = CSEG * t + j, c = g / PL, u = g - c * PL;
-    lw[j] = g < NLANE ? lm[c * MSEG + u] : 0u;
-    wp[j] = stage + ((b * NCH + c) * MSEG + u) * (int64_t)LANE_WORDS;
-  }
+  // segment j of this thread's eight (the block's segment 8t + j) on the parse: walked with
+  // lit(byte) and mat(length, distance)
+  auto each_seg = [&](auto lit, auto mat) __attribute__((always_inline)) {
+    for (int j = 0; j < CSEG; j++) {
+      const int g = CSEG * t + j, c = g / PL, u = g - c * PL;
+      if (g >= NLANE) break;
+      const uint32_t* w = swb + c * MSEG + u;
+      const uint32_t rg = w[SW_RANGE * NCH * MSEG];
+      if (rg == SW_NONE) continue;
+      const uint32_t ow = w[SW_OWN * NCH * MSEG], om = w[SW_OWNM * NCH * MSEG], cm = w[SW_CONTM * NCH * MSEG];
+      const uint32_t* dense = stage + (b * NCH + c) * STAGE_CH_WORDS;
+      const uint8_t* cb = L.src + max(0, c * CH - XW);  // the chunk's position 0
+      walk_segment(cb, rg, ow, part_words(dense, om), (int)((om >> 16) & 255),
+                   part_words(dense, cm), (int)((cm >> 16) & 255), lit, mat);
+    }
+  };
   const bool has_eob = CSEG * t + CSEG - 1 == NLANE - 1;  // the block's last segment ends with EOB
   uint32_t vd = 0, vf = 0;
   {
     const uint32_t* cll = reinterpret_cast<const uint32_t*>(H + C_LL);
     const uint32_t* cd = reinterpret_cast<const uint32_t*>(H + C_D);
-#pragma unroll
-    for (int j = 0; j < CSEG; j++) {
-      for_each_sym(lw[j], wp[j], [&](uint32_t x) {
-        const int ll = (int)sym_ll(x);
-        int extra = 0;
-        if (ll > 256) {
-          const int d = (int)sym_d(x);
-          extra = lextra_bits(ll) + dextra_bits(d);
-          vd += cd[d] >> 16;
-          vf += 5;
-        }
-        vd += (cll[ll] >> 16) + extra;
-        vf += fixed_len_of(ll) + extra;
-      });
-    }
+    each_seg(
+        [&](uint32_t by) __attribute__((always_inline)) {
+          vd += cll[by] >> 16;
+          vf += by < 144 ? 8 : 9;
+        },
+        [&](int ml, int md) __attribute__((always_inline)) {
+          int sy, nx, xv, ds, dnx, dxv;
+          len_code(ml, sy, nx, xv);
+          dist_code(md, ds, dnx, dxv);
+          vd += (cll[sy] >> 16) + (cd[ds] >> 16) + (uint32_t)(nx + dnx);
+          vf += (uint32_t)(fixed_len_of(sy) + nx + 5 + dnx);
+        });
     if (has_eob) {
       vd += cll[256] >> 16;
       vf += 7;
@@ -1297,13 +1408,19 @@ __global__ __launch_bounds__(CWG) void bgzf_code_kernel(const uint8_t* __restric
     dsum += __shfl_xor(dsum, o, 64);
     fsum += __shfl_xor(fsum, o, 64);
   }
+  constexpr int NW = CWG / 64;
   if (lane == 0) {
     L.wsum[wv] = dsum;
-    L.wsum[4 + wv] = fsum;
+    L.wsum[NW + wv] = fsum;
   }
   __syncthreads();
-  dsum = L.wsum[0] + L.wsum[1] + L.wsum[2] + L.wsum[3];
-  fsum = L.wsum[4] + L.wsum[5] + L.wsum[6] + L.wsum[7];
+  dsum = 0;
+  fsum = 0;
+#pragma unroll
+  for (int w = 0; w < NW; w++) {
+    dsum += L.wsum[w];
+    fsum += L.wsum[NW + w];
+  }
   const bool dyn = (uint32_t)L.misc[6] + dsum < 3u + fsum;
   const uint32_t hdr_bits = dyn ? (uint32_t)L.misc[6] : 3u;
   const uint32_t sm = dyn ? vd : vf;
@@ -1312,11 +1429,14 @@ __global__ __launch_bounds__(CWG) void bgzf_code_kernel(const uint8_t* __restric
     const uint32_t y = __shfl_up(inc, d, 64);
     if (lane >= d) inc += y;
   }
-  if (lane == 63) L.wsum[8 + wv] = inc;
+  if (lane == 63) L.wsum[2 * NW + wv] = inc;
   __syncthreads();
-  uint32_t off = hdr_bits + inc - sm;
-  for (int w = 0; w < wv; w++) off += L.wsum[8 + w];
-  const uint32_t total_bits = hdr_bits + L.wsum[8] + L.wsum[9] + L.wsum[10] + L.wsum[11];
+  uint32_t off = hdr_bits + inc - sm, total_bits = hdr_bits;
+#pragma unroll
+  for (int w = 0; w < NW; w++) {
+    off += w < wv ? L.wsum[2 * NW + w] : 0u;
+    total_bits += L.wsum[2 * NW + w];
+  }
   DTS();
   if (!dyn) {  // the fixed code into the code tables
     uint32_t* cll = reinterpret_cast<uint32_t*>(H + C_LL);
@@ -1330,15 +1450,17 @@ __global__ __launch_bounds__(CWG) void bgzf_code_kernel(const uint8_t* __restric
     if (t < 30) cd[t] = rev((uint32_t)t, 5) | (5u << 16);
   }
   const int dbytes = (int)((total_bits + 7) / 8);
-  uint8_t* o = out_slots + b * 65536;
+  uint8_t* o = out_slots + b * (int64_t)SLOT;
   const uint32_t crc = (uint32_t)L.misc[1];
   // stored when the code is no shorter than the bytes themselves (and always when it would not fit)
   const bool stored = over || dbytes > min(MAX_DEFLATE, n + 5);
   int payload;
   if (!stored) {
-    // ---- the header, then every lane's symbols, OR-ed into the LDS image
+    // ---- the header, then every thread's segments, OR-ed into the LDS image; then the image
+    //      to the slot in 16-byte stores (the payload is 16-byte aligned there)
     uint32_t* img = reinterpret_cast<uint32_t*>(L.img);
-    for (int i = t; i < (int)(sizeof(L.img) / 4); i += CWG) img[i] = 0;
+    const int nw = (int)(total_bits >> 5) + 1;
+    for (int i = t; i < nw; i += CWG) img[i] = 0;
     __syncthreads();
     if (t == 0) {
       ImgOut io(img, 0);
@@ -1367,47 +1489,51 @@ __global__ __launch_bounds__(CWG) void bgzf_code_kernel(const uint8_t* __restric
       const uint32_t* cll = reinterpret_cast<const uint32_t*>(H + C_LL);
       const uint32_t* cd = reinterpret_cast<const uint32_t*>(H + C_D);
       ImgOut io(img, off);
-#pragma unroll
-      for (int j = 0; j < CSEG; j++) {
-        for_each_sym(lw[j], wp[j], [&](uint32_t x) {
-          const int ll = (int)sym_ll(x);
-          io.put(cll[ll] & 0xffff, (int)(cll[ll] >> 16));
-          if (ll > 256) {
-            const int lx = lextra_bits(ll);
-            if (lx) io.put(sym_lx(x), lx);
-            const int d = (int)sym_d(x);
-            io.put(cd[d] & 0xffff, (int)(cd[d] >> 16));
-            const int dx = dextra_bits(d);
-            if (dx) io.put(sym_dx(x), dx);
-          }
-        });
-      }
+      each_seg(
+          [&](uint32_t by) __attribute__((always_inline)) {
+            const uint32_t e = cll[by];
+            io.put(e & 0xffff, (int)(e >> 16));
+          },
+          [&](int ml, int md) __attribute__((always_inline)) {
+            int sy, nx, xv, ds, dnx, dxv;
+            len_code(ml, sy, nx, xv);
+            dist_code(md, ds, dnx, dxv);
+            io.put(cll[sy] & 0xffff, (int)(cll[sy] >> 16));
+            if (nx) io.put((uint32_t)xv, nx);
+            io.put(cd[ds] & 0xffff, (int)(cd[ds] >> 16));
+            if (dnx) io.put((uint32_t)dxv, dnx);
+          });
       if (has_eob) io.put(cll[256] & 0xffff, (int)(cll[256] >> 16));
       io.flush();
     }
     __syncthreads();
     DTS();
     payload = dbytes;
-    // o + 18 is 2 mod 16: bytes
-    for (int i = t; i < payload; i += CWG) o[18 + i] = L.img[i];
+    const uint4* si = reinterpret_cast<const uint4*>(L.img);
+    uint4* di = reinterpret_cast<uint4*>(o + SLOT_PAY);
+    for (int i = t; i < (payload + 15) / 16; i += CWG) di[i] = si[i];
+    __syncthreads();  // (the trailer over the last store's padding)
   } else {
     // stored block: BFINAL 1, BTYPE 00, LEN, NLEN, the bytes
     payload = n + 5;
+    uint8_t* pb = o + SLOT_PAY;
     if (t == 0) {
-      o[18] = 1;
-      o[19] = (uint8_t)n;
-      o[20] = (uint8_t)(n >> 8);
-      o[21] = (uint8_t)~n;
-      o[22] = (uint8_t)(~n >> 8);
+      pb[0] = 1;
+      pb[1] = (uint8_t)n;
+      pb[2] = (uint8_t)(n >> 8);
+      pb[3] = (uint8_t)~n;
+      pb[4] = (uint8_t)(~n >> 8);
     }
-    for (int i = t; i < n; i += CWG) o[23 + i] = src[base + i];
+    for (int i = t; i < n; i += CWG) pb[5 + i] = L.src[i];
   }
   if (t == 0) {
     const int bsize = 18 + payload + 8 - 1;
-    const uint8_t hdr[18] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 'B', 'C', 2, 0,
-                             (uint8_t)bsize, (uint8_t)(bsize >> 8)};
-    for (int i = 0; i < 18; i++) o[i] = hdr[i];
-    uint8_t* tr = o + 18 + payload;
+    uint8_t* hd = o + SLOT_HDR;
+    hd[0] = 0x1f; hd[1] = 0x8b; hd[2] = 8; hd[3] = 4;
+    hd[4] = 0; hd[5] = 0; hd[6] = 0; hd[7] = 0; hd[8] = 0; hd[9] = 0xff;
+    hd[10] = 6; hd[11] = 0; hd[12] = 'B'; hd[13] = 'C'; hd[14] = 2; hd[15] = 0;
+    hd[16] = (uint8_t)bsize; hd[17] = (uint8_t)(bsize >> 8);
+    uint8_t* tr = o + SLOT_PAY + payload;
     tr[0] = (uint8_t)crc; tr[1] = (uint8_t)(crc >> 8); tr[2] = (uint8_t)(crc >> 16); tr[3] = (uint8_t)(crc >> 24);
     tr[4] = (uint8_t)n; tr[5] = (uint8_t)(n >> 8); tr[6] = (uint8_t)(n >> 16); tr[7] = (uint8_t)(n >> 24);
     out_size[b] = bsize + 1;
@@ -1418,14 +1544,15 @@ __global__ __launch_bounds__(CWG) void bgzf_code_kernel(const uint8_t* __restric
 }
 #undef DTS
 
-// Packs the fixed-stride block slots into one contiguous BGZF stream: one workgroup per block.
+// Packs the block slots (the member from SLOT_HDR on) into one contiguous BGZF stream: one
+// workgroup per block.
 __global__ __launch_bounds__(256) void bgzf_pack_kernel(const uint8_t* __restrict__ slots,
                                                         const int32_t* __restrict__ size,
                                                         const int64_t* __restrict__ off, int64_t nblk,
                                                         uint8_t* __restrict__ out) {
   const int64_t b = blockIdx.x;
   if (b >= nblk) return;
-  const uint8_t* s = slots + b * 65536;
+  const uint8_t* s = slots + b * (int64_t)SLOT + SLOT_HDR;
   uint8_t* d = out + off[b];
   const int n = size[b];
   for (int i = threadIdx.x; i < n; i += 256) d[i] = s[i];
@@ -1471,8 +1598,9 @@ DefTables g_def[64];
 }  // namespace
 
 int64_t bgzf_block_count(int64_t n) { return n <= 0 ? 0 : (n + BLK_U - 1) / BLK_U; }
-size_t bgzf_stage_bytes(int64_t nblk) { return (size_t)nblk * NCH * MSEG * LANE_WORDS * 4; }
+size_t bgzf_stage_bytes(int64_t nblk) { return (size_t)nblk * NCH * STAGE_CH_WORDS * 4; }
 size_t bgzf_meta_bytes(int64_t nblk) { return (size_t)nblk * META_WORDS * 4; }
+size_t bgzf_slot_bytes(int64_t nblk) { return (size_t)nblk * SLOT; }
 
 bool deflate_tables(int device) {
   if (device < 0 || device >= 64) return false;

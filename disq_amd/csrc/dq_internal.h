@@ -327,8 +327,9 @@ uint64_t dq_chk_take_deflate();
 int64_t bgzf_block_count(int64_t n);
 size_t bgzf_stage_bytes(int64_t nblk);
 size_t bgzf_meta_bytes(int64_t nblk);
+size_t bgzf_slot_bytes(int64_t nblk);  // the blocks' output slots
 bool deflate_tables(int device);
-// Blocks [blk0, blk0 + nblk) of src[0, n_in) (65280 bytes each) into fixed 64 KiB slots: the
+// Blocks [blk0, blk0 + nblk) of src[0, n_in) (65280 bytes each) into fixed-size slots: the
 // chunk parse kernel, the Huffman kernel, then the code/emit kernel.  tim (DQ_DEFLATE_TIMING): 8
 // words per parse workgroup (2 per block), then 8 per block for each of the other two kernels.
 void launch_bgzf_deflate(const uint8_t* src, int64_t n_in, int64_t blk0, int64_t nblk,

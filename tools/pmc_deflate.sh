@@ -25,9 +25,11 @@ for f in glob.glob(out + "/p*/**/*counter_collection.csv", recursive=True):
 for k in sorted(agg): print(f"{k[0]:6s} {k[1]:28s} {agg[k]:.4g}  (dispatch-rows {nd[k]})")
 # HBM traffic per input byte (MI355X_MICROARCH.md: FETCH_SIZE x 2 on gfx950; both in KiB)
 import json, re
-gb = None
+gb = zgb = None
 for line in open(out + "/p1.log"):
-    if line.startswith("{") and '"input_gb"' in line: gb = json.loads(line)["input_gb"]
+    if line.startswith("{") and '"input_gb"' in line:
+        j = json.loads(line)
+        gb, zgb = j["input_gb"], j["compressed_gb"]
 if gb:
     tot = 0.0
     for kn in ("parse", "huff", "code"):
@@ -36,4 +38,5 @@ if gb:
         tot += f + w
         print(f"traffic {kn:6s} fetch {f / 1e9:.3f} GB  write {w / 1e9:.3f} GB  ({(f + w) / (gb * 1e9):.2f}x input)")
     print(f"traffic total {tot / 1e9:.3f} GB over {gb} GB of input (one rep): {tot / (gb * 1e9):.2f}x")
+    print(f"algorithmic bytes (input read + output written) {gb + zgb:.3f} GB: traffic {tot / ((gb + zgb) * 1e9):.2f}x")
 PY
