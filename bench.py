@@ -67,6 +67,9 @@ def parse():
     ap.add_argument("--intervals", type=int, default=10000,
                     help="BED-like intervals for the N = 1 interval-filter measurement (0 = skip)")
     ap.add_argument("--e2e", type=int, default=1, help="N = 1 end-to-end measurement (0 = skip)")
+    ap.add_argument("--write-records", type=int, default=2000000,
+                    help="N = 1 write-path (SURVEY.md section 8 row f3) measurement: records of the "
+                         "WGS stream compressed on the GPU (0 = skip)")
     ap.add_argument("--gen-budget-s", type=float, default=150.0,
                     help="N > 1: generation seconds per rank before the ranks tile a chunk pool")
     ap.add_argument("--e2e-window-gb", type=float, default=2.0,
@@ -310,8 +313,10 @@ def main():
         traffic = tj.get("traffic_bytes_per_launch")
         traffic_src = f"profiles/{TRAFFIC_PROFILE} (FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction)"
 
-    interval_mode = e2e = cpu = parity = None
+    interval_mode = e2e = cpu = parity = wpath = None
     if world == 1:
+        if args.write_records > 0:
+            wpath = write_path_bench(args)
         if bai is not None:
             interval_mode = interval_bench(ctx, rs, shard, file_len, header, bai, args, cpu_data,
                                            ncores)
@@ -382,6 +387,7 @@ def main():
                                   tiled=bool(gen_desc.get("tiled_chunks"))),
                 "interval_mode": interval_mode,
                 "end_to_end": e2e,
+                "write_path": wpath,
                 "parity": parity,
                 # whole-pipeline algorithmic bytes C + 2U + 60R (unfused
                 # record walk) over the step time, against the spec and the measured HBM peaks
@@ -678,6 +684,40 @@ def cpu_baseline(data, ctx, rs, shard, file_len, header, args, ncores):
                   f"({', '.join(f'{r:.2f}' for r in runs)} s; {cnt.sum() / el:.0f} reads/s)",
     }
     return cpu, parity
+
+
+def write_path_bench(args):
+    """Row f3: the decompressed stream of a synthetic WGS BAM, resident in
+    HBM, compressed into htsjdk's 65280-byte BGZF blocks by the GPU (dq_bgzf_compress_resident,
+    HIP events around the deflate kernels); the output re-inflated by the GPU read path must give
+    the stream back (digest).  The same measurement as tools/deflate_bench.py."""
+    import hashlib
+    from disq_amd import _lib, synth
+    r = synth.generate(args.write_records, seed=1, nthreads=max(1, min(16, usable_cores()[2])))
+    eof = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+    with _lib.Context(verify_crc=True) as c:
+        c.open_bytes(r.bam)
+        c.run_resident()
+        u = c.inflated()
+        runs = [c.bgzf_compress_resident() for _ in range(4)]  # a warm-up and 3 timed
+        n = runs[-1][0]
+        z = c.bgzf_fetch(n).tobytes()
+    ms = sorted(x[1] for x in runs[1:])[1]
+    with _lib.Context(verify_crc=True) as c:
+        c.text_open_bytes(z + eof)
+        c.text_run(False)
+        back = c.inflated()
+    ok = hashlib.sha256(u.tobytes()).digest() == hashlib.sha256(back.tobytes()).digest()
+    out = {"workload": f"decompressed stream of {args.write_records} synthetic WGS records",
+           "input_gb": round(len(u) / 1e9, 4), "compressed_gb": round(n / 1e9, 4),
+           "ratio": round(len(u) / n, 3), "device_ms_median": round(ms, 3),
+           "input_gbs": round(len(u) / ms / 1e6, 2),
+           "htsjdk_level5_ratio": round(len(u) / len(r.bam), 3),
+           "roundtrip_gpu_inflate": "match" if ok else "MISMATCH",
+           "evidence": "profiles/r4au_deflate_dense_stage.txt, profiles/r4au_deflate_pmc.txt "
+                       "(traffic 3.9x the input read + output written)"}
+    log("write path:", out)
+    return out
 
 
 def end_to_end(data, args, resident_digest=None, header=None):

@@ -375,6 +375,7 @@ __device__ inline int mw_dist(uint32_t w) { return (int)(w >> 17) + 1; }
 
 
 constexpr int SCAT_WAVES = 4;  // waves of the bucket scatter: one position range each
+constexpr int CRC_BYTES = CH / (PWG - 64 * SCAT_WAVES) + 1;  // per thread of the other waves (the CRC)
 struct alignas(16) PLds {
   uint8_t in[NPMAX + 16];     // bytes [r0, ce) of the block (+ zero pad for the 4/8-byte compares)
   uint16_t bl[NPMAX];         // positions grouped by hash bucket, ascending inside a bucket
@@ -382,7 +383,6 @@ struct alignas(16) PLds {
                               // chunk's histograms
   union {
     struct {
-      uint32_t crc_t[256];
       uint32_t seg_exit[MSEG];  // the parse's exit of each segment; later jump pointers, first symbols
       uint32_t seg_mrg[MSEG];   // continuation: merge segment | symbol << 11 | count << 18 | over << 26
       uint8_t seg_mark[MSEG];   // on the chunk's parse
@@ -806,7 +806,8 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
   for (int i = t; i < (1 << HBITS); i += PWG) L.head[i] = 0;
   for (int i = t; i < (SCAT_WAVES - 1) << (HBITS - 1); i += PWG) (&L.cnt[0][0])[i] = 0;
   if (t < 8) L.misc[t] = 0;
-  for (int i = t; i < CI_CRC; i += PWG) L.hist[i] = 0;
+  // (the histogram words hold the CRC table until the bucket lists are built)
+  for (int i = t; i < CI_CRC; i += PWG) L.hist[i] = i < 256 ? (int32_t)c_dcrc[i] : 0;
   {
     const uint8_t* s = src + base + r0;
     const int head = (int)((16 - (reinterpret_cast<uintptr_t>(s) & 15)) & 15);
@@ -898,24 +899,25 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
         L.bl[rank] = (uint16_t)x;
       }
     }
+  } else {
+    // meanwhile the other waves: CRC32 of CRC_BYTES bytes per thread (raw register, init 0),
+    // moved to the chunk end, XOR-ed
+    const uint32_t* crc_t = reinterpret_cast<const uint32_t*>(L.hist);
+    const int c0 = min(np, xs + CRC_BYTES * (t - 64 * SCAT_WAVES)), c1 = min(np, c0 + CRC_BYTES);
+    uint32_t cr = 0;
+    for (int i = c0; i < c1; i++) cr = crc_t[(cr ^ L.in[i]) & 0xff] ^ (cr >> 8);
+    if (c1 > c0) cr = gf2_mul(x8n((uint32_t)(np - c1)), cr);
+    for (int o = 32; o >= 1; o >>= 1) cr ^= __shfl_xor(cr, o, 64);
+    if (lane == 0) L.wred[8 + wv - SCAT_WAVES] = cr;
   }
   __syncthreads();
   {  // bucket ends: the last range's cursors
     const uint16_t* const c16 = reinterpret_cast<const uint16_t*>(&L.cnt[SCAT_WAVES - 2][0]);
     for (int h = t; h < (1 << HBITS); h += PWG) L.head[h] = c16[h];
   }
-  for (int i = t; i < 256; i += PWG) L.crc_t[i] = c_dcrc[i];  // (over the dead counts)
+  for (int i = t; i < CI_CRC; i += PWG) L.hist[i] = 0;  // (the CRC table is dead)
   __syncthreads();
   DTS();
-  // ---- CRC32 of 64 bytes per thread (raw register, init 0), moved to the chunk end, XOR-ed
-  {
-    const int c0 = min(np, xs + 64 * t), c1 = min(np, c0 + 64);
-    uint32_t cr = 0;
-    for (int i = c0; i < c1; i++) cr = L.crc_t[(cr ^ L.in[i]) & 0xff] ^ (cr >> 8);
-    if (c1 > c0) cr = gf2_mul(x8n((uint32_t)(np - c1)), cr);
-    for (int o = 32; o >= 1; o >>= 1) cr ^= __shfl_xor(cr, o, 64);
-    if (lane == 0) L.wred[8 + wv] = cr;
-  }
   // ---- speculative parses: segment j (32 bytes) from its start to the first symbol boundary at
   //      or past its end (a match may run on past it).  Thread t starts on segment 2t; a lane that
   //      ends an even segment claims the odd one after it and parses straight on into it (from
@@ -1169,7 +1171,7 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
   for (int i = t; i < CI_CRC; i += PWG) ci[i] = L.hist[i];
   if (t == 0) {
     uint32_t cr = 0;
-    for (int w = 0; w < PWG / 64; w++) cr ^= L.wred[8 + w];
+    for (int w = 0; w < PWG / 64 - SCAT_WAVES; w++) cr ^= L.wred[8 + w];
     ci[CI_CRC] = (int32_t)cr;
     ci[CI_OVER] = L.misc[7];
     ci[CI_BYTES] = ce - cs;
@@ -1227,20 +1229,24 @@ __global__ __launch_bounds__(HWG) void bgzf_huff_kernel(int64_t n_in, int64_t bl
   __syncthreads();
   if (t == 0) {
     H[H_LL + 256] += 1;  // end of block
-    int over = 0;
-    uint32_t cr = 0;
-    for (int c = 0; c < NCH; c++) {  // raw(A B) = raw(A) x^(8 |B|) + raw(B)
-      over |= ci[c * CI_WORDS + CI_OVER];
-      cr = gf2_mul(x8n((uint32_t)ci[c * CI_WORDS + CI_BYTES]), cr) ^ (uint32_t)ci[c * CI_WORDS + CI_CRC];
-    }
-    L.misc[1] = (int32_t)(cr ^ gf2_mul(x8n((uint32_t)n), 0xffffffffu) ^ 0xffffffffu);
-    L.misc[7] = over;
   }
   __syncthreads();
   DTS();
   // ---- dynamic Huffman codes: wave 0 the literal/length alphabet, wave 1 the distances
   if (wv == 0) build_lengths(H + H_LL, 286, 15, H + H_SORT, H + H_W, H + H_LEN, H + H_CNT, lane);
-  if (wv == 1) build_lengths(H + H_D, 30, 15, H + H_SORT_D, H + H_W_D, H + H_LEN_D, H + H_CNT_D, lane);
+  if (wv == 1) {
+    build_lengths(H + H_D, 30, 15, H + H_SORT_D, H + H_W_D, H + H_LEN_D, H + H_CNT_D, lane);
+    if (lane == 0) {  // the member's CRC (while wave 0 builds the longer code)
+      int over = 0;
+      uint32_t cr = 0;
+      for (int c = 0; c < NCH; c++) {  // raw(A B) = raw(A) x^(8 |B|) + raw(B)
+        over |= ci[c * CI_WORDS + CI_OVER];
+        cr = gf2_mul(x8n((uint32_t)ci[c * CI_WORDS + CI_BYTES]), cr) ^ (uint32_t)ci[c * CI_WORDS + CI_CRC];
+      }
+      L.misc[1] = (int32_t)(cr ^ gf2_mul(x8n((uint32_t)n), 0xffffffffu) ^ 0xffffffffu);
+      L.misc[7] = over;
+    }
+  }
   __syncthreads();
   DTS();
   // codes by waves 0 and 1; wave 1's first lane then run-length codes the code lengths
