@@ -591,12 +591,13 @@ struct Finder {
 // end at the chunk end np.  emit(length, distance, position) takes a symbol (length 0: the
 // literal at position); between steps next(x) says what the lane does after a step that ended at
 // x (or first, at its start): the position of its next step, NX_WAIT (ask again in the next pass)
-// or NX_STOP.
+// or NX_STOP.  `lazy` and the end `n` a step's matches stop at are read at every step (next() may
+// change them: a forced merge's greedy steps up to a boundary).
 enum { NX_WAIT = -1, NX_STOP = -2 };
 template <class Emit, class Next>
-__device__ __attribute__((always_inline)) inline void parse_lanes(const Finder& F, int lazy, int x0,
-                                                                  Emit emit, Next next) {
-  const int n = F.np;
+__device__ __attribute__((always_inline)) inline void parse_lanes(const Finder& F, const int& lazy,
+                                                                  const int& n, int x0, Emit emit,
+                                                                  Next next) {
   Finder::Search S;
   int x = x0, l = 0, d = 0;
   bool lz = false;    // the current search is the look-ahead at x + 1
@@ -954,8 +955,9 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
     const int j0 = 2 * t < nlc ? 2 * t : pull();
     if (j0 < nlc) take(j0, xs + PSEG * j0);
     else j = nlc;
+    const int own_lazy = lazy, own_end = np;
     parse_lanes(
-        F, lazy, s0,
+        F, own_lazy, own_end, s0,
         [&](int l, int d, int p) __attribute__((always_inline)) {
           if (p - s0 < PSEG) st |= 1u << (p - s0);
           if (l) {
@@ -994,10 +996,23 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
   {
     int j = t < nlc ? t : nlc;
     int u = 0, pm = 0, nc = 0, pe = 0;  // merge segment, merge position, symbols, last match end
+    int fpu = -1, c_lazy = lazy, c_end = np;  // forced merge: the boundary its greedy steps end on
     bool over = false;
     MBuf mb{pool, &L.misc[3], &L.misc[7], CONT_CAP, 0};
     // the merge test at E: NX_STOP (merged, the chunk's end, overflowed) or E (parse a step)
     auto check = [&](int E) __attribute__((always_inline)) -> int {
+      if (fpu >= 0) {  // a forced merge's greedy steps, cut to end exactly on fpu
+        DQ_CHK(E <= fpu, CHK_Z_STAGE);
+        if (E >= fpu) {
+          pm = fpu - (xs + PSEG * u);
+          return NX_STOP;
+        }
+        if (nc >= CONT_WORDS) {  // (a gap of literals longer than the staging: stored)
+          over = true;
+          return NX_STOP;
+        }
+        return E;
+      }
       for (;;) {
         if (E >= np) {  // the chunk's end
           u = MSEG;
@@ -1027,23 +1042,10 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
           // pu > E, with matches cut to fit and literals for the last < 3 bytes -- a valid parse
           // that merges
           const uint32_t after = E - su + 1 < PSEG ? ub >> (E - su + 1) : 0u;
-          const int pu = E < su + PSEG && after ? E + 1 + (int)__builtin_ctz(after) : eu;
-          while (E < pu && nc < CONT_WORDS) {
-            int d = 0;
-            const int l = F.find(E, min(MAXM, pu - E), &d, F.chain);
-            nc++;
-            if (l) {
-              mb.put(mword(E - pe, l, d));
-              pe = E + l;
-            }
-            E += l ? l : 1;
-          }
-          if (E != pu) {  // (a gap of literals longer than the staging: stored)
-            over = true;
-            return NX_STOP;
-          }
-          pm = pu - su;
-          return NX_STOP;
+          fpu = E < su + PSEG && after ? E + 1 + (int)__builtin_ctz(after) : eu;  // > E
+          c_end = fpu;  // greedy steps (no lazy look-ahead) with matches cut to end on fpu
+          c_lazy = 0;
+          return E;
         }
         return E;
       }
@@ -1057,6 +1059,9 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
       over = false;
       pe = (int)L.seg_exit[j];
       mb.n = 0;
+      fpu = -1;
+      c_lazy = lazy;
+      c_end = np;
       return check(pe);
     };
     auto finish = [&]() __attribute__((always_inline)) {
@@ -1072,7 +1077,7 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
       j = PWG + atomicAdd(&L.misc[1], 1);
     }
     parse_lanes(
-        F, lazy, x0 >= 0 ? x0 : 0,
+        F, c_lazy, c_end, x0 >= 0 ? x0 : 0,
         [&](int l, int d, int p) __attribute__((always_inline)) {
           DQ_CHK(nc < CONT_WORDS && p - pe < 512, CHK_Z_STAGE);
           nc++;
