@@ -80,7 +80,11 @@ constexpr int WIN = 32768;               // DEFLATE window
 // area at an offset taken from an LDS counter when the part ends; a part with more goes whole to
 // the chunk's overflow pool (OWN_CAP or CONT_CAP words taken from another counter when its ninth
 // match comes; a pathological chunk that exhausts the pool has its block stored).
-constexpr int MB_INL = 8;
+#ifndef DQ_MB_INL
+#define DQ_MB_INL 8  // (<= 8; a build with fewer spills to the pool more often)
+#endif
+constexpr int MB_INL = DQ_MB_INL;
+static_assert(MB_INL >= 1 && MB_INL <= 8, "register-held matches");
 constexpr int CONT_WORDS = 156;          // continuation symbols at most
 constexpr int OWN_CAP = 16;              // own matches (a 32-byte segment's, + one past its end)
 constexpr int CONT_CAP = 160;            // continuation matches (<= CONT_WORDS)
