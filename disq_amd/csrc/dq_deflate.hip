@@ -89,6 +89,10 @@ constexpr int CONT_WORDS = 156;          // continuation symbols at most
 constexpr int OWN_CAP = 16;              // own matches (a 32-byte segment's, + one past its end)
 constexpr int CONT_CAP = 160;            // continuation matches (<= CONT_WORDS)
 constexpr int DENSE_WORDS = 2 * MSEG * MB_INL;  // per chunk
+#ifndef DQ_DEFLATE_STEAL
+#define DQ_DEFLATE_STEAL 1  // idle lanes take odd segments nobody flowed into yet (6 % faster; 0: the
+                            // output is the same on every run, profiles/r4bg_deflate_steal_ab.txt)
+#endif
 #ifndef DQ_POOL_WORDS
 #define DQ_POOL_WORDS 32768  // (a build with a small pool exercises the exhaustion path)
 #endif
@@ -950,11 +954,15 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
     };
     // the next odd segment from the counter that no lane has flowed into (nlc: none left)
     auto pull = [&]() __attribute__((always_inline)) -> int {
+#if DQ_DEFLATE_STEAL
       for (;;) {
         const int q = 2 * atomicAdd(&L.misc[0], 1) + 1;
         if (q >= nlc) return nlc;
         if (atomicCAS(&L.seg_mrg[q], 0u, 1u) == 0u) return q;
       }
+#else
+      return nlc;
+#endif
     };
     const int j0 = 2 * t < nlc ? 2 * t : pull();
     if (j0 < nlc) take(j0, xs + PSEG * j0);
