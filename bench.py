@@ -714,7 +714,7 @@ def write_path_bench(args):
            "input_gbs": round(len(u) / ms / 1e6, 2),
            "htsjdk_level5_ratio": round(len(u) / len(r.bam), 3),
            "roundtrip_gpu_inflate": "match" if ok else "MISMATCH",
-           "evidence": "profiles/r4az_deflate_rocprof.txt, profiles/r4az_deflate_pmc.txt "
+           "evidence": "profiles/r4bd_deflate_forced_steps_ab.txt, profiles/r4az_deflate_pmc.txt "
                        "(traffic 3.9x the input read + output written)"}
     log("write path:", out)
     return out
