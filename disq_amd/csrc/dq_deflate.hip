@@ -335,18 +335,22 @@ __device__ inline uint64_t ld8(const uint8_t* in, int x) {
 
 __device__ inline int fixed_len_of(int s) { return s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8; }
 
-struct ImgOut {  // LSB-first bits OR-ed into the LDS image from bit position p on
+// LSB-first bits into the LDS image from bit position p on: the first word (when p is inside it)
+// and the last are shared with the neighbouring bit ranges and OR-ed; the words between are stored
+struct ImgOut {
   uint32_t* img;
   uint64_t acc;
   int n;
-  uint32_t w;
-  __device__ ImgOut(uint32_t* im, uint32_t p) : img(im), acc(0), n((int)(p & 31)), w(p >> 5) {}
+  uint32_t w, w0;
+  __device__ ImgOut(uint32_t* im, uint32_t p)
+      : img(im), acc(0), n((int)(p & 31)), w(p >> 5), w0((p & 31) ? p >> 5 : ~0u) {}
   __device__ void put(uint32_t v, int len) {
     acc |= (uint64_t)v << n;
     n += len;
     if (n >= 32) {
       DQ_CHK(w < 65536 / 4, CHK_Z_IMAGE);
-      atomicOr(&img[w], (uint32_t)acc);
+      if (w == w0) atomicOr(&img[w], (uint32_t)acc);
+      else img[w] = (uint32_t)acc;
       w++;
       acc >>= 32;
       n -= 32;
