@@ -5,8 +5,11 @@ the merges -- checking that the chunks' effective symbols rebuild the block exac
 
   python tools/deflate_parse_emu.py [--blocks 20] [--seed 1]
 
-Sizes are scaled down (chunk 2040 bytes, 8-byte lanes, 1024 bytes of reach) so the logic paths
-(many lanes, merges, overruns, forced merges) run in seconds; the kernel's are 32640 / 64 / 15000.
+Sizes are scaled down (chunk 2040 bytes, 8-byte segments, 1024 bytes of reach) so the logic paths
+(many segments, merges, overruns, forced merges) run in seconds; the kernel's are 32640 / 32 /
+13600.  It models the merge rule (segments' own parses, continuations until a later segment's
+symbol boundary, forced merges, pointer jumping); the kernel's staging (matches only, with literal
+gaps; dense per-chunk areas) and its run-time segment claims are not modelled.
 """
 import argparse
 import random
