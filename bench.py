@@ -439,7 +439,7 @@ def shard_parity(rs, shard, offsets, rank, file_len, header, split_size, ctx, di
     import torch
     from oracle import oracle as O
     t0 = time.perf_counter()
-    ok, nparts, nrec, short = 1, 0, 0, 0
+    ok, nparts, nrec, short, failed = 1, 0, 0, 0, 0
     if not shard.empty:
         # in groups of about 1 GB of partitions, so a rank's host copy stays small (8 ranks x a
         # 12.5 GB shard at once would be 100 GB of host memory); each group's window runs from its
@@ -475,9 +475,14 @@ def shard_parity(rs, shard, offsets, rank, file_len, header, split_size, ctx, di
             ocnt, odig = np.concatenate(ocnt), np.concatenate(odig)
             ok = int(np.array_equal(gcnt, ocnt) and np.array_equal(gdig, odig))
             nparts, nrec = len(ocnt), int(ocnt.sum())
-        except O.OracleError:
-            ok, short = 0, 1
-    row = torch.tensor([ok, nparts, nrec, short, int(1e3 * (time.perf_counter() - t0))],
+        except Exception as e:  # every rank must still reach the all_gather below
+            ok = 0
+            if isinstance(e, O.OracleError) and "short" in str(e):
+                short = 1
+            else:
+                failed = 1
+                print(f"[bench] rank {rank}: shard parity failed: {e!r}", file=sys.stderr, flush=True)
+    row = torch.tensor([ok, nparts, nrec, short, int(1e3 * (time.perf_counter() - t0)), failed],
                        dtype=torch.int64, device=cdev)
     if dist is not None:
         rows = [torch.zeros_like(row) for _ in range(world)]
@@ -489,6 +494,7 @@ def shard_parity(rs, shard, offsets, rank, file_len, header, split_size, ctx, di
             "ranks_matching": int(every[:, 0].sum()), "ranks": int(len(every)),
             "partitions_checked": int(every[:, 1].sum()), "records_checked": int(every[:, 2].sum()),
             "ranks_window_too_short": int(every[:, 3].sum()),
+            "ranks_failed": int(every[:, 5].sum()),
             "oracle_s_max_over_ranks": round(float(every[:, 4].max()) / 1e3, 1),
             "oracle_threads_per_rank": threads,
             "checked": "per rank, untimed: the oracle over the rank's resident + RCCL-received "

@@ -54,7 +54,7 @@ class DqBatch(C.Structure):
                 ("n_partitions", C.c_int64),
                 ("part_offset", C.POINTER(C.c_int64)),
                 ("part_digest", C.POINTER(C.c_uint64)),
-                ("in_arena", C.c_int32), ("reserved", C.c_int32)]
+                ("in_arena", C.c_int32), ("reserved", C.c_int32), ("arena_hold", C.c_void_p)]
 
 
 class DqTextBatch(C.Structure):
@@ -204,24 +204,17 @@ FIELDS = (("voffset", np.uint64), ("block_size", np.int32), ("ref_id", np.int32)
 
 class _BatchOwner:
     """Frees a dq_batch once no numpy view of its arrays is left.  An arena batch's arrays live in
-    its context's pinned export arena (dq_set_export_arena): a context closed while such a batch is
-    still referenced hands its handle over (ctx_h), and the arena is freed with the last view."""
+    its context's pinned export arena (dq_set_export_arena); the C ABI keeps that arena alive for
+    the batch even past dq_ctx_destroy and releases it in dq_batch_free."""
 
     def __init__(self, bp):
         self.bp = bp
-        self.ctx_h = None
 
     def __del__(self):
         try:
             lib().dq_batch_free(self.bp)
         except Exception:
             pass
-        if self.ctx_h:
-            try:
-                lib().dq_ctx_destroy(self.ctx_h)
-            except Exception:
-                pass
-            self.ctx_h = None
 
 
 _CT = {np.uint64: C.c_uint64, np.int64: C.c_int64, np.int32: C.c_int32, np.uint16: C.c_uint16,
@@ -281,20 +274,17 @@ class Context:
         return r() if r is not None else None
 
     def _arena_guard(self, what):
-        """The library writes every batch of an arena context into the same pinned memory: refuse
-        a new batch (or a new arena) while the previous arena batch is still referenced."""
+        """The library writes every batch of an arena context into the same pinned memory and
+        refuses (DQ_EINVAL) a new one while the previous arena batch is alive; this raises the same
+        refusal before any device work."""
         if self._arena_live() is not None:
             raise DqError(DQ_EINVAL, f"{what}: the previous batch of this context lives in its "
                           "export arena and is still referenced; drop it (or copy its arrays) "
                           "before the next batch")
 
     def close(self):
-        if self._h:
-            owner = self._arena_live()
-            if owner is not None:  # views of the arena are alive: it goes with the last of them
-                owner.ctx_h = self._h
-            else:
-                lib().dq_ctx_destroy(self._h)
+        if self._h:  # (a live arena batch keeps its arena: dq_ctx_destroy leaves it to the batch)
+            lib().dq_ctx_destroy(self._h)
             self._h = None
 
     def __enter__(self):

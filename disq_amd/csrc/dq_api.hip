@@ -20,6 +20,7 @@
 #include <string>
 #include <thread>
 #include <sys/mman.h>
+#include <mutex>
 #include <vector>
 
 #include "../../include/disq_gpu.h"
@@ -53,6 +54,17 @@ struct DevBuf {
 
 struct Interval {
   int32_t ref, start, end;
+};
+
+// The export arena's ownership, shared by the context and the batch exported into it (a JNI
+// caller frees batches from its own threads, AutocloseIteratorWrapper.java:26-36 style): while a
+// batch lives, the context may not export another batch there (DQ_EINVAL), resize it, or free it
+// -- dq_ctx_destroy leaves the arena to the batch, whose dq_batch_free releases it.
+struct ArenaHold {
+  std::mutex mu;
+  uint8_t* arena = nullptr;
+  bool live = false;    // a batch's arrays are in the arena
+  bool orphan = false;  // the context was destroyed first: the batch frees the arena
 };
 
 // A .bai (SAMv1 section 5.2) as htsjdk's index reads it: per reference its bins' chunks (the
@@ -120,8 +132,9 @@ struct dq_ctx {
   uint8_t* pin[2] = {nullptr, nullptr};
   size_t pin_cap = 0;
   hipEvent_t pin_ev[2] = {nullptr, nullptr};
-  // dq_set_export_arena: batches land in this pinned arena (DMA, no staging copies), valid until
-  // the next batch of the context
+  // dq_set_export_arena: batches land in this pinned arena (DMA, no staging copies); it holds one
+  // batch at a time, owned by the batch until dq_batch_free (ArenaHold)
+  ArenaHold* ah = nullptr;
   uint8_t* arena = nullptr;
   size_t arena_cap = 0;
   DevBuf x_bs4, x_boff, x_voff, x_parts;  // batch export: raw offsets, voffsets, digests
@@ -1368,6 +1381,10 @@ static int make_batch(dq_ctx* ctx, const std::vector<std::pair<int64_t, int64_t>
   b->n_records = n;
   int rc = 0;
   auto fail = [&](int code) {
+    // copies queued on the second export stream may still write into the batch's arrays (the
+    // arena): let them land before the arrays are given up
+    if (ctx->sx) (void)hipStreamSynchronize(ctx->sx);
+    (void)hipStreamSynchronize(s);
     dq_batch_free(b);
     return code;
   };
@@ -1466,6 +1483,16 @@ static int make_batch(dq_ctx* ctx, const std::vector<std::pair<int64_t, int64_t>
                            8 * ((2 * m + 7) / 8) * 3 + 8 * ((m + 7) / 8) * 2;
   const size_t want = soa_bytes + (with_raw ? (size_t)std::max<int64_t>(1, raw_len) : 0) + 64 * 20;
   const bool in_arena = ctx->arena && want <= ctx->arena_cap;
+  if (in_arena) {
+    std::lock_guard<std::mutex> lk(ctx->ah->mu);
+    if (ctx->ah->live) {
+      ctx->err = "the export arena still holds a batch: dq_batch_free it before the next batch";
+      free(b);
+      return DQ_EINVAL;
+    }
+    ctx->ah->live = true;  // released by dq_batch_free (also on the failure paths below)
+    b->arena_hold = ctx->ah;
+  }
   size_t used = 0;
   auto halloc = [&](size_t bytes) -> void* {
     if (!in_arena) return host_alloc(bytes);
@@ -2287,15 +2314,29 @@ int dq_ctx_create(dq_ctx** out, const dq_opts* opts) {
 void dq_ctx_destroy(dq_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->o.device);
+  // both streams drained before any pinned buffer they copy into is released
   if (ctx->s) (void)hipStreamSynchronize(ctx->s);
+  if (ctx->sx) (void)hipStreamSynchronize(ctx->sx);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   for (int k = 0; k < 2; k++) {
     if (ctx->pin_ev[k]) (void)hipEventDestroy(ctx->pin_ev[k]);
     if (ctx->pin[k]) (void)hipHostFree(ctx->pin[k]);
   }
-  if (ctx->arena) (void)hipHostFree(ctx->arena);
-  if (ctx->sx) (void)hipStreamSynchronize(ctx->sx);
+  if (ctx->ah) {  // a live arena batch keeps the arena: its dq_batch_free releases it
+    bool keep;
+    {
+      std::lock_guard<std::mutex> lk(ctx->ah->mu);
+      keep = ctx->ah->live;
+      ctx->ah->orphan = true;
+    }
+    if (!keep) {
+      if (ctx->ah->arena) (void)hipHostFree(ctx->ah->arena);
+      delete ctx->ah;
+    }
+    ctx->ah = nullptr;
+    ctx->arena = nullptr;
+  }
   for (auto& e : ctx->ev_x)
     if (e) (void)hipEventDestroy(e);
   if (ctx->sx) (void)hipStreamDestroy(ctx->sx);
@@ -3194,18 +3235,39 @@ int dq_bgzf_fetch(dq_ctx* ctx, uint8_t* host_out, int64_t cap) {
 int dq_set_export_arena(dq_ctx* ctx, int64_t bytes) {
   if (!ctx || bytes < 0) return DQ_EINVAL;
   ON_DEVICE(ctx);
+  if (!ctx->ah) ctx->ah = new ArenaHold();
+  {
+    std::lock_guard<std::mutex> lk(ctx->ah->mu);
+    if (ctx->ah->live)
+      RET(DQ_EINVAL, "the export arena still holds a batch: dq_batch_free it before resizing the arena");
+  }
+  if (ctx->s) HIPCHK(hipStreamSynchronize(ctx->s));
+  if (ctx->sx) HIPCHK(hipStreamSynchronize(ctx->sx));
   if (ctx->arena) (void)hipHostFree(ctx->arena);
-  ctx->arena = nullptr;
+  ctx->arena = ctx->ah->arena = nullptr;
   ctx->arena_cap = 0;
   if (bytes == 0) return 0;
   HIPCHK(hipHostMalloc((void**)&ctx->arena, (size_t)bytes, hipHostMallocDefault));
+  ctx->ah->arena = ctx->arena;
   ctx->arena_cap = (size_t)bytes;
   return ensure_pinned(ctx);  // the upload staging too: every long-lived host buffer up front
 }
 
 void dq_batch_free(dq_batch* b) {
   if (!b) return;
-  if (b->in_arena) {  // the arrays live in the context's export arena
+  if (b->in_arena) {  // the arrays live in the context's export arena: give it back
+    if (ArenaHold* h = static_cast<ArenaHold*>(b->arena_hold)) {
+      bool last;
+      {
+        std::lock_guard<std::mutex> lk(h->mu);
+        h->live = false;
+        last = h->orphan;
+      }
+      if (last) {  // the context is gone: this batch owned the arena
+        if (h->arena) (void)hipHostFree(h->arena);
+        delete h;
+      }
+    }
     free(b->part_offset);
     free(b->part_digest);
     free(b);

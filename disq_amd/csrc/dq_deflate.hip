@@ -90,8 +90,10 @@ constexpr int OWN_CAP = 16;              // own matches (a 32-byte segment's, + 
 constexpr int CONT_CAP = 160;            // continuation matches (<= CONT_WORDS)
 constexpr int DENSE_WORDS = 2 * MSEG * MB_INL;  // per chunk
 #ifndef DQ_DEFLATE_STEAL
-#define DQ_DEFLATE_STEAL 1  // idle lanes take odd segments nobody flowed into yet (6 % faster; 0: the
-                            // output is the same on every run, profiles/r4bg_deflate_steal_ab.txt)
+#define DQ_DEFLATE_STEAL 0  // 1: idle lanes take odd segments nobody flowed into yet -- 6 % faster,
+                            // but whether an odd segment's parse starts at its own start or at the
+                            // even exit depends on a race, so the bytes differ from run to run
+                            // (profiles/r4bg_deflate_steal_ab.txt); htsjdk's writer is deterministic
 #endif
 #ifndef DQ_POOL_WORDS
 #define DQ_POOL_WORDS 32768  // (a build with a small pool exercises the exhaustion path)
@@ -1390,7 +1392,7 @@ __global__ __launch_bounds__(CWG) void bgzf_code_kernel(const uint8_t* __restric
   __syncthreads();
   const bool over = L.misc[7] != 0;
   DTS();
-  // ---- bits of this thread's eight segments under the dynamic and the fixed code
+  // ---- bits of this thread's two segments (CSEG) under the dynamic and the fixed code
   // segment j of this thread's eight (the block's segment 8t + j) on the parse: walked with
   // lit(byte) and mat(length, distance)
   auto each_seg = [&](auto lit, auto mat) __attribute__((always_inline)) {

@@ -110,6 +110,7 @@ typedef struct dq_batch {
   uint64_t* part_digest; /* ordered digest of each partition's record hashes */
   int32_t in_arena;      /* 1: the arrays live in the context's export arena (dq_set_export_arena) */
   int32_t reserved;
+  void* arena_hold;      /* library-internal: the arena's ownership record (NULL off the arena) */
 } dq_batch;
 
 /* Interval traversal (HtsjdkReadsTraversalParameters, D/HtsjdkReadsTraversalParameters.java):
@@ -364,10 +365,12 @@ int dq_bgzf_compress_resident(dq_ctx* ctx, int64_t* out_len, double* ms);
 int dq_bgzf_fetch(dq_ctx* ctx, uint8_t* host_out, int64_t cap);
 
 /* Export arena: batches of this context (dq_read, dq_decode*) place their arrays in `bytes` of
- * pinned host memory owned by the context, copied by DMA with no staging copies (a batch that does
- * not fit takes heap memory as before).  An arena batch's arrays stay valid until the next batch
- * of the context, dq_set_export_arena or dq_ctx_destroy: a streaming consumer's recycled buffers
- * (one Spark task's records at a time).  bytes = 0 releases the arena. */
+ * pinned host memory, copied by DMA with no staging copies (a batch that does not fit takes heap
+ * memory as before): a streaming consumer's recycled buffers, one Spark task's records at a time.
+ * The arena holds ONE batch: while it is alive (until dq_batch_free), a batch that would go to
+ * the arena and dq_set_export_arena return DQ_EINVAL, and dq_ctx_destroy leaves the arena to the
+ * batch, whose dq_batch_free releases it (per-task ownership with auto-close,
+ * AutocloseIteratorWrapper.java:26-36).  bytes = 0 releases the arena. */
 int dq_set_export_arena(dq_ctx* ctx, int64_t bytes);
 void dq_batch_free(dq_batch* b);
 void dq_free(void* p);

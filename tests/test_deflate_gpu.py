@@ -158,3 +158,21 @@ def test_randomized_length_roundtrip_sweep():
             os.environ.pop("DQ_DEFLATE", None)
         else:
             os.environ["DQ_DEFLATE"] = old
+
+
+def test_output_is_deterministic():
+    """Two compressions of the same bytes are byte-identical, as htsjdk's
+    BlockCompressedOutputStream under HeaderlessBamOutputFormat.java:26-50 is: a WGS stream and the
+    period-3 stream whose ratio moved between runs while odd segments were raced for
+    (DQ_DEFLATE_STEAL, off by default)."""
+    r = synth.generate(20000, seed=5, nthreads=4)
+    wgs = B.inflate_all(r.bam)
+    per3 = (b"ACG" * 200000)[:500000]
+    with _lib.Context() as c:
+        for data in (wgs, per3):
+            a = c.bgzf_compress(data)
+            b = c.bgzf_compress(data)
+            assert a == b
+            assert b"".join(members(a)) == data
+    with _lib.Context() as c2:  # and a fresh context
+        assert c2.bgzf_compress(per3) == a
