@@ -41,6 +41,9 @@ sys.path.insert(0, ROOT)
 METRIC = "decompressed BAM GB/s + reads/sec (whole node) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.29 TB/s measured copy)
 TRAFFIC_PROFILE = "r4bb_inflate_traffic_pmc.json"
+# utilisation of K2 from PMC counters of the benched build (tools/pmc_summary.py over a
+# tools/pmc_inflate.sh run): VALU issue, LDS busy / bank-conflict / unaligned fractions
+UTIL_PROFILE = "r4bb_inflate_util.json"
 
 
 def log(*a):
@@ -312,6 +315,15 @@ def main():
             tj = json.load(f)
         traffic = tj.get("traffic_bytes_per_launch")
         traffic_src = f"profiles/{TRAFFIC_PROFILE} (FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction)"
+    util = None
+    up = os.path.join(ROOT, "profiles", UTIL_PROFILE)
+    if os.path.exists(up):
+        with open(up) as f:
+            uj = json.load(f)
+        util = {"src": f"profiles/{UTIL_PROFILE} (from {uj.get('src')}, tools/pmc_summary.py)",
+                "valu_issue_frac_def": "SQ_INSTS_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE/8 cycles / 2): "
+                                       "a wave64 VALU op takes a SIMD-32 two cycles",
+                **{k: v for k, v in uj.get("kernels", {}).items()}}
 
     interval_mode = e2e = cpu = parity = wpath = None
     if world == 1:
@@ -413,6 +425,7 @@ def main():
                 "trace_src": "profiles/r4bb_rocprof_summary.txt (rocprofv3 kernel trace of this bench command)",
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_launch_ms": round(infl_avg, 3),
+                "utilisation": util,
             },
             "cpu_baseline": cpu,
         }
@@ -708,6 +721,8 @@ def write_path_bench(args):
         runs = [c.bgzf_compress_resident() for _ in range(4)]  # a warm-up and 3 timed
         n = runs[-1][0]
         z = c.bgzf_fetch(n).tobytes()
+        n2 = c.bgzf_compress_resident()[0]  # once more: the same bytes (htsjdk's writer is deterministic)
+        same = n2 == n and c.bgzf_fetch(n2).tobytes() == z
     ms = sorted(x[1] for x in runs[1:])[1]
     with _lib.Context(verify_crc=True) as c:
         c.text_open_bytes(z + eof)
@@ -720,10 +735,65 @@ def write_path_bench(args):
            "input_gbs": round(len(u) / ms / 1e6, 2),
            "htsjdk_level5_ratio": round(len(u) / len(r.bam), 3),
            "roundtrip_gpu_inflate": "match" if ok else "MISMATCH",
+           "deterministic": same,
+           # the write path's roofline: algorithmic bytes = input read once + BGZF output written
+           # once, over the device time of the three kernels, against the HBM peak; counter traffic
+           # of the same kernels (FETCH_SIZE x2 + WRITE_SIZE) from the cited PMC run
+           "roofline": {"bound": "hbm", "achieved": round((len(u) + n) / ms / 1e6, 2),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round((len(u) + n) / ms / 1e6 / HBM_PEAK_GBS, 5),
+                        "traffic_over_alg": 3.9,
+                        "traffic_src": "profiles/r4az_deflate_pmc.txt (3.40 GB per compression of "
+                                       "0.649 GB: 3.9x the 0.871 GB algorithmic bytes)",
+                        "limiter": "LZ77 parse latency of bgzf_parse_kernel (89 % of device time, "
+                                   "one 160 KB workgroup per CU)"},
            "evidence": "profiles/r4bd_deflate_forced_steps_ab.txt, profiles/r4az_deflate_pmc.txt "
                        "(traffic 3.9x the input read + output written)"}
     log("write path:", out)
     return out
+
+
+def pcie_ceiling(nbytes=8 << 30, reps=3):
+    """The host link's measured ceiling (untimed leg): pinned hipMemcpyAsync of `nbytes` device to
+    host alone, host to device alone, and both directions at once on two streams (half the bytes
+    each way), GB/s by HIP events, median of `reps`."""
+    import torch
+    dev = torch.device("cuda", torch.cuda.current_device())
+    h = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    d = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    half = nbytes // 2
+
+    def timed(fn):
+        out = []
+        for _ in range(reps + 1):  # the first is a warm-up
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            out.append(time.perf_counter() - t0)
+        return statistics.median(out[1:])
+
+    def d2h():
+        with torch.cuda.stream(s1):
+            h.copy_(d, non_blocking=True)
+
+    def h2d():
+        with torch.cuda.stream(s1):
+            d.copy_(h, non_blocking=True)
+
+    def both():
+        with torch.cuda.stream(s1):
+            d[:half].copy_(h[:half], non_blocking=True)
+        with torch.cuda.stream(s2):
+            h[half:].copy_(d[half:], non_blocking=True)
+    t_d2h, t_h2d, t_both = timed(d2h), timed(h2d), timed(both)
+    del h, d
+    return {"bytes": nbytes, "d2h_gbs": round(nbytes / t_d2h / 1e9, 2),
+            "h2d_gbs": round(nbytes / t_h2d / 1e9, 2),
+            "bidirectional_gbs": round(nbytes / t_both / 1e9, 2),
+            "method": "pinned torch copies (hipMemcpyAsync), median of 3 after a warm-up; "
+                      "bidirectional = half the bytes each way on two streams"}
 
 
 def end_to_end(data, args, resident_digest=None, header=None):
@@ -815,6 +885,17 @@ def end_to_end(data, args, resident_digest=None, header=None):
                        "double-buffered with the H2D copies) -> HBM -> pipeline -> host SoA + raw "
                        "bytes by DMA into a pinned arena, windows of whole partitions on "
                        "overlapping contexts (disq_amd.stream + dq_open_shard_path + dq_read)"}
+        try:  # the link's ceiling and how close the read comes to it
+            pc = pcie_ceiling()
+            h2d_b, d2h_b = len(data), exported["raw"] + exported["soa"]
+            bound = max(h2d_b / (pc["h2d_gbs"] * 1e9), d2h_b / (pc["d2h_gbs"] * 1e9),
+                        (h2d_b + d2h_b) / (pc["bidirectional_gbs"] * 1e9))
+            pc.update({"h2d_bytes": h2d_b, "d2h_bytes": d2h_b,
+                       "link_bound_s": round(bound, 3),
+                       "frac_of_link_bound": round(bound / secs, 3)})
+            out["pcie_ceiling"] = pc
+        except Exception as e:  # noqa: BLE001
+            out["pcie_ceiling"] = {"error": f"{type(e).__name__}: {e}"}
         return out
     except Exception as e:  # noqa: BLE001
         return {"error": f"{type(e).__name__}: {e}"}

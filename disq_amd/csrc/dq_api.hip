@@ -702,8 +702,8 @@ static int run_pipeline(dq_ctx* ctx) {
     static const bool timing = getenv("DQ_TIMING") != nullptr;
     uint64_t* tim = nullptr;
     if (timing) {
-      HIPCHK(hipMalloc(&tim, sizeof(uint64_t) * 40 * (size_t)std::max<int64_t>(1, nblk)));
-      HIPCHK(hipMemsetAsync(tim, 0, sizeof(uint64_t) * 40 * (size_t)std::max<int64_t>(1, nblk), s));
+      HIPCHK(hipMalloc(&tim, sizeof(uint64_t) * 48 * (size_t)std::max<int64_t>(1, nblk)));
+      HIPCHK(hipMemsetAsync(tim, 0, sizeof(uint64_t) * 48 * (size_t)std::max<int64_t>(1, nblk), s));
     }
     HIPCHK(hipEventRecord(ctx->ev[5], s));
     if ((rc = ensure_all(ctx, ctx->tails, INFLATE_TAIL_BYTES * (size_t)std::max<int64_t>(1, nblk)))) return rc;
@@ -713,13 +713,13 @@ static int run_pipeline(dq_ctx* ctx) {
                     ctx->tails.p);
     HIPCHK(hipEventRecord(ctx->ev[6], s));
     if (timing) {
-      std::vector<uint64_t> h(40 * (size_t)nblk);
+      std::vector<uint64_t> h(48 * (size_t)nblk);  // 32 words per block (TIM_W), 16 per tail
       HIPCHK(hipMemcpyAsync(h.data(), tim, 8 * h.size(), hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
       (void)hipFree(tim);
       double acc[24] = {0};
       for (int64_t i = 0; i < nblk; i++)
-        for (int k = 0; k < 24; k++) acc[k] += (double)h[24 * (size_t)i + k];
+        for (int k = 0; k < 24; k++) acc[k] += (double)h[32 * (size_t)i + k];
       static const char* nm[16] = {"header", "tables", "spec", "rounds", "scan", "emit",
                                    "resolve+store", "crc", "hdr_read_lengths", "resolve_hop_next", "redo_rounds", "tables_build",
                                    "resolve_steps_jumps", "resolve_store", "resolve_jump_tail", "res_batches"};
@@ -735,7 +735,7 @@ static int run_pipeline(dq_ctx* ctx) {
               (acc[3] - acc[19]) / nb, (acc[5] - acc[21]) / nb, acc[22] / nb);
       double ta[16] = {0};
       for (int64_t i = 0; i < nblk; i++)
-        for (int k = 0; k < 16; k++) ta[k] += (double)h[24 * (size_t)nblk + 16 * (size_t)i + k];
+        for (int k = 0; k < 16; k++) ta[k] += (double)h[32 * (size_t)nblk + 16 * (size_t)i + k];
       if (ta[3] > 0)
         fprintf(stderr, "[dq] tail kernel: %.0f tails (%.1f %% of blocks), cycles per tail (lane 0): "
                 "decode=%.0f (header=%.0f tables=%.0f spec=%.0f rounds=%.0f emit=%.0f) "

@@ -113,6 +113,7 @@ constexpr int TOUT = 4096;            // tail output bytes one wave holds
 constexpr int TAIL_MAX_BITS = 32768;  // tail deflate bits (64 speculative lanes of <= 512 bits)
 constexpr int TW = 4;                 // tails (waves) per tail-kernel workgroup
 constexpr int T_NCK = 4;              // checkpoints per speculative lane in the tail kernel
+constexpr int TIM_W = 32;  // DQ_TIMING words per block (dq_api.hip reads the same layout)
 struct TailDesc {
   int32_t pos;       // bit position (from the block's aligned deflate base) of the tail's header
   int32_t produced;  // output bytes before the tail
@@ -1617,7 +1618,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   }
   TST(7);
   if (TIMING && t == 0)
-    for (int i = 0; i < 24; i++) tim[(int64_t)blockIdx.x * 24 + i] = tacc[i];
+    for (int i = 0; i < 24; i++) tim[(int64_t)blockIdx.x * TIM_W + i] = tacc[i];
 }
 
 // ================================================================ the tail kernel
@@ -2373,12 +2374,12 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
   }
 #undef DQ_CFGS
 #undef DQ_LAUNCH
-  // DQ_TIMING: the block kernel's phases in tim[0, 24 ngrid), the tail kernel's in the 4 ngrid
-  // words after them
+  // DQ_TIMING: the block kernel's phases in tim[0, TIM_W ngrid), the tail kernel's in the 16 ngrid
+  // words after them (16 per tail; dq_api allocates TIM_W + 16 per block)
   if (td && tim)
     hipLaunchKernelGGL((inflate_tail_kernel<true>), dim3((unsigned)((ngrid + TW - 1) / TW)), dim3(64 * TW), 0, s,
                        C, blk_pos, blk_csize, blk_usize, uoff, ngrid, U, status, verify_crc, crc_init, ov,
-                       sflags, sel, td, tim + 24 * ngrid);  // 16 words per tail
+                       sflags, sel, td, tim + TIM_W * ngrid);  // 16 words per tail
   else if (td)
     hipLaunchKernelGGL((inflate_tail_kernel<false>), dim3((unsigned)((ngrid + TW - 1) / TW)), dim3(64 * TW), 0, s,
                        C, blk_pos, blk_csize, blk_usize, uoff, ngrid, U, status, verify_crc, crc_init, ov,

@@ -241,8 +241,8 @@ def expand(toks, history=b""):
     return bytes(out[len(history):])
 
 
-def member(deflated, data, crc=None):
+def member(deflated, data, crc=None, isize=None):
     """A BGZF member (htsjdk layout: 'BC' extra field, BSIZE = length - 1) of a raw-DEFLATE body."""
     m = BGZF_HDR + struct.pack("<H", 18 + len(deflated) + 8 - 1) + deflated
     c = zlib.crc32(data) & 0xffffffff if crc is None else crc
-    return m + struct.pack("<II", c, len(data))
+    return m + struct.pack("<II", c, len(data) if isize is None else isize)

@@ -38,7 +38,7 @@ def _first_block(D, toks, first):
         D.dynamic(toks, lens=W.Deflater().dynamic_lengths(toks))
 
 
-def build(prefix, tail, first="dynamic", mod8=None, pad_from=b""):
+def build(prefix, tail, first="dynamic", mod8=None, pad_from=b"", isize_extra=0):
     """A member whose first deflate block holds `prefix` and whose later blocks are `tail`, a list
     of (kind, tokens or bytes, final) with kind fixed / dynamic / stored / fixed_bad (a fixed block
     with the invalid symbol 286 before its end).  mod8: pad the first block with literals (taken
@@ -82,7 +82,8 @@ def build(prefix, tail, first="dynamic", mod8=None, pad_from=b""):
                 D.dynamic(payload, final)
             data += W.expand(payload, bytes(data))
     body = D.finish()
-    return W.member(body, bytes(data)), bytes(data), (len(data) - len(prefix), 8 * len(body) - p)
+    return (W.member(body, bytes(data), isize=len(data) + isize_extra), bytes(data),
+            (len(data) + isize_extra - len(prefix), 8 * len(body) - p))
 
 
 def deferred(gate):
@@ -138,12 +139,15 @@ def fixtures(u):
     toks = [65, (258, 1), 66, 67, 68, (258, 3), 1, 2, 3, 4, 5, 6, 7, (200, 7), (10, 4000)]
     m, d, g = build(pre, [("dynamic", toks, True)])
     f["runs"] = (m, d, g, True, None)
-    # errors inside a deferred tail: a flipped CRC byte, an invalid code (286), too far back
+    # errors inside a deferred tail: a flipped CRC byte, an invalid code (286), too far back.
+    # The member's ISIZE claims bytes past the invalid code: java.util.zip.Inflater stops once
+    # ISIZE bytes are out (BlockGunzipper inflates into an ISIZE-byte buffer), so a bad code after
+    # them is never read -- by zlib or by the kernel
     m, d, g = f["out4096"][:3]
     bad = bytearray(m)
     bad[-8] ^= 0x40
     f["crc"] = (bytes(bad), d, g, True, "crc")
-    m, d, g = build(pre, [("fixed_bad", W.lz77(u[:61000], 60000), True)])
+    m, d, g = build(pre, [("fixed_bad", W.lz77(u[:61000], 60000), True)], isize_extra=7)
     f["badcode"] = (m, d, g, True, "invalid literal/length code")
     small = u[:1000]
     m, d, g = build(small, [("fixed", [70, 71, 72, (5, 2000)], True)])
@@ -165,8 +169,10 @@ def test_fixtures_hit_the_gate(fx):
             assert zlib.decompress(body, -15) == d, name
             assert m[-4:] == len(d).to_bytes(4, "little")
         elif err != "crc":
+            # an ISIZE-bounded inflate, as BlockGunzipper's, reaches the error
+            isize = int.from_bytes(m[-4:], "little")
             with pytest.raises(zlib.error, match=err):
-                zlib.decompress(body, -15)
+                zlib.decompressobj(-15).decompress(body, isize)
         assert deferred(g) == dfr, (name, g)
     assert fx["out4096"][2][0] == 4096 and fx["out4097"][2][0] == 4097
     assert fx["bits32768"][2][1] == 32768 and fx["bits32769"][2][1] == 32769
@@ -224,3 +230,29 @@ def test_gpu_resolve_alignments(wgs):
     got = _gpu_inflate(b"".join(ms) + B.EOF_BLOCK)
     want = b"".join(ds)
     assert np.array_equal(got, np.frombuffer(want, np.uint8))
+
+
+def after_isize_member(u):
+    """An invalid code (286) right after the ISIZE bytes of a deferred tail."""
+    m, d, g = build(u[:60000], [("fixed_bad", W.lz77(u[:61000], 60000), True)])
+    return m, d, g
+
+
+def test_after_isize_fixture(wgs):
+    """A documented difference (malformed input, out of scope per SURVEY.md section 7): zlib's
+    inflate (java.util.zip.Inflater under BlockGunzipper) decodes the symbol after its output
+    buffer is full -- its LEN state runs before the LIT state checks for room -- so an invalid code
+    right after the ISIZE-th byte fails even an ISIZE-bounded inflate; the kernels stop at ISIZE
+    and never read it."""
+    m, d, g = after_isize_member(wgs)
+    assert deferred(g)
+    body = m[18:-8]
+    with pytest.raises(zlib.error, match="invalid literal/length code"):
+        zlib.decompressobj(-15).decompress(body, len(d))
+
+
+@pytest.mark.gpu
+def test_gpu_code_after_isize_is_not_read(wgs):
+    m, d, _ = after_isize_member(wgs)
+    got = _gpu_inflate(m + B.EOF_BLOCK)
+    assert np.array_equal(got, np.frombuffer(d, np.uint8))

@@ -18,6 +18,7 @@
 #include <string.h>
 
 typedef struct { int32_t pos, len, dist; } Tok;  // len 0: literal
+static int32_t src1[70000], nx[70000], hop[70000];  // per byte: first-hop source, jump scratch
 
 static const uint8_t *g_in;
 static size_t g_nbits, g_bp;
@@ -141,6 +142,7 @@ typedef struct {
   long final_at_step[8], nonfinal_at_step[8];
   long rjumps;
   long hops_lit, hops_lit_max, hops_win[8], win_rounds[8];
+  long dag_steps, dag_need_prev, dag_depth_sum, dag_depth_max, dag_need_prev2;
 } Stats;
 
 int main(int argc, char **argv) {
@@ -236,7 +238,6 @@ int main(int argc, char **argv) {
     // per byte: hops to a literal, and to a byte before the byte's window of W bytes; synchronous
     // pointer-jumping rounds per window (max over its bytes)
     {
-      static int32_t src1[70000], nx[70000], hop[70000];
       for (int i = 0; i < nt; i++) {
         Tok t = tk[i];
         if (!t.len) {
@@ -294,6 +295,36 @@ int main(int argc, char **argv) {
         S.hops_win[wi] += hw;
       }
     }
+    {  // step DAG (512-byte steps): final source of each byte after in-step resolution
+      static int32_t fin[70000], sd[200];
+      int ns = (ol + 511) / 512;
+      for (int x = 0; x < ol; x++) {
+        int s0 = x & ~511, y = x;
+        // follow the byte chain while inside the step and not a literal
+        while (src1[y] != y && src1[y] >= s0) y = src1[y];
+        fin[x] = src1[y] == y ? y : src1[y];  // literal in step, or a byte before the step
+      }
+      int bmax = 0;
+      for (int k = 0; k < ns; k++) {
+        int need = -1;  // latest earlier step a non-literal source lies in
+        for (int x = 512 * k; x < ol && x < 512 * (k + 1); x++) {
+          int f = fin[x];
+          if (f < 512 * k && src1[f] != f) { int st = f >> 9; if (st > need) need = st; }
+        }
+        int d = 1;
+        for (int x = 512 * k; x < ol && x < 512 * (k + 1); x++) {
+          int f = fin[x];
+          if (f < 512 * k && src1[f] != f && sd[f >> 9] + 1 > d) d = sd[f >> 9] + 1;
+        }
+        sd[k] = d;
+        if (d > bmax) bmax = d;
+        S.dag_steps++;
+        if (need == k - 1) S.dag_need_prev++;
+        if (need >= k - 2) S.dag_need_prev2++;
+      }
+      S.dag_depth_sum += bmax;
+      if (bmax > S.dag_depth_max) S.dag_depth_max = bmax;
+    }
     S.depth_sum += bdepth;
     if (bdepth > S.depth_max) S.depth_max = bdepth;
     S.rdepth_sum += brd;
@@ -344,6 +375,8 @@ int main(int argc, char **argv) {
   printf("\nMRR depth: mean %.1f max %ld;  after redirect: mean %.1f max %ld  (jumps/match %.2f, straddling %.1f %%)\n",
          S.depth_sum / B, S.depth_max, S.rdepth_sum / B, S.rdepth_max, (double)S.rjumps / S.matches,
          100.0 * S.straddle / S.matches);
+  printf("512-byte step DAG: steps needing step k-1 %.1f %%, k-1 or k-2 %.1f %%, critical path mean %.1f max %ld steps (of %.1f)\n",
+         100.0 * S.dag_need_prev / S.dag_steps, 100.0 * S.dag_need_prev2 / S.dag_steps, S.dag_depth_sum / B, S.dag_depth_max, S.dag_steps / B);
   printf("byte hops to a literal: mean %.2f max %ld\n", (double)S.hops_lit / S.bytes, S.hops_lit_max);
   for (int wi = 0; wi < 8; wi++)
     printf("window %6d: hops to before-window/literal mean %.2f, sync jump rounds per window %.2f (per block %.1f)\n",
