@@ -739,7 +739,7 @@ static int run_pipeline(dq_ctx* ctx) {
       if (ta[3] > 0)
         fprintf(stderr, "[dq] tail kernel: %.0f tails (%.1f %% of blocks), cycles per tail (lane 0): "
                 "decode=%.0f (header=%.0f tables=%.0f spec=%.0f rounds=%.0f emit=%.0f) "
-                "resolve_start=%.0f rows_store_crc=%.0f\n", ta[3], 100.0 * ta[3] / nb, ta[0] / ta[3],
+                "rows=%.0f store_crc=%.0f\n", ta[3], 100.0 * ta[3] / nb, ta[0] / ta[3],
                 ta[4] / ta[3], ta[5] / ta[3], ta[6] / ta[3], ta[7] / ta[3], ta[8] / ta[3],
                 ta[1] / ta[3], ta[2] / ta[3]);
     }

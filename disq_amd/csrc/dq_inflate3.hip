@@ -122,6 +122,10 @@ struct TailDesc {
 };
 
 struct alignas(16) LdsI {
+  // decode-table layout (dsym, ll_second, d_second): the second-level tables follow each root
+  static constexpr int kLSUB = T_LSUB, kDROOT = T_DROOT, kDSUB = T_DSUB;
+  [[maybe_unused]] static constexpr int kTEND = T_END;  // DQ_CHK bound
+  static constexpr bool kPair = true;  // literal-pair table (dsym)
   uint8_t out[OUTCAP];            // output image: byte x at out[sh + x]
   alignas(8) uint32_t bm[2048];   // match-start bitmap (read as 64-bit words in resolve)
   union {
@@ -183,7 +187,8 @@ static_assert(HB_WORDS * 4 <= T_END * 2, "header staging fits the decode table")
 __device__ inline uint32_t* emit_dummy(LdsI& L) { return L.scratch; }
 
 __constant__ uint32_t c_crc4[4][256];
-__constant__ uint32_t c_x2n[32];  // x^(2^k) mod P (reflected): the tail kernel's CRC shifts
+__constant__ uint32_t c_x2n[32];  // x^(2^k) mod P (reflected)
+__constant__ uint32_t c_x8n[TOUT + 1];  // x^(8 k) mod P, k <= TOUT: the tail kernel's CRC shifts
 // CRC slices: 132 bytes (33 words), so the 64 lanes of a wave read 64 different LDS banks (128-byte
 // slices put every lane of a wave in the same bank: a 32-way conflict on every data read)
 constexpr int CRC_SL = 132;
@@ -296,9 +301,9 @@ DQ_AI uint32_t load_desc(const LT& L, int a) {
 template <bool SLOW, class LT>
 DQ_AI uint32_t ll_second(const LT& L, uint32_t e, uint32_t bb) {
   const uint32_t sb = (e >> 4) & 7;
-  DQ_CHK(T_LSUB + (e >> 7) + ((bb >> LR) & ((1u << sb) - 1)) < (uint32_t)T_DROOT, CHK_K2_TABLE);
-  if (!SLOW) return L.u.d.T[T_LSUB + (e >> 7) + ((bb >> LR) & ((1u << sb) - 1))];
-  if (sb) return L.u.d.T[T_LSUB + (e >> 7) + ((bb >> LR) & ((1u << sb) - 1))];
+  DQ_CHK(LT::kLSUB + (e >> 7) + ((bb >> LR) & ((1u << sb) - 1)) < (uint32_t)LT::kDROOT, CHK_K2_TABLE);
+  if (!SLOW) return L.u.d.T[LT::kLSUB + (e >> 7) + ((bb >> LR) & ((1u << sb) - 1))];
+  if (sb) return L.u.d.T[LT::kLSUB + (e >> 7) + ((bb >> LR) & ((1u << sb) - 1))];
   if (!(e & E_SLOW)) return 0u;
   int l = 0;
   const int k = canon_decode(bb, L.u.d.hl, LR + 1, &l);
@@ -307,9 +312,9 @@ DQ_AI uint32_t ll_second(const LT& L, uint32_t e, uint32_t bb) {
 template <bool SLOW, class LT>
 DQ_AI uint32_t d_second(const LT& L, uint32_t e, uint32_t bb) {
   const uint32_t sb = (e >> 4) & 7;
-  DQ_CHK(T_DSUB + (e >> 7) + ((bb >> DR) & ((1u << sb) - 1)) < (uint32_t)T_END, CHK_K2_TABLE);
-  if (!SLOW) return L.u.d.T[T_DSUB + (e >> 7) + ((bb >> DR) & ((1u << sb) - 1))];
-  if (sb) return L.u.d.T[T_DSUB + (e >> 7) + ((bb >> DR) & ((1u << sb) - 1))];
+  DQ_CHK(LT::kDSUB + (e >> 7) + ((bb >> DR) & ((1u << sb) - 1)) < (uint32_t)LT::kTEND, CHK_K2_TABLE);
+  if (!SLOW) return L.u.d.T[LT::kDSUB + (e >> 7) + ((bb >> DR) & ((1u << sb) - 1))];
+  if (sb) return L.u.d.T[LT::kDSUB + (e >> 7) + ((bb >> DR) & ((1u << sb) - 1))];
   if (!(e & E_SLOW)) return 0u;
   int l = 0;
   const int k = canon_decode(bb, L.u.d.hd, DR + 1, &l);
@@ -335,7 +340,8 @@ DQ_AI bool dsym(BitR& r, const S& W, const LT& L, uint32_t p, uint32_t lim,
   uint32_t bb = (uint32_t)r.bb;
   const uint32_t ri = bb & ((1u << LR) - 1);
   uint32_t e = L.u.d.T[ri];
-  const uint32_t pe = L.u.d.x.pair[ri];
+  uint32_t pe = 0;
+  if constexpr (LT::kPair) pe = L.u.d.x.pair[ri];
   if ((e & 15) == 0) e = ll_second<SLOW>(L, e, bb);
   const uint32_t nb = e & 15;
   const uint32_t lx = __builtin_amdgcn_ubfe(e, 5, 3);
@@ -346,7 +352,7 @@ DQ_AI bool dsym(BitR& r, const S& W, const LT& L, uint32_t p, uint32_t lim,
   br_take(r, nb + lx + (two ? (pe & 15) : 0u));
   br_refill(r, W);  // >= 33 bits: a distance code + its extra bits (<= 28)
   bb = (uint32_t)r.bb;
-  uint32_t e2 = L.u.d.T[T_DROOT + (bb & ((1u << DR) - 1))];
+  uint32_t e2 = L.u.d.T[LT::kDROOT + (bb & ((1u << DR) - 1))];
   if (is_m && (e2 & 15) == 0) e2 = d_second<SLOW>(L, e2, bb);
   const uint32_t nb2 = e2 & 15, dx = __builtin_amdgcn_ubfe(e2, 4, 4);
   dist = (__builtin_amdgcn_ubfe(e2, 12, 2) << __builtin_amdgcn_ubfe(e2, 8, 4)) + 1u +
@@ -1371,6 +1377,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   constexpr int BATCH = NB * CH;
   constexpr int NE = NB * G;
   static_assert(BATCH <= RES_NXT, "the batch's next-pointers fit the resolve scratch");
+  static_assert(65536 / BATCH <= 32, "one carry slot per batch");
   uint16_t* nxt = L.u.r.nxt;
   // (a) sources of batch `b0`.  First hop, every byte: its owner (one 64-bit bitmap word, one
   //     last_start) and the owner's descriptor give the copy source (G <= 4 bytes have at most
@@ -1624,15 +1631,20 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
 // ================================================================ the tail kernel
 // Per-wave LDS of inflate_tail_kernel (~13 KB: four tails per workgroup, three workgroups per CU).
 struct alignas(16) LdsW {
+  // root tables only: a tail's codes longer than the roots take the canonical path (E_SLOW), and
+  // code-less root indices hold invalid-code entries (build_tables_wave), so the second-level
+  // areas are never read (their offsets point into the litlen root only to stay in bounds)
+  static constexpr int kLSUB = 0, kDROOT = 1 << LR, kDSUB = 0, kTEND = (1 << LR) + (1 << DR);
+  // no literal-pair table: with it a tail takes 11.3 KB and four 4-wave workgroups do not fit a CU
+  static constexpr bool kPair = false;
   union {
     struct {
-      uint16_t T[T_END];
+      uint16_t T[kTEND];
       HuffCanon hl, hd;
       uint16_t lend[16], dend[16];
       uint16_t lent[288];
       uint16_t dent[32];
       union {
-        uint16_t pair[1 << LR];
         struct {
           uint8_t lens[320];
           uint8_t clen[20];
@@ -1642,19 +1654,17 @@ struct alignas(16) LdsW {
         } h;
       } x;
     } d;
-    struct {
-      uint64_t carry[TOUT / 64];  // per row, desc << 32 | (start + 1) of the match carried in
-    } r;
-    uint32_t crc[256];            // CRC: the slice-by-1 table
+    uint32_t crc4[4][256];        // CRC: the slice-by-4 tables
   } u;
-  uint8_t out[TOUT + 32];             // the tail's output image: tail byte k at out[sh + k]
+  alignas(16) uint8_t out[TOUT + 32]; // the tail's output image: tail byte k at out[sh + k]
   alignas(8) uint32_t bm[TOUT / 32];  // match-start bitmap of the tail (bit k: tail byte k)
-  uint32_t ck[T_NCK * 64];            // checkpoints [j * 64 + lane]; emit's dummy words
+  uint32_t ck[T_NCK * 64];            // checkpoints [j * 64 + lane]; emit's dummy words; the
+                                      // resolve's next pointers (256 x 16 bits)
   int32_t misc[8];
   uint32_t scratch[16];               // run_seg's dummy words
 };
-static_assert(HB_WORDS * 4 <= T_END * 2, "header staging fits the decode table");
-static_assert(4 * sizeof(LdsW) <= 54 * 1024, "four tails per workgroup, three workgroups per CU");
+static_assert(HB_WORDS * 4 <= LdsW::kTEND * 2, "header staging fits the decode table");
+static_assert(4 * 4 * sizeof(LdsW) <= 160 * 1024, "four tails per workgroup, four workgroups per CU");
 DQ_AI uint32_t* emit_dummy(LdsW& L) { return L.ck; }
 
 // The code-length sequence of a dynamic header, decoded by one wave, 64 bits at a time: lane i
@@ -1858,13 +1868,15 @@ DQ_AI void build_tables_wave(LdsW& L, int nlen, int ndist) {
                          L.u.d.hl.count[14] + L.u.d.hl.count[15] > 0;
   const bool dslow = L.u.d.hd.count[9] + L.u.d.hd.count[10] + L.u.d.hd.count[11] + L.u.d.hd.count[12] +
                          L.u.d.hd.count[13] + L.u.d.hd.count[14] + L.u.d.hd.count[15] > 0;
+  // (an index with no code in an incomplete code -- zlib allows one code of length 1 -- gets an
+  // invalid-code entry of length 1: decoding it stops the run, as zlib's "invalid code")
   for (int i = lane; i < (1 << LR); i += 64) {
     const uint16_t v = root_entry<LR>(L, L.u.d.hl, L.u.d.lend, L.u.d.lent, bitrev((uint32_t)i, LR));
-    L.u.d.T[i] = v == 0 && lslow ? E_SLOW : v;
+    L.u.d.T[i] = v ? v : lslow ? E_SLOW : (uint16_t)(LL_BAD | 1u);
   }
   for (int i = lane; i < (1 << DR); i += 64) {
     const uint16_t v = root_entry<DR>(L, L.u.d.hd, L.u.d.dend, L.u.d.dent, bitrev((uint32_t)i, DR));
-    L.u.d.T[T_DROOT + i] = v == 0 && dslow ? E_SLOW : v;
+    L.u.d.T[LdsW::kDROOT + i] = v ? v : dslow ? E_SLOW : (uint16_t)0x4001u;
   }
   __builtin_amdgcn_wave_barrier();
 }
@@ -1885,7 +1897,7 @@ DQ_AI uint32_t x8n_tail(uint32_t n) {
 // in the same row waits for its lane.  Stores the tail's bytes and finishes the block's CRC32 from
 // the prefix's CRC register.  No workgroup barrier: the waves of a workgroup are independent.
 template <bool TIMING>
-__global__ __launch_bounds__(64 * TW, 3) void inflate_tail_kernel(
+__global__ __launch_bounds__(64 * TW, 4) void inflate_tail_kernel(
     const uint8_t* __restrict__ C, const int64_t* __restrict__ blk_pos,
     const int32_t* __restrict__ blk_csize, const int32_t* __restrict__ blk_usize,
     const int64_t* __restrict__ uoff, int64_t ngrid, uint8_t* __restrict__ U,
@@ -2007,20 +2019,9 @@ __global__ __launch_bounds__(64 * TW, 3) void inflate_tail_kernel(
       }
     }
     tick(0);
-    // ---- tables, pair table
+    // ---- tables
     build_tables_wave(L, nlen, ndist);
     if (L.misc[M_ERR]) break;
-    for (int i = lane; i < (1 << LR); i += 64) {
-      const uint32_t e1 = L.u.d.T[i];
-      const uint32_t l1 = e1 & 15;
-      uint16_t v = 0;
-      if (l1 > 0 && !(e1 & 16) && l1 < (uint32_t)LR) {
-        const uint32_t e2 = L.u.d.T[(uint32_t)i >> l1];
-        const uint32_t l2 = e2 & 15;
-        if (l2 > 0 && !(e2 & 16) && l1 + l2 <= (uint32_t)LR) v = (uint16_t)e2;
-      }
-      L.u.d.x.pair[i] = v;
-    }
     __builtin_amdgcn_wave_barrier();
     const bool slow = L.misc[M_SLOW] != 0;
     if (a > endbits) {
@@ -2114,104 +2115,163 @@ __global__ __launch_bounds__(64 * TW, 3) void inflate_tail_kernel(
     return;
   }
   const uint64_t t1 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
-  // ---- resolve the tail, row by row (64 bytes: one per lane)
+  // ---- resolve the tail in rows of 256 image bytes, in order, lane l owning image bytes
+  //      4 l .. 4 l + 3 (one dword: every write is one aligned ds_write_b32).  Per row: every
+  //      byte's copy source from the bitmap (at most two owners per lane; the match carried into
+  //      the row held in registers); the bytes whose source lies before the tail are loaded from
+  //      U three rows ahead (software-pipelined: the HBM latency overlaps three rows' work) and written
+  //      in place with the literals; the rest follow in-row pointers by lock-step pointer jumping
+  //      (256 16-bit next pointers in the dead checkpoint area) to a byte in place or of an earlier
+  //      row, then copy.  Round 4 resolved 64-byte rows by ballot rounds, a lane copying once its
+  //      source lane had: in-row chains of short distances ran one lane per round.
   const int32_t n = isize - p0;
-  const int nrows = (n + 63) >> 6;
+  const int nrows = (sh + n + 255) >> 8;
   uint8_t* const O = L.out + sh;  // tail byte k at O[k]
-  const uint64_t* bm64 = reinterpret_cast<const uint64_t*>(L.bm);
-  {  // the match carried into every row (its descriptor is overwritten once its row is resolved)
-    int run = -1;
-    for (int r0 = 0; r0 < nrows; r0 += 64) {
-      const int r = r0 + lane;
-      const uint64_t m = r < nrows ? bm64[r] : 0ull;
-      const int lastr = m ? 64 * r + 63 - (int)__clzll(m) : -1;
-      const int incl = max(wave_incl_max(lastr), run);
-      int ex = __shfl_up(incl, 1, 64);
-      if (lane == 0) ex = run;
-      uint64_t cr = 0;
-      if (r < nrows && ex >= 0) {
-        const uint32_t d = load_desc(L, sh + ex);
-        if (ex + (int32_t)(d >> 15) + 3 > 64 * r) cr = (uint64_t)d << 32 | (uint32_t)(ex + 1);
-      }
-      if (r < nrows) L.u.r.carry[r] = cr;
-      run = __shfl(incl, 63, 64);
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  }
   const uint8_t* Ub = U + ub + p0;  // the tail's first byte in U: sources before it are final
-  // the first hop of byte x = 64 row + lane: its owner (this row's bitmap word, else the carried
-  // match) and the copy source (< 0: a byte before the tail, in U); descriptors of this row and
-  // the next are intact until this row is resolved
-  auto hop = [&](int row, bool& copy) -> int32_t {
-    const int32_t x = 64 * row + lane;
-    const uint64_t mi = bm64[row] & (~0ull >> (63 - lane));
-    int32_t ms;
-    uint32_t desc;
-    if (mi) {
-      ms = 64 * row + 63 - (int32_t)__clzll(mi);
-      desc = load_desc(L, sh + ms);
-    } else {
-      const uint64_t cr = L.u.r.carry[row];
-      ms = (int32_t)(uint32_t)cr - 1;
-      desc = (uint32_t)(cr >> 32);
-    }
-    const int32_t len = (int32_t)(desc >> 15) + 3, D = (int32_t)(desc & 0x7fff) + 1;
-    copy = x < n && ms >= 0 && x < ms + len;
-    const int32_t jj = x - ms;
-    int32_t r = jj;
-    if (__builtin_expect(__any(copy && jj >= D), 0)) {
-      const int32_t q = (int32_t)((float)jj * __builtin_amdgcn_rcpf((float)D));
-      r = jj - q * D;
-      r = r >= D ? r - D : r;
-    }
-    return ms - D + r;
-  };
-  // rows in order, software-pipelined eight rows deep: the first hop of row r + 8 (its
-  // descriptors are intact until row r + 8 is resolved) and, for a source before the tail, its
-  // load from U (not in cache: one row's load at a time was most of this kernel's time) are issued
-  // while row r is resolved; the eight rows' sources and values wait in registers
-  int32_t sv[8];
-  bool cv[8];
-  uint8_t gv[8];
-#pragma unroll
-  for (int j = 0; j < 8; j++) {  // (j < nrows is uniform)
-    bool c = false;
-    sv[j] = j < nrows ? hop(j, c) : 0;
-    cv[j] = c;
-    gv[j] = c && sv[j] < 0 ? Ub[sv[j]] : (uint8_t)0;
-  }
-  const uint64_t t2 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
-  for (int r0 = 0; r0 < nrows; r0 += 8) {
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      const int row = r0 + j;
-      if (row < nrows) {  // uniform
-        const int32_t x = 64 * row + lane;
-        const int32_t src = sv[j];
-        const bool copy = cv[j];
-        DQ_CHK(!copy || (src >= -p0 && src < x), CHK_K2_SRC);
-        const bool local = copy && src >= 64 * row;
-        if (copy && !local) O[x] = src < 0 ? gv[j] : O[src];
-        uint64_t pend = __ballot(local);
-        uint64_t done = ~pend;
-        while (pend) {  // same-row sources: a lane copies once its source lane's byte is final
-          const bool go = local && ((pend >> lane) & 1) && ((done >> (src & 63)) & 1);
-          if (go) O[x] = O[src];
-          const uint64_t g = __ballot(go);
-          done |= g;
-          pend &= ~g;
-        }
-        __builtin_amdgcn_wave_barrier();
-        // row + 8's first hop and U load into this slot
-        bool c = false;
-        sv[j] = row + 8 < nrows ? hop(row + 8, c) : 0;
-        cv[j] = c;
-        gv[j] = c && sv[j] < 0 ? Ub[sv[j]] : (uint8_t)0;
+  // the copy sources of row `row`: src[i] (tail coordinates, < 0 before the tail), copy bits, and
+  // the carried match (cms, cdesc) advanced past the row (its descriptor read while intact)
+  auto hops = [&](int row, int32_t& cms, uint32_t& cdesc, int32_t (&src)[4], uint32_t& cpy) {
+    const int32_t x0 = 256 * row + 4 * lane - sh;  // tail byte of the lane's first byte
+    const int32_t nval = min(max(n - x0, 0), 4);
+    uint32_t b4 = 0;
+    if (nval > 0) {
+      if (x0 >= 0) {
+        const int32_t wi = x0 >> 5;
+        b4 = __builtin_amdgcn_alignbit(L.bm[min(wi + 1, TOUT / 32 - 1)], L.bm[wi], (uint32_t)x0 & 31u);
+      } else if (x0 > -4) {
+        b4 = L.bm[0] << (-x0);
       }
+      b4 &= (1u << nval) - 1u;
+    }
+    const int32_t lst = b4 ? x0 + 31 - (int32_t)__clz(b4) : -1;
+    const int32_t incl = wave_incl_max(lst);
+    int32_t pre = __shfl_up(incl, 1, 64);
+    pre = lane == 0 ? -1 : pre;
+    const int32_t o0 = (b4 & 1u) ? x0 : max(pre, cms);
+    const uint32_t r1 = b4 & ~1u;  // a second start in the lane (>= 3 bytes after the first)
+    const int32_t p1 = r1 ? x0 + (int32_t)__builtin_ctz(r1) : -1;
+    const uint32_t d0 = o0 < 0 ? 0u : (o0 == cms ? cdesc : load_desc(L, sh + o0));
+    const uint32_t d1 = p1 < 0 ? 0u : load_desc(L, sh + p1);
+    const int32_t last = max(__builtin_amdgcn_readlane(incl, 63), cms);  // uniform
+    if (last != cms) {
+      cdesc = load_desc(L, sh + last);
+      cms = last;
+    }
+    cpy = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int32_t x = x0 + i;
+      const bool at1 = p1 >= 0 && x >= p1;
+      const int32_t ms = at1 ? p1 : o0;
+      const uint32_t ds = at1 ? d1 : d0;
+      const int32_t len = (int32_t)(ds >> 15) + 3, D = (int32_t)(ds & 0x7fff) + 1;
+      const bool copy = ms >= 0 && i < nval && x >= 0 && x < ms + len;
+      const int32_t jj = x - ms;
+      int32_t rm = jj;  // (x - ms) mod D: only past the first period of an overlapping match
+      if (__builtin_expect(__any(copy && jj >= D), 0)) {
+        const int32_t q = (int32_t)((float)jj * __builtin_amdgcn_rcpf((float)D));
+        rm = jj - q * D;
+        rm = rm >= D ? rm - D : rm;
+      }
+      src[i] = ms - D + rm;
+      DQ_CHK(!copy || (src[i] >= -p0 && src[i] < x), CHK_K2_SRC);
+      cpy |= copy ? 1u << i : 0u;
+    }
+  };
+  const int32_t Yend = sh + n;  // image bytes of the tail: [sh, Yend)
+  const uint64_t t2 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
+  {  // the rows in order; a row's sources before the tail are loaded from U three rows ahead
+    constexpr uint32_t TERM = 0x8000u;  // next pointer of a byte whose value is in place
+    uint16_t* const nx = reinterpret_cast<uint16_t*>(L.ck);  // the row's 256 next pointers
+    int32_t cms = -1;
+    uint32_t cdesc = 0;
+    // a row's sources and its loads from U: unconditional loads (a byte that needs none loads the
+    // prefix's last byte) into fixed registers per slot, so the compiler's wait for a slot's
+    // values counts only the loads issued before them (no branch, no register shuffling)
+    auto prefetch = [&](int row, int32_t (&s)[4], uint32_t& c, uint32_t (&g)[4]) {
+      c = 0;
+      hops(row, cms, cdesc, s, c);  // rows in order (the carry); past the last row: no copies
+#pragma unroll
+      for (int i = 0; i < 4; i++) g[i] = Ub[((c >> i) & 1u) && s[i] < 0 ? s[i] : -1];
+    };
+    auto do_row = [&](int row, const int32_t (&src)[4], uint32_t cpy, const uint32_t (&g)[4]) {
+      const int32_t Y = 256 * row + 4 * lane;  // the lane's image dword
+      const int32_t x0 = Y - sh, xr = 256 * row - sh;
+      const bool live = Y < Yend;
+      // (a) bytes whose value is known now -- literals (in place) and sources before the tail
+      //     (loaded) -- are written and marked terminal; the others' next pointers published
+      uint32_t own = live ? *reinterpret_cast<const uint32_t*>(L.out + Y) : 0u;
+      uint32_t pend = 0;
+      int32_t p[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const bool c = (cpy >> i) & 1u;
+        const bool pre = c && src[i] < 0;
+        own = pre ? (own & ~(0xffu << (8 * i))) | (g[i] << (8 * i)) : own;
+        p[i] = !c || pre ? (int32_t)((uint32_t)(x0 + i) | TERM) : src[i];
+        pend |= c && !pre && src[i] >= xr ? 1u << i : 0u;
+      }
+      if (live) *reinterpret_cast<uint32_t*>(L.out + Y) = own;
+      auto publish = [&]() {
+        uint2 w;
+        w.x = ((uint32_t)p[0] & 0xffffu) | ((uint32_t)p[1] << 16);
+        w.y = ((uint32_t)p[2] & 0xffffu) | ((uint32_t)p[3] << 16);
+        *reinterpret_cast<uint2*>(nx + 4 * lane) = w;
+        // the pointers are read back as 16-bit words: no reordering across the 8-byte store (a
+        // different type, so the compiler could otherwise move the next reads above it)
+        asm volatile("" ::: "memory");
+      };
+      publish();
+      // (b) pointer jumping inside the row (lock-step: a round's reads precede its writes): a
+      //     pending pointer into the row takes that byte's pointer; a terminal byte or a byte of
+      //     an earlier row ends it
+      for (int rnd = 0; __any(pend != 0) && rnd < 10; rnd++) {
+        uint32_t q[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const bool pd = (pend >> i) & 1u;
+          DQ_CHK(!pd || (p[i] - xr >= 0 && p[i] - xr < 256), CHK_K2_NXT);
+          q[i] = nx[pd ? p[i] - xr : 4 * lane + i];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const bool pd = (pend >> i) & 1u;
+          // q: a terminal (the byte holding the value, flagged), a byte of an earlier row, or a
+          // byte of this row further down the chain
+          const bool fin = pd && ((q[i] & TERM) || (int32_t)q[i] < xr);
+          p[i] = pd ? (int32_t)q[i] : p[i];
+          pend &= fin ? ~(1u << i) : ~0u;
+        }
+        publish();
+      }
+      // (c) the copies: every pointer is now a byte in place (terminal) or of an earlier row
+      uint32_t v = own;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const bool c = (cpy >> i) & 1u;
+        const int32_t s = (int32_t)((uint32_t)p[i] & ~TERM);
+        const bool done = !c || src[i] < 0;
+        const uint32_t b = done ? 0u : (uint32_t)O[s];
+        v = done ? v : (v & ~(0xffu << (8 * i))) | (b << (8 * i));
+      }
+      if (live) *reinterpret_cast<uint32_t*>(L.out + Y) = v;
+    };
+    int32_t sA[4], sB[4], sC[4];
+    uint32_t cA = 0, cB = 0, cC = 0, gA[4], gB[4], gC[4];
+    prefetch(0, sA, cA, gA);
+    prefetch(1, sB, cB, gB);
+    prefetch(2, sC, cC, gC);
+    for (int row = 0; row < nrows; row += 3) {  // three rows per pass, a fixed slot each
+      do_row(row, sA, cA, gA);
+      prefetch(row + 3, sA, cA, gA);
+      do_row(row + 1, sB, cB, gB);
+      prefetch(row + 4, sB, cB, gB);
+      do_row(row + 2, sC, cC, gC);
+      prefetch(row + 5, sC, cC, gC);
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const uint64_t t3 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
   // ---- store: bytes up to the first 16-byte line of U, the lines, the last bytes
   uint8_t* dst = U + ub + p0;
   const int head = min((16 - sh) & 15, n);
@@ -2226,17 +2286,27 @@ __global__ __launch_bounds__(64 * TW, 3) void inflate_tail_kernel(
   for (int x = head + 16 * lines + lane; x < n; x += 64) dst[x] = O[x];
   // ---- CRC32 of the block: the prefix's register shifted past the tail, xor the tail's
   if (verify_crc) {
-    for (int i = lane; i < 256; i += 64) L.u.crc[i] = c_crc4[0][i];
+    // slice-by-4 over a slice of ceil(n / 64) bytes per lane (dwords where the image allows),
+    // moved to the tail's end by x^(8 k) from a table (round 4: byte steps, and the shift by a
+    // loop of one 32-step multiply per bit of k)
+    for (int i = lane; i < 1024; i += 64) (&L.u.crc4[0][0])[i] = (&c_crc4[0][0])[i];
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     const int32_t sl = (n + 63) >> 6;
     const int32_t s0 = min(n, lane * sl), s1 = min(n, s0 + sl);
     uint32_t cr = 0;
-    for (int32_t x = s0; x < s1; x++) cr = L.u.crc[(cr ^ O[x]) & 0xff] ^ (cr >> 8);
-    cr = gf2_mulmod(x8n_tail((uint32_t)(n - s1)), cr);
+    int32_t x = s0;
+    while (x < s1 && ((sh + x) & 3)) cr = L.u.crc4[0][(cr ^ O[x++]) & 0xff] ^ (cr >> 8);
+    for (; x + 4 <= s1; x += 4) {
+      const uint32_t v = cr ^ *reinterpret_cast<const uint32_t*>(O + x);
+      cr = L.u.crc4[3][v & 0xff] ^ L.u.crc4[2][(v >> 8) & 0xff] ^ L.u.crc4[1][(v >> 16) & 0xff] ^
+           L.u.crc4[0][v >> 24];
+    }
+    while (x < s1) cr = L.u.crc4[0][(cr ^ O[x++]) & 0xff] ^ (cr >> 8);
+    cr = gf2_mulmod(c_x8n[n - s1], cr);
     cr = (uint32_t)__shfl((int)wave_incl_xor(cr), 63, 64);
     if (lane == 0) {
-      const uint32_t raw = gf2_mulmod(x8n_tail((uint32_t)n), td.crc_raw) ^ cr;
+      const uint32_t raw = gf2_mulmod(c_x8n[n], td.crc_raw) ^ cr;
       const uint32_t crc = (raw ^ crc_init[isize]) ^ 0xffffffffu;
       const uint8_t* tr = C + cpos + csize - 8;
       const uint32_t want = (uint32_t)tr[0] | ((uint32_t)tr[1] << 8) | ((uint32_t)tr[2] << 16) | ((uint32_t)tr[3] << 24);
@@ -2246,8 +2316,8 @@ __global__ __launch_bounds__(64 * TW, 3) void inflate_tail_kernel(
   if (warm == 0x9e3779b9u && lane == 64) status[b] = 0;  // (keeps the warming load alive)
   if (TIMING && lane == 0) {
     tim[gi * 16] = t1 - t0;      // decode: headers, tables, spec, rounds, emit
-    tim[gi * 16 + 1] = t2 - t1;  // resolve: carries, the first eight rows' hops and U loads
-    tim[gi * 16 + 2] = __builtin_amdgcn_s_memtime() - t2;  // rows, store, CRC
+    tim[gi * 16 + 1] = t3 - t2;  // resolve: the rows
+    tim[gi * 16 + 2] = __builtin_amdgcn_s_memtime() - t3;  // store, CRC
     tim[gi * 16 + 3] = 1;
     for (int k = 0; k < 5; k++) tim[gi * 16 + 4 + k] = tph[k];
   }
@@ -2271,6 +2341,7 @@ struct HostTables {
   uint32_t crc4[4][256];
   uint32_t slice[WG];
   uint32_t x2n[32];  // x^(2^k) mod P
+  uint32_t x8n[TOUT + 1];  // x^(8 n) mod P, n <= TOUT
   std::vector<uint32_t> init;  // CRC of n zero bytes with initial register ~0, n = 0..65536
   HostTables() : init(65537) {
     for (uint32_t i = 0; i < 256; i++) {
@@ -2292,6 +2363,7 @@ struct HostTables {
     uint32_t x8 = 1u << 31;          // x^0
     const uint32_t x8step = x2n[3];  // x^8
     for (int n = 0; n <= 65536; n++) {
+      if (n <= TOUT) x8n[n] = x8;
       init[(size_t)n] = h_mul(x8, 0xffffffffu);
       x8 = h_mul(x8, x8step);
     }
@@ -2323,6 +2395,7 @@ const uint32_t* inflate3_tables(int device) {
     ok = ok && hipMemcpyToSymbol(HIP_SYMBOL(c_crc4), H.crc4, sizeof H.crc4) == hipSuccess;
     ok = ok && hipMemcpyToSymbol(HIP_SYMBOL(c_slice_shift), H.slice, sizeof H.slice) == hipSuccess;
     ok = ok && hipMemcpyToSymbol(HIP_SYMBOL(c_x2n), H.x2n, sizeof H.x2n) == hipSuccess;
+    ok = ok && hipMemcpyToSymbol(HIP_SYMBOL(c_x8n), H.x8n, sizeof H.x8n) == hipSuccess;
     ok = ok && hipMalloc(&D.crc_init, sizeof(uint32_t) * H.init.size()) == hipSuccess;
     ok = ok && hipMemcpy(D.crc_init, H.init.data(), sizeof(uint32_t) * H.init.size(),
                          hipMemcpyHostToDevice) == hipSuccess;
@@ -2344,13 +2417,6 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
       (getenv("DQ_STORE") ? (uint32_t)atoi(getenv("DQ_STORE")) & 3u : 2u) |
       (getenv("DQ_NDEC") ? (uint32_t)(atoi(getenv("DQ_NDEC")) & 1023) << 8 : 0u) |
       (getenv("DQ_SEGBITS") ? (uint32_t)(atoi(getenv("DQ_SEGBITS")) & 1023) << 20 : 0u);
-  // DQ_CFG="nb,g" (tuning experiments: 4,1 default, 2,1 or 1,4); a function-local static const is
-  // initialised once, thread-safely (dq_decode_file_multi launches from one host thread per device)
-  static const int cfg = [] {
-    int nb = 4, g = 1;
-    if (const char* e = getenv("DQ_CFG")) sscanf(e, "%d,%d", &nb, &g);
-    return g == 4 ? 1 : nb == 2 ? 4 : 0;
-  }();
   // DQ_LDSPAD: extra dynamic LDS per workgroup (occupancy experiments: 80000 = one workgroup per CU)
   static const unsigned ldspad = getenv("DQ_LDSPAD") ? (unsigned)atoi(getenv("DQ_LDSPAD")) : 0u;
   // DQ_TAIL=0: no tail kernel (the block kernel decodes every deflate block itself)
@@ -2361,18 +2427,11 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
   hipLaunchKernelGGL((inflate_block_kernel<TM, NBT, GT>), dim3((unsigned)ngrid), dim3(WG), ldspad, s, C, \
                      blk_pos, blk_csize, blk_usize, uoff, ngrid, U, status, verify_crc, crc_init, tim, ov, \
                      sflags, sel, td)
-#define DQ_CFGS(TM)                       \
-  switch (cfg) {                          \
-    case 1: DQ_LAUNCH(TM, 1, 4); break;   \
-    case 4: DQ_LAUNCH(TM, 2, 1); break;   \
-    default: DQ_LAUNCH(TM, 4, 1); break;  \
-  }
-  if (tim) {
-    DQ_CFGS(true)
-  } else {
-    DQ_CFGS(false)
-  }
-#undef DQ_CFGS
+  // NB = 4 chunks of G = 1 byte per thread: (1, 4) measures the same, (2, 1) slower (round 5)
+  if (tim)
+    DQ_LAUNCH(true, 4, 1);
+  else
+    DQ_LAUNCH(false, 4, 1);
 #undef DQ_LAUNCH
   // DQ_TIMING: the block kernel's phases in tim[0, TIM_W ngrid), the tail kernel's in the 16 ngrid
   // words after them (16 per tail; dq_api allocates TIM_W + 16 per block)
