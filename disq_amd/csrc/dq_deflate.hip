@@ -68,7 +68,7 @@ constexpr int CH = BLK_U / NCH;          // 32640 bytes per chunk
 constexpr int PSEG = 32;                 // bytes per parse segment
 constexpr int PL = CH / PSEG;            // 1020 segments per chunk
 constexpr int MSEG = 1024;               // segment slots per chunk (staging, lane words)
-constexpr int PWG = 512;                 // threads per chunk workgroup
+constexpr int PWG = 1024;                // threads per chunk workgroup: one per segment
 constexpr int XW = 13600;                // window reach before the chunk start
 constexpr int NPMAX = CH + XW;           // bytes (positions) a chunk workgroup holds
 constexpr int HBITS = 11;                // hash buckets
@@ -89,12 +89,6 @@ constexpr int CONT_WORDS = 156;          // continuation symbols at most
 constexpr int OWN_CAP = 16;              // own matches (a 32-byte segment's, + one past its end)
 constexpr int CONT_CAP = 160;            // continuation matches (<= CONT_WORDS)
 constexpr int DENSE_WORDS = 2 * MSEG * MB_INL;  // per chunk
-#ifndef DQ_DEFLATE_STEAL
-#define DQ_DEFLATE_STEAL 0  // 1: idle lanes take odd segments nobody flowed into yet -- 6 % faster,
-                            // but whether an odd segment's parse starts at its own start or at the
-                            // even exit depends on a race, so the bytes differ from run to run
-                            // (profiles/r4bg_deflate_steal_ab.txt); htsjdk's writer is deterministic
-#endif
 #ifndef DQ_POOL_WORDS
 #define DQ_POOL_WORDS 32768  // (a build with a small pool exercises the exhaustion path)
 #endif
@@ -126,7 +120,7 @@ constexpr uint32_t SW_NONE = 0xffffffffu;
 constexpr int CI_OFF = 4 * NCH * MSEG;
 constexpr int TB_OFF = CI_OFF + NCH * CI_WORDS;
 constexpr int META_WORDS = TB_OFF + TB_WORDS;
-static_assert(PL * PSEG == CH && PL <= MSEG && NLANE <= CSEG * CWG, "segment layout");
+static_assert(PL * PSEG == CH && PL <= MSEG && PL <= PWG && NLANE <= CSEG * CWG, "segment layout");
 static_assert(CONT_WORDS < 256 && DENSE_WORDS <= 65536, "segment word fields");
 
 __constant__ uint32_t c_dcrc[256];
@@ -389,6 +383,7 @@ __device__ inline int mw_dist(uint32_t w) { return (int)(w >> 17) + 1; }
 
 
 constexpr int SCAT_WAVES = 4;  // waves of the bucket scatter: one position range each
+constexpr int NQ = (MSEG + PWG - 1) / PWG;  // segments per thread in the merge phase
 constexpr int CRC_BYTES = CH / (PWG - 64 * SCAT_WAVES) + 1;  // per thread of the other waves (the CRC)
 struct alignas(16) PLds {
   uint8_t in[NPMAX + 16];     // bytes [r0, ce) of the block (+ zero pad for the 4/8-byte compares)
@@ -408,7 +403,7 @@ struct alignas(16) PLds {
     uint32_t cnt[SCAT_WAVES - 1][1 << (HBITS - 1)];
   };
   int32_t hist[CI_CRC];       // literal/length and distance histograms of every symbol parsed
-  uint32_t wred[16];
+  uint32_t wred[2 * (PWG / 64)];  // scan totals per wave, then the CRC waves' registers
   int32_t misc[8];
 };
 static_assert(sizeof(PLds) <= 160 * 1024, "one chunk workgroup per CU");
@@ -923,7 +918,7 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
     for (int i = c0; i < c1; i++) cr = crc_t[(cr ^ L.in[i]) & 0xff] ^ (cr >> 8);
     if (c1 > c0) cr = gf2_mul(x8n((uint32_t)(np - c1)), cr);
     for (int o = 32; o >= 1; o >>= 1) cr ^= __shfl_xor(cr, o, 64);
-    if (lane == 0) L.wred[8 + wv - SCAT_WAVES] = cr;
+    if (lane == 0) L.wred[PWG / 64 + wv - SCAT_WAVES] = cr;
   }
   __syncthreads();
   {  // bucket ends: the last range's cursors
@@ -933,46 +928,19 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
   for (int i = t; i < CI_CRC; i += PWG) L.hist[i] = 0;  // (the CRC table is dead)
   __syncthreads();
   DTS();
-  // ---- speculative parses: segment j (32 bytes) from its start to the first symbol boundary at
-  //      or past its end (a match may run on past it).  Thread t starts on segment 2t; a lane that
-  //      ends an even segment claims the odd one after it and parses straight on into it (from
-  //      where it stands: that segment's parse starts where its predecessor's ended, so the
-  //      predecessor needs no continuation); the odd segments nobody flowed into are handed out by
-  //      an LDS counter, so a lane whose segments parse quickly takes more of them instead of
-  //      idling until the wave's slowest lane is done.
+  // ---- speculative parses: thread j parses segment j (32 bytes) from its start to the first
+  //      symbol boundary at or past its end (a match may run on past it).  Where a segment's parse
+  //      starts never depends on another lane's progress, so the output is the same on every run.
   uint32_t* const dense = stage + (b * NCH + c) * STAGE_CH_WORDS;
   uint32_t* const pool = dense + DENSE_WORDS;
   const Finder F{L, np, min(chain, MAXCAND), nice, good};
-  for (int i = t; i < MSEG; i += PWG) L.seg_mrg[i] = 0;  // odd segments' claim flags
-  __syncthreads();
   {
-    int j = 2 * t, s0 = 0, s1 = 0, x0 = 0, pe = 0;
+    const int j = t < nlc ? t : nlc;
+    const int s0 = xs + PSEG * j, s1 = min(np, s0 + PSEG);
+    int pe = s0;
     uint32_t st = 0;  // symbol starts in the segment (a deferred literal past its end: left out)
     MBuf mb{pool, &L.misc[3], &L.misc[7], OWN_CAP, 0};
-    auto take = [&](int jj, int x) __attribute__((always_inline)) {
-      j = jj;
-      s0 = xs + PSEG * j;
-      s1 = min(np, s0 + PSEG);
-      x0 = x;
-      pe = x;
-      st = 0;
-      mb.n = 0;
-    };
-    // the next odd segment from the counter that no lane has flowed into (nlc: none left)
-    auto pull = [&]() __attribute__((always_inline)) -> int {
-#if DQ_DEFLATE_STEAL
-      for (;;) {
-        const int q = 2 * atomicAdd(&L.misc[0], 1) + 1;
-        if (q >= nlc) return nlc;
-        if (atomicCAS(&L.seg_mrg[q], 0u, 1u) == 0u) return q;
-      }
-#else
-      return nlc;
-#endif
-    };
-    const int j0 = 2 * t < nlc ? 2 * t : pull();
-    if (j0 < nlc) take(j0, xs + PSEG * j0);
-    else j = nlc;
+    mb.n = 0;
     const int own_lazy = lazy, own_end = np;
     parse_lanes(
         F, own_lazy, own_end, s0,
@@ -985,24 +953,14 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
           }
         },
         [&](int x) __attribute__((always_inline)) -> int {
-          while (j < nlc && x >= s1) {  // segment j is parsed: publish it
-            sw[SW_OWNM * NCH * MSEG + j] = mb.publish(dense, &L.misc[2]);
-            sw[SW_OWN * NCH * MSEG + j] = (uint32_t)x0 | (uint32_t)x << 16;
-            L.seg_exit[j] = (uint32_t)x;
-            L.sbits[j] = st;
-            if (!(j & 1) && j + 1 < nlc && atomicCAS(&L.seg_mrg[j + 1], 0u, 1u) == 0u) {
-              take(j + 1, x);  // flow on into the odd segment after it, from x
-              continue;        // (x may lie past it too: then it is published empty)
-            }
-            const int q = pull();
-            if (q >= nlc) {
-              j = nlc;
-              break;
-            }
-            take(q, xs + PSEG * q);
-            return s0;
-          }
-          return j < nlc ? x : NX_STOP;
+          if (j >= nlc) return NX_STOP;
+          if (x < s1) return x;
+          // segment j is parsed: publish it
+          sw[SW_OWNM * NCH * MSEG + j] = mb.publish(dense, &L.misc[2]);
+          sw[SW_OWN * NCH * MSEG + j] = (uint32_t)s0 | (uint32_t)x << 16;
+          L.seg_exit[j] = (uint32_t)x;
+          L.sbits[j] = st;
+          return NX_STOP;
         });
   }
   __threadfence_block();
@@ -1129,9 +1087,9 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
   }
   __syncthreads();
   for (int r = 0; (1 << r) < nlc; r++) {
-    uint32_t jj[2] = {MSEG, MSEG};
+    uint32_t jj[NQ];
 #pragma unroll
-    for (int q = 0; q < 2; q++) {
+    for (int q = 0; q < NQ; q++) {
       const int i = t + q * PWG;
       const uint32_t g = i < nlc ? jmp[i] : (uint32_t)MSEG;
       if (g < (uint32_t)MSEG && L.seg_mark[i]) L.seg_mark[g] = 1;
@@ -1139,15 +1097,15 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
     }
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < 2; q++)
+    for (int q = 0; q < NQ; q++)
       if (t + q * PWG < nlc) jmp[t + q * PWG] = jj[q];
     __syncthreads();
   }
   // the first position of each segment on the parse: set by the segment that merged into it
-  bool rch[2];
-  uint32_t mw[2];
+  bool rch[NQ];
+  uint32_t mw[NQ];
 #pragma unroll
-  for (int q = 0; q < 2; q++) {
+  for (int q = 0; q < NQ; q++) {
     const int i = t + q * PWG;
     rch[q] = i < nlc && L.seg_mark[i];
     mw[q] = i < nlc ? L.seg_mrg[i] : 0u;
@@ -1155,7 +1113,7 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
   __syncthreads();
   if (t == 0) jmp[0] = (uint32_t)xs;
 #pragma unroll
-  for (int q = 0; q < 2; q++) {
+  for (int q = 0; q < NQ; q++) {
     const int g = mrg_lane(mw[q]);
     if (rch[q] && g < MSEG) jmp[g] = (uint32_t)(xs + PSEG * g + mrg_off(mw[q]));
     if (rch[q] && mrg_over(mw[q])) L.misc[7] = 1;
@@ -1164,7 +1122,7 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
   // each segment's range on the parse, and the histograms of the parse's symbols: its literals'
   // bytes and its matches, walked as the code kernel walks them
 #pragma unroll
-  for (int q = 0; q < 2; q++) {
+  for (int q = 0; q < NQ; q++) {
     const int i = t + q * PWG;
     if (i >= MSEG) continue;
     if (!rch[q]) {
@@ -1194,7 +1152,7 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
   for (int i = t; i < CI_CRC; i += PWG) ci[i] = L.hist[i];
   if (t == 0) {
     uint32_t cr = 0;
-    for (int w = 0; w < PWG / 64 - SCAT_WAVES; w++) cr ^= L.wred[8 + w];
+    for (int w = 0; w < PWG / 64 - SCAT_WAVES; w++) cr ^= L.wred[PWG / 64 + w];
     ci[CI_CRC] = (int32_t)cr;
     ci[CI_OVER] = L.misc[7];
     ci[CI_BYTES] = ce - cs;

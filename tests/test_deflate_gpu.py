@@ -81,7 +81,7 @@ def zlib5_bgzf_size(data):
 
 @pytest.mark.parametrize("name", ["1.bam", "hiseq_part-r-00000.bam", "HiSeq.10000.vcf.bgz", "wgs"])
 def test_ratio_at_zlib_level5(golden, name):
-    """The chunked LDS parse (two 32640-byte chunks per block, 15000 bytes of reach before a chunk, a 4-byte bucket key) keeps
+    """The chunked LDS parse (two 32640-byte chunks per block, 13600 bytes of reach before a chunk, a 4-byte bucket key) keeps
     htsjdk's level-5 ratio on the golden BAM / VCF streams and the synthetic WGS stream
     (tools/deflate_model.c, profiles/r4_deflate_chunk_model.txt): at most 0.5 % larger."""
     if name == "wgs":
@@ -163,8 +163,8 @@ def test_randomized_length_roundtrip_sweep():
 def test_output_is_deterministic():
     """Two compressions of the same bytes are byte-identical, as htsjdk's
     BlockCompressedOutputStream under HeaderlessBamOutputFormat.java:26-50 is: a WGS stream and the
-    period-3 stream whose ratio moved between runs while odd segments were raced for
-    (DQ_DEFLATE_STEAL, off by default)."""
+    period-3 stream whose ratio moved between runs while round 4's lanes raced for odd segments
+    (each segment's parse now starts at its own start, one lane per segment)."""
     r = synth.generate(20000, seed=5, nthreads=4)
     wgs = B.inflate_all(r.bam)
     per3 = (b"ACG" * 200000)[:500000]

@@ -290,6 +290,13 @@ int main(int argc, char** argv) {
       {"  4-byte hash, 12/8/16", 64, 1, 0, 12, 11, 0, 8, 16, 0, 32640, 15000, 0, 1},
       {"  4-byte hash, 8/8/16", 64, 1, 0, 8, 11, 0, 8, 16, 0, 32640, 15000, 0, 1},
       {"  4-byte hash, 8/4/16", 64, 1, 0, 8, 11, 0, 4, 16, 0, 32640, 15000, 0, 1},
+      // round 5: two parse workgroups per CU need < 80 KB of LDS each: quarter-block chunks
+      {"4-byte 32/16/32 halves C=32640 X=13600 seg64 (round 4)", 64, 1, 0, 32, 11, 0, 16, 32, 0, 32640, 13600, 0, 1},
+      {"4-byte 32/16/32 quarters C=16320 X=4096 seg32", 32, 1, 0, 32, 11, 0, 16, 32, 0, 16320, 4096, 0, 1},
+      {"4-byte 32/16/32 quarters C=16320 X=6144 seg32", 32, 1, 0, 32, 11, 0, 16, 32, 0, 16320, 6144, 0, 1},
+      {"4-byte 32/16/32 quarters C=16320 X=6896 seg32", 32, 1, 0, 32, 11, 0, 16, 32, 0, 16320, 6896, 0, 1},
+      {"4-byte 32/16/32 quarters C=16320 X=8192 seg32", 32, 1, 0, 32, 11, 0, 16, 32, 0, 16320, 8192, 0, 1},
+      {"4-byte 32/16/32 quarters C=16320 X=16384 seg32", 32, 1, 0, 32, 11, 0, 16, 32, 0, 16320, 16384, 0, 1},
   };
   int nc = sizeof cfgs / sizeof cfgs[0];
   long nb = (n + BLK - 1) / BLK;
