@@ -1906,7 +1906,9 @@ __global__ __launch_bounds__(64 * TW, 4) void inflate_tail_kernel(
     const TailDesc* __restrict__ tails, uint64_t* __restrict__ tim) {
   constexpr uint32_t CKI = CKI_DEFAULT;
   __shared__ LdsW Ls[TW];
-  const int wv = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+  // the wave's index is uniform: the tail's descriptor and block fields become scalar loads held in
+  // SGPRs (as vector loads they held 10 VGPRs for the whole kernel and forced spills to scratch)
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = (int)(threadIdx.x & 63);
   const int64_t gi = (int64_t)blockIdx.x * TW + wv;
   if (gi >= ngrid) return;
   const TailDesc td = tails[gi];

@@ -13,6 +13,11 @@ done
 for v in "$@"; do
   echo "== $v"
   f=$(find $out/kt_$v -name "*kernel_stats.csv" | head -1)
+  if [ -z "$f" ]; then  # (this rocprofv3 writes a rocpd database by default)
+    db=$(find $out/kt_$v -name "*.db" | head -1)
+    f=$out/kt_$v/kernel_stats.csv
+    python3 tools/rocpd_stats.py "$db" "$f" > /dev/null
+  fi
   python3 - "$f" <<'PY'
 import csv, sys
 for r in csv.DictReader(open(sys.argv[1])):
