@@ -742,13 +742,13 @@ def write_path_bench(args):
            "roofline": {"bound": "hbm", "achieved": round((len(u) + n) / ms / 1e6, 2),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round((len(u) + n) / ms / 1e6 / HBM_PEAK_GBS, 5),
-                        "traffic_over_alg": 3.9,
-                        "traffic_src": "profiles/r4az_deflate_pmc.txt (3.40 GB per compression of "
-                                       "0.649 GB: 3.9x the 0.871 GB algorithmic bytes)",
-                        "limiter": "LZ77 parse latency of bgzf_parse_kernel (89 % of device time, "
-                                   "one 160 KB workgroup per CU)"},
-           "evidence": "profiles/r4bd_deflate_forced_steps_ab.txt, profiles/r4az_deflate_pmc.txt "
-                       "(traffic 3.9x the input read + output written)"}
+                        "traffic_over_alg": 4.01,
+                        "traffic_src": "profiles/r5o_deflate_pmc.txt (0.872 GB per compression of "
+                                       "0.162 GB: 4.01x the 0.218 GB algorithmic bytes)",
+                        "limiter": "LZ77 parse latency of bgzf_parse_kernel (~88 % of device time; "
+                                   "one 160 KB, 1024-thread workgroup per CU: 16 waves)"},
+           "evidence": "profiles/r5n_deflate_parse_1024.txt (A/B, per-phase cycles), "
+                       "profiles/r5o_deflate_pmc.txt (SQ counters and traffic of the three kernels)"}
     log("write path:", out)
     return out
 
