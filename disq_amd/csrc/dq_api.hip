@@ -160,7 +160,7 @@ struct dq_ctx {
   DevBuf plans, plan_best;  // plan_best: the record guesser's per-split minima (planning scratch)
   std::vector<SplitPlan> plans_h;
   // records
-  DevBuf segs, segcnt, segbase, rec_lin, pages;
+  DevBuf segs, segcnt, segbase, segoff, rec_lin, pages;
   DevBuf long_ent, long_cnt;  // long records' pieces (decode_records: hashed by many threads)
   DevBuf f_voff, f_bs, f_ref, f_pos, f_lseq, f_nref, f_npos, f_tlen, f_flag, f_bin, f_ncig, f_mapq,
       f_lrn, f_hash;
@@ -918,9 +918,15 @@ static int run_pipeline(dq_ctx* ctx) {
     if ((rc = ensure_all(ctx, ctx->segs, sizeof(Seg) * (size_t)(nseg + 1)))) return rc;
     if ((rc = ensure_all(ctx, ctx->segcnt, sizeof(int64_t) * (size_t)(nseg + 1)))) return rc;
     if ((rc = ensure_all(ctx, ctx->segbase, sizeof(int64_t) * (size_t)(nseg + 1)))) return rc;
+    // the walk's recorded record starts (64 KiB segments): 1 KiB per segment, 1.6 % of U
+    uint16_t* offs = nullptr;
+    if (SEG <= 65536) {
+      if ((rc = ensure_all(ctx, ctx->segoff, 2 * (size_t)SEG_OFF_CAP * (size_t)nseg))) return rc;
+      offs = ctx->segoff.as<uint16_t>();
+    }
     HIPCHK(hipMemsetAsync(d_broken, 0, 8, s));
     launch_seg_spec(ctx->U.as<uint8_t>(), ulen, is_eof, chain_end, ctx->d_ref_len.as<int32_t>(), ctx->n_ref,
-                    ctx->segs.as<Seg>(), nseg, SEG, start_lin, s);
+                    ctx->segs.as<Seg>(), nseg, SEG, start_lin, offs, s);
     launch_seg_link(ctx->segs.as<Seg>(), nseg, SEG, start_lin, chain_end, d_broken, s);
     // the link check and the record count come back together; a broken link (a guesser false
     // positive) is repaired serially and the count taken again
@@ -949,7 +955,7 @@ static int run_pipeline(dq_ctx* ctx) {
     const size_t nr = (size_t)std::max<int64_t>(1, nrec);
     if ((rc = ensure_all(ctx, ctx->rec_lin, 8 * nr))) return rc;
     launch_seg_emit2(ctx->U.as<uint8_t>(), ulen, ctx->segs.as<Seg>(), ctx->segbase.as<int64_t>(),
-                     nseg, ctx->rec_lin.as<int64_t>(), s);
+                     nseg, ctx->rec_lin.as<int64_t>(), s, offs, SEG, start_lin);
     DevBuf* b8[] = {&ctx->f_voff, &ctx->f_hash};
     DevBuf* b4[] = {&ctx->f_bs, &ctx->f_ref, &ctx->f_pos, &ctx->f_lseq, &ctx->f_nref, &ctx->f_npos,
                     &ctx->f_tlen};

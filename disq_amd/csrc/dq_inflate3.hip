@@ -113,6 +113,10 @@ constexpr int TOUT = 4096;            // tail output bytes one wave holds
 constexpr int TAIL_MAX_BITS = 32768;  // tail deflate bits (64 speculative lanes of <= 512 bits)
 constexpr int TW = 4;                 // tails (waves) per tail-kernel workgroup
 constexpr int T_NCK = 4;              // checkpoints per speculative lane in the tail kernel
+#ifndef DQ_TAIL_SEG
+#define DQ_TAIL_SEG 96
+#endif
+constexpr int TAIL_SEG_MIN = DQ_TAIL_SEG;  // shortest speculative segment of a tail (bits)
 constexpr int TIM_W = 32;  // DQ_TIMING words per block (dq_api.hip reads the same layout)
 struct TailDesc {
   int32_t pos;       // bit position (from the block's aligned deflate base) of the tail's header
@@ -2033,7 +2037,7 @@ __global__ __launch_bounds__(64 * TW, 4) void inflate_tail_kernel(
     tick(1);
     // ---- speculative segments, one per lane (registers hold the per-lane arrays)
     const uint32_t span = endbits - a;
-    const int nl = (int)max(1u, min(64u, span / 96u));
+    const int nl = (int)max(1u, min(64u, span / (uint32_t)TAIL_SEG_MIN));
     const uint32_t seg = (span + nl - 1) / nl;
     const bool act = lane < nl;
     const uint32_t sB = a + (uint32_t)lane * seg;

@@ -180,13 +180,15 @@ struct Seg {
   int64_t start;   // speculated / exact first chain position in the segment (-1 none)
   int64_t exit;    // first chain position >= segment end reached from `start`
   int64_t count;   // records started in [start, segment end)
-  int32_t exact;
+  int32_t exact;   // bit 1: seg_walk recorded the record starts (SEG_OFF_CAP u16 offsets from the
+                   // segment start); a re-walk by seg_fix clears it
   int32_t status;
 };
+constexpr int SEG_OFF_CAP = 512;  // record starts one segment's walk records (64 KiB segments)
 // Segments cover [start_lin, chain_end) (record starts wanted); ulen bounds the readable bytes.
 void launch_seg_spec(const uint8_t* U, int64_t ulen, int32_t u_is_eof, int64_t chain_end,
                      const int32_t* ref_len, int32_t n_ref, Seg* segs, int64_t nseg,
-                     int64_t seg_bytes, int64_t start_lin, hipStream_t s);
+                     int64_t seg_bytes, int64_t start_lin, uint16_t* offs, hipStream_t s);
 void launch_seg_link(const Seg* segs, int64_t nseg, int64_t seg_bytes, int64_t start_lin,
                      int64_t ulen, int32_t* d_broken, hipStream_t s);
 void launch_seg_fix2(const uint8_t* U, int64_t ulen, int32_t u_is_eof, int64_t chain_end,
@@ -194,7 +196,8 @@ void launch_seg_fix2(const uint8_t* U, int64_t ulen, int32_t u_is_eof, int64_t c
                      int64_t seg_bytes, int64_t start_lin, int32_t* d_status, hipStream_t s);
 void launch_seg_counts(const Seg* segs, int64_t nseg, int64_t* counts, hipStream_t s);
 void launch_seg_emit2(const uint8_t* U, int64_t ulen, const Seg* segs, const int64_t* base,
-                      int64_t nseg, int64_t* rec_lin, hipStream_t s);
+                      int64_t nseg, int64_t* rec_lin, hipStream_t s, const uint16_t* offs = nullptr,
+                      int64_t seg_bytes = 0, int64_t start_lin = 0);
 
 // Sparse (windowed) record chains: every window is a run of inflated U bytes (whole-file layout)
 // with an exact first record start; segments [seg0, next window's seg0) belong to it.

@@ -656,18 +656,60 @@ __global__ __launch_bounds__(NT) void seg_spec_kernel(const uint8_t* __restrict_
 }
 
 // The walks of all segments, one lane each (a walk is a chain of dependent loads: many walks per
-// wave keep many in flight).
+// wave keep many in flight).  With `offs` (64 KiB segments), the walk also records its record
+// starts as 16-bit offsets from the segment start, four per 8-byte store, so that seg_emit copies
+// them instead of walking the chain a second time (round 5: the re-walk fetched a line of U per
+// record again, 2.9 ms of the 12.5 GB file's 214 ms step).
 __global__ __launch_bounds__(256) void seg_walk_kernel(const uint8_t* __restrict__ U, int64_t ulen,
                                                        int32_t u_is_eof, Seg* __restrict__ segs,
                                                        int64_t nseg, int64_t seg_bytes,
-                                                       int64_t start_lin, int64_t chain_end) {
+                                                       int64_t start_lin, int64_t chain_end,
+                                                       uint16_t* __restrict__ offs) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nseg) return;
   Seg g = segs[s];
   if (g.start < 0) return;
-  const int64_t se = min(chain_end, start_lin + (s + 1) * seg_bytes);
-  int64_t ex, cnt;
-  const int r = walk(U, ulen, u_is_eof, g.start, se, &ex, &cnt);
+  const int64_t sb = start_lin + s * seg_bytes;
+  const int64_t se = min(chain_end, sb + seg_bytes);
+  int64_t ex = 0, cnt = 0;
+  int r;
+  if (offs) {
+    uint64_t* const o64 = reinterpret_cast<uint64_t*>(offs + s * SEG_OFF_CAP);
+    int64_t p = g.start, n = 0;
+    uint64_t acc = 0;
+    r = 0;
+    for (;;) {
+      if (p >= se) {
+        ex = p;
+        break;
+      }
+      if (p + 4 > ulen) {
+        if (u_is_eof) {
+          ex = END_CHAIN;
+          break;
+        }
+        r = 4;
+        break;
+      }
+      const int32_t bs = ld32(U, p);
+      if (bs < 32) {
+        r = ST_BAD_CODE;
+        break;
+      }
+      acc |= (uint64_t)(uint16_t)(p - sb) << (16 * (n & 3));
+      if ((n & 3) == 3 && n < SEG_OFF_CAP) {
+        o64[n >> 2] = acc;
+        acc = 0;
+      }
+      n++;
+      p += 4 + (int64_t)bs;
+    }
+    if (r == 0 && (n & 3) && n <= SEG_OFF_CAP) o64[n >> 2] = acc;
+    cnt = n;
+    g.exact = (g.exact & 1) | (r == 0 && n <= SEG_OFF_CAP ? 2 : 0);
+  } else {
+    r = walk(U, ulen, u_is_eof, g.start, se, &ex, &cnt);
+  }
   g.status = r;
   if (r == 0) {
     g.exit = ex;
@@ -703,6 +745,7 @@ __global__ void seg_fix_kernel(const uint8_t* __restrict__ U, int64_t ulen, int3
     if (g.start != in || g.status != 0) {
       int64_t ex = -1, cnt = 0;
       int r = walk(U, ulen, u_is_eof, in, se, &ex, &cnt);
+      g.exact = 0;  // the recorded starts were another walk's
       g.start = in;
       g.status = r;
       g.exit = ex;
@@ -712,7 +755,7 @@ __global__ void seg_fix_kernel(const uint8_t* __restrict__ U, int64_t ulen, int3
         return;
       }
     }
-    g.exact = 1;
+    g.exact |= 1;
     in = g.exit;
   }
 }
@@ -759,7 +802,7 @@ __global__ __launch_bounds__(64) void seg_emit_kernel(const uint8_t* __restrict_
     const Seg g = segs[s];
     p = g.start;
     o = base[s];
-    left = g.count;
+    left = (g.exact & 2) ? 0 : g.count;  // recorded by the walk: seg_copy_kernel writes them
   }
   for (;;) {
     const int n = (int)min(left, (int64_t)EMIT_R);
@@ -778,6 +821,22 @@ __global__ __launch_bounds__(64) void seg_emit_kernel(const uint8_t* __restrict_
     }
     o += n;
     left -= n;
+  }
+}
+
+// The record starts the walk recorded (Seg.exact bit 1): one wave per segment copies them to
+// rec_lin, consecutive lanes on consecutive entries (grid-stride over the segments).
+__global__ __launch_bounds__(64) void seg_copy_kernel(const Seg* __restrict__ segs,
+                                                      const int64_t* __restrict__ base, int64_t nseg,
+                                                      const uint16_t* __restrict__ offs,
+                                                      int64_t seg_bytes, int64_t start_lin,
+                                                      int64_t* __restrict__ rec_lin) {
+  for (int64_t s = blockIdx.x; s < nseg; s += gridDim.x) {
+    const int32_t ex = segs[s].exact;
+    if (!(ex & 2)) continue;
+    const int64_t cnt = segs[s].count, o = base[s], sb = start_lin + s * seg_bytes;
+    const uint16_t* of = offs + s * SEG_OFF_CAP;
+    for (int64_t k = threadIdx.x; k < cnt; k += 64) rec_lin[o + k] = sb + (int64_t)of[k];
   }
 }
 
@@ -1562,7 +1621,7 @@ void launch_first_record(const uint8_t* U, int64_t ulen, int32_t u_is_eof, const
 void launch_seg_spec(const uint8_t* U, int64_t ulen, int32_t u_is_eof, int64_t chain_end,
                      const int32_t* ref_len,
                      int32_t n_ref, Seg* segs, int64_t nseg, int64_t seg_bytes, int64_t start_lin,
-                     hipStream_t s) {
+                     uint16_t* offs, hipStream_t s) {
   if (nseg <= 0) return;
   if (seg_bytes > 64 * 1024)  // long records (segments sized from the guesser's record span)
     hipLaunchKernelGGL(seg_spec_kernel<256>, dim3((unsigned)std::min<int64_t>(nseg, 16384)), dim3(256), 0, s, U,
@@ -1571,7 +1630,8 @@ void launch_seg_spec(const uint8_t* U, int64_t ulen, int32_t u_is_eof, int64_t c
     hipLaunchKernelGGL(seg_spec_kernel<64>, dim3((unsigned)std::min<int64_t>(nseg, 16384)), dim3(64), 0, s, U,
                        ulen, u_is_eof, ref_len, n_ref, segs, nseg, seg_bytes, start_lin, chain_end);
   hipLaunchKernelGGL(seg_walk_kernel, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, U, ulen,
-                     u_is_eof, segs, nseg, seg_bytes, start_lin, chain_end);
+                     u_is_eof, segs, nseg, seg_bytes, start_lin, chain_end,
+                     seg_bytes <= 65536 ? offs : nullptr);
 }
 
 void launch_seg_fix2(const uint8_t* U, int64_t ulen, int32_t u_is_eof, int64_t chain_end,
@@ -1594,9 +1654,13 @@ void launch_seg_counts(const Seg* segs, int64_t nseg, int64_t* counts, hipStream
 }
 
 void launch_seg_emit2(const uint8_t* U, int64_t, const Seg* segs, const int64_t* base,
-                      int64_t nseg, int64_t* rec_lin, hipStream_t s) {
+                      int64_t nseg, int64_t* rec_lin, hipStream_t s, const uint16_t* offs,
+                      int64_t seg_bytes, int64_t start_lin) {
   hipLaunchKernelGGL(seg_emit_kernel, dim3((unsigned)((nseg + 63) / 64)), dim3(64), 0, s, U, segs,
                      base, nseg, rec_lin);
+  if (offs && seg_bytes <= 65536)
+    hipLaunchKernelGGL(seg_copy_kernel, dim3((unsigned)std::min<int64_t>(nseg, 32768)), dim3(64), 0, s,
+                       segs, base, nseg, offs, seg_bytes, start_lin, rec_lin);
 }
 
 void launch_block_stats(const int64_t* blk_pos, const int32_t* blk_cs, const int64_t* uoff,
