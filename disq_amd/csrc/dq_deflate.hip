@@ -33,7 +33,7 @@
 //      claimed it first.  A parse step depends on its position alone, so two parses that reach the
 //      same position continue identically: from its exit, each segment's parse is continued until
 //      it hits a symbol boundary of a later segment's parse (usually within a few symbols) and the
-//      merge is recorded; after `fmerge` continuation symbols without one (default 2) it is ended
+//      merge is recorded; after `fmerge` continuation symbols without one (default 1) it is ended
 //      on the next boundary of the later segment with a shortened match.  Pointer jumping over the
 //      merges from segment 0 marks the segments on the chunk's one parse and the symbol each
 //      starts from.  The merged parse is valid but not always the one a single sequential pass
@@ -94,7 +94,7 @@ constexpr int DENSE_WORDS = 2 * MSEG * MB_INL;  // per chunk
 #endif
 constexpr int POOL_WORDS = DQ_POOL_WORDS;       // per chunk
 constexpr int64_t STAGE_CH_WORDS = DENSE_WORDS + POOL_WORDS;  // per chunk
-constexpr int FMERGE = 2;  // continuation symbols before a forced merge (default; profiles/r4aj_*)
+constexpr int FMERGE = 1;  // continuation symbols before a forced merge (default; profiles/r4aj_*, r5zc_*)
 constexpr int MAX_DEFLATE = 65536 - 26;  // BSIZE limit: 18-byte header + payload + 8 trailer
 // a block's output slot: the member's 18-byte header at SLOT_HDR, the deflate payload 16-byte
 // aligned at SLOT_HDR + 18, the trailer after it
@@ -1631,9 +1631,10 @@ void launch_bgzf_deflate(const uint8_t* src, int64_t n_in, int64_t blk0, int64_t
   // DQ_DEFLATE="chain,lazy,nice[,good[,fmerge]]": match-search effort (default 32,16,32,8: zlib
   // level 5's own settings; with the 4-byte bucket key that is ratio 2.92 on the WGS stream against
   // htsjdk's 2.857, profiles/r4m_deflate_sweep.txt; good 0 = always the full chain) and the
-  // continuation symbols before a forced merge (default 2: ratio 2.919 against 2.924 at 116, 7%
-  // faster, profiles/r4aj_deflate_fmerge.txt); read at every launch, so a test can sweep settings
-  // in one process
+  // continuation symbols before a forced merge (default 1: ratio 2.912, 14.55 GB/s, against 2.918
+  // and 14.03 at 2 -- round 4's default, 2.924 at 116; 0 gives 2.902 and takes the HiSeq part past
+  // zlib level 5 + 0.5 %: profiles/r4aj_deflate_fmerge.txt, r5zc_deflate_fmerge.txt); read at
+  // every launch, so a test can sweep settings in one process
   int cc = 32, cl = 16, cn = 32, cg = 8, cf = FMERGE;
   if (const char* e = getenv("DQ_DEFLATE")) sscanf(e, "%d,%d,%d,%d,%d", &cc, &cl, &cn, &cg, &cf);
   cf = std::max(0, std::min(cf, CONT_WORDS - 40));
