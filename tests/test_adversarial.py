@@ -131,6 +131,28 @@ def giant_bam():
     return B.bgzf(u2, level=5), off, len(giant)
 
 
+def dense_bam(n_tiny=6000):
+    """6000 minimal records (44 bytes: a one-base read named "a") in a row inside a synthetic WGS
+    BAM: a 64 KiB record-chain segment holds ~1490 starts there, more than the 512 the chain walk
+    records (SEG_OFF_CAP), so those segments are walked a second time while their neighbours are
+    copied from the recorded starts."""
+    import struct
+    r = synth.generate(900, seed=31, nthreads=4)
+    u = B.inflate_all(r.bam)
+    off, _ = B.record_spans(u)[450]
+    ref_id, pos = struct.unpack_from("<ii", u, off + 4)
+    tiny = B.make_record(ref_id, pos, b"a", 1)
+    assert len(tiny) == 44
+    return B.bgzf(u[:off] + tiny * n_tiny + u[off:], level=5), n_tiny
+
+
+def test_oracle_dense_records():
+    bam, n_tiny = dense_bam()
+    allr = O.OracleBam(bam).read_all()
+    assert len(allr) == 900 + n_tiny  # (synth's unplaced tail is part of the 900)
+    assert (allr["block_size"] == 40).sum() == n_tiny
+
+
 def test_oracle_max_read_size_empty_partition():
     """Split 1 starts two blocks into the giant record and its blocks reach past the record's
     end: the first 10 M positions hold no record start, so the split gets no chunk, and the
@@ -205,3 +227,12 @@ def test_gpu_max_read_size_empty_partition():
     b = assert_parity(bam, split)
     # getPathChunks drops the null chunk: split 1 contributes no partition
     assert len(b["part_offset"]) - 1 == 1
+
+
+@pytest.mark.gpu
+def test_gpu_dense_records_recorded_and_rewalked_segments():
+    from test_gpu_parity import assert_parity
+    bam, n_tiny = dense_bam()
+    for split in (0, 70000, 150001):
+        b = assert_parity(bam, split)
+    assert (b["block_size"] == 40).sum() == n_tiny
