@@ -64,6 +64,16 @@ constexpr int NDEC = 512;         // speculative decode lanes (<= WG)
 constexpr uint32_t OV_DEFAULT = 96;  // speculative warm-up bits before each segment
 constexpr int OUTCAP = 65536 + 24;  // + alignment shift (<= 15) + descriptor overhang; bm 8-aligned
 constexpr int RES_NXT = 2048;        // resolve batch bytes (NB * G * WG) at most
+// resolve shape (tuning builds): NB chunks of G * WG bytes per batch; DQ_CSTEP = 1: one ordered
+// step per chunk instead of per 512 bytes (longer in-step chains, fewer barriers)
+#ifndef DQ_CSTEP
+#define DQ_CSTEP 0
+#endif
+#ifndef DQ_RES_NB
+#define DQ_RES_NB 4
+#define DQ_RES_G 1
+#endif
+
 
 // 16-bit decode table layout: [litlen root | litlen subtables | dist root | dist subtables]
 constexpr int LR = 10, DR = 8;            // root bits
@@ -1380,6 +1390,8 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   constexpr int CH = G * WG;
   constexpr int BATCH = NB * CH;
   constexpr int NE = NB * G;
+  // DQ_CSTEP: one step (and one barrier) per chunk of G * 512 bytes instead of per 512 bytes
+  constexpr bool CSTEP = DQ_CSTEP != 0 && G > 1;
   static_assert(BATCH <= RES_NXT, "the batch's next-pointers fit the resolve scratch");
   static_assert(65536 / BATCH <= 32, "one carry slot per batch");
   uint16_t* nxt = L.u.r.nxt;
@@ -1418,7 +1430,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
 #pragma unroll
     for (int k = 0; k < NB; k++) {
       const int32_t g0 = b0 + k * CH + G * t;
-      const int32_t sbk = b0 + k * CH + ((G * t) & ~511);
+      const int32_t sbk = b0 + k * CH + (CSTEP ? 0 : ((G * t) & ~511));
 #pragma unroll
       for (int i = 0; i < G; i++) {
         const int e = k * G + i;
@@ -1464,7 +1476,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     for (int e = 0; e < NE; e++) {
       const bool pd = (pending >> e) & 1;
       const int32_t p = xs[e], q = qv[e];
-      const int32_t sbk = b0 + (e / G) * CH + ((G * t) & ~511);
+      const int32_t sbk = b0 + (e / G) * CH + (CSTEP ? 0 : ((G * t) & ~511));
       const bool fin = pd && (q == p || q < sbk);
       fr[e] = fin ? q : fr[e];
       xs[e] = pd && !fin ? q : p;
@@ -1519,8 +1531,8 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
 #pragma unroll
     for (int k = 0; k < NB; k++) {
 #pragma unroll
-      for (int j = 0; j < G; j++) {
-        const bool mine = ((G * t) >> 9) == j;
+      for (int j = 0; j < (CSTEP ? 1 : G); j++) {
+        const bool mine = CSTEP || ((G * t) >> 9) == j;
         const int32_t g0 = bs + k * CH + G * t;
         uint8_t v[G];
         if (mine)
@@ -2435,9 +2447,9 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
                      sflags, sel, td)
   // NB = 4 chunks of G = 1 byte per thread: (1, 4) measures the same, (2, 1) slower (round 5)
   if (tim)
-    DQ_LAUNCH(true, 4, 1);
+    DQ_LAUNCH(true, DQ_RES_NB, DQ_RES_G);
   else
-    DQ_LAUNCH(false, 4, 1);
+    DQ_LAUNCH(false, DQ_RES_NB, DQ_RES_G);
 #undef DQ_LAUNCH
   // DQ_TIMING: the block kernel's phases in tim[0, TIM_W ngrid), the tail kernel's in the 16 ngrid
   // words after them (16 per tail; dq_api allocates TIM_W + 16 per block)
