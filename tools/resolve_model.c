@@ -136,6 +136,7 @@ static int tokenize(const uint8_t *d, size_t n, Tok *tk, int cap, int *nblocks, 
 // per block statistics, summed
 typedef struct {
   long blocks, toks, lits, matches, mbytes, bytes, overlap, short16;
+  long lvl_sum, rlvl_sum, lvl_h[6], rlvl_h[6];  // match levels (round in which its source is final)
   long depth_sum, depth_max, rdepth_sum, rdepth_max, straddle;
   long lenh[8], disth[8];
   long step_rounds[8][2];  // steps S = 256 << i: [sum of max rounds per step over steps, steps]
@@ -214,6 +215,8 @@ int main(int argc, char **argv) {
       }
       depth[i] = dm + 1;
       if (depth[i] > bdepth) bdepth = depth[i];
+      S.lvl_sum += depth[i];
+      S.lvl_h[depth[i] <= 1 ? 0 : depth[i] <= 2 ? 1 : depth[i] <= 4 ? 2 : depth[i] <= 8 ? 3 : depth[i] <= 32 ? 4 : 5]++;
       // redirect: while [s, e) lies inside one match's output, move it back by that distance
       int jumps = 0;
       for (;;) {
@@ -234,6 +237,8 @@ int main(int argc, char **argv) {
       S.straddle += strad;
       rd[i] = rm + 1;
       if (rd[i] > brd) brd = rd[i];
+      S.rlvl_sum += rd[i];
+      S.rlvl_h[rd[i] <= 1 ? 0 : rd[i] <= 2 ? 1 : rd[i] <= 4 ? 2 : rd[i] <= 8 ? 3 : rd[i] <= 32 ? 4 : 5]++;
     }
     // per byte: hops to a literal, and to a byte before the byte's window of W bytes; synchronous
     // pointer-jumping rounds per window (max over its bytes)
@@ -375,6 +380,14 @@ int main(int argc, char **argv) {
   printf("\nMRR depth: mean %.1f max %ld;  after redirect: mean %.1f max %ld  (jumps/match %.2f, straddling %.1f %%)\n",
          S.depth_sum / B, S.depth_max, S.rdepth_sum / B, S.rdepth_max, (double)S.rjumps / S.matches,
          100.0 * S.straddle / S.matches);
+  printf("match level (MRR round): mean %.2f, <=1 %.1f%% <=2 %.1f%% <=4 %.1f%% <=8 %.1f%% <=32 %.1f%% >32 %.1f%%\n",
+         (double)S.lvl_sum / S.matches, 100.0 * S.lvl_h[0] / S.matches, 100.0 * S.lvl_h[1] / S.matches,
+         100.0 * S.lvl_h[2] / S.matches, 100.0 * S.lvl_h[3] / S.matches, 100.0 * S.lvl_h[4] / S.matches,
+         100.0 * S.lvl_h[5] / S.matches);
+  printf("after redirect: mean %.2f, <=1 %.1f%% <=2 %.1f%% <=4 %.1f%% <=8 %.1f%% <=32 %.1f%% >32 %.1f%%\n",
+         (double)S.rlvl_sum / S.matches, 100.0 * S.rlvl_h[0] / S.matches, 100.0 * S.rlvl_h[1] / S.matches,
+         100.0 * S.rlvl_h[2] / S.matches, 100.0 * S.rlvl_h[3] / S.matches, 100.0 * S.rlvl_h[4] / S.matches,
+         100.0 * S.rlvl_h[5] / S.matches);
   printf("512-byte step DAG: steps needing step k-1 %.1f %%, k-1 or k-2 %.1f %%, critical path mean %.1f max %ld steps (of %.1f)\n",
          100.0 * S.dag_need_prev / S.dag_steps, 100.0 * S.dag_need_prev2 / S.dag_steps, S.dag_depth_sum / B, S.dag_depth_max, S.dag_steps / B);
   printf("byte hops to a literal: mean %.2f max %ld\n", (double)S.hops_lit / S.bytes, S.hops_lit_max);
