@@ -848,11 +848,14 @@ def end_to_end(data, args, resident_digest=None, header=None):
             t0 = time.perf_counter()
             stream.stream_read(path, len(data), header, window=window, depth=args.e2e_depth,
                                split_size=args.split_size, verify_crc=not args.no_crc,
-                               on_window=lambda *a: a[1].read(with_raw=True), contexts=ctxs)
+                               on_window=lambda *a: a[1].read(with_raw=True), contexts=ctxs,
+                               ramp=True)
             warm_s = time.perf_counter() - t0
+            # ramp: quarter and half windows first and last, so the first export starts sooner and
+            # the last one drains faster (profiles/r5zg_e2e_ramp_ab.txt)
             res = stream.stream_read(path, len(data), header, window=window, depth=args.e2e_depth,
                                      split_size=args.split_size, verify_crc=not args.no_crc,
-                                     on_window=export, contexts=ctxs)
+                                     on_window=export, contexts=ctxs, ramp=True)
         finally:
             del keep[:]
             for c in ctxs:

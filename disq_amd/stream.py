@@ -28,19 +28,35 @@ def stream_read(read_bytes, file_len: int, header: bytes,
                 window: int = 8 << 30, depth: int = 2, split_size: int = 0,
                 use_nio: bool = False, hadoop_block_size: int = 0, device: int = 0,
                 verify_crc: bool = True, halo: int = 4 << 20, on_window=None,
-                contexts=None) -> dict:
+                contexts=None, ramp: bool = False) -> dict:
     """Decode the whole file in windows of ~`window` compressed bytes on one GPU.
 
     read_bytes(a, b) returns the file's bytes [a, b) (page cache, host memory or a generator), or
     read_bytes is a path: the library reads each window itself (dq_open_shard_path).
     on_window(k, ctx, shard), if given, runs on the window's context after its pipeline (e.g. to
     export records with ctx.read()).  contexts: `depth` open Contexts to use (e.g. set up with an
-    export arena beforehand); they stay open.  Returns the per-partition counts and digests, the
+    export arena beforehand); they stay open.  ramp: smaller first and last windows (the pipeline's
+    fill and drain).  Returns the per-partition counts and digests, the
     whole-file digest, record and decompressed byte totals, and timings."""
     from . import _lib
     split_opts = dict(split_size=split_size, use_nio=use_nio, hadoop_block_size=hadoop_block_size)
     nwin = max(1, math.ceil(file_len / max(1, window)))
-    plan = [s for s in P.shard_plan(file_len, nwin, **split_opts) if not s.empty]
+    offsets = None
+    if ramp and file_len > 2 * window:
+        # windows of window/4, window/2, then window, ..., then window/2, window/4: the first
+        # export starts after a quarter window's read and pipeline instead of a whole one's, and
+        # the last one drains a quarter window's export
+        sizes = [window // 4, window // 2]
+        tail = [window // 2, window // 4]
+        mid = file_len - sum(sizes) - sum(tail)
+        nmid = max(1, math.ceil(mid / window))
+        sizes += [mid // nmid + (1 if i < mid % nmid else 0) for i in range(nmid)] + tail
+        offsets = [0]
+        for z in sizes:
+            offsets.append(offsets[-1] + z)
+        offsets[-1] = file_len
+        nwin = len(sizes)
+    plan = [s for s in P.shard_plan(file_len, nwin, offsets=offsets, **split_opts) if not s.empty]
     nsplit = len(P.path_splits(file_len, **split_opts))
     counts = np.zeros(nsplit, np.int64)
     digests = np.zeros(nsplit, np.uint64)

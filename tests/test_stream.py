@@ -9,8 +9,9 @@ from disq_amd import _lib, stream, synth
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("window,depth", [(3 << 20, 2), (5 << 20, 3), (1 << 40, 1)])
-def test_stream_equals_whole_file(window, depth):
+@pytest.mark.parametrize("window,depth,ramp", [(3 << 20, 2, False), (5 << 20, 3, False),
+                                              (1 << 40, 1, False), (4 << 20, 3, True)])
+def test_stream_equals_whole_file(window, depth, ramp):
     r = synth.generate(150000, seed=31, nthreads=8)
     data = r.bam
     with _lib.Context(split_size=1 << 20, verify_crc=True) as c:
@@ -19,7 +20,9 @@ def test_stream_equals_whole_file(window, depth):
         cnt, dig = c.partition_digests()
         header = c.header()[1]
     out = stream.stream_read(lambda a, b: data[a:b], len(data), header, window=window, depth=depth,
-                             split_size=1 << 20, halo=64 << 10)
+                             split_size=1 << 20, halo=64 << 10, ramp=ramp)
+    if ramp:  # quarter, half, whole ..., half, quarter windows
+        assert out["windows"] >= 5
     assert np.array_equal(out["counts"], cnt)
     assert np.array_equal(out["digests"], dig)
     assert out["digest"] == st.digest and out["n_records"] == st.n_records == 150000

@@ -31,7 +31,7 @@ def gen(path, gb):
     print(json.dumps({"path": path, "file_gb": round(res.bam_len / 1e9, 3), "records": n}))
 
 
-def run(path, window_gb, depth, reps, arena_factor):
+def run(path, window_gb, depth, reps, arena_factor, ramp=False):
     import torch  # noqa: F401 -- one HIP runtime
     from disq_amd import _lib, parallel as P, stream
     flen = os.path.getsize(path)
@@ -54,7 +54,7 @@ def run(path, window_gb, depth, reps, arena_factor):
                 got["raw"] += 0 if b["raw"] is None else len(b["raw"])
                 got["digests"].append((shard.p0, b["part_digest"].copy()))
         res = stream.stream_read(path, flen, header, window=window, depth=depth,
-                                 on_window=export, contexts=ctxs)
+                                 on_window=export, contexts=ctxs, ramp=ramp)
         dg = [0] * len(res["digests"])
         for p0, d in got["digests"]:
             for i, x in enumerate(d):
@@ -62,7 +62,7 @@ def run(path, window_gb, depth, reps, arena_factor):
         secs = res["seconds"]
         print(json.dumps({
             "rep": rep, "mmap": os.environ.get("DQ_MMAP", "0"), "window_gb": window_gb,
-            "depth": depth, "seconds": round(secs, 3),
+            "depth": depth, "ramp": ramp, "windows": res["windows"], "seconds": round(secs, 3),
             "decompressed_gbs": round(res["owned_bytes"] / secs / 1e9, 2),
             "file_gbs": round(flen / secs / 1e9, 2),
             "open_h2d_s": round(res["open_s"], 3), "pipeline_s": round(res["run_s"], 3),
@@ -82,8 +82,9 @@ if __name__ == "__main__":
     ap.add_argument("--depth", type=int, default=3)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--arena-factor", type=float, default=3.7)
+    ap.add_argument("--ramp", action="store_true")
     a = ap.parse_args()
     if a.mode == "gen":
         gen(a.path, a.gb)
     else:
-        run(a.path, a.window_gb, a.depth, a.reps, a.arena_factor)
+        run(a.path, a.window_gb, a.depth, a.reps, a.arena_factor, a.ramp)
