@@ -1449,28 +1449,53 @@ __global__ __launch_bounds__(CWG) void bgzf_code_kernel(const uint8_t* __restric
     const int nw = (int)(total_bits >> 5) + 1;
     for (int i = t; i < nw; i += CWG) img[i] = 0;
     __syncthreads();
-    if (t == 0) {
-      ImgOut io(img, 0);
+    // the header, by wave 0 in parallel: item 0 the 17 bits of BFINAL, BTYPE, HLIT, HDIST, HCLEN,
+    // then the HCLEN code-length code lengths, then the run-length tokens (code + extra bits), each
+    // lane one item: offsets by a wave scan of the items' bit lengths, bits OR-ed into the zeroed
+    // image (round 4: thread 0 put them one by one while its wave waited, ~300 dependent steps)
+    if (wv == 0) {
       if (!dyn) {
-        io.put(3u, 3);  // BFINAL 1, BTYPE 01
+        if (lane == 0) atomicOr(&img[0], 3u);  // BFINAL 1, BTYPE 01
       } else {
-        io.put(5u, 3);  // BFINAL 1, BTYPE 10
-        io.put((uint32_t)(L.misc[2] - 257), 5);
-        io.put((uint32_t)(L.misc[3] - 1), 5);
-        const int ncl = L.misc[5];
-        io.put((uint32_t)(ncl - 4), 4);
-        for (int k = 0; k < ncl; k++) io.put((uint32_t)H[H_LEN_CL + c_clord[k]], 3);
+        const int ncl = L.misc[5], ntok = L.misc[4];
+        const int nitem = 1 + ncl + ntok;
         const uint16_t* tok = reinterpret_cast<const uint16_t*>(H + H_TOK);
         const uint32_t* ccl = reinterpret_cast<const uint32_t*>(H + C_CL);
-        for (int k = 0; k < L.misc[4]; k++) {
-          const int sy = tok[k] & 31, ex = tok[k] >> 5;
-          io.put(ccl[sy] & 0xffff, (int)(ccl[sy] >> 16));
-          if (sy == 16) io.put((uint32_t)ex, 2);
-          else if (sy == 17) io.put((uint32_t)ex, 3);
-          else if (sy == 18) io.put((uint32_t)ex, 7);
+        uint32_t base = 0;
+        for (int i0 = 0; i0 < nitem; i0 += 64) {
+          const int i = i0 + lane;
+          uint32_t v = 0;
+          int len = 0;
+          if (i == 0) {
+            v = 5u | (uint32_t)(L.misc[2] - 257) << 3 | (uint32_t)(L.misc[3] - 1) << 8 |
+                (uint32_t)(ncl - 4) << 13;
+            len = 17;
+          } else if (i <= ncl) {
+            v = (uint32_t)H[H_LEN_CL + c_clord[i - 1]];
+            len = 3;
+          } else if (i < nitem) {
+            const int k = i - 1 - ncl;
+            const int sy = tok[k] & 31, ex = tok[k] >> 5;
+            const int cl = (int)(ccl[sy] >> 16);
+            const int xl = sy == 16 ? 2 : sy == 17 ? 3 : sy == 18 ? 7 : 0;
+            v = (ccl[sy] & 0xffffu) | (uint32_t)ex << cl;
+            len = cl + xl;
+          }
+          int inc = len;
+          for (int d = 1; d < 64; d <<= 1) {
+            const int y = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += y;
+          }
+          const uint32_t pos = base + (uint32_t)(inc - len);
+          if (len) {
+            const uint64_t bits = (uint64_t)v << (pos & 31);
+            DQ_CHK((pos >> 5) + 1 < 65536 / 4, CHK_Z_IMAGE);
+            atomicOr(&img[pos >> 5], (uint32_t)bits);
+            if ((pos & 31) + (uint32_t)len > 32) atomicOr(&img[(pos >> 5) + 1], (uint32_t)(bits >> 32));
+          }
+          base += (uint32_t)__shfl(inc, 63, 64);
         }
       }
-      io.flush();
     }
     {
       const uint32_t* cll = reinterpret_cast<const uint32_t*>(H + C_LL);
