@@ -89,6 +89,9 @@ constexpr int CONT_WORDS = 156;          // continuation symbols at most
 constexpr int OWN_CAP = 16;              // own matches (a 32-byte segment's, + one past its end)
 constexpr int CONT_CAP = 160;            // continuation matches (<= CONT_WORDS)
 constexpr int DENSE_WORDS = 2 * MSEG * MB_INL;  // per chunk
+#ifndef DQ_SCAT_ATOMIC
+#define DQ_SCAT_ATOMIC 1  // bucket scatter by LDS atomics (0: by ballot ranking, round 4)
+#endif
 #ifndef DQ_POOL_WORDS
 #define DQ_POOL_WORDS 32768  // (a build with a small pool exercises the exhaustion path)
 #endif
@@ -478,16 +481,18 @@ struct Finder {
     __builtin_memcpy(&qq, &L.bl[i0 - 7], 16);
     const uint32_t qw[4] = {qq.x, qq.y, qq.z, qq.w};
 #endif
+    // (an entry below lo is the sentinel x itself: one unsigned compare, x - q - 1 < WIN, then
+    // rejects it with a candidate at or past x -- which a bucket list out of order could hold --
+    // and one beyond the window)
 #pragma unroll
     for (int k = 0; k < 8; k++) {
 #if DQ_LDS_UNALIGNED
-      q8[k] = i0 - k >= lo ? (int)((qw[(7 - k) >> 1] >> (16 * ((7 - k) & 1))) & 0xffffu) : -1;
+      q8[k] = i0 - k >= lo ? (int)((qw[(7 - k) >> 1] >> (16 * ((7 - k) & 1))) & 0xffffu) : x;
 #else
-      q8[k] = i0 - k >= lo ? (int)L.bl[i0 - k] : -1;
+      q8[k] = i0 - k >= lo ? (int)L.bl[i0 - k] : x;
 #endif
-      const int q = q8[k] >= 0 ? q8[k] : x;
-      ya[k] = ld8(L.in, q) ^ S.pa;
-      yb[k] = ld8(L.in, q + 8) ^ S.pb;
+      ya[k] = ld8(L.in, q8[k]) ^ S.pa;
+      yb[k] = ld8(L.in, q8[k] + 8) ^ S.pb;
     }
 #if DQ_BATCH_REDUCE
     // the 8 lengths without a branch per candidate, the winner by one max over keys
@@ -498,7 +503,7 @@ struct Finder {
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       const int q = q8[k];
-      const bool valid = q >= 0 && x - q <= WIN;
+      const bool valid = (uint32_t)(x - q - 1) < (uint32_t)WIN;
       stop |= !valid;  // the bucket's list or the window ended (candidates: most recent first)
       int l = ya[k] ? (int)(__builtin_ctzll(ya[k]) >> 3)
                     : yb[k] ? 8 + (int)(__builtin_ctzll(yb[k]) >> 3) : 16;
@@ -526,7 +531,7 @@ struct Finder {
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       const int q = q8[k];
-      if (q < 0 || x - q > WIN) {  // past the window (candidates are most recent first)
+      if ((uint32_t)(x - q - 1) >= (uint32_t)WIN) {  // past the window (candidates are most recent first)
         more = false;
         break;
       }
@@ -887,6 +892,27 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
   if (wv < SCAT_WAVES) {
     uint16_t* const cur16 = wv ? reinterpret_cast<uint16_t*>(&L.cnt[wv - 1][0]) : nullptr;
     const int xe = min(npos, (wv + 1) * rng);
+#if DQ_SCAT_ATOMIC
+    // one LDS atomic per position: the lanes of one ds_add_rtn that hit the same cursor get its
+    // values in lane order on gfx950 (tools/micro/lds_atomic_order.hip: no violation in 168 M
+    // atomics), so equal-hash positions of a step get ascending slots, as the ballot ranking below
+    // gave them (round 4: 11 ballots per 64 positions).  Whatever the order, a candidate at or
+    // past the position it is searched for is never taken (Finder::batch), so the output stays a
+    // valid DEFLATE stream; its bytes are the same on every run while the order holds.
+    uint32_t* const cur32 = wv ? reinterpret_cast<uint32_t*>(&L.cnt[wv - 1][0]) : nullptr;
+    for (int x = wv * rng + lane; x < xe; x += 64) {
+      const uint32_t h = hash4a(L.in, x);
+      int rank;
+      if (wv) {
+        const uint32_t sh = 16u * (h & 1u);
+        rank = (int)((atomicAdd(cur32 + (h >> 1), 1u << sh) >> sh) & 0xffffu);
+      } else {
+        rank = atomicAdd(&L.head[h], 1);
+      }
+      DQ_CHK(rank < npos, CHK_Z_BL);
+      L.bl[rank] = (uint16_t)x;
+    }
+#else
     for (int x0 = wv * rng; x0 < xe; x0 += 64) {
       const int x = x0 + lane;
       const bool valid = x < xe;
@@ -909,6 +935,7 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
         L.bl[rank] = (uint16_t)x;
       }
     }
+#endif
   } else {
     // meanwhile the other waves: CRC32 of CRC_BYTES bytes per thread (raw register, init 0),
     // moved to the chunk end, XOR-ed
