@@ -742,13 +742,14 @@ def write_path_bench(args):
            "roofline": {"bound": "hbm", "achieved": round((len(u) + n) / ms / 1e6, 2),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round((len(u) + n) / ms / 1e6 / HBM_PEAK_GBS, 5),
-                        "traffic_over_alg": 4.01,
-                        "traffic_src": "profiles/r5o_deflate_pmc.txt (0.872 GB per compression of "
-                                       "0.162 GB: 4.01x the 0.218 GB algorithmic bytes)",
+                        "traffic_over_alg": 3.98,
+                        "traffic_src": "profiles/r5zl_deflate_pmc.txt (0.868 GB per compression of "
+                                       "0.162 GB: 3.98x the 0.218 GB algorithmic bytes)",
                         "limiter": "LZ77 parse latency of bgzf_parse_kernel (~88 % of device time; "
                                    "one 160 KB, 1024-thread workgroup per CU: 16 waves)"},
-           "evidence": "profiles/r5n_deflate_parse_1024.txt (A/B, per-phase cycles), "
-                       "profiles/r5o_deflate_pmc.txt (SQ counters and traffic of the three kernels)"}
+           "evidence": "profiles/r5n_deflate_parse_1024.txt, r5zc_deflate_fmerge.txt, "
+                       "r5zi_deflate_parallel_header.txt, r5zk_deflate_atomic_scatter.txt (A/Bs, "
+                       "per-phase cycles), profiles/r5zl_deflate_pmc.txt (SQ counters and traffic)"}
     log("write path:", out)
     return out
 
