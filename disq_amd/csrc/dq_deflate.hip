@@ -10,7 +10,7 @@
 // BGZF whose blocks inflate to exactly htsjdk's block contents.
 //
 // Three kernels per batch of blocks, everything the match finder touches in LDS:
-//   bgzf_parse_kernel: one 512-thread workgroup per CHUNK, half a block (32640 bytes), holding the
+//   bgzf_parse_kernel: one 1024-thread workgroup per CHUNK, half a block (32640 bytes), holding the
 //      chunk's bytes plus up to 13600 bytes before it (its window reach) and the hash-bucket lists of
 //      all those positions (3 bytes of LDS per position: 160 KB, one workgroup per CU).  A chunk's
 //      matches end inside it and reach back at most 13600 bytes before its start (the 32 KiB DEFLATE
@@ -19,18 +19,19 @@
 //   1. Match finder: every position with a 4-byte suffix goes into one of 2048 hash buckets of its
 //      first 4 bytes (a 4-byte key keeps 3-byte candidates, which rarely pay for their distance,
 //      out of the chain), ascending inside its bucket: counts by LDS atomics, bucket starts by a
-//      scan, then four waves scatter four position ranges in order with their own cursors (the
-//      lanes of a 64-position step with equal hashes ranked by one ballot per hash bit): no
-//      barrier, no position hashed twice.  A position's candidates are the entries before it in
+//      scan, then four waves scatter four position ranges in order with their own cursors (one
+//      LDS atomic add per position: the lanes of one atomic that hit the same cursor get its
+//      values in lane order on gfx950, so equal-hash positions of a step get ascending slots):
+//      no barrier, no position hashed twice.  A position's candidates are the entries before it in
 //      its bucket, most recent first (its own slot is found by a 16-way search of the bucket): a
 //      contiguous run of the list, so a search loads 8 candidates and their first 16 bytes at
 //      once instead of chasing zlib's hash-chain links one dependent load at a time.
-//   2. Parse: the chunk is cut into 32-byte segments; thread t parses segment 2t from its start
+//   2. Parse: the chunk is cut into 32-byte segments; thread t parses segment t from its start
 //      with zlib-style lazy evaluation (a match shorter than `lazy` is deferred while the next
 //      position's is longer; the look-ahead search walks chain / 4 candidates once the current
-//      match is `good` long, as zlib's deflate_slow), the longest match among `chain` candidates
-//      (stopping at `nice`), and flows on into segment 2t + 1 unless a thread that finished early
-//      claimed it first.  A parse step depends on its position alone, so two parses that reach the
+//      match is `good` long, as zlib's deflate_slow) and the longest match among `chain`
+//      candidates (stopping at `nice`); nothing depends on which lane runs first, so the output
+//      is the same on every run.  A parse step depends on its position alone, so two parses that reach the
 //      same position continue identically: from its exit, each segment's parse is continued until
 //      it hits a symbol boundary of a later segment's parse (usually within a few symbols) and the
 //      merge is recorded; after `fmerge` continuation symbols without one (default 1) it is ended
@@ -46,11 +47,12 @@
 //      the distance code (a rank sort, Moffat-Katajainen minimum-redundancy lengths, a Kraft
 //      fix-up capping them at 15), the code-length sequence is run-length coded; the tables go to
 //      the block's record.
-//   bgzf_code_kernel: one 256-thread workgroup per block (73 KB of LDS, two per CU).
+//   bgzf_code_kernel: one 1024-thread workgroup per block (136 KB of LDS).
 //   4. Emit: the block is coded dynamic (BTYPE 10) or fixed (01), whichever is shorter -- one
 //      DEFLATE block per member, as zlib writes a 64 KiB input; each thread's bit count gives its
-//      offset by an exclusive scan; every thread OR-s its eight segments' bits into the LDS image
-//      of the block.  A block whose code would not fit BSIZE (or whose parse overflowed its
+//      offset by an exclusive scan; wave 0 writes the dynamic header (an item per lane, offsets by
+//      a wave scan) while every thread OR-s its two segments' bits into the LDS image of the
+//      block.  A block whose code would not fit BSIZE (or whose parse overflowed its
 //      staging) is stored (BTYPE 00).
 // CRC32: per-lane table CRC over the segment, combined with x^(8 n) mod P multipliers.
 // (Defaults chain 32, lazy 16, nice 32, good 8: zlib level 5's.)
