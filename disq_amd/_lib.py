@@ -189,6 +189,12 @@ class DqError(RuntimeError):
         self.code = code
 
 
+def _copy_out(ptr, n):
+    """n bytes at a library-owned address as bytes (ctypes.string_at takes a C int size, so a
+    buffer past 2 GiB needs the array view)."""
+    return bytes((C.c_ubyte * n).from_address(ptr)) if n else b""
+
+
 def check(ctx, rc):
     if rc != DQ_OK:
         raise DqError(rc, lib().dq_last_error(ctx).decode(errors="replace") if ctx else "")
@@ -378,7 +384,7 @@ class Context:
         check(self._h, lib().dq_bgzf_compress(self._h, buf.ctypes.data if len(buf) else None,
                                               len(buf), C.byref(out), C.byref(n)))
         try:
-            return C.string_at(out, n.value) if n.value else b""
+            return _copy_out(out.value, n.value)
         finally:
             lib().dq_free(out)
 
@@ -477,7 +483,7 @@ class Context:
         p = C.POINTER(C.c_uint8)()
         n = C.c_int64()
         check(self._h, lib().dq_write_sbi(self._h, granularity, C.byref(p), C.byref(n)))
-        out = C.string_at(p, n.value)
+        out = _copy_out(C.cast(p, C.c_void_p).value, n.value)
         lib().dq_free(C.cast(p, C.c_void_p))
         return out
 

@@ -107,11 +107,14 @@ def generate(n_records: int, seed: int = 1, shape: int = WGS, level: int = 5, nt
         def free():
             _L().dq_synth_free(C.byref(r))
         return r, free
+    def copy(ptr, n):
+        # (ctypes.string_at takes a C int size: a file past 2 GiB needs the array view)
+        return bytes((C.c_ubyte * n).from_address(ptr)) if n else b""
     try:
         return SynthBam(
-            C.string_at(r.bam, r.bam_len),
-            C.string_at(r.bai, r.bai_len) if r.bai else None,
-            C.string_at(r.sbi, r.sbi_len) if r.sbi else None,
+            copy(r.bam, r.bam_len),
+            copy(r.bai, r.bai_len) if r.bai else None,
+            copy(r.sbi, r.sbi_len) if r.sbi else None,
             r.n_records, r.n_blocks, r.record_bytes)
     finally:
         _L().dq_synth_free(C.byref(r))
