@@ -1832,52 +1832,24 @@ DQ_AI void build_tables_wave(LdsW& L, int nlen, int ndist) {
     return;
   }
   __builtin_amdgcn_wave_barrier();
-  // ranks among equal lengths, chunk by chunk (one-hot packed counters, 8 bits per length: at most
-  // 64 per chunk), and the decoded entries at their canonical positions
+  // ranks among equal lengths, chunk by chunk: one LDS atomic add per symbol on its length's
+  // running count (the lanes of one atomic that hit the same count get its values in lane order on
+  // gfx950, tools/micro/lds_atomic_order.hip; chunks in order), and the decoded entries at their
+  // canonical positions (round 4: eight packed-counter wave scans per chunk)
   for (int k0 = 0; k0 < 320; k0 += 64) {
     const int k = k0 + lane;
     const bool isl = k < 288;
     const int sym = isl ? k : k - 288;
     const int len = k < 320 ? (isl ? (k < nlen ? H.lens[k] : 0) : (sym < ndist ? H.lens[k] : 0)) : 0;
-    // the chunk 256..319 mixes the alphabets: count each alphabet's lanes separately
-    uint32_t c[4], cd[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      c[j] = (isl && len && (len >> 2) == j) ? 1u << (8 * (len & 3)) : 0u;
-      cd[j] = (!isl && len && (len >> 2) == j) ? 1u << (8 * (len & 3)) : 0u;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      c[j] = (uint32_t)wave_incl_scan((int)c[j], lane);
-      cd[j] = (uint32_t)wave_incl_scan((int)cd[j], lane);
-    }
     if (len) {
-      // (selected register by register: a pointer to either array put both in scratch)
-      const uint32_t m0 = isl ? c[0] : cd[0], m1 = isl ? c[1] : cd[1], m2 = isl ? c[2] : cd[2],
-                     m3 = isl ? c[3] : cd[3];
-      const uint32_t mine = (len >> 2) == 0 ? m0 : (len >> 2) == 1 ? m1 : (len >> 2) == 2 ? m2 : m3;
-      const int rank = (int)((mine >> (8 * (len & 3))) & 0xffu) - 1 + H.run[(isl ? 0 : 16) + len];
+      const int rank = atomicAdd(&H.run[(isl ? 0 : 16) + len], 1);
       const HuffCanon& hh = isl ? L.u.d.hl : L.u.d.hd;
       const int q = hh.offs[len] + rank;
       if (isl) L.u.d.lent[q] = ent_ll((uint32_t)sym, (uint32_t)len);
       else L.u.d.dent[q] = ent_d((uint32_t)sym, (uint32_t)len);
     }
-    // the chunk's totals (lane 63's inclusive counters) into the running ranks
-    uint32_t tl[4], tdd[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      tl[j] = (uint32_t)__builtin_amdgcn_readlane((int)c[j], 63);
-      tdd[j] = (uint32_t)__builtin_amdgcn_readlane((int)cd[j], 63);
-    }
-    __builtin_amdgcn_wave_barrier();
-    if (lane < 32) {
-      const int l = lane & 15;
-      const uint32_t q = (l >> 2) == 0 ? (lane < 16 ? tl[0] : tdd[0]) : (l >> 2) == 1 ? (lane < 16 ? tl[1] : tdd[1])
-                       : (l >> 2) == 2 ? (lane < 16 ? tl[2] : tdd[2]) : (lane < 16 ? tl[3] : tdd[3]);
-      H.run[lane] += l ? (int)((q >> (8 * (l & 3))) & 0xffu) : 0;
-    }
-    __builtin_amdgcn_wave_barrier();
   }
+  __builtin_amdgcn_wave_barrier();
   // root tables: 16 litlen and 4 distance entries per lane; an index without a short code is the
   // prefix of long codes (a complete code), decoded canonically
   const bool lslow = L.u.d.hl.count[11] + L.u.d.hl.count[12] + L.u.d.hl.count[13] +
