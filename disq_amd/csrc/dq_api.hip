@@ -733,6 +733,12 @@ static int run_pipeline(dq_ctx* ctx) {
               "BGZF block %.3f\n", acc[16] / nb, acc[17] / nb, acc[18] / nb, acc[19] / nb, acc[21] / nb,
               (acc[0] - acc[16]) / nb, (acc[1] - acc[17]) / nb, (acc[2] - acc[18]) / nb,
               (acc[3] - acc[19]) / nb, (acc[5] - acc[21]) / nb, acc[22] / nb);
+      double rr[7] = {0};
+      for (int64_t i = 0; i < nblk; i++)
+        for (int k = 0; k < 7; k++) rr[k] += (double)h[32 * (size_t)i + 24 + k];
+      fprintf(stderr, "[dq] rounds' re-decodes per BGZF block: lanes=%.2f merged=%.2f (mean checkpoint %.2f) "
+              "unmerged: spec err/eob=%.2f spec exit=%.2f other=%.2f\n", rr[0] / nb, rr[2] / nb,
+              rr[3] / std::max(1.0, rr[2]), rr[4] / nb, rr[5] / nb, rr[6] / nb);
       double ta[16] = {0};
       for (int64_t i = 0; i < nblk; i++)
         for (int k = 0; k < 16; k++) ta[k] += (double)h[32 * (size_t)nblk + 16 * (size_t)i + k];

@@ -1038,12 +1038,18 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   const int32_t dbytes = csize - 26;
   const uint32_t endbits = a0 + 8u * (uint32_t)max(dbytes, 0);
 
+  // DQ_WARM (sflags bit 4): one load per 128-byte line of the deflate data, issued first and
+  // waited for at the barrier below, so the speculative lanes' first reads hit L2 instead of each
+  // taking an HBM round trip after the header
+  uint32_t warm = 0;
+  if ((sflags & 16) && 128u * (uint32_t)t < (uint32_t)(mis + max(dbytes, 0))) warm = W[32 * t];
   for (int i = t; i < 2048; i += WG) L.bm[i] = 0;
   if (t < 32) L.misc[t] = 0;
   if (t == 0) {
     if (isize < 0 || isize > 65536) L.misc[M_ERR] = ST_ISIZE;
     else if (dbytes < 0) L.misc[M_ERR] = ST_OVERREAD;
   }
+  asm volatile("" ::"v"(warm));
   __syncthreads();
   int32_t produced = 0;
   uint32_t pos = a0;  // bit position of the next deflate block's header
@@ -1262,6 +1268,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
         AE[lt] = ae;
         AC[lt] = c;
         if (TIMING) {
+          atomicAdd(&L.misc[21], 1);
           if (jmerge >= 0) {
             atomicAdd(&L.misc[23], 1);
             atomicAdd(&L.misc[24], jmerge);
@@ -1642,6 +1649,8 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   TST(7);
   if (TIMING && t == 0)
     for (int i = 0; i < 24; i++) tim[(int64_t)blockIdx.x * TIM_W + i] = tacc[i];
+  if (TIMING && t == 0)  // [24..30] the rounds' re-decodes: lanes, merges, checkpoint sum, non-merges
+    for (int i = 0; i < 7; i++) tim[(int64_t)blockIdx.x * TIM_W + 24 + i] = (uint64_t)L.misc[21 + i];
 }
 
 // ================================================================ the tail kernel
@@ -2406,7 +2415,8 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
   static const uint32_t sflags =
       (getenv("DQ_STORE") ? (uint32_t)atoi(getenv("DQ_STORE")) & 3u : 2u) |
       (getenv("DQ_NDEC") ? (uint32_t)(atoi(getenv("DQ_NDEC")) & 1023) << 8 : 0u) |
-      (getenv("DQ_SEGBITS") ? (uint32_t)(atoi(getenv("DQ_SEGBITS")) & 1023) << 20 : 0u);
+      (getenv("DQ_SEGBITS") ? (uint32_t)(atoi(getenv("DQ_SEGBITS")) & 1023) << 20 : 0u) |
+      (getenv("DQ_WARM") && atoi(getenv("DQ_WARM")) ? 16u : 0u);
   // DQ_LDSPAD: extra dynamic LDS per workgroup (occupancy experiments: 80000 = one workgroup per CU)
   static const unsigned ldspad = getenv("DQ_LDSPAD") ? (unsigned)atoi(getenv("DQ_LDSPAD")) : 0u;
   // DQ_TAIL=0: no tail kernel (the block kernel decodes every deflate block itself)
