@@ -69,16 +69,6 @@ constexpr int RES_NXT = 2048;        // resolve batch bytes (NB * G * WG) at mos
 #ifndef DQ_CSTEP
 #define DQ_CSTEP 0
 #endif
-// DQ_REPLAY (experiment, profiles/r5zf_token_replay_experiment.txt): 1 = the emit replays symbol
-// tokens recorded by the speculative pass and the rounds; 2 = tokens recorded, never replayed (the
-// recording's cost alone); 0 (default) = neither, the decode emit.
-#ifndef DQ_REPLAY
-#define DQ_REPLAY 0
-#endif
-constexpr bool TOKREC = DQ_REPLAY != 0, REPLAY = DQ_REPLAY == 1;
-#ifndef DQ_REPLAY_GROUP
-#define DQ_REPLAY_GROUP 4
-#endif
 #ifndef DQ_RES_NB
 #define DQ_RES_NB 4
 #define DQ_RES_G 1
@@ -222,7 +212,6 @@ __constant__ uint8_t c_clorder3[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 
 
 // misc slots
 enum { M_ERR = 0, M_SLOW = 1 /* an E_SLOW root entry in this deflate block's tables */, M_A = 4, M_LAST, M_MORE, M_MORE1,
-       M_SLOT = 8 /* the workgroup's token slot (9: thread 0's claim before the misc reset is seen) */,
        M_LQ0 = 15, M_LQN, M_DQ0, M_DQN, M_NEXT,
        M_LASTF, M_RCNT = 28 /* and 29: redo-list counters of even / odd rounds */,
        M_DIRTY = 30 /* and 31: a re-decoded exit changed, even / odd rounds */ };
@@ -396,34 +385,6 @@ DQ_AI bool dsym(BitR& r, const S& W, const LT& L, uint32_t p, uint32_t lim,
 
 enum : int32_t { F_DEAD = 4 };  // speculative path found no boundary >= sB (garbage)
 
-// Symbol tokens (block kernel): the speculative pass and the rounds' re-decodes record each counted
-// symbol as one 32-bit token, so the emit replays tokens instead of decoding a third time.  A match
-// token is bit 31 | the emit's 3-byte descriptor ((dist - 1) | (len - 3) << 15); a literal token is
-// the byte | the pair's second byte << 8 | bit 16 when there is one.  Token k of lane t is word
-// k * TOK_LANES + t of its region (the lanes of a wave store and load 256 contiguous bytes); a
-// workgroup owns one slot (a spec and a redo region) between its claim and its release.  A lane with
-// more than NTOK tokens keeps the decode emit.
-constexpr int NTOK = 96;                 // tokens per lane and region (row NTOK: overflow sink)
-constexpr int TOK_LANES = 512;           // lanes per region row (= NDEC)
-constexpr uint32_t TOK_REGION = (uint32_t)(NTOK + 1) * TOK_LANES * 4;
-constexpr uint32_t TOK_SLOT_BYTES = 2 * TOK_REGION;
-constexpr int TOK_SLOTS = 1024;          // > resident block workgroups (2 per CU x 256 CUs)
-// checkpoint word: (p - sB) << 23 | tokens before p (7 bits, saturating) << 16 | bytes before p
-DQ_AI uint32_t ck_word(uint32_t dp, uint32_t ntok, int32_t cnt) {
-  return (dp << 23) | (min(ntok, 127u) << 16) | (uint32_t)cnt;
-}
-DQ_AI uint32_t tok_of(bool m, uint32_t len, uint32_t dist, uint32_t lit2) {
-  return m ? (0x80000000u | (dist - 1) | ((len - 3) << 15))
-           : (len | (lit2 != 0xffffffffu ? (lit2 << 8) | 0x10000u : 0u));
-}
-// token k's byte offset in a region (k saturates at the overflow row)
-DQ_AI uint32_t tok_off(uint32_t col, uint32_t k) {
-  return col + min(k, (uint32_t)NTOK) * (uint32_t)(TOK_LANES * 4);
-}
-DQ_AI void tok_put(uint8_t* base, uint32_t off, uint32_t v) {
-  *reinterpret_cast<uint32_t*>(base + off) = v;
-}
-
 // Decode from `start`; output is counted from the first symbol boundary >= sB (*Bp) and the
 // run stops at the first boundary >= sE (*Ep).  Returns F_EXIT / F_EOB (*Ep = bit after EOB) /
 // F_ERR / F_END (ran off the data) / F_DEAD (no boundary >= sB before an error, EOB or the end).
@@ -431,17 +392,15 @@ constexpr int NCK_DEFAULT = 8;  // checkpoints per speculative lane
 constexpr uint32_t CKI_DEFAULT = 48;  // checkpoint spacing in bits (>= the longest symbol: a symbol
                                 // crosses at most one threshold; most paths re-synchronise
                                 // within ~100 bits, segments are ~160-1000 bits)
-static_assert(CKI_DEFAULT * (NCK_DEFAULT + 1) + 48 < 511, "a checkpoint's bit offset fits its 9 bits");
 
 // Speculative lanes also record checkpoints: the first symbol boundary at or past sB + CKI * (j+1)
 // (offset from sB << 16 | bytes counted so far), j < nck, at ck[j * ckstride] (nullptr: none).
 // A spacing below the longest symbol only loses merges: a merge needs equal bit positions, and
 // equal positions at symbol boundaries are equal decoder states whatever the checkpoint index.
-template <bool SLOW, bool TOK = false, class S, class LT>
+template <bool SLOW, class S, class LT>
 DQ_AI int run_seg(const S& W, const LT& L, uint32_t start, uint32_t sB,
                   uint32_t sE, uint32_t endbits, int32_t* Bp, int32_t* Ep, int32_t* cntp,
-                  uint32_t* ck, int ckstride, uint32_t CKI, int NCK, uint8_t* tokb = nullptr,
-                  uint32_t tcol = 0, uint32_t* ntokp = nullptr) {
+                  uint32_t* ck, int ckstride, uint32_t CKI, int NCK) {
   BitR r;
   br_init(r, W, start);
   uint32_t p = br_pos(r);
@@ -450,7 +409,6 @@ DQ_AI int run_seg(const S& W, const LT& L, uint32_t start, uint32_t sB,
   // warm-up: to the first symbol boundary >= sB, nothing counted (one compare per step: the
   // data end is folded into the bound and tested once after the loop)
   const uint32_t sBe = min(sB, endbits);
-  if constexpr (TOK) *ntokp = 0;
   while (p < sBe) {
     if (dsym<SLOW>(r, W, L, p, sBe, len, dist, lit2, m)) {
       *Ep = (int32_t)(len != 0xffffffffu ? len : p);
@@ -477,10 +435,9 @@ DQ_AI int run_seg(const S& W, const LT& L, uint32_t start, uint32_t sB,
   uint32_t* const dummy = const_cast<uint32_t*>(L.scratch) + (tid_fresh() & 15);
   uint32_t* ckp = ck;  // checkpoint j (advanced, not multiplied out)
   const uint32_t sEe = min(sE, endbits);  // one compare (one branch) for both ends
-  uint32_t ntok = 0;
   for (;;) {
     const bool cross = p >= thr;
-    *(cross ? ckp : dummy) = ck_word(p - sB, TOK ? ntok : 0u, cnt);
+    *(cross ? ckp : dummy) = ((p - sB) << 16) | (uint32_t)cnt;
     ckp += cross ? ckstride : 0;
     j += cross ? 1 : 0;
     thr = cross ? (j < NCK ? thr + CKI : 0xffffffffu) : thr;
@@ -495,15 +452,10 @@ DQ_AI int run_seg(const S& W, const LT& L, uint32_t start, uint32_t sB,
       break;
     }
     cnt += m ? (int32_t)len : (lit2 != 0xffffffffu ? 2 : 1);
-    if constexpr (TOK) {
-      tok_put(tokb, tok_off(tcol, ntok), tok_of(m, len, dist, lit2));
-      ntok++;
-    }
     p = br_pos(r);
   }
   *Bp = B;
   *cntp = cnt;
-  if constexpr (TOK) *ntokp = ntok;
   return f;
 }
 
@@ -511,13 +463,10 @@ DQ_AI int run_seg(const S& W, const LT& L, uint32_t start, uint32_t sB,
 // threshold the path is compared with the speculative one: the same boundary means the same
 // decoder state, so the rest of the segment is the speculative run's (exit `se` = E << 3 | flag,
 // `sc` bytes from its first boundary) and the decode stops there.
-// TOK: the re-decode's tokens go to the lane's redo region; *tinfo = tokens (saturating at 255) |
-// 1 << 17 on a merge | the speculative token index at the merge << 24.
-template <bool SLOW, bool TOK = false, class S, class LT>
+template <bool SLOW, class S, class LT>
 DQ_AI int run_redo(const S& W, const LT& L, uint32_t s0, uint32_t sB,
                    uint32_t sE, uint32_t endbits, const uint32_t* ck, int ckstride, int32_t se,
-                   int32_t sc, int32_t* Ep, int32_t* cntp, uint32_t CKI, int NCK, int* jm = nullptr,
-                   uint8_t* tokb = nullptr, uint32_t tcol = 0, uint32_t* tinfo = nullptr) {
+                   int32_t sc, int32_t* Ep, int32_t* cntp, uint32_t CKI, int NCK, int* jm = nullptr) {
   BitR r;
   br_init(r, W, s0);
   int32_t cnt = 0;
@@ -527,20 +476,18 @@ DQ_AI int run_redo(const S& W, const LT& L, uint32_t s0, uint32_t sB,
   const uint32_t* ckq = ck;  // checkpoint min(j, NCK - 1)
   const uint32_t sEe = min(sE, endbits);
   int j = 0;
-  uint32_t ntok = 0, mi = 0;
   for (;;) {
     const uint32_t p = br_pos(r);
     // at a checkpoint threshold: the same boundary as the speculative run merges (one exit branch
     // for the segment end, the data end and a merge; the threshold update is branch-free)
     const bool cross = p >= thr;
-    const bool merge = cross && (cur >> 23) == p - sB;
+    const bool merge = cross && (cur >> 16) == p - sB;
     if (p >= sEe || merge) {
       if (merge) {
         *Ep = se >> 3;
         f = se & 7;
         cnt += sc - (int32_t)(cur & 0xffffu);
         if (jm) *jm = j;
-        mi = (1u << 17) | (((cur >> 16) & 127u) << 24);
       } else {
         *Ep = (int32_t)p;
         f = p >= sE ? F_EXIT : F_END;
@@ -560,13 +507,8 @@ DQ_AI int run_redo(const S& W, const LT& L, uint32_t s0, uint32_t sB,
       break;
     }
     cnt += m ? (int32_t)len : (lit2 != 0xffffffffu ? 2 : 1);
-    if constexpr (TOK) {
-      tok_put(tokb, tok_off(tcol, ntok), tok_of(m, len, dist, lit2));
-      ntok++;
-    }
   }
   *cntp = cnt;
-  if constexpr (TOK) *tinfo = min(ntok, 255u) | mi;
   return f;
 }
 
@@ -608,51 +550,6 @@ DQ_AI void emit_seg(const S& W, LT& L, uint32_t start, uint32_t target,
     *(m ? o + 2 : dummy) = (uint8_t)(desc >> 16);
     atomicOr(m ? &L.bm[(p - ibase) >> 5] : dummy32, 1u << ((p - ibase) & 31));
     p += m ? (int32_t)len : (two ? 2 : 1);
-  }
-}
-
-// Emit by replaying recorded tokens (the block kernel): tokens [0, na) of the region column at
-// offset colA, then [kb, kb + nb) of colB, output from absolute position p (image base 0); the same
-// stores, bounds and far-distance check as emit_seg.  Tokens are loaded a group at a time (one L2
-// round trip per group, not per token; DQ_REPLAY_GROUP tokens).
-template <class LT>
-DQ_AI void replay_seg(const uint8_t* tokb, uint32_t colA, uint32_t na, uint32_t colB, uint32_t kb,
-                      uint32_t nb, LT& L, int32_t p, int32_t isize, int sh) {
-  typedef volatile __attribute__((address_space(3))) uint8_t lds8;
-  uint32_t* const dummy32 = emit_dummy(L) + (tid_fresh() & 63);
-  lds8* const dummy = (lds8*)dummy32;
-  const uint32_t n = na + nb;
-  bool live = n > 0;
-  for (uint32_t i0 = 0; live; i0 += DQ_REPLAY_GROUP) {
-    constexpr int RG = DQ_REPLAY_GROUP;
-    uint32_t tv[RG];
-#pragma unroll
-    for (int k = 0; k < RG; k++) {
-      const uint32_t i = min(i0 + (uint32_t)k, n - 1);
-      tv[k] = *reinterpret_cast<const uint32_t*>(tokb + (i < na ? tok_off(colA, i) : tok_off(colB, kb + i - na)));
-    }
-#pragma unroll
-    for (int k = 0; k < RG; k++) {
-      live = live && i0 + (uint32_t)k < n && p < isize;
-      if (live) {
-        const uint32_t v = tv[k];
-        const bool m = (v >> 31) != 0;
-        const int32_t dist = (int32_t)(v & 0x7fffu) + 1;
-        if (m && dist > p) {
-          set_err(L, ST_BAD_DIST);
-          live = false;
-        } else {
-          const bool two = !m && (v & 0x10000u) && p + 1 < isize;
-          DQ_CHK(sh + p + 2 < (int)sizeof(L.out) && (p >> 5) < (int)(sizeof(L.bm) / 4), CHK_K2_IMAGE);
-          lds8* const o = (lds8*)(L.out + sh + p);
-          o[0] = (uint8_t)v;
-          *(m || two ? o + 1 : dummy) = (uint8_t)(v >> 8);
-          *(m ? o + 2 : dummy) = (uint8_t)(v >> 16);
-          atomicOr(m ? &L.bm[p >> 5] : dummy32, 1u << (p & 31));
-          p += m ? (int32_t)((v >> 15) & 0xffu) + 3 : (two ? 2 : 1);
-        }
-      }
-    }
   }
 }
 
@@ -1101,7 +998,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     const int64_t* __restrict__ uoff, int64_t nblk, uint8_t* __restrict__ U,
     int32_t* __restrict__ status, int32_t verify_crc, const uint32_t* __restrict__ crc_init,
     uint64_t* __restrict__ tim, uint32_t OV, uint32_t sflags, const int32_t* __restrict__ sel,
-    TailDesc* __restrict__ tails, uint8_t* __restrict__ tokpool) {
+    TailDesc* __restrict__ tails) {
   // compile-time checkpoints (the spacing/count sweep's choice, profiles/r3ij_*): the decode loops
   // fold the threshold updates and hold fewer SGPRs (spec + rounds -8 k cycles per block, r3y)
   constexpr uint32_t CKI = CKI_DEFAULT;
@@ -1153,24 +1050,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     else if (dbytes < 0) L.misc[M_ERR] = ST_OVERREAD;
   }
   asm volatile("" ::"v"(warm));
-  // the token slot: thread 0 claims a free bit of the pool's bitmap (more slots than resident
-  // workgroups, so a free one is found; if not, the dummy slot and no replay)
-  if (TOKREC && t == 0) {
-    uint32_t* const tokbits = reinterpret_cast<uint32_t*>(tokpool + (size_t)(TOK_SLOTS + 1) * TOK_SLOT_BYTES);
-    uint32_t myslot = TOK_SLOTS;
-    uint32_t sl = (uint32_t)blockIdx.x & (TOK_SLOTS - 1);
-    for (int k = 0; k < 2 * TOK_SLOTS; k++) {
-      const uint32_t bit = 1u << (sl & 31);
-      if (!(atomicOr(&tokbits[sl >> 5], bit) & bit)) {
-        myslot = sl;
-        break;
-      }
-      sl = (sl + 1) & (TOK_SLOTS - 1);
-    }
-    L.misc[M_SLOT + 1] = (int32_t)myslot;
-  }
   __syncthreads();
-  if (TOKREC && t == 0) L.misc[M_SLOT] = L.misc[M_SLOT + 1];  // published by the header's barriers
   int32_t produced = 0;
   uint32_t pos = a0;  // bit position of the next deflate block's header
   bool deferred = false;  // the rest of the block goes to the tail kernel
@@ -1281,8 +1161,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     const uint32_t span = endbits - a;
     // per-lane arrays live in the not-yet-written tail of the output image
     const int ob = (sh + produced + 3) & ~3;
-    constexpr int NARR = REPLAY ? 8 : 7;  // per-lane arrays besides the checkpoints
-    const int cap = (sh + isize - ob) / (4 * (NARR + NCK));  // NCK: this launch's checkpoints
+    const int cap = (sh + isize - ob) / (4 * (7 + NCK));  // NCK: this launch's checkpoints
     int32_t* AB;  // verified start (first boundary >= segment start), -1 none
     int32_t* AE;  // exit << 3 | flag
     int32_t* AC;  // output bytes in [B, E)
@@ -1290,8 +1169,6 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     int32_t* ST;  // redo list: start
     int32_t* SE;  // speculative exit << 3 | flag
     int32_t* SC;  // speculative byte count
-    uint32_t* TS = nullptr;  // tokens: spec count (bits 0-7), redo count (8-15), merged (16),
-                             // re-decoded (17), spec index at the merge (24-30)
     uint32_t* CK = nullptr;  // checkpoints, [j * nl + lane]
     // lanes: one per >= 128 bits, at most NDEC (tuning: sflags bits 8-17 cap the lanes, bits
     // 20-29 set the minimum segment bits)
@@ -1309,15 +1186,8 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     ST = LS + nl;
     SE = ST + nl;
     SC = SE + nl;
-    if (cap >= 8) {
-      TS = REPLAY ? reinterpret_cast<uint32_t*>(SC + nl) : nullptr;
-      CK = reinterpret_cast<uint32_t*>(SC + nl) + (REPLAY ? nl : 0);
-    }
-    DQ_CHK(cap < 8 || (ob >= sh + produced && ob + 4 * nl * (NARR + NCK) <= OUTCAP), CHK_K2_LANES);
-    // tokens: recorded by the fast-path decodes; replayed when this deflate block has the arrays
-    const uint32_t slot = TOKREC ? (uint32_t)__builtin_amdgcn_readfirstlane(L.misc[M_SLOT]) : 0u;
-    uint8_t* const tokb = TOKREC ? tokpool + (size_t)slot * TOK_SLOT_BYTES : nullptr;
-    const bool tk = REPLAY && slot < (uint32_t)TOK_SLOTS && TS != nullptr && !slow;
+    if (cap >= 8) CK = reinterpret_cast<uint32_t*>(SC + nl);
+    DQ_CHK(cap < 8 || (ob >= sh + produced && ob + 4 * nl * (7 + NCK) <= OUTCAP), CHK_K2_LANES);
 #ifdef DQ_CHECKED
     GSrc gsrc{W, (endbits >> 5) + 8, 1u << 12};
 #else
@@ -1335,13 +1205,10 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       int32_t B = -1, E = 0, c = 0;
       if (CK)
         for (int j = 0; j < NCK; j++) CK[j * nl + t] = 0xffffffffu;
-      uint32_t ns = 0;
       const int f = slow ? run_seg<true>(gsrc, L, start, sB, sE, endbits, &B, &E, &c,
                                          CK ? CK + t : nullptr, nl, CKI, NCK)
-                         : run_seg<false, TOKREC>(gsrc, L, start, sB, sE, endbits, &B, &E, &c,
-                                                CK ? CK + t : nullptr, nl, CKI, NCK, tokb,
-                                                4u * (uint32_t)t, &ns);
-      if (tk) TS[t] = min(ns, 255u);
+                         : run_seg<false>(gsrc, L, start, sB, sE, endbits, &B, &E, &c,
+                                          CK ? CK + t : nullptr, nl, CKI, NCK);
       AB[t] = B;
       AE[t] = (E << 3) | f;
       AC[t] = c;
@@ -1389,17 +1256,12 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
         int jmerge = -1;
         const uint32_t sB = a + (uint32_t)lt * seg;
         // a speculative lane that found no boundary (F_DEAD) recorded no checkpoints
-        uint32_t ti = 0;
         const int f = slow ? run_redo<true>(gsrc, L, s0, sB, sE, endbits, CK ? CK + lt : nullptr,
                                             nl, SE[lt], SC[lt], &E, &c, CKI, NCK,
                                             TIMING ? &jmerge : nullptr)
-                           : run_redo<false, TOKREC>(gsrc, L, s0, sB, sE, endbits, CK ? CK + lt : nullptr,
-                                                   nl, SE[lt], SC[lt], &E, &c, CKI, NCK,
-                                                   TIMING ? &jmerge : nullptr, tokb + TOK_REGION,
-                                                   4u * (uint32_t)lt, &ti);
-        if (tk)
-          TS[lt] = (TS[lt] & 0xffu) | ((ti & 0xffu) << 8) | (((ti >> 17) & 1u) << 16) | (1u << 17) |
-                   (ti & 0x7f000000u);
+                           : run_redo<false>(gsrc, L, s0, sB, sE, endbits, CK ? CK + lt : nullptr,
+                                             nl, SE[lt], SC[lt], &E, &c, CKI, NCK,
+                                             TIMING ? &jmerge : nullptr);
         const int32_t ae = (E << 3) | f;
         if (ae != AE[lt]) L.misc[M_DIRTY + (round & 1)] = 1;  // the successor's start moved
         AB[lt] = (int32_t)s0;
@@ -1460,27 +1322,9 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     gsrc.tag = 3u << 12;
 #endif
     if (t <= last && myoff < isize) {
-      // replay the lane's tokens: its speculative ones, or its last re-decode's and, after a
-      // merge, the speculative ones from the merge on; else (a region overflowed) decode again
-      bool done = false;
-      if (tk) {
-        const uint32_t ts = TS[t];
-        const uint32_t ns = ts & 0xffu, nr = (ts >> 8) & 0xffu, ks = (ts >> 24) & 0x7fu;
-        const bool redone = (ts >> 17) & 1u, merged = (ts >> 16) & 1u;
-        if (!redone && ns <= (uint32_t)NTOK) {
-          replay_seg(tokb, 4u * (uint32_t)t, ns, 0u, 0u, 0u, L, myoff, isize, sh);
-          done = true;
-        } else if (redone && nr <= (uint32_t)NTOK && (!merged || (ns <= (uint32_t)NTOK && ks <= ns))) {
-          replay_seg(tokb, TOK_REGION + 4u * (uint32_t)t, nr, 4u * (uint32_t)t, ks, merged ? ns - ks : 0u,
-                     L, myoff, isize, sh);
-          done = true;
-        }
-      }
-      if (!done) {
-        const uint32_t sE = t == nl - 1 ? 0xffffffffu : a + (uint32_t)(t + 1) * seg;
-        if (slow) emit_seg<true>(gsrc, L, (uint32_t)myB, sE, endbits, myoff, isize, sh);
-        else emit_seg<false>(gsrc, L, (uint32_t)myB, sE, endbits, myoff, isize, sh);
-      }
+      const uint32_t sE = t == nl - 1 ? 0xffffffffu : a + (uint32_t)(t + 1) * seg;
+      if (slow) emit_seg<true>(gsrc, L, (uint32_t)myB, sE, endbits, myoff, isize, sh);
+      else emit_seg<false>(gsrc, L, (uint32_t)myB, sE, endbits, myoff, isize, sh);
     }
     const int32_t nextpos = L.misc[M_NEXT];
     __syncthreads();
@@ -1503,11 +1347,6 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
     }
   }
   __syncthreads();
-  if (TOKREC && t == 0) {  // release the token slot (every replay read is done: the emit's barrier)
-    const uint32_t sl = (uint32_t)L.misc[M_SLOT];
-    uint32_t* const tokbits = reinterpret_cast<uint32_t*>(tokpool + (size_t)(TOK_SLOTS + 1) * TOK_SLOT_BYTES);
-    if (sl < (uint32_t)TOK_SLOTS) atomicAnd(&tokbits[sl >> 5], ~(1u << (sl & 31)));
-  }
   int32_t err = L.misc[M_ERR];
   if (!err && !deferred && produced != isize) err = ST_SHORT;
   // the bytes this workgroup resolves, stores and checksums: the whole block, or those before the
@@ -2536,7 +2375,6 @@ constexpr int kMaxDevices = 64;
 struct DevTables {
   std::once_flag once;
   uint32_t* crc_init = nullptr;
-  uint8_t* tokpool = nullptr;  // TOK_SLOTS + 1 token slots, then the slots' claim bitmap
   bool ok = false;
 };
 DevTables g_dev[kMaxDevices];
@@ -2560,11 +2398,6 @@ const uint32_t* inflate3_tables(int device) {
     ok = ok && hipMalloc(&D.crc_init, sizeof(uint32_t) * H.init.size()) == hipSuccess;
     ok = ok && hipMemcpy(D.crc_init, H.init.data(), sizeof(uint32_t) * H.init.size(),
                          hipMemcpyHostToDevice) == hipSuccess;
-    if (TOKREC) {
-      const size_t pool = (size_t)(TOK_SLOTS + 1) * TOK_SLOT_BYTES;
-      ok = ok && hipMalloc(&D.tokpool, pool + TOK_SLOTS / 8) == hipSuccess;
-      ok = ok && hipMemset(D.tokpool + pool, 0, TOK_SLOTS / 8) == hipSuccess;
-    }
     D.ok = ok;
     if (prev >= 0) (void)hipSetDevice(prev);
   });
@@ -2590,14 +2423,10 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
   static const bool tail_on = !getenv("DQ_TAIL") || atoi(getenv("DQ_TAIL")) != 0;
   TailDesc* td = tail_on ? static_cast<TailDesc*>(tails_buf) : nullptr;
   if (td) (void)hipMemsetAsync(td, 0, sizeof(TailDesc) * (size_t)ngrid, s);
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  if (dev < 0 || dev >= kMaxDevices || !inflate3_tables(dev)) return;  // the caller checked it
-  uint8_t* const tokpool = g_dev[dev].tokpool;
 #define DQ_LAUNCH(TM, NBT, GT)                                                                  \
   hipLaunchKernelGGL((inflate_block_kernel<TM, NBT, GT>), dim3((unsigned)ngrid), dim3(WG), ldspad, s, C, \
                      blk_pos, blk_csize, blk_usize, uoff, ngrid, U, status, verify_crc, crc_init, tim, ov, \
-                     sflags, sel, td, tokpool)
+                     sflags, sel, td)
   // NB = 4 chunks of G = 1 byte per thread: (1, 4) measures the same, (2, 1) slower (round 5)
   if (tim)
     DQ_LAUNCH(true, DQ_RES_NB, DQ_RES_G);
