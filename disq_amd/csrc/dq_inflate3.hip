@@ -140,7 +140,6 @@ struct alignas(16) LdsI {
   static constexpr int kLSUB = T_LSUB, kDROOT = T_DROOT, kDSUB = T_DSUB;
   [[maybe_unused]] static constexpr int kTEND = T_END;  // DQ_CHK bound
   static constexpr bool kPair = true;  // literal-pair table (dsym)
-  uint8_t out[OUTCAP];            // output image: byte x at out[sh + x]
   alignas(8) uint32_t bm[2048];   // match-start bitmap (read as 64-bit words in resolve)
   union {
     struct {
@@ -192,8 +191,12 @@ struct alignas(16) LdsI {
     // `small` may hold the arrays), one per lane in the emit (both dead)
     uint32_t scratch[16 + 8 * 7];
   };
+  // output image: byte x at out[sh + x].  Last, so every table above sits below 64 KiB and its
+  // constant offset folds into the ds_read/ds_write offset field (one VALU add fewer per lookup)
+  alignas(16) uint8_t out[OUTCAP];
 };
 static_assert(sizeof(((LdsI*)nullptr)->scratch) >= 64 * 4, "one emit dummy word per lane");
+static_assert(offsetof(LdsI, out) < 65536 - 4096, "the tables' offsets fit the DS offset field");
 static_assert(sizeof(LdsI) <= 81920, "two workgroups per CU");
 static_assert(HB_WORDS * 4 <= T_END * 2, "header staging fits the decode table");
 
