@@ -78,6 +78,10 @@ def parse():
     ap.add_argument("--e2e-window-gb", type=float, default=2.0,
                     help="end-to-end: compressed GB per window")
     ap.add_argument("--e2e-depth", type=int, default=3, help="end-to-end: overlapping windows")
+    ap.add_argument("--e2e-export", choices=("lean", "raw"), default="lean",
+                    help="end-to-end export: lean = voffsets + raw record bytes (DQ_EXPORT_LEAN, "
+                         "the fields are parsed from the raw bytes as BAMRecordCodec.decode does), "
+                         "raw = also every SoA field, hash and raw offset")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="generation rehearsal: generate rank 0's share of an N-rank run under "
                          "the N-rank thread budget, report the time as JSON and exit (no GPU work)")
@@ -802,12 +806,15 @@ def end_to_end(data, args, resident_digest=None, header=None):
     timed with the steps): the file is in /dev/shm (RAM, as the page cache would hold it) and is
     read in windows of whole partitions by `depth` contexts on their own host threads and HIP
     streams (disq_amd.stream): one window's file -> pinned -> HBM copy, another's pipeline and a
-    third's export of every record's SoA row and raw bytes to host memory (dq_read) run at once,
+    third's export of every record (lean, the default: its voffset and raw bytes; --e2e-export raw:
+    also its SoA row) to host memory (dq_read) run at once,
     as Disq's tasks overlap their prefetcher's reads with decoding
     (SeekableByteChannelPrefetcher.java:253-298).  The whole-file digest must equal the resident
     run's."""
     if data is None:
         return None
+    import numpy as np
+
     from disq_amd import _lib, stream
     path = f"/dev/shm/disq_bench_{os.getpid()}.bam"
     try:
@@ -820,12 +827,25 @@ def end_to_end(data, args, resident_digest=None, header=None):
         keep = []
         lk = __import__("threading").Lock()
 
+        mode = "lean" if args.e2e_export == "lean" else True
+
         def export(k, c, shard):
-            b = c.read(with_raw=True)
+            b = c.read(with_raw=mode)
             n = len(b["voffset"])
             raw = 0 if b["raw"] is None else len(b["raw"])
-            # the consumer's view: the last record's raw bytes end where its offsets say
-            assert raw == (int(b["raw_offset"][-1]) + 4 + int(b["block_size"][-1]) if n else 0)
+            if mode == "lean":
+                # the consumer's view: the first records parse from the raw bytes (record i + 1
+                # starts 4 + block_size bytes after record i) and their voffsets ascend
+                m = min(n, 256)
+                if m:
+                    o = 0
+                    for i in range(m):
+                        o += 4 + int.from_bytes(bytes(b["raw"][o:o + 4]), "little")
+                    assert o <= raw and (m < n or o == raw)
+                    assert bool(np.all(np.diff(b["voffset"][:m].astype(np.int64)) > 0))
+            else:
+                # the last record's raw bytes end where its offsets say
+                assert raw == (int(b["raw_offset"][-1]) + 4 + int(b["block_size"][-1]) if n else 0)
             with lk:
                 exported["records"] += n
                 exported["raw"] += raw
@@ -849,7 +869,7 @@ def end_to_end(data, args, resident_digest=None, header=None):
             t0 = time.perf_counter()
             stream.stream_read(path, len(data), header, window=window, depth=args.e2e_depth,
                                split_size=args.split_size, verify_crc=not args.no_crc,
-                               on_window=lambda *a: a[1].read(with_raw=True), contexts=ctxs,
+                               on_window=lambda *a: a[1].read(with_raw=mode), contexts=ctxs,
                                ramp=True)
             warm_s = time.perf_counter() - t0
             # ramp: quarter and half windows first and last, so the first export starts sooner and
@@ -879,6 +899,7 @@ def end_to_end(data, args, resident_digest=None, header=None):
                "overlap": round((res["open_s"] + res["run_s"] + res["on_window_s"]) / secs, 2),
                "records": exported["records"], "raw_gb": round(exported["raw"] / 1e9, 3),
                "soa_gb": round(exported["soa"] / 1e9, 3),
+               "export_mode": args.e2e_export,
                "digest": f"{res['digest']:016x}",
                "digest_match": None if resident_digest is None else res["digest"] == resident_digest,
                "exported_digest_match": exported_digest == res["digest"],
@@ -887,7 +908,8 @@ def end_to_end(data, args, resident_digest=None, header=None):
                "arena_gb_per_context": round(arena / 1e9, 2),
                "path": "page cache (/dev/shm) -> pinned staging (16 pread threads per piece, "
                        "double-buffered with the H2D copies) -> HBM -> pipeline -> host SoA + raw "
-                       "bytes by DMA into a pinned arena, windows of whole partitions on "
+                       "bytes (lean: + voffsets only) by DMA into a pinned arena, windows of "
+                       "whole partitions on "
                        "overlapping contexts (disq_amd.stream + dq_open_shard_path + dq_read)"}
         try:  # the link's ceiling and how close the read comes to it
             pc = pcie_ceiling()

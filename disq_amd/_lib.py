@@ -25,6 +25,9 @@ class DqOpts(C.Structure):
 
 
 COMPAT_DISQ_EXACT, COMPAT_DEDUPE = 0, 1
+# export modes (the with_raw argument; include/disq_gpu.h)
+EXPORT_FIELDS, EXPORT_RAW, EXPORT_LEAN = 0, 1, 2
+ABI_VERSION = 2  # DQ_ABI_VERSION this binding maps dq_batch for
 
 
 class DqChunk(C.Structure):
@@ -110,7 +113,7 @@ EXPORTS = ("dq_ctx_create", "dq_ctx_destroy", "dq_last_error", "dq_version", "dq
            "dq_text_open_path", "dq_text_run", "dq_text_read", "dq_text_batch_free",
            "dq_bgzf_compress", "dq_bgzf_compress_resident", "dq_bgzf_fetch",
            "dq_text_set_index", "dq_text_set_intervals", "dq_decode_file_multi",
-           "dq_set_export_arena", "dq_checked_report")
+           "dq_set_export_arena", "dq_checked_report", "dq_abi_version")
 
 _lib = None
 _lock = threading.Lock()
@@ -135,6 +138,10 @@ def lib():
         L.dq_last_error.restype = C.c_char_p
         L.dq_last_error.argtypes = [vp]
         L.dq_version.restype = C.c_char_p
+        L.dq_abi_version.restype = C.c_int32
+        if L.dq_abi_version() != ABI_VERSION:  # dq_batch's layout is what this binding maps
+            raise RuntimeError(f"{_build.gpu_lib_path()}: ABI {L.dq_abi_version()}, binding expects "
+                               f"{ABI_VERSION}")
         L.dq_open_memory.argtypes = [vp, vp, C.c_int64]
         L.dq_open_path.argtypes = [vp, C.c_char_p]
         L.dq_set_index.argtypes = [vp, vp, C.c_int64]
@@ -206,6 +213,45 @@ FIELDS = (("voffset", np.uint64), ("block_size", np.int32), ("ref_id", np.int32)
           ("next_pos", np.int32), ("tlen", np.int32), ("flag", np.uint16), ("bin", np.uint16),
           ("n_cigar", np.uint16), ("mapq", np.uint8), ("l_read_name", np.uint8),
           ("hash", np.uint64), ("raw_offset", np.int64))
+
+
+def export_mode(with_raw):
+    """True / False / "lean" (or the DQ_EXPORT_* value) -> the C ABI's export mode."""
+    if isinstance(with_raw, str):
+        if with_raw != "lean":
+            raise ValueError(f"unknown export mode {with_raw!r}")
+        return EXPORT_LEAN
+    if isinstance(with_raw, (bool, np.bool_)):
+        return EXPORT_RAW if with_raw else EXPORT_FIELDS
+    return int(with_raw)
+
+
+# the fixed fields of a BAM record as its first 36 raw bytes hold them (SAMv1 section 4.2), parsed
+# the way htsjdk's BAMRecordCodec.decode reads them (H/BAMFileReader2.java:929-931)
+LEAN_HEAD = np.dtype([("block_size", "<i4"), ("ref_id", "<i4"), ("pos", "<i4"),
+                      ("l_read_name", "u1"), ("mapq", "u1"), ("bin", "<u2"), ("n_cigar", "<u2"),
+                      ("flag", "<u2"), ("l_seq", "<i4"), ("next_ref_id", "<i4"),
+                      ("next_pos", "<i4"), ("tlen", "<i4")])
+
+
+def parse_lean(raw, n):
+    """A DQ_EXPORT_LEAN batch's records as a consumer reads them: walk the raw bytes (record i + 1
+    starts 4 + block_size bytes after record i) and take the fixed fields from each record's first
+    36 bytes.  Returns (raw_offset, fields) with fields a dict of arrays like a full batch's.  A
+    plain loop over the block sizes: for tests and small batches (a JVM consumer walks the same
+    way in BAMRecordCodec.decode)."""
+    raw = np.asarray(raw, np.uint8)
+    off = np.zeros(n, np.int64)
+    o = 0
+    bs = raw.view(np.uint8)
+    for i in range(n):
+        off[i] = o
+        o += 4 + int.from_bytes(bs[o:o + 4].tobytes(), "little")
+    if o != len(raw):
+        raise ValueError(f"lean batch: {n} records end at byte {o}, raw holds {len(raw)}")
+    idx = off[:, None] + np.arange(36)[None, :]
+    head = raw[idx].copy().view(LEAN_HEAD).reshape(n)
+    return off, {k: head[k].copy() for k in LEAN_HEAD.names}
 
 
 class _BatchOwner:
@@ -337,11 +383,11 @@ class Context:
         bp = C.POINTER(DqBatch)()
         if traversal is None:
             check(self._h, lib().dq_decode_chunk(self._h, os.fsencode(path), vstart, vend,
-                                                 int(with_raw), C.byref(bp)))
+                                                 export_mode(with_raw), C.byref(bp)))
         else:
             t, keep = self._traversal(traversal)
             check(self._h, lib().dq_decode_chunk_filtered(self._h, os.fsencode(path), vstart, vend,
-                                                          C.byref(t), int(with_raw), C.byref(bp)))
+                                                          C.byref(t), export_mode(with_raw), C.byref(bp)))
         return batch_to_numpy(bp, self)
 
     def stats(self):
@@ -523,11 +569,11 @@ class Context:
         self._arena_guard("decode")
         bp = C.POINTER(DqBatch)()
         if traversal is None:
-            check(self._h, lib().dq_decode(self._h, vstart, vend, int(with_raw), C.byref(bp)))
+            check(self._h, lib().dq_decode(self._h, vstart, vend, export_mode(with_raw), C.byref(bp)))
         else:
             t, keep = self._traversal(traversal)
             check(self._h, lib().dq_decode_filtered(self._h, vstart, vend, C.byref(t),
-                                                    int(with_raw), C.byref(bp)))
+                                                    export_mode(with_raw), C.byref(bp)))
         return batch_to_numpy(bp, self)
 
     def set_export_arena(self, nbytes):
@@ -542,7 +588,7 @@ class Context:
         bp = C.POINTER(DqBatch)()
         t, keep = self._traversal(traversal)
         check(self._h, lib().dq_read(self._h, C.byref(t) if t is not None else None,
-                                     int(with_raw), C.byref(bp)))
+                                     export_mode(with_raw), C.byref(bp)))
         return batch_to_numpy(bp, self)
 
     def run_resident(self, traversal=None):

@@ -1233,10 +1233,14 @@ static int bgzf_compress_dev(dq_ctx* ctx, const uint8_t* d_src, int64_t len, dou
   if (!deflate_tables(ctx->o.device)) RET(DQ_EDEVICE, "deflate table initialisation failed");
   hipStream_t s = ctx->s;
   const int64_t nblk = bgzf_block_count(len);
+#ifdef DQ_TUNING
   static const int64_t max_batch = [] {
     const char* e = getenv("DQ_DEFLATE_BATCH");
     return e && atoll(e) > 0 ? (int64_t)atoll(e) : (int64_t)16384;
   }();
+#else
+  constexpr int64_t max_batch = 16384;  // blocks per launch (profiles/r4au_deflate_dense_stage.txt)
+#endif
   // (the batches evenly sized: the last one no shorter than the others)
   const int64_t nbat = std::max<int64_t>(1, (nblk + max_batch - 1) / max_batch);
   const int64_t batch = std::max<int64_t>(1, (nblk + nbat - 1) / nbat);
@@ -1377,6 +1381,7 @@ static int make_batch(dq_ctx* ctx, const std::vector<std::pair<int64_t, int64_t>
                       const std::vector<int64_t>* explicit_idx, int32_t with_raw,
                       const std::vector<int64_t>& part_bounds, dq_batch** out) {
   hipStream_t s = ctx->s;
+  if (with_raw < DQ_EXPORT_FIELDS || with_raw > DQ_EXPORT_LEAN) RET(DQ_EINVAL, "unknown export mode");
   // adjacent ranges (consecutive partitions) form one run of the resident arrays
   std::vector<std::pair<int64_t, int64_t>> ranges;
   for (auto& r : ranges_in) {
@@ -1493,7 +1498,11 @@ static int make_batch(dq_ctx* ctx, const std::vector<std::pair<int64_t, int64_t>
   // host arrays: the pinned arena when it is set and large enough, else heap memory
   const size_t soa_bytes = 8 * ((8 * m + 7) / 8) * 3 + 8 * ((4 * m + 7) / 8) * 7 +
                            8 * ((2 * m + 7) / 8) * 3 + 8 * ((m + 7) / 8) * 2;
-  const size_t want = soa_bytes + (with_raw ? (size_t)std::max<int64_t>(1, raw_len) : 0) + 64 * 20;
+  // DQ_EXPORT_LEAN: voffsets + raw bytes only -- every other field is in each record's first 36
+  // raw bytes, where htsjdk's BAMRecordCodec.decode parses it (H/BAMFileReader2.java:929-931)
+  const bool lean = with_raw == DQ_EXPORT_LEAN;
+  const size_t want = (lean ? 8 * ((8 * m + 7) / 8) : soa_bytes) +
+                      (with_raw ? (size_t)std::max<int64_t>(1, raw_len) : 0) + 64 * 20;
   const bool in_arena = ctx->arena && want <= ctx->arena_cap;
   if (in_arena) {
     std::lock_guard<std::mutex> lk(ctx->ah->mu);
@@ -1514,31 +1523,38 @@ static int make_batch(dq_ctx* ctx, const std::vector<std::pair<int64_t, int64_t>
   };
   b->in_arena = in_arena ? 1 : 0;
   b->voffset = (uint64_t*)halloc(8 * m);
-  b->block_size = (int32_t*)halloc(4 * m);
-  b->ref_id = (int32_t*)halloc(4 * m);
-  b->pos = (int32_t*)halloc(4 * m);
-  b->l_seq = (int32_t*)halloc(4 * m);
-  b->next_ref_id = (int32_t*)halloc(4 * m);
-  b->next_pos = (int32_t*)halloc(4 * m);
-  b->tlen = (int32_t*)halloc(4 * m);
-  b->flag = (uint16_t*)halloc(2 * m);
-  b->bin = (uint16_t*)halloc(2 * m);
-  b->n_cigar = (uint16_t*)halloc(2 * m);
-  b->mapq = (uint8_t*)halloc(m);
-  b->l_read_name = (uint8_t*)halloc(m);
-  b->hash = (uint64_t*)halloc(8 * m);
-  b->raw_offset = (int64_t*)halloc(8 * m);
-  if (!b->voffset || !b->block_size || !b->ref_id || !b->pos || !b->l_seq || !b->next_ref_id ||
-      !b->next_pos || !b->tlen || !b->flag || !b->bin || !b->n_cigar || !b->mapq ||
-      !b->l_read_name || !b->hash || !b->raw_offset)
-    return fail(DQ_ENOMEM);
+  if (!lean) {
+    b->block_size = (int32_t*)halloc(4 * m);
+    b->ref_id = (int32_t*)halloc(4 * m);
+    b->pos = (int32_t*)halloc(4 * m);
+    b->l_seq = (int32_t*)halloc(4 * m);
+    b->next_ref_id = (int32_t*)halloc(4 * m);
+    b->next_pos = (int32_t*)halloc(4 * m);
+    b->tlen = (int32_t*)halloc(4 * m);
+    b->flag = (uint16_t*)halloc(2 * m);
+    b->bin = (uint16_t*)halloc(2 * m);
+    b->n_cigar = (uint16_t*)halloc(2 * m);
+    b->mapq = (uint8_t*)halloc(m);
+    b->l_read_name = (uint8_t*)halloc(m);
+    b->hash = (uint64_t*)halloc(8 * m);
+    b->raw_offset = (int64_t*)halloc(8 * m);
+    if (!b->block_size || !b->ref_id || !b->pos || !b->l_seq || !b->next_ref_id ||
+        !b->next_pos || !b->tlen || !b->flag || !b->bin || !b->n_cigar || !b->mapq ||
+        !b->l_read_name || !b->hash || !b->raw_offset)
+      return fail(DQ_ENOMEM);
+  }
+  if (!b->voffset) return fail(DQ_ENOMEM);
   // pinned destination: one DMA per array (with DQ_EXPORT_STREAMS=2 the arrays, and the halves of
   // the raw bytes, alternate between two streams so two DMA engines run); heap: through the staging
   // buffers
+#ifdef DQ_TUNING
   static const bool two = [] {
     const char* e = getenv("DQ_EXPORT_STREAMS");
     return e && atoi(e) == 2;
   }();
+#else
+  constexpr bool two = false;  // two export streams gained nothing (profiles/r4x_*): tuning only
+#endif
   const bool split = in_arena && two && n > 0;
   if (split) {
     if (!ctx->sx) {
@@ -1563,14 +1579,16 @@ static int make_batch(dq_ctx* ctx, const std::vector<std::pair<int64_t, int64_t>
     auto fld = [&](const void* dbase, size_t esz, void* dst) {
       return d2h((const char*)dbase + (size_t)first * esz, (size_t)n * esz, dst);
     };
-    if ((rc = d2h(d_voff, 8 * (size_t)n, b->voffset)) || (rc = fld(rows.block_size, 4, b->block_size)) ||
-        (rc = fld(rows.ref_id, 4, b->ref_id)) || (rc = fld(rows.pos, 4, b->pos)) ||
-        (rc = fld(rows.l_seq, 4, b->l_seq)) || (rc = fld(rows.next_ref_id, 4, b->next_ref_id)) ||
-        (rc = fld(rows.next_pos, 4, b->next_pos)) || (rc = fld(rows.tlen, 4, b->tlen)) ||
-        (rc = fld(rows.flag, 2, b->flag)) || (rc = fld(rows.bin, 2, b->bin)) ||
-        (rc = fld(rows.n_cigar, 2, b->n_cigar)) || (rc = fld(rows.mapq, 1, b->mapq)) ||
-        (rc = fld(rows.l_read_name, 1, b->l_read_name)) || (rc = fld(rows.hash, 8, b->hash)) ||
-        (rc = d2h(ctx->x_boff.p, 8 * (size_t)n, b->raw_offset)))
+    if ((rc = d2h(d_voff, 8 * (size_t)n, b->voffset))) return fail(rc);
+    if (!lean &&
+        ((rc = fld(rows.block_size, 4, b->block_size)) ||
+         (rc = fld(rows.ref_id, 4, b->ref_id)) || (rc = fld(rows.pos, 4, b->pos)) ||
+         (rc = fld(rows.l_seq, 4, b->l_seq)) || (rc = fld(rows.next_ref_id, 4, b->next_ref_id)) ||
+         (rc = fld(rows.next_pos, 4, b->next_pos)) || (rc = fld(rows.tlen, 4, b->tlen)) ||
+         (rc = fld(rows.flag, 2, b->flag)) || (rc = fld(rows.bin, 2, b->bin)) ||
+         (rc = fld(rows.n_cigar, 2, b->n_cigar)) || (rc = fld(rows.mapq, 1, b->mapq)) ||
+         (rc = fld(rows.l_read_name, 1, b->l_read_name)) || (rc = fld(rows.hash, 8, b->hash)) ||
+         (rc = d2h(ctx->x_boff.p, 8 * (size_t)n, b->raw_offset))))
       return fail(rc);
   }
   if (with_raw && n > 0) {
@@ -2054,12 +2072,16 @@ static void reset_open(dq_ctx* ctx, int64_t len) {
 // Bytes [off, off + len) of an open file into C (plus the 4 KiB zero pad): read() into two pinned
 // staging buffers in turn, each copied asynchronously while the next piece is read from the page
 // cache (the role of Disq's 2 x 4 MB NIO prefetcher, SeekableByteChannelPrefetcher.java:45).
-// DQ_MMAP=1: the same by DMA straight from the file's page-cache pages (the range mapped read-only
+// DQ_MMAP=1 (tuning builds, -DDQ_TUNING): the same by DMA straight from the file's page-cache pages (the range mapped read-only
 // and registered with the device, one copy into C).  Measured slower than the staging path (page
 // registration of 2 GB windows: end-to-end 14.9-19.9 GB/s against 27.5-35.3 GB/s,
 // profiles/r3s_e2e_ab.txt), so it is off by default.  Returns 1 when it is off or unavailable.
 static int upload_file_range_mapped(dq_ctx* ctx, int fd, int64_t off, int64_t len) {
+#ifdef DQ_TUNING
   static const bool enabled = getenv("DQ_MMAP") && atoi(getenv("DQ_MMAP")) == 1;
+#else
+  constexpr bool enabled = false;  // measured slower than pinned staging (profiles/r3s_e2e_ab.txt)
+#endif
   if (!enabled || len < (64 << 20)) return 1;
   const int64_t pg = (int64_t)sysconf(_SC_PAGESIZE);
   const int64_t a = off & ~(pg - 1), d = off - a, mlen = len + d;
@@ -2220,8 +2242,9 @@ static int chunk_run(dq_ctx* ctx, int fd, int64_t flen, uint64_t vstart, uint64_
   return 0;
 }
 
-// One batch holding the records of `parts` in order (a single partition).
-static int concat_batches(dq_ctx* ctx, const std::vector<dq_batch*>& parts, dq_batch** out) {
+// One batch holding the records of `parts` in order (a single partition).  The parts carry every
+// field (the digest needs the hashes); lean: the result keeps only voffset and raw.
+static int concat_batches(dq_ctx* ctx, const std::vector<dq_batch*>& parts, bool lean, dq_batch** out) {
   int64_t n = 0, raw = 0;
   bool with_raw = true;
   for (const dq_batch* b : parts) {
@@ -2234,49 +2257,54 @@ static int concat_batches(dq_ctx* ctx, const std::vector<dq_batch*>& parts, dq_b
   const size_t m = (size_t)std::max<int64_t>(1, n);
   o->n_records = n;
   o->voffset = (uint64_t*)malloc(8 * m);
-  o->block_size = (int32_t*)malloc(4 * m);
-  o->ref_id = (int32_t*)malloc(4 * m);
-  o->pos = (int32_t*)malloc(4 * m);
-  o->l_seq = (int32_t*)malloc(4 * m);
-  o->next_ref_id = (int32_t*)malloc(4 * m);
-  o->next_pos = (int32_t*)malloc(4 * m);
-  o->tlen = (int32_t*)malloc(4 * m);
-  o->flag = (uint16_t*)malloc(2 * m);
-  o->bin = (uint16_t*)malloc(2 * m);
-  o->n_cigar = (uint16_t*)malloc(2 * m);
-  o->mapq = (uint8_t*)malloc(m);
-  o->l_read_name = (uint8_t*)malloc(m);
-  o->hash = (uint64_t*)malloc(8 * m);
-  o->raw_offset = (int64_t*)malloc(8 * m);
+  if (!lean) {
+    o->block_size = (int32_t*)malloc(4 * m);
+    o->ref_id = (int32_t*)malloc(4 * m);
+    o->pos = (int32_t*)malloc(4 * m);
+    o->l_seq = (int32_t*)malloc(4 * m);
+    o->next_ref_id = (int32_t*)malloc(4 * m);
+    o->next_pos = (int32_t*)malloc(4 * m);
+    o->tlen = (int32_t*)malloc(4 * m);
+    o->flag = (uint16_t*)malloc(2 * m);
+    o->bin = (uint16_t*)malloc(2 * m);
+    o->n_cigar = (uint16_t*)malloc(2 * m);
+    o->mapq = (uint8_t*)malloc(m);
+    o->l_read_name = (uint8_t*)malloc(m);
+    o->hash = (uint64_t*)malloc(8 * m);
+    o->raw_offset = (int64_t*)malloc(8 * m);
+  }
   o->raw = with_raw ? (uint8_t*)malloc((size_t)std::max<int64_t>(1, raw)) : nullptr;
   o->raw_len = raw;
   o->n_partitions = 1;
   o->part_offset = (int64_t*)malloc(16);
   o->part_digest = (uint64_t*)calloc(2, sizeof(uint64_t));
-  if (!o->voffset || !o->block_size || !o->ref_id || !o->pos || !o->l_seq || !o->next_ref_id ||
-      !o->next_pos || !o->tlen || !o->flag || !o->bin || !o->n_cigar || !o->mapq ||
-      !o->l_read_name || !o->hash || !o->raw_offset || (with_raw && !o->raw) || !o->part_offset ||
-      !o->part_digest) {
+  if (!o->voffset || (with_raw && !o->raw) || !o->part_offset || !o->part_digest ||
+      (!lean && (!o->block_size || !o->ref_id || !o->pos || !o->l_seq || !o->next_ref_id ||
+                 !o->next_pos || !o->tlen || !o->flag || !o->bin || !o->n_cigar || !o->mapq ||
+                 !o->l_read_name || !o->hash || !o->raw_offset))) {
     dq_batch_free(o);
     RET(DQ_ENOMEM, "out of host memory");
   }
   int64_t k = 0, r = 0;
+  uint64_t d = 0;
   for (const dq_batch* b : parts) {
     const size_t c = (size_t)b->n_records;
 #define CP(f, sz) memcpy(o->f + k, b->f, (sz) * c)
-    CP(voffset, 8); CP(block_size, 4); CP(ref_id, 4); CP(pos, 4); CP(l_seq, 4); CP(next_ref_id, 4);
-    CP(next_pos, 4); CP(tlen, 4); CP(flag, 2); CP(bin, 2); CP(n_cigar, 2); CP(mapq, 1);
-    CP(l_read_name, 1); CP(hash, 8);
+    CP(voffset, 8);
+    if (!lean) {
+      CP(block_size, 4); CP(ref_id, 4); CP(pos, 4); CP(l_seq, 4); CP(next_ref_id, 4);
+      CP(next_pos, 4); CP(tlen, 4); CP(flag, 2); CP(bin, 2); CP(n_cigar, 2); CP(mapq, 1);
+      CP(l_read_name, 1); CP(hash, 8);
+      for (size_t i = 0; i < c; i++) o->raw_offset[k + (int64_t)i] = b->raw_offset[i] + r;
+    }
 #undef CP
-    for (size_t i = 0; i < c; i++) o->raw_offset[k + (int64_t)i] = b->raw_offset[i] + r;
+    for (size_t i = 0; i < c; i++) d += dq_mix64(b->hash[i] + (uint64_t)(k + (int64_t)i + 1) * DQ_K_LEN);
     if (with_raw && b->raw_len) memcpy(o->raw + r, b->raw, (size_t)b->raw_len);
     k += (int64_t)c;
     r += b->raw_len;
   }
   o->part_offset[0] = 0;
   o->part_offset[1] = n;
-  uint64_t d = 0;
-  for (int64_t i = 0; i < n; i++) d += dq_mix64(o->hash[i] + (uint64_t)(i + 1) * DQ_K_LEN);
   o->part_digest[0] = d;
   *out = o;
   return 0;
@@ -2294,7 +2322,8 @@ static int check_tail_reachable(dq_ctx* ctx, const dq_traversal* tr) {
 
 extern "C" {
 
-const char* dq_version(void) { return "disq_amd 0.1 (gfx950)"; }
+const char* dq_version(void) { return "disq_amd 0.2 (gfx950)"; }
+int32_t dq_abi_version(void) { return DQ_ABI_VERSION; }
 
 int dq_ctx_create(dq_ctx** out, const dq_opts* opts) {
   if (!out) return DQ_EINVAL;
@@ -2462,6 +2491,10 @@ int dq_decode_chunk_filtered(dq_ctx* ctx, const char* path, uint64_t vstart, uin
   if (!tr->has_intervals && !tr->traverse_unplaced_unmapped)
     RET(DQ_EINVAL, "Traversing mapped reads only is not supported.");
   if (!ctx->have_bai) RET(DQ_EINVAL, "Intervals set but no index file found");
+  if (with_raw < DQ_EXPORT_FIELDS || with_raw > DQ_EXPORT_LEAN) RET(DQ_EINVAL, "unknown export mode");
+  // the windows' batches carry every field (their hashes make the chunk's digest); a lean result
+  // keeps voffset + raw of them (concat_batches)
+  const int32_t part_mode = with_raw == DQ_EXPORT_LEAN ? DQ_EXPORT_RAW : with_raw;
   Fd f;
   int64_t flen = 0;
   int rc = open_fd(ctx, path, f, &flen);
@@ -2526,7 +2559,7 @@ int dq_decode_chunk_filtered(dq_ctx* ctx, const char* path, uint64_t vstart, uin
             if (keep[(size_t)k]) kept.push_back(idx[(size_t)k]);
         }
         dq_batch* b = nullptr;
-        if ((rc = make_batch(ctx, {}, &kept, with_raw, {0, (int64_t)kept.size()}, &b))) return cleanup(rc);
+        if ((rc = make_batch(ctx, {}, &kept, part_mode, {0, (int64_t)kept.size()}, &b))) return cleanup(rc);
         parts.push_back(b);
       }
       i = j;
@@ -2549,14 +2582,14 @@ int dq_decode_chunk_filtered(dq_ctx* ctx, const char* path, uint64_t vstart, uin
       size_t k = 0;
       while (k < refs.size() && refs[k] != -1) k++;
       dq_batch* b = nullptr;
-      if ((rc = make_batch(ctx, {{r.begin + (int64_t)k, r.end}}, nullptr, with_raw,
+      if ((rc = make_batch(ctx, {{r.begin + (int64_t)k, r.end}}, nullptr, part_mode,
                            {0, r.end - r.begin - (int64_t)k}, &b)))
         return cleanup(rc);
       parts.push_back(b);
     }
   }
   dq_batch* all = nullptr;
-  if ((rc = concat_batches(ctx, parts, &all))) return cleanup(rc);
+  if ((rc = concat_batches(ctx, parts, with_raw == DQ_EXPORT_LEAN, &all))) return cleanup(rc);
   cleanup(0);
   *out = all;
   return 0;

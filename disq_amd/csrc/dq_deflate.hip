@@ -21,7 +21,8 @@
 //      out of the chain), ascending inside its bucket: counts by LDS atomics, bucket starts by a
 //      scan, then four waves scatter four position ranges in order with their own cursors (one
 //      LDS atomic add per position: the lanes of one atomic that hit the same cursor get its
-//      values in lane order on gfx950, so equal-hash positions of a step get ascending slots):
+//      values in lane order on gfx950 -- observed, not documented -- so equal-hash positions of a
+//      step get ascending slots; DQ_SCAT_ATOMIC=0, the `ballot` build, ranks them by ballots):
 //      no barrier, no position hashed twice.  A position's candidates are the entries before it in
 //      its bucket, most recent first (its own slot is found by a 16-way search of the bucket): a
 //      contiguous run of the list, so a search loads 8 candidates and their first 16 bytes at
@@ -31,7 +32,9 @@
 //      position's is longer; the look-ahead search walks chain / 4 candidates once the current
 //      match is `good` long, as zlib's deflate_slow) and the longest match among `chain`
 //      candidates (stopping at `nice`); nothing depends on which lane runs first, so the output
-//      is the same on every run.  A parse step depends on its position alone, so two parses that reach the
+//      is a function of the input: by construction in the ballot build, and in the default
+//      build while the hardware keeps the lane order above (tests/test_deflate_gpu.py compares
+//      the two builds' bytes).  A parse step depends on its position alone, so two parses that reach the
 //      same position continue identically: from its exit, each segment's parse is continued until
 //      it hits a symbol boundary of a later segment's parse (usually within a few symbols) and the
 //      merge is recorded; after `fmerge` continuation symbols without one (default 1) it is ended
@@ -892,7 +895,6 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
   __syncthreads();
   DTS();
   if (wv < SCAT_WAVES) {
-    uint16_t* const cur16 = wv ? reinterpret_cast<uint16_t*>(&L.cnt[wv - 1][0]) : nullptr;
     const int xe = min(npos, (wv + 1) * rng);
 #if DQ_SCAT_ATOMIC
     // one LDS atomic per position: the lanes of one ds_add_rtn that hit the same cursor get its
@@ -900,7 +902,9 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
     // atomics), so equal-hash positions of a step get ascending slots, as the ballot ranking below
     // gave them (round 4: 11 ballots per 64 positions).  Whatever the order, a candidate at or
     // past the position it is searched for is never taken (Finder::batch), so the output stays a
-    // valid DEFLATE stream; its bytes are the same on every run while the order holds.
+    // valid DEFLATE stream; its bytes are the same on every run, and equal to the ballot build's
+    // (DQ_SCAT_ATOMIC=0, `make ballot`; test_atomic_scatter_equals_ballot_build), while the order
+    // holds.
     uint32_t* const cur32 = wv ? reinterpret_cast<uint32_t*>(&L.cnt[wv - 1][0]) : nullptr;
     for (int x = wv * rng + lane; x < xe; x += 64) {
       const uint32_t h = hash4a(L.in, x);
@@ -915,6 +919,7 @@ __global__ __launch_bounds__(PWG) void bgzf_parse_kernel(const uint8_t* __restri
       L.bl[rank] = (uint16_t)x;
     }
 #else
+    uint16_t* const cur16 = wv ? reinterpret_cast<uint16_t*>(&L.cnt[wv - 1][0]) : nullptr;
     for (int x0 = wv * rng; x0 < xe; x0 += 64) {
       const int x = x0 + lane;
       const bool valid = x < xe;

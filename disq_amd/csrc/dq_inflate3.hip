@@ -71,6 +71,8 @@ constexpr int RES_NXT = 2048;        // resolve batch bytes (NB * G * WG) at mos
 #endif
 #ifndef DQ_RES_NB
 #define DQ_RES_NB 4
+#endif
+#ifndef DQ_RES_G
 #define DQ_RES_G 1
 #endif
 
@@ -1844,22 +1846,35 @@ DQ_AI void build_tables_wave(LdsW& L, int nlen, int ndist) {
     return;
   }
   __builtin_amdgcn_wave_barrier();
-  // ranks among equal lengths, chunk by chunk: one LDS atomic add per symbol on its length's
-  // running count (the lanes of one atomic that hit the same count get its values in lane order on
-  // gfx950, tools/micro/lds_atomic_order.hip; chunks in order), and the decoded entries at their
-  // canonical positions (round 4: eight packed-counter wave scans per chunk)
+  // ranks among equal lengths, chunk by chunk: the lanes with the same key (alphabet, length) are
+  // found by five ballots on the key's bits, a symbol's rank is the number of those peers below it
+  // plus the key's running count over the earlier chunks, and the key's highest lane advances that
+  // count (deterministic: round 5 took the rank from one LDS atomic add per symbol, which relied on
+  // gfx950 returning the values of same-address lanes in lane order -- observed, not documented)
+  const uint64_t below = lanes_below(lane);
   for (int k0 = 0; k0 < 320; k0 += 64) {
     const int k = k0 + lane;
     const bool isl = k < 288;
     const int sym = isl ? k : k - 288;
     const int len = k < 320 ? (isl ? (k < nlen ? H.lens[k] : 0) : (sym < ndist ? H.lens[k] : 0)) : 0;
+    const int key = (isl ? 0 : 16) + len;  // 5 bits
+    uint64_t peers = ~0ull;
+#pragma unroll
+    for (int bt = 0; bt < 5; bt++) {
+      const uint64_t bl = __ballot((key >> bt) & 1);
+      peers &= ((key >> bt) & 1) ? bl : ~bl;
+    }
+    const int run0 = H.run[key];
+    const int rank = run0 + __popcll(peers & below);
+    __builtin_amdgcn_wave_barrier();  // every lane has read its count before the updates
+    if (len && (peers >> lane) == 1ull) H.run[key] = run0 + __popcll(peers);  // the key's last lane
     if (len) {
-      const int rank = atomicAdd(&H.run[(isl ? 0 : 16) + len], 1);
       const HuffCanon& hh = isl ? L.u.d.hl : L.u.d.hd;
       const int q = hh.offs[len] + rank;
       if (isl) L.u.d.lent[q] = ent_ll((uint32_t)sym, (uint32_t)len);
       else L.u.d.dent[q] = ent_d((uint32_t)sym, (uint32_t)len);
     }
+    __builtin_amdgcn_wave_barrier();
   }
   __builtin_amdgcn_wave_barrier();
   // root tables: 16 litlen and 4 distance entries per lane; an index without a short code is the
@@ -2188,13 +2203,20 @@ __global__ __launch_bounds__(64 * TW, 4) void inflate_tail_kernel(
     int32_t cms = -1;
     uint32_t cdesc = 0;
     // a row's sources and its loads from U: unconditional loads (a byte that needs none loads the
-    // prefix's last byte) into fixed registers per slot, so the compiler's wait for a slot's
-    // values counts only the loads issued before them (no branch, no register shuffling)
+    // prefix's last byte, or the tail's first when the prefix is empty -- p0 = 0 after an empty
+    // first deflate block: Ub[-1] would lie before the block, for block 0 before U) into fixed
+    // registers per slot, so the compiler's wait for a slot's values counts only the loads issued
+    // before them (no branch, no register shuffling)
+    const int32_t dmy = p0 > 0 ? -1 : 0;  // uniform
     auto prefetch = [&](int row, int32_t (&s)[4], uint32_t& c, uint32_t (&g)[4]) {
       c = 0;
       hops(row, cms, cdesc, s, c);  // rows in order (the carry); past the last row: no copies
 #pragma unroll
-      for (int i = 0; i < 4; i++) g[i] = Ub[((c >> i) & 1u) && s[i] < 0 ? s[i] : -1];
+      for (int i = 0; i < 4; i++) {
+        const int32_t gi = ((c >> i) & 1u) && s[i] < 0 ? s[i] : dmy;
+        DQ_CHK(gi >= -p0 && gi < max(n, 1), CHK_K2_SRC);
+        g[i] = Ub[gi];
+      }
     };
     auto do_row = [&](int row, const int32_t (&src)[4], uint32_t cpy, const uint32_t (&g)[4]) {
       const int32_t Y = 256 * row + 4 * lane;  // the lane's image dword
@@ -2414,16 +2436,26 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
   if (nblk <= 0) return;
   const int64_t ngrid = sel ? nsel : nblk;
   if (ngrid <= 0) return;
+#ifdef DQ_TUNING
+  // Decode-shape knobs of the tuning builds only (tools/build_variant.sh NAME -DDQ_TUNING): the
+  // product library has a single configuration, so an executor's inherited environment cannot
+  // select an untested path.  DQ_OV warm-up bits, DQ_STORE U store mode (bit 0 whole block at the
+  // end, bit 1 non-temporal), DQ_NDEC lane cap, DQ_SEGBITS minimum segment bits, DQ_WARM L2 warm-up,
+  // DQ_LDSPAD extra dynamic LDS (80000 = one workgroup per CU), DQ_TAIL=0 no tail kernel.
   static const uint32_t ov = getenv("DQ_OV") ? (uint32_t)atoi(getenv("DQ_OV")) : OV_DEFAULT;
   static const uint32_t sflags =
       (getenv("DQ_STORE") ? (uint32_t)atoi(getenv("DQ_STORE")) & 3u : 2u) |
       (getenv("DQ_NDEC") ? (uint32_t)(atoi(getenv("DQ_NDEC")) & 1023) << 8 : 0u) |
       (getenv("DQ_SEGBITS") ? (uint32_t)(atoi(getenv("DQ_SEGBITS")) & 1023) << 20 : 0u) |
       (getenv("DQ_WARM") && atoi(getenv("DQ_WARM")) ? 16u : 0u);
-  // DQ_LDSPAD: extra dynamic LDS per workgroup (occupancy experiments: 80000 = one workgroup per CU)
   static const unsigned ldspad = getenv("DQ_LDSPAD") ? (unsigned)atoi(getenv("DQ_LDSPAD")) : 0u;
-  // DQ_TAIL=0: no tail kernel (the block kernel decodes every deflate block itself)
   static const bool tail_on = !getenv("DQ_TAIL") || atoi(getenv("DQ_TAIL")) != 0;
+#else
+  constexpr uint32_t ov = OV_DEFAULT;
+  constexpr uint32_t sflags = 2u;  // U lines stored per batch, non-temporal
+  constexpr unsigned ldspad = 0u;
+  constexpr bool tail_on = true;
+#endif
   TailDesc* td = tail_on ? static_cast<TailDesc*>(tails_buf) : nullptr;
   if (td) (void)hipMemsetAsync(td, 0, sizeof(TailDesc) * (size_t)ngrid, s);
 #define DQ_LAUNCH(TM, NBT, GT)                                                                  \

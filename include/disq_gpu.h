@@ -36,6 +36,11 @@
 extern "C" {
 #endif
 
+/* ABI version: 2 = dq_batch with the trailing arena_hold pointer (round 5) and the export modes
+ * below (round 6).  A JNI / FFM binding compares dq_abi_version() with the value it was built
+ * against before it maps dq_batch. */
+#define DQ_ABI_VERSION 2
+
 #define DQ_OK 0
 #define DQ_EIO (-1)
 #define DQ_EFORMAT (-2)
@@ -85,7 +90,23 @@ typedef struct dq_chunk {
 
 /* Records as structure-of-arrays (fixed BAM fields, SAMv1 §4.2), host memory owned by the
  * library.  raw holds each record's 4 + block_size bytes (what htsjdk's
- * SAMRecordFactory.createBAMRecord needs as restOfData) at raw_offset[i]. */
+ * SAMRecordFactory.createBAMRecord needs as restOfData) at raw_offset[i].
+ *
+ * Export modes (the `with_raw` argument of the decode calls):
+ *   DQ_EXPORT_FIELDS  every SoA field, hash and raw_offset; raw = NULL
+ *   DQ_EXPORT_RAW     the same plus the raw bytes
+ *   DQ_EXPORT_LEAN    voffset and raw only (every other pointer NULL, partition digests kept): the
+ *                     fields are the first 36 bytes of each record's raw bytes (block_size, refID,
+ *                     pos, bin_mq_nl, flag_nc, l_seq, next_refID, next_pos, tlen: what htsjdk's
+ *                     BAMRecordCodec.decode reads, H/BAMFileReader2.java:929-931), and record i+1
+ *                     starts 4 + block_size bytes after record i.  52 fewer bytes per record
+ *                     cross PCIe.
+ * dq_batch_free may release pinned memory (an arena batch) after dq_ctx_destroy: a JNI consumer
+ * must free its batches before the HIP runtime shuts down (not from a JVM shutdown hook that can
+ * run after it). */
+#define DQ_EXPORT_FIELDS 0
+#define DQ_EXPORT_RAW 1
+#define DQ_EXPORT_LEAN 2
 typedef struct dq_batch {
   int64_t n_records;
   uint64_t* voffset;     /* htsjdk start file pointer of the record */
@@ -162,6 +183,7 @@ int dq_ctx_create(dq_ctx** out, const dq_opts* opts);
 void dq_ctx_destroy(dq_ctx* ctx);
 const char* dq_last_error(const dq_ctx* ctx);
 const char* dq_version(void);
+int32_t dq_abi_version(void); /* DQ_ABI_VERSION of the library */
 
 /* Open a BAM from host memory (copied to HBM) or from a path.  The resident file is used by
  * every call below until the next open. */

@@ -18,6 +18,7 @@ from oracle import oracle as O
 import bamutil as B
 
 pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def members(bgzf):
@@ -176,3 +177,39 @@ def test_output_is_deterministic():
             assert b"".join(members(a)) == data
     with _lib.Context() as c2:  # and a fresh context
         assert c2.bgzf_compress(per3) == a
+
+
+_BALLOT_SCRIPT = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+from disq_amd import _lib
+src = open(sys.argv[2], "rb").read()
+with _lib.Context() as c:
+    out = c.bgzf_compress(src)
+open(sys.argv[3], "wb").write(out)
+"""
+
+
+@pytest.mark.gpu
+def test_atomic_scatter_equals_ballot_build(tmp_path):
+    """The product library ranks equal-hash positions of the bucket scatter by lane-ordered LDS
+    atomics (observed on gfx950, not documented); the ballot build (DQ_SCAT_ATOMIC=0, `make
+    ballot`) ranks them by ballots, deterministic by construction.  Both must write the same
+    bytes: if the hardware ever returned the atomics out of lane order the parse would see other
+    candidates and this comparison would fail (the output would still be valid DEFLATE)."""
+    import subprocess
+    import sys
+    lib = os.path.join(ROOT, "disq_amd", "_build", "libdisq_gpu_ballot.so")
+    if not os.path.exists(lib):
+        pytest.fail("libdisq_gpu_ballot.so is not built (make -C disq_amd/csrc ballot)")
+    r = synth.generate(20000, seed=9, nthreads=4)
+    data = B.inflate_all(r.bam) + (b"ACG" * 100000)
+    src, dst = tmp_path / "in.bin", tmp_path / "out.bgzf"
+    src.write_bytes(data)
+    env = dict(os.environ, DQ_GPU_LIB=lib)
+    subprocess.run([sys.executable, "-c", _BALLOT_SCRIPT, ROOT, str(src), str(dst)], env=env,
+                   check=True, timeout=300)
+    with _lib.Context() as c:
+        mine = c.bgzf_compress(data)
+    assert dst.read_bytes() == mine
+    assert b"".join(members(mine)) == data

@@ -7,7 +7,7 @@ inflate_block_kernel decodes a BGZF member's first deflate block and, when what 
 against the block kernel's output in U and finishes the member's CRC from the prefix's CRC
 register.  htsjdk's level 5 makes such a tail in almost every block, so these members put the
 boundary exactly where the gate decides: tails of 4096 / 4097 output bytes, of 32768 / 32769
-bits, tails of several deflate blocks (stored + fixed + dynamic), a match at distance 32768 into
+bits, a tail after an empty first deflate block, tails of several deflate blocks (stored + fixed + dynamic), a match at distance 32768 into
 the prefix, short-distance runs, and a flipped CRC, an invalid code and a too-far distance inside a
 tail.  The members are written bit by bit (tests/deflate_writer.py) and checked against zlib here;
 the GPU tests compare the decompressed stream with zlib's and expect the errors zlib raises (the
@@ -109,6 +109,10 @@ def fixtures(u):
     """name -> (member bytes, decompressed bytes, gate, expected deferral, zlib error or None)."""
     rng = np.random.default_rng(7)
     f = {}
+    # an empty, non-final first deflate block (only its EOB) and a small tail: the tail starts at
+    # output byte 0 of the member (p0 = 0), so nothing of it lies in a prefix
+    m, d, g = build(b"", [("fixed", W.lz77(u[:3000]), True)], first="fixed")
+    f["empty_first"] = (m, d, g, True, None)
     pre = u[:60000]
     for n in (4096, 4097):
         data = u[:60000 + n]
@@ -209,6 +213,17 @@ def test_gpu_tail_boundaries(fx):
     got = _gpu_inflate(b"".join(m for m, _ in good) + B.EOF_BLOCK)
     want = b"".join(d for _, d in good)
     assert len(got) == len(want)
+    assert np.array_equal(got, np.frombuffer(want, np.uint8))
+
+
+@pytest.mark.gpu
+def test_gpu_tail_after_empty_first_block(fx):
+    """The empty-first-block member as the file's first block (its tail begins at U's first byte),
+    then a deferred tail with a prefix: both equal zlib's output (advisor round 5: the tail resolve's
+    dummy load must stay inside U when the prefix is empty; the checked build bounds it)."""
+    a, b = fx["empty_first"], fx["out4096"]
+    got = _gpu_inflate(a[0] + b[0] + B.EOF_BLOCK)
+    want = a[1] + b[1]
     assert np.array_equal(got, np.frombuffer(want, np.uint8))
 
 

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Phase cycles of the inflate kernels at two block workgroups per CU (default) and at one
-# (DQ_LDSPAD=80000 pads the dynamic LDS): equal per-block cycles mean latency-bound phases.
+# (DQ_LDSPAD=80000 pads the dynamic LDS; a -DDQ_TUNING build: DQ_GPU_LIB=.../libdisq_gpu_tune.so): equal per-block cycles mean latency-bound phases.
 # usage: tools/gpu_occupancy_probe.sh TAG
 set -eo pipefail
 out=gpurun_out/$1
