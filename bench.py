@@ -331,6 +331,11 @@ def main():
 
     interval_mode = e2e = cpu = parity = wpath = None
     if world == 1:
+        # the end-to-end leg first, on a host whose memory the other legs have not churned (after
+        # the write path, interval and CPU-baseline legs it measured 1.00 s against 0.77-0.81 s
+        # here, with every stage slower: profiles/r6b_e2e_sweep.txt)
+        if args.e2e:
+            e2e = end_to_end(cpu_data, args, digest, header)
         if args.write_records > 0:
             wpath = write_path_bench(args)
         if bai is not None:
@@ -338,8 +343,6 @@ def main():
                                            ncores)
         if cpu_data is not None:
             cpu, parity = cpu_baseline(cpu_data, ctx, rs, shard, file_len, header, args, ncores)
-        if args.e2e:
-            e2e = end_to_end(cpu_data, args, digest, header)
     if world > 1:
         # every rank, untimed: the oracle over the bytes it decoded (resident + halo received in
         # the timed steps), its owned partitions vs the GPU's descriptors of the last timed step

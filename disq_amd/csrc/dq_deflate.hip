@@ -393,11 +393,14 @@ __device__ inline int mw_dist(uint32_t w) { return (int)(w >> 17) + 1; }
 constexpr int SCAT_WAVES = 4;  // waves of the bucket scatter: one position range each
 constexpr int NQ = (MSEG + PWG - 1) / PWG;  // segments per thread in the merge phase
 constexpr int CRC_BYTES = CH / (PWG - 64 * SCAT_WAVES) + 1;  // per thread of the other waves (the CRC)
+// head first, then in and bl: every array a search reads starts below 64 KiB, so its constant
+// offset folds into the ds_read offset field (one VALU add fewer per access; round 5 had head past
+// in and bl, at 138 KiB, as the inflate's tables were before its image moved last)
 struct alignas(16) PLds {
-  uint8_t in[NPMAX + 16];     // bytes [r0, ce) of the block (+ zero pad for the 4/8-byte compares)
-  uint16_t bl[NPMAX];         // positions grouped by hash bucket, ascending inside a bucket
   int32_t head[1 << HBITS];   // bucket counts -> starts (wave 0's cursors) -> ends; later the
                               // chunk's histograms
+  uint8_t in[NPMAX + 16];     // bytes [r0, ce) of the block (+ zero pad for the 4/8-byte compares)
+  uint16_t bl[NPMAX];         // positions grouped by hash bucket, ascending inside a bucket
   union {
     struct {
       uint32_t seg_exit[MSEG];  // the parse's exit of each segment; later jump pointers, first symbols
@@ -415,6 +418,7 @@ struct alignas(16) PLds {
   int32_t misc[8];
 };
 static_assert(sizeof(PLds) <= 160 * 1024, "one chunk workgroup per CU");
+static_assert(offsetof(PLds, bl) < 65536 - 4096, "the search arrays' offsets fit the DS offset field");
 static_assert(PSEG == 32, "a segment's symbol starts are one word of sbits");
 
 // Match finder over the chunk's hash buckets: bl holds every local position x with a 4-byte

@@ -59,22 +59,31 @@ using namespace dqi;
 
 #define DQ_HD __device__ __host__ __attribute__((always_inline)) inline
 
-constexpr int WG = 512;           // threads per workgroup
-constexpr int NDEC = 512;         // speculative decode lanes (<= WG)
+// threads per block workgroup (= speculative lanes): two workgroups per CU (the LDS image), so
+// WG / 128 waves per SIMD, which bounds the VGPRs (MI355X_MICROARCH.md: 512 / waves per SIMD)
+#ifndef DQ_BLK_WG
+#define DQ_BLK_WG 512
+#endif
+constexpr int WG = DQ_BLK_WG;
+static_assert(WG % 128 == 0 && WG >= 512 && WG <= 1024, "whole waves on every SIMD");
+constexpr int NWV = WG / 64;      // waves per workgroup
+constexpr int NDEC = WG;          // speculative decode lanes (<= WG)
 constexpr uint32_t OV_DEFAULT = 96;  // speculative warm-up bits before each segment
 constexpr int OUTCAP = 65536 + 24;  // + alignment shift (<= 15) + descriptor overhang; bm 8-aligned
-constexpr int RES_NXT = 2048;        // resolve batch bytes (NB * G * WG) at most
 // resolve shape (tuning builds): NB chunks of G * WG bytes per batch; DQ_CSTEP = 1: one ordered
-// step per chunk instead of per 512 bytes (longer in-step chains, fewer barriers)
+// step per chunk instead of per 512 bytes (longer in-step chains, fewer barriers; always so when
+// a chunk is not a whole number of 512-byte steps)
 #ifndef DQ_CSTEP
 #define DQ_CSTEP 0
 #endif
 #ifndef DQ_RES_NB
-#define DQ_RES_NB 4
+#define DQ_RES_NB (WG == 512 ? 4 : 2)
 #endif
 #ifndef DQ_RES_G
 #define DQ_RES_G 1
 #endif
+constexpr int RES_NXT = DQ_RES_NB * DQ_RES_G * WG;  // resolve batch bytes (NB * G * WG)
+constexpr int NCARRY = (65536 + RES_NXT - 1) / RES_NXT + 1;  // batches of a block (carry slots)
 
 
 // 16-bit decode table layout: [litlen root | litlen subtables | dist root | dist subtables]
@@ -158,17 +167,17 @@ struct alignas(16) LdsI {
           uint16_t clt[128];      // code-length code: sym << 3 | len (len 0 = invalid)
           union {
             struct {              // build_tables
-              int32_t cntw[8];    // per-wave counts of second-level tables
-              int32_t cnts[8];    // per-wave second-level entries
+              int32_t cntw[NWV];  // per-wave counts of second-level tables
+              int32_t cnts[NWV];  // per-wave second-level entries
               uint32_t ginfo[MAXGRP + 32];  // per second-level table (litlen, then distance): offset | sb << 16
               uint32_t cntp[8][8];  // per-wave counts of each code length, 16 bits per length
               uint16_t pref[320];   // root prefix of each long code, by canonical position
             };
             struct {              // read_lengths: one 128-bit window per wave
-              uint8_t exitm[8][16];  // window w entered at offset e < 16 -> entry offset into w + 1
-              int32_t ent[9];        // true entry offset of each window (255: none)
-              int32_t wt[8];         // lengths the window's path symbols write
-              int32_t lv[8];         // the window's last non-repeat value (-1 none)
+              uint8_t exitm[NWV][16];  // window w entered at offset e < 16 -> entry offset into w + 1
+              int32_t ent[NWV + 1];    // true entry offset of each window (255: none)
+              int32_t wt[NWV];         // lengths the window's path symbols write
+              int32_t lv[NWV];         // the window's last non-repeat value (-1 none)
               int32_t endp;          // bit position after the last code-length symbol
             };
           };
@@ -178,8 +187,8 @@ struct alignas(16) LdsI {
     struct {
       uint16_t last_start[1024];  // last match start <= end of 64-bit bitmap word (0xffff none)
       uint16_t nxt[RES_NXT];      // next pointer of each byte of the batch
-      int32_t carry_ms[32];       // the match carried into batch k + 1 (start, -1 none), and its
-      uint32_t carry_desc[32];    // descriptor: read before any step overwrites a descriptor
+      int32_t carry_ms[NCARRY];    // the match carried into batch k + 1 (start, -1 none), and its
+      uint32_t carry_desc[NCARRY]; // descriptor: read before any step overwrites a descriptor
     } r;
     uint32_t crc4[4][256];
   } u;
@@ -199,7 +208,7 @@ struct alignas(16) LdsI {
 };
 static_assert(sizeof(((LdsI*)nullptr)->scratch) >= 64 * 4, "one emit dummy word per lane");
 static_assert(offsetof(LdsI, out) < 65536 - 4096, "the tables' offsets fit the DS offset field");
-static_assert(sizeof(LdsI) <= 81920, "two workgroups per CU");
+static_assert(2 * sizeof(LdsI) <= 160 * 1024, "two workgroups per CU");
 static_assert(HB_WORDS * 4 <= T_END * 2, "header staging fits the decode table");
 
 // emit's per-lane dummy words (one per lane of a wave): dead scratch during the emit
@@ -208,11 +217,12 @@ __device__ inline uint32_t* emit_dummy(LdsI& L) { return L.scratch; }
 __constant__ uint32_t c_crc4[4][256];
 __constant__ uint32_t c_x2n[32];  // x^(2^k) mod P (reflected)
 __constant__ uint32_t c_x8n[TOUT + 1];  // x^(8 k) mod P, k <= TOUT: the tail kernel's CRC shifts
-// CRC slices: 132 bytes (33 words), so the 64 lanes of a wave read 64 different LDS banks (128-byte
-// slices put every lane of a wave in the same bank: a 32-way conflict on every data read)
-constexpr int CRC_SL = 132;
+// CRC slices: an odd number of words (132 bytes = 33 words at 512 threads), so the 64 lanes of a
+// wave read 64 different LDS banks (128-byte slices put every lane of a wave in the same bank: a
+// 32-way conflict on every data read)
+constexpr int CRC_SL = 4 * (((65536 / 4 + WG - 1) / WG) | 1);
 static_assert(CRC_SL * WG >= 65536, "the slices cover the largest block");
-__constant__ uint32_t c_slice_shift[WG];  // x^(8 * CRC_SL * k) mod P, k = 0..511
+__constant__ uint32_t c_slice_shift[WG];  // x^(8 * CRC_SL * k) mod P, k = 0..WG-1
 __constant__ uint8_t c_clorder3[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 // misc slots
@@ -224,17 +234,7 @@ enum { M_ERR = 0, M_SLOW = 1 /* an E_SLOW root entry in this deflate block's tab
 template <class LT>
 __device__ __attribute__((always_inline)) inline void set_err(LT& L, int32_t code) { atomicCAS(&L.misc[M_ERR], 0, code); }
 
-// Bit reader: a 64-bit LSB-first buffer refilled 32 bits at a time from `nw`, the next input word,
-// which every refill call reloads unconditionally (one global_load_dword, almost always an L1/L2
-// hit): the load lands in a loop-carried register and is first waited for at the next call, half
-// a symbol later.  (A 16-byte group load needs a 4-way select of the word on every refill:
-// 3 compares + 3 cndmasks + hazard nops per refill, 2 refills per symbol.)
-struct BitR {
-  uint64_t bb;
-  uint32_t bc;
-  uint32_t wp;    // word index of the next word to enter bb (br_pos = 32 * wp - bc)
-  uint32_t nw;    // W[wp]
-};
+
 #define DQ_AI __device__ __attribute__((always_inline)) inline
 
 // The thread index behind an empty volatile asm: values derived from it cannot be hoisted out of
@@ -274,6 +274,21 @@ struct GSrc {
   }
 };
 
+#ifndef DQ_BR64
+#define DQ_BR64 0
+#endif
+#if DQ_BR64
+// Bit reader (round 5): a 64-bit LSB-first buffer refilled 32 bits at a time from `nw`, the next
+// input word, which every refill call reloads unconditionally (one global_load_dword, almost
+// always an L1/L2 hit): the load lands in a loop-carried register and is first waited for at the
+// next call, half a symbol later.  (A 16-byte group load needs a 4-way select of the word on every
+// refill: 3 compares + 3 cndmasks + hazard nops per refill, 2 refills per symbol.)
+struct BitR {
+  uint64_t bb;
+  uint32_t bc;
+  uint32_t wp;    // word index of the next word to enter bb (br_pos = 32 * wp - bc)
+  uint32_t nw;    // W[wp]
+};
 template <class S>
 DQ_AI void br_init(BitR& r, const S& W, uint32_t bitpos) {
   const uint32_t wi = bitpos >> 5;
@@ -293,12 +308,48 @@ DQ_AI void br_refill(BitR& r, const S& W) {
   r.nw = W[r.wp];
 }
 DQ_AI uint32_t br_pos(const BitR& r) { return r.wp * 32 - r.bc; }
-DQ_AI uint32_t br_take(BitR& r, uint32_t n) {
-  const uint32_t v = (uint32_t)(r.bb & ((1ull << n) - 1));
+DQ_AI uint32_t br_peek(const BitR& r) { return (uint32_t)r.bb; }
+template <class S>
+DQ_AI void br_take(BitR& r, const S&, uint32_t n) {
   r.bb >>= n;
   r.bc -= n;
-  return v;
 }
+#else
+// Bit reader: the bit position p and the two input words holding bits [32 (p >> 5), +64); a peek
+// is one v_alignbit of them (32 bits from p: a litlen code + its extra bits <= 20, a distance
+// code + its extra bits <= 28), an advance of n <= 28 bits crosses at most one word, which shifts
+// in `nw` = W[(p >> 5) + 2].  nw is reloaded unconditionally after every advance (one
+// global_load_dword, almost always an L1/L2 hit) and first waited for at the next crossing, half a
+// symbol later.  No 64-bit shifts or ORs, and the position needs no arithmetic (round 5 kept a
+// 64-bit buffer: a 64-bit shift and two ORs per refill, a 64-bit shift per take, and 32 wp - bc
+// for every position test).
+struct BitR {
+  uint32_t p;       // bit position of the next bit
+  uint32_t w0, w1;  // W[p >> 5], W[(p >> 5) + 1]
+  uint32_t nw;      // W[(p >> 5) + 2]
+};
+template <class S>
+DQ_AI void br_init(BitR& r, const S& W, uint32_t bitpos) {
+  const uint32_t wi = bitpos >> 5;
+  r.w0 = W[wi];
+  r.w1 = W[wi + 1];
+  r.nw = W[wi + 2];
+  r.p = bitpos;
+}
+template <class S>
+DQ_AI void br_refill(BitR&, const S&) {}
+DQ_AI uint32_t br_pos(const BitR& r) { return r.p; }
+DQ_AI uint32_t br_peek(const BitR& r) { return __builtin_amdgcn_alignbit(r.w1, r.w0, r.p); }
+template <class S>
+DQ_AI void br_take(BitR& r, const S& W, uint32_t n) {
+  const uint32_t q = r.p + n;
+  const bool c = (q ^ r.p) >= 32u;  // crossed into the next word
+  r.w0 = c ? r.w1 : r.w0;
+  r.w1 = c ? r.nw : r.w1;
+  r.p = q;
+  r.nw = W[(q >> 5) + 2];
+}
+#endif
 // n (<= 25) bits at an arbitrary bit position
 DQ_AI uint32_t peek_bits(const uint32_t* __restrict__ W, uint32_t pos, uint32_t n) {
   const uint32_t wi = pos >> 5;
@@ -311,6 +362,19 @@ template <class LT>
 DQ_AI uint32_t load_desc(const LT& L, int a) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(L.out + (a & ~3));
   return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)a & 3u) & 0xffffffu;
+}
+
+// A 16-bit table entry as a plain 32-bit value (ds_read_u16 zero-extends): behind an empty asm the
+// compiler cannot narrow the entry's uses to 16-bit operations, which it then widened again with
+// a v_and 0xffff per lookup (two per decode step in the ISA of round 5).
+DQ_AI uint32_t zx16(uint16_t v) {
+#ifndef DQ_NO_ZX16
+  uint32_t x = v;
+  asm("" : "+v"(x));
+  return x;
+#else
+  return v;
+#endif
 }
 
 // Second-level / canonical lookup for a root entry that is not a code.  SLOW = false (no E_SLOW
@@ -355,12 +419,12 @@ DQ_AI uint32_t d_second(const LT& L, uint32_t e, uint32_t bb) {
 template <bool SLOW, class S, class LT>
 DQ_AI bool dsym(BitR& r, const S& W, const LT& L, uint32_t p, uint32_t lim,
                 uint32_t& len, uint32_t& dist, uint32_t& lit2, bool& is_m) {
-  br_refill(r, W);  // >= 33 bits: a litlen code + its extra bits (<= 20)
-  uint32_t bb = (uint32_t)r.bb;
+  br_refill(r, W);  // >= 32 bits: a litlen code + its extra bits (<= 20)
+  uint32_t bb = br_peek(r);
   const uint32_t ri = bb & ((1u << LR) - 1);
   uint32_t e = L.u.d.T[ri];
   uint32_t pe = 0;
-  if constexpr (LT::kPair) pe = L.u.d.x.pair[ri];
+  if constexpr (LT::kPair) pe = zx16(L.u.d.x.pair[ri]);
   if ((e & 15) == 0) e = ll_second<SLOW>(L, e, bb);
   const uint32_t nb = e & 15;
   const uint32_t lx = __builtin_amdgcn_ubfe(e, 5, 3);
@@ -368,15 +432,15 @@ DQ_AI bool dsym(BitR& r, const S& W, const LT& L, uint32_t p, uint32_t lim,
   len = (e >> 8) + (is_m ? 3u : 0u) + __builtin_amdgcn_ubfe(bb, nb, lx);
   const bool two = pe != 0 && p + nb < lim;  // pe != 0: the root entry is a literal
   lit2 = two ? pe >> 8 : 0xffffffffu;
-  br_take(r, nb + lx + (two ? (pe & 15) : 0u));
-  br_refill(r, W);  // >= 33 bits: a distance code + its extra bits (<= 28)
-  bb = (uint32_t)r.bb;
-  uint32_t e2 = L.u.d.T[LT::kDROOT + (bb & ((1u << DR) - 1))];
+  br_take(r, W, nb + lx + (two ? (pe & 15) : 0u));
+  br_refill(r, W);  // >= 32 bits: a distance code + its extra bits (<= 28)
+  bb = br_peek(r);
+  uint32_t e2 = zx16(L.u.d.T[LT::kDROOT + (bb & ((1u << DR) - 1))]);
   if (is_m && (e2 & 15) == 0) e2 = d_second<SLOW>(L, e2, bb);
   const uint32_t nb2 = e2 & 15, dx = __builtin_amdgcn_ubfe(e2, 4, 4);
   dist = (__builtin_amdgcn_ubfe(e2, 12, 2) << __builtin_amdgcn_ubfe(e2, 8, 4)) + 1u +
          __builtin_amdgcn_ubfe(bb, nb2, dx);
-  br_take(r, is_m ? nb2 + dx : 0u);
+  br_take(r, W, is_m ? nb2 + dx : 0u);
   // SLOW = false: a code-less index reads the invalid sentinels build_tables leaves at the first
   // second-level entries, so no entry here has code length 0
   const bool stop = (SLOW && nb == 0) || (e & 0xFEF0u) == 0xF810u ||
@@ -433,31 +497,38 @@ DQ_AI int run_seg(const S& W, const LT& L, uint32_t start, uint32_t sB,
   int32_t cnt = 0;
   int f;
   uint32_t thr = ck ? sB + CKI : 0xffffffffu;
-  int j = 0;
   // a lane crosses a checkpoint every few symbols, so some lane of the wave does on most steps:
   // written branch-free, the step that crosses none stores to the lane's dummy word (wsum is
-  // dead during the speculative pass; `small` may hold the per-lane arrays)
+  // dead during the speculative pass; `small` may hold the per-lane arrays).  The threshold keeps
+  // advancing past the last checkpoint (checkpoint j < NCK is the pointer test ckp < cke): no
+  // checkpoint counter and no saturated threshold (four VALU ops per step fewer than round 5; the
+  // later thresholds only bound the literal pairs, which never changes a boundary the pass sees)
   uint32_t* const dummy = const_cast<uint32_t*>(L.scratch) + (tid_fresh() & 15);
   uint32_t* ckp = ck;  // checkpoint j (advanced, not multiplied out)
+  const uint32_t* const cke = ck + NCK * ckstride;
   const uint32_t sEe = min(sE, endbits);  // one compare (one branch) for both ends
+  bool stopped;
   for (;;) {
     const bool cross = p >= thr;
-    *(cross ? ckp : dummy) = ((p - sB) << 16) | (uint32_t)cnt;
-    ckp += cross ? ckstride : 0;
-    j += cross ? 1 : 0;
-    thr = cross ? (j < NCK ? thr + CKI : 0xffffffffu) : thr;
-    if (p >= sEe) {
-      *Ep = (int32_t)p;
-      f = p >= sE ? F_EXIT : F_END;
-      break;
-    }
-    if (dsym<SLOW>(r, W, L, p, min(thr, sEe), len, dist, lit2, m)) {
-      *Ep = (int32_t)(len != 0xffffffffu ? len : p);
-      f = len != 0xffffffffu ? F_EOB : F_ERR;
-      break;
-    }
+    const bool st = cross && ckp < cke;
+    *(st ? ckp : dummy) = ((p - sB) << 16) | (uint32_t)cnt;
+    ckp += st ? ckstride : 0;
+    thr += cross ? CKI : 0u;
+    // the exits only record why they left (the exit state is computed after the loop: no
+    // exit-block work and fewer loop-carried copies per step)
+    stopped = false;
+    if (p >= sEe) break;
+    stopped = true;
+    if (dsym<SLOW>(r, W, L, p, min(thr, sEe), len, dist, lit2, m)) break;
     cnt += m ? (int32_t)len : (lit2 != 0xffffffffu ? 2 : 1);
     p = br_pos(r);
+  }
+  if (stopped) {
+    *Ep = (int32_t)(len != 0xffffffffu ? len : p);
+    f = len != 0xffffffffu ? F_EOB : F_ERR;
+  } else {
+    *Ep = (int32_t)p;
+    f = p >= sE ? F_EXIT : F_END;
   }
   *Bp = B;
   *cntp = cnt;
@@ -478,40 +549,44 @@ DQ_AI int run_redo(const S& W, const LT& L, uint32_t s0, uint32_t sB,
   int f;
   uint32_t thr = ck ? sB + CKI : 0xffffffffu;
   uint32_t cur = ck ? ck[0] : 0xffffffffu;
-  const uint32_t* ckq = ck;  // checkpoint min(j, NCK - 1)
+  const uint32_t* ckq = ck;  // checkpoint j (the last one once j >= NCK)
+  const uint32_t* const ckl = ck + (NCK - 1) * ckstride;
   const uint32_t sEe = min(sE, endbits);
   int j = 0;
+  int why;  // 0: the segment or the data ended, 1: merged, 2: dsym stopped
+  uint32_t p, len = 0;
   for (;;) {
-    const uint32_t p = br_pos(r);
+    p = br_pos(r);
     // at a checkpoint threshold: the same boundary as the speculative run merges (one exit branch
-    // for the segment end, the data end and a merge; the threshold update is branch-free)
+    // for the segment end, the data end and a merge; the threshold update is branch-free, and the
+    // exit state is computed after the loop)
     const bool cross = p >= thr;
     const bool merge = cross && (cur >> 16) == p - sB;
-    if (p >= sEe || merge) {
-      if (merge) {
-        *Ep = se >> 3;
-        f = se & 7;
-        cnt += sc - (int32_t)(cur & 0xffffu);
-        if (jm) *jm = j;
-      } else {
-        *Ep = (int32_t)p;
-        f = p >= sE ? F_EXIT : F_END;
-      }
-      break;
-    }
-    j += cross ? 1 : 0;
-    ckq += cross && j < NCK ? ckstride : 0;
+    why = merge ? 1 : 0;
+    if (p >= sEe || merge) break;
+    const bool more = ckq < ckl;
+    if (jm) j += cross ? 1 : 0;
+    ckq += cross && more ? ckstride : 0;
     const uint32_t nxt = ck ? *ckq : 0xffffffffu;
-    thr = cross ? (j < NCK ? thr + CKI : 0xffffffffu) : thr;
-    cur = cross ? (j < NCK ? nxt : 0xffffffffu) : cur;
-    uint32_t len = 0, dist = 0, lit2;
+    thr += cross ? CKI : 0u;  // past the last checkpoint: cur never merges again
+    cur = cross ? (more ? nxt : 0xffffffffu) : cur;
+    uint32_t dist = 0, lit2;
     bool m;
-    if (dsym<SLOW>(r, W, L, p, min(thr, sEe), len, dist, lit2, m)) {
-      *Ep = (int32_t)(len != 0xffffffffu ? len : p);
-      f = len != 0xffffffffu ? F_EOB : F_ERR;
-      break;
-    }
+    why = 2;
+    if (dsym<SLOW>(r, W, L, p, min(thr, sEe), len, dist, lit2, m)) break;
     cnt += m ? (int32_t)len : (lit2 != 0xffffffffu ? 2 : 1);
+  }
+  if (why == 1) {
+    *Ep = se >> 3;
+    f = se & 7;
+    cnt += sc - (int32_t)(cur & 0xffffu);
+    if (jm) *jm = j;
+  } else if (why == 2) {
+    *Ep = (int32_t)(len != 0xffffffffu ? len : p);
+    f = len != 0xffffffffu ? F_EOB : F_ERR;
+  } else {
+    *Ep = (int32_t)p;
+    f = p >= sE ? F_EXIT : F_END;
   }
   *cntp = cnt;
   return f;
@@ -534,17 +609,16 @@ DQ_AI void emit_seg(const S& W, LT& L, uint32_t start, uint32_t target,
   BitR r;
   br_init(r, W, start);
   const uint32_t te = min(target, endbits);
+  bool bad = false;
   for (;;) {
     const uint32_t q = br_pos(r);
-    if (q >= te || p >= isize) return;
+    if (q >= te || p >= isize) break;
     uint32_t len = 0, dist = 0, lit2;
     bool m;
     const bool stop = dsym<SLOW>(r, W, L, q, te, len, dist, lit2, m);
     const bool far = m && (int32_t)dist > p;  // a distance before the block's first byte
-    if (stop || far) {  // one exit branch: EOB / bad code (accounted for by the rounds) or far
-      if (!stop) set_err(L, ST_BAD_DIST);
-      return;
-    }
+    bad = far && !stop;
+    if (stop || far) break;  // one exit branch: EOB / bad code (accounted for by the rounds) or far
     const bool two = !m && lit2 != 0xffffffffu && p + 1 < isize;
     DQ_CHK(p >= ibase && sh + p - ibase + 2 < (int)sizeof(L.out) &&
                ((p - ibase) >> 5) < (int)(sizeof(L.bm) / 4), CHK_K2_IMAGE);
@@ -556,6 +630,7 @@ DQ_AI void emit_seg(const S& W, LT& L, uint32_t start, uint32_t target,
     atomicOr(m ? &L.bm[(p - ibase) >> 5] : dummy32, 1u << ((p - ibase) & 31));
     p += m ? (int32_t)len : (two ? 2 : 1);
   }
+  if (bad) set_err(L, ST_BAD_DIST);
 }
 
 __device__ inline uint32_t gf2_mulmod(uint32_t a, uint32_t b) {  // reflected, poly 0xEDB88320
@@ -767,8 +842,8 @@ DQ_AI void build_tables(LdsI& L, int nlen, int ndist) {
   }
   __syncthreads();
   // root tables, one entry per thread and index (no per-code replica loops)
-  L.u.d.T[t] = root_entry<LR>(L, L.u.d.hl, L.u.d.lend, L.u.d.lent, bitrev((uint32_t)t, LR));
-  L.u.d.T[t + WG] = root_entry<LR>(L, L.u.d.hl, L.u.d.lend, L.u.d.lent, bitrev((uint32_t)(t + WG), LR));
+  for (int i = t; i < (1 << LR); i += WG)
+    L.u.d.T[i] = root_entry<LR>(L, L.u.d.hl, L.u.d.lend, L.u.d.lent, bitrev((uint32_t)i, LR));
   if (t < (1 << DR))
     L.u.d.T[T_DROOT + t] = root_entry<DR>(L, L.u.d.hd, L.u.d.dend, L.u.d.dent, bitrev((uint32_t)t, DR));
   // second-level tables: thread t handles canonical position t of each alphabet.  The long codes
@@ -829,7 +904,7 @@ DQ_AI void build_tables(LdsI& L, int nlen, int ndist) {
 
 // Dynamic header: decode the code-length sequence into L.u.d.x.h.lens, all eight waves at once.
 // Returns the bit position after the header, or sets M_ERR.
-// Wave w takes the 128-bit window w of a 1024-bit pass: lane l decodes the symbol at offsets l and
+// Wave w takes the 128-bit window w of a (128 * NWV)-bit pass: lane l decodes the symbol at offsets l and
 // 64 + l of its window (entries e = l and 64 + l) and the window's successor table is doubled
 // (successor^(2^b), b < 7, by lane shuffles of both halves).  A window's true path enters at one of
 // its first 14 offsets (a code-length symbol is at most 7 + 7 bits), so each wave first maps every
@@ -895,11 +970,11 @@ DQ_AI uint32_t read_lengths(LdsI& L, uint32_t P, int nlen, int ndist, uint32_t e
     __syncthreads();
     if (t == 0) {
       int e = 0;
-      for (int v = 0; v < 8; v++) {
+      for (int v = 0; v < NWV; v++) {
         H.ent[v] = e;
         e = e < 16 ? H.exitm[v][e] : 255;
       }
-      H.ent[8] = e;
+      H.ent[NWV] = e;
     }
     __syncthreads();
     const int entry = H.ent[w];
@@ -938,7 +1013,7 @@ DQ_AI uint32_t read_lengths(LdsI& L, uint32_t P, int nlen, int ndist, uint32_t e
     }
     __syncthreads();
     int have_w = have, prev_w = prev, wsum = 0, lvall = prev;
-    for (int v = 0; v < 8; v++) {
+    for (int v = 0; v < NWV; v++) {
       const int wt = H.wt[v], lv = H.lv[v];
       if (v < w) {
         have_w += wt;
@@ -980,8 +1055,8 @@ DQ_AI uint32_t read_lengths(LdsI& L, uint32_t P, int nlen, int ndist, uint32_t e
     }
     have += wsum;
     prev = lvall;
-    const uint32_t nextP = P + 1024u + (uint32_t)H.ent[8];
-    if (have < total && H.ent[8] >= 16) {  // the path met an invalid code before total
+    const uint32_t nextP = P + 128u * NWV + (uint32_t)H.ent[NWV];
+    if (have < total && H.ent[NWV] >= 16) {  // the path met an invalid code before total
       set_err(L, ST_BAD_TABLE);
       return P;
     }
@@ -997,7 +1072,7 @@ DQ_AI uint32_t read_lengths(LdsI& L, uint32_t P, int nlen, int ndist, uint32_t e
 }
 
 template <bool TIMING, int NB, int G>
-__global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
+__global__ __launch_bounds__(WG, WG / 128) void inflate_block_kernel(
     const uint8_t* __restrict__ C, const int64_t* __restrict__ blk_pos,
     const int32_t* __restrict__ blk_csize, const int32_t* __restrict__ blk_usize,
     const int64_t* __restrict__ uoff, int64_t nblk, uint8_t* __restrict__ U,
@@ -1371,12 +1446,12 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   }
   // ---- 6. resolve matches, chunk by chunk
   const uint64_t* bm64 = reinterpret_cast<const uint64_t*>(L.bm);
-  {  // last_start: max-scan over 64-bit bitmap words (2 words per thread)
+  {  // last_start: max-scan over 64-bit bitmap words (2 words per thread, threads >= 512 none)
     int ls[2];
     int run = -1;
 #pragma unroll
     for (int k = 0; k < 2; k++) {
-      const uint64_t m = bm64[2 * t + k];
+      const uint64_t m = 2 * t + k < 1024 ? bm64[min(2 * t + k, 1023)] : 0ull;
       if (m) run = 64 * (2 * t + k) + 63 - __clzll(m);
       ls[k] = run;
     }
@@ -1389,7 +1464,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
 #pragma unroll
     for (int k = 0; k < 2; k++) {
       const int v = max(ex, ls[k]);
-      L.u.r.last_start[2 * t + k] = v < 0 ? (uint16_t)0xffff : (uint16_t)v;
+      if (WG == 512 || 2 * t + k < 1024) L.u.r.last_start[2 * t + k] = v < 0 ? (uint16_t)0xffff : (uint16_t)v;
     }
     __syncthreads();
   }
@@ -1403,9 +1478,9 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   constexpr int BATCH = NB * CH;
   constexpr int NE = NB * G;
   // DQ_CSTEP: one step (and one barrier) per chunk of G * 512 bytes instead of per 512 bytes
-  constexpr bool CSTEP = DQ_CSTEP != 0 && G > 1;
+  constexpr bool CSTEP = (DQ_CSTEP != 0 && G > 1) || CH % 512 != 0;
   static_assert(BATCH <= RES_NXT, "the batch's next-pointers fit the resolve scratch");
-  static_assert(65536 / BATCH <= 32, "one carry slot per batch");
+  static_assert((65536 + BATCH - 1) / BATCH <= NCARRY, "one carry slot per batch");
   uint16_t* nxt = L.u.r.nxt;
   // (a) sources of batch `b0`.  First hop, every byte: its owner (one 64-bit bitmap word, one
   //     last_start) and the owner's descriptor give the copy source (G <= 4 bytes have at most
@@ -1605,7 +1680,7 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
   uint32_t ct0 = 0, ct1 = 0, cshift = 0, cinit = 0, cwant = 0;
   if (verify_crc) {
     ct0 = (&c_crc4[0][0])[t];
-    ct1 = (&c_crc4[0][0])[t + WG];
+    ct1 = t + WG < 1024 ? (&c_crc4[0][0])[t + WG] : 0u;
     cshift = c_slice_shift[WG - 1 - t];
     if (t == 0) {
       cinit = crc_init[rsize];  // x^(8 rsize) * 0xffffffff mod P
@@ -1613,15 +1688,15 @@ __global__ __launch_bounds__(WG, 4) void inflate_block_kernel(
       cwant = (uint32_t)tr[0] | ((uint32_t)tr[1] << 8) | ((uint32_t)tr[2] << 16) | ((uint32_t)tr[3] << 24);
     }
   }
-  static_assert(2 * WG == 1024, "two CRC table words per thread");
+  static_assert(2 * WG >= 1024, "at most two CRC table words per thread");
   for (int x = t; x < head; x += WG) dstU[x] = O[x];
   for (int x = head + 16 * lines_done + t; x < rsize; x += WG) dstU[x] = O[x];
   TST(6);
   // ---- 7. CRC32: thread t hashes the CRC_SL-byte slice ending (511 - t) * CRC_SL bytes before rsize
   if (verify_crc) {
     __syncthreads();  // the resolve scratch is dead: the CRC tables reuse it
-    (&L.u.crc4[0][0])[t] = ct0;
-    (&L.u.crc4[0][0])[t + WG] = ct1;
+    if (t < 1024) (&L.u.crc4[0][0])[t] = ct0;
+    if (t + WG < 1024) (&L.u.crc4[0][0])[t + WG] = ct1;
     __syncthreads();
     const int32_t e = rsize - (WG - 1 - t) * CRC_SL;
     const int32_t s0 = max(0, e - CRC_SL);
@@ -2378,10 +2453,11 @@ struct HostTables {
     uint32_t p = 1u << 30;  // x^1
     x2n[0] = p;
     for (int k = 1; k < 32; k++) x2n[k] = p = h_mul(p, p);
-    // x^(8 * CRC_SL * k) mod P: x^1056 = x^1024 * x^32 = x2n[10] * x2n[5]; powers by repeated
-    // multiplication
-    static_assert(CRC_SL == 132, "x^(8 * CRC_SL) below");
-    const uint32_t step = h_mul(x2n[10], x2n[5]);
+    // x^(8 * CRC_SL * k) mod P: x^(8 CRC_SL) from the x^(2^k) of its set bits; powers by
+    // repeated multiplication
+    uint32_t step = 1u << 31;  // x^0
+    for (int k = 0; k < 31; k++)
+      if (((uint32_t)(8 * CRC_SL) >> k) & 1u) step = h_mul(step, x2n[k]);
     slice[0] = 1u << 31;  // x^0
     for (int k = 1; k < WG; k++) slice[k] = h_mul(slice[k - 1], step);
     uint32_t x8 = 1u << 31;          // x^0
