@@ -406,8 +406,9 @@ DQ_AI uint32_t d_second(const LT& L, uint32_t e, uint32_t bb) {
 
 
 // One full symbol: a literal (value in len, is_m false) or a match (len, dist, is_m true); returns
-// true instead when the symbol ends the run: EOB (len = the bit after it) or an invalid code
-// (len = 0xffffffff).  Straight-line: every lane does the litlen and the distance lookup (a
+// true instead when the symbol ends the run: EOB or an invalid code, told apart after the caller's
+// loop by stop_end(e, p) from the litlen entry `e` (the bit after the EOB, or 0xffffffff) -- so
+// the decode step itself carries no EOB arithmetic.  Straight-line: every lane does the litlen and the distance lookup (a
 // literal lane consumes no distance bits), so a wave mixing literals and matches does not execute
 // both paths one after the other.  The table entries carry the values (ent_ll / ent_d): a length
 // is value + 3 + its extra bits, a distance m << s + 1 + its extra bits, each extra field one
@@ -418,11 +419,11 @@ DQ_AI uint32_t d_second(const LT& L, uint32_t e, uint32_t bb) {
 // `lit2` is the second (else 0xffffffff) -- the boundaries the caller sees are unchanged.
 template <bool SLOW, class S, class LT>
 DQ_AI bool dsym(BitR& r, const S& W, const LT& L, uint32_t p, uint32_t lim,
-                uint32_t& len, uint32_t& dist, uint32_t& lit2, bool& is_m) {
+                uint32_t& len, uint32_t& dist, uint32_t& lit2, bool& is_m, uint32_t& e) {
   br_refill(r, W);  // >= 32 bits: a litlen code + its extra bits (<= 20)
   uint32_t bb = br_peek(r);
   const uint32_t ri = bb & ((1u << LR) - 1);
-  uint32_t e = L.u.d.T[ri];
+  e = L.u.d.T[ri];
   uint32_t pe = 0;
   if constexpr (LT::kPair) pe = zx16(L.u.d.x.pair[ri]);
   if ((e & 15) == 0) e = ll_second<SLOW>(L, e, bb);
@@ -443,13 +444,14 @@ DQ_AI bool dsym(BitR& r, const S& W, const LT& L, uint32_t p, uint32_t lim,
   br_take(r, W, is_m ? nb2 + dx : 0u);
   // SLOW = false: a code-less index reads the invalid sentinels build_tables leaves at the first
   // second-level entries, so no entry here has code length 0
-  const bool stop = (SLOW && nb == 0) || (e & 0xFEF0u) == 0xF810u ||
-                    (is_m && ((SLOW && nb2 == 0) || (e2 & 0x4000u)));
-  if (stop) {  // rare: EOB (an M entry, so the distance bits taken above are not the stream's)
-    const bool eob = nb != 0 && (e & 0xFFF0u) == LL_EOB;
-    len = eob ? p + nb : 0xffffffffu;
-  }
-  return stop;
+  // (EOB is an M entry, so the distance bits taken above are not the stream's: the caller stops)
+  return (SLOW && nb == 0) || (e & 0xFEF0u) == 0xF810u ||
+         (is_m && ((SLOW && nb2 == 0) || (e2 & 0x4000u)));
+}
+// After dsym stopped at position p with litlen entry e: the bit after the EOB, or 0xffffffff for an
+// invalid code (in the litlen or the distance alphabet)
+DQ_AI uint32_t stop_end(uint32_t e, uint32_t p) {
+  return (e & 15) != 0 && (e & 0xFFF0u) == LL_EOB ? p + (e & 15) : 0xffffffffu;
 }
 
 enum : int32_t { F_DEAD = 4 };  // speculative path found no boundary >= sB (garbage)
@@ -473,13 +475,14 @@ DQ_AI int run_seg(const S& W, const LT& L, uint32_t start, uint32_t sB,
   BitR r;
   br_init(r, W, start);
   uint32_t p = br_pos(r);
-  uint32_t len = 0, dist = 0, lit2;
+  uint32_t len = 0, dist = 0, lit2, e = 0;
   bool m;
   // warm-up: to the first symbol boundary >= sB, nothing counted (one compare per step: the
   // data end is folded into the bound and tested once after the loop)
   const uint32_t sBe = min(sB, endbits);
   while (p < sBe) {
-    if (dsym<SLOW>(r, W, L, p, sBe, len, dist, lit2, m)) {
+    if (dsym<SLOW>(r, W, L, p, sBe, len, dist, lit2, m, e)) {
+      len = stop_end(e, p);
       *Ep = (int32_t)(len != 0xffffffffu ? len : p);
       *Bp = -1;
       *cntp = 0;
@@ -519,11 +522,12 @@ DQ_AI int run_seg(const S& W, const LT& L, uint32_t start, uint32_t sB,
     stopped = false;
     if (p >= sEe) break;
     stopped = true;
-    if (dsym<SLOW>(r, W, L, p, min(thr, sEe), len, dist, lit2, m)) break;
+    if (dsym<SLOW>(r, W, L, p, min(thr, sEe), len, dist, lit2, m, e)) break;
     cnt += m ? (int32_t)len : (lit2 != 0xffffffffu ? 2 : 1);
     p = br_pos(r);
   }
   if (stopped) {
+    len = stop_end(e, p);
     *Ep = (int32_t)(len != 0xffffffffu ? len : p);
     f = len != 0xffffffffu ? F_EOB : F_ERR;
   } else {
@@ -554,7 +558,7 @@ DQ_AI int run_redo(const S& W, const LT& L, uint32_t s0, uint32_t sB,
   const uint32_t sEe = min(sE, endbits);
   int j = 0;
   int why;  // 0: the segment or the data ended, 1: merged, 2: dsym stopped
-  uint32_t p, len = 0;
+  uint32_t p, len = 0, e = 0;
   for (;;) {
     p = br_pos(r);
     // at a checkpoint threshold: the same boundary as the speculative run merges (one exit branch
@@ -573,7 +577,7 @@ DQ_AI int run_redo(const S& W, const LT& L, uint32_t s0, uint32_t sB,
     uint32_t dist = 0, lit2;
     bool m;
     why = 2;
-    if (dsym<SLOW>(r, W, L, p, min(thr, sEe), len, dist, lit2, m)) break;
+    if (dsym<SLOW>(r, W, L, p, min(thr, sEe), len, dist, lit2, m, e)) break;
     cnt += m ? (int32_t)len : (lit2 != 0xffffffffu ? 2 : 1);
   }
   if (why == 1) {
@@ -582,6 +586,7 @@ DQ_AI int run_redo(const S& W, const LT& L, uint32_t s0, uint32_t sB,
     cnt += sc - (int32_t)(cur & 0xffffu);
     if (jm) *jm = j;
   } else if (why == 2) {
+    len = stop_end(e, p);
     *Ep = (int32_t)(len != 0xffffffffu ? len : p);
     f = len != 0xffffffffu ? F_EOB : F_ERR;
   } else {
@@ -615,7 +620,8 @@ DQ_AI void emit_seg(const S& W, LT& L, uint32_t start, uint32_t target,
     if (q >= te || p >= isize) break;
     uint32_t len = 0, dist = 0, lit2;
     bool m;
-    const bool stop = dsym<SLOW>(r, W, L, q, te, len, dist, lit2, m);
+    uint32_t e;
+    const bool stop = dsym<SLOW>(r, W, L, q, te, len, dist, lit2, m, e);
     const bool far = m && (int32_t)dist > p;  // a distance before the block's first byte
     bad = far && !stop;
     if (stop || far) break;  // one exit branch: EOB / bad code (accounted for by the rounds) or far

@@ -67,15 +67,12 @@ def main():
     seen = {}
     for name, body in loops(ker):
         g = sum(x.startswith("global_load") for x in body)
-        if g != 2:
-            continue
+        if g != 2 or any(x.startswith("v_bfrev_b32") for x in body):
+            continue  # not a decode step, or the canonical (SLOW) instantiation
         v = sum(x.startswith("v_") for x in body)
         s = sum(x.startswith("s_") for x in body)
         d = sum(x.startswith("ds_") for x in body)
         kind = classify(body)
-        # the first loop of each kind is the common-path instantiation (SLOW = false comes first
-        # in the source order of the kernel's `slow ? run<true> : run<false>` branches' layout);
-        # report the smallest VALU count of the kind, which is the non-SLOW loop
         if kind not in seen or v < seen[kind][1]:
             seen[kind] = (name, v, s, d)
     for k in ("warm-up", "spec", "redo", "emit"):
