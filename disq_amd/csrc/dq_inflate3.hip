@@ -1495,8 +1495,8 @@ __global__ __launch_bounds__(WG, WG / 128) void inflate_block_kernel(
   //     publishes its source in nxt.  The match straddling the batch start is the carry (cms,
   //     cdesc): its descriptor lies before the batch.
   auto first_hop = [&](int32_t b0, int32_t cms, uint32_t cdesc, int32_t* fr, int32_t* xs,
-                       uint32_t& pending) {
-    pending = 0;
+                       bool& pending) {
+    pending = false;
     uint64_t mw[NB];
     int32_t lsv[NB];
 #pragma unroll
@@ -1505,7 +1505,7 @@ __global__ __launch_bounds__(WG, WG / 128) void inflate_block_kernel(
       const int w = min(g0 >> 6, 1023);  // bytes past rsize: read anything, copy = false
       DQ_CHK(w >= 0 && w - 1 < 1024, CHK_K2_LAST);
       mw[k] = bm64[w];
-      lsv[k] = w ? (int32_t)L.u.r.last_start[w - 1] : 0xffff;
+      lsv[k] = w ? (int32_t)zx16(L.u.r.last_start[w - 1]) : 0xffff;
     }
     int32_t msv[NE];
     uint32_t da[NB], db[NB];
@@ -1545,8 +1545,8 @@ __global__ __launch_bounds__(WG, WG / 128) void inflate_block_kernel(
         DQ_CHK(!copy || (src >= 0 && src < x), CHK_K2_SRC);
         const bool done = !copy || src < sbk;
         fr[e] = copy ? src : x;
-        xs[e] = src;
-        pending |= done ? 0u : 1u << e;
+        xs[e] = done ? x : src;  // a final entry points at its own byte (see jump_round)
+        pending = pending || !done;
         nxt[x - b0] = (uint16_t)(copy ? src : x);  // a final source (or the literal), else in-step
       }
     }
@@ -1555,33 +1555,38 @@ __global__ __launch_bounds__(WG, WG / 128) void inflate_block_kernel(
   // publishes how far it got, so a byte that reads an advanced pointer skips that byte's chain.
   // Every value read is a byte of the same chain, so no barrier orders the rounds and each read
   // advances at least one hop; it ends at a literal (nxt[p] == p) or a byte before the step.
-  auto jump_round = [&](int32_t b0, int32_t* fr, int32_t* xs, uint32_t& pending) {
-    // branch-free over the entries: a final entry re-reads and re-writes its own next pointer,
-    // which holds its final source already
+  auto jump_round = [&](int32_t b0, int32_t* fr, int32_t* xs, bool& pending) {
+    // branch-free over the entries: a final entry points at its own byte (xs == own), so it
+    // re-reads and re-writes its own next pointer, which holds its final source already -- the
+    // pending state is the pointer itself (round 5 kept a bit per entry: an extract, a select of
+    // the read address and a bit update per entry and round)
     int32_t qv[NE];
 #pragma unroll
     for (int e = 0; e < NE; e++) {
-      const bool pd = (pending >> e) & 1;
-      DQ_CHK(!pd || (xs[e] - b0 >= 0 && xs[e] - b0 < BATCH), CHK_K2_NXT);
-      qv[e] = (int32_t)nxt[pd ? xs[e] - b0 : (e / G) * CH + G * t + e % G];
+      DQ_CHK(xs[e] - b0 >= 0 && xs[e] - b0 < BATCH, CHK_K2_NXT);
+      qv[e] = (int32_t)zx16(nxt[xs[e] - b0]);
     }
+    bool any = false;
 #pragma unroll
     for (int e = 0; e < NE; e++) {
-      const bool pd = (pending >> e) & 1;
+      const int32_t own = (e / G) * CH + G * t + e % G;  // relative to b0
       const int32_t p = xs[e], q = qv[e];
+      const bool pd = p != b0 + own;
       const int32_t sbk = b0 + (e / G) * CH + (CSTEP ? 0 : ((G * t) & ~511));
       const bool fin = pd && (q == p || q < sbk);
+      const bool go = pd && !fin;
       fr[e] = fin ? q : fr[e];
-      xs[e] = pd && !fin ? q : p;
-      pending &= fin ? ~(1u << e) : ~0u;
-      nxt[(e / G) * CH + G * t + e % G] = (uint16_t)q;
+      xs[e] = go ? q : b0 + own;
+      any = any || go;
+      nxt[own] = (uint16_t)q;
     }
+    pending = any;
   };
   // Software pipeline over batches: while batch k's ordered steps (b) run, batch k+1 takes its
   // first hop (its descriptors are intact until its own steps) and one jump round after each
   // step barrier (nxt holds batch k+1 only: batch k's sources are final in registers by then).
   int32_t frA[NE], xsA[NE];
-  uint32_t pendA = 0;
+  bool pendA = false;
   int32_t cms = -1;     // carry into the current batch
   uint32_t cdesc = 0;
   first_hop(0, cms, cdesc, frA, xsA, pendA);
@@ -1606,7 +1611,7 @@ __global__ __launch_bounds__(WG, WG / 128) void inflate_block_kernel(
     L.u.r.carry_desc[t] = ncdesc;
   }
   __syncthreads();
-  for (int hop = 0; pendA != 0 && hop < WG + 2; hop++) jump_round(0, frA, xsA, pendA);
+  for (int hop = 0; pendA && hop < WG + 2; hop++) jump_round(0, frA, xsA, pendA);
   for (int32_t bs = 0; bs < rsize; bs += BATCH) {
     const uint64_t tb0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
     const int32_t nbs = bs + BATCH;
@@ -1615,7 +1620,7 @@ __global__ __launch_bounds__(WG, WG / 128) void inflate_block_kernel(
     const int32_t ncms = more ? L.u.r.carry_ms[bs / BATCH] : -1;
     const uint32_t ncdesc = more ? L.u.r.carry_desc[bs / BATCH] : 0u;
     int32_t frB[NE], xsB[NE];
-    uint32_t pendB = 0;
+    bool pendB = false;
     if (more) first_hop(nbs, ncms, ncdesc, frB, xsB, pendB);
     const uint64_t tb1 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
     // (b) batch k's 512-byte steps in order: one LDS read + write per copied byte, one barrier.
@@ -1657,7 +1662,7 @@ __global__ __launch_bounds__(WG, WG / 128) void inflate_block_kernel(
       lines_done = lines_to;
     }
     const uint64_t tb3 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
-    for (int hop = 0; pendB != 0 && hop < WG + 2; hop++) jump_round(nbs, frB, xsB, pendB);
+    for (int hop = 0; pendB && hop < WG + 2; hop++) jump_round(nbs, frB, xsB, pendB);
 #pragma unroll
     for (int e = 0; e < NE; e++) frA[e] = frB[e];
     cms = ncms;
@@ -2336,7 +2341,7 @@ __global__ __launch_bounds__(64 * TW, 4) void inflate_tail_kernel(
         for (int i = 0; i < 4; i++) {
           const bool pd = (pend >> i) & 1u;
           DQ_CHK(!pd || (p[i] - xr >= 0 && p[i] - xr < 256), CHK_K2_NXT);
-          q[i] = nx[pd ? p[i] - xr : 4 * lane + i];
+          q[i] = zx16(nx[pd ? p[i] - xr : 4 * lane + i]);
         }
 #pragma unroll
         for (int i = 0; i < 4; i++) {
