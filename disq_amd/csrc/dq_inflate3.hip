@@ -1517,8 +1517,10 @@ __global__ __launch_bounds__(WG, WG / 128) void inflate_block_kernel(
         const uint64_t mi = mw[k] & (~0ull >> (63 - ((g0 + i) & 63)));
         msv[k * G + i] = mi ? (g0 | 63) - (int32_t)__clzll(mi) : lsv[k];
       }
-      da[k] = load_desc(L, sh + min(max(msv[k * G], b0), 65535));
-      db[k] = G > 1 ? load_desc(L, sh + min(max(msv[k * G + G - 1], b0), 65535)) : da[k];
+      // (an owner before the batch reads a stale descriptor, in range and unused: the carry's is
+      // taken instead)
+      da[k] = load_desc(L, sh + min(msv[k * G], 65535));
+      db[k] = G > 1 ? load_desc(L, sh + min(msv[k * G + G - 1], 65535)) : da[k];
     }
 #pragma unroll
     for (int k = 0; k < NB; k++) {
@@ -1530,18 +1532,20 @@ __global__ __launch_bounds__(WG, WG / 128) void inflate_block_kernel(
         const int32_t x = g0 + i, ms = msv[e];
         const bool before = ms < b0;  // descriptors before the batch are overwritten: the carry
         const uint32_t desc = before ? cdesc : (ms == msv[k * G + G - 1] ? db[k] : da[k]);
-        const int32_t len = (int32_t)(desc >> 15) + 3, D = (int32_t)(desc & 0x7fff) + 1;
+        const int32_t len = (int32_t)(desc >> 15) + 3, D1 = (int32_t)(desc & 0x7fff);  // D - 1
         const bool copy = x < rsize && ms != 0xffff && (!before || ms == cms) && x < ms + len;
         // src = ms - D + (x - ms) mod D; x - ms <= 257: a float reciprocal + one fix-up is exact,
-        // needed only by bytes past the first period of an overlapping match (skipped per wave)
+        // needed only by bytes past the first period of an overlapping match (skipped per wave);
+        // otherwise src = x - D = (D1 ^ ~0) + x, one v_xad
         const int32_t jj = x - ms;
-        int32_t r = jj;
-        if (__builtin_expect(__any(copy && jj >= D), 0)) {
+        int32_t src = (int32_t)((uint32_t)D1 ^ ~0u) + x;
+        if (__builtin_expect(__any(copy && jj > D1), 0)) {
+          const int32_t D = D1 + 1;
           const int32_t q = (int32_t)((float)jj * __builtin_amdgcn_rcpf((float)D));
-          r = jj - q * D;
+          int32_t r = jj - q * D;
           r = r >= D ? r - D : r;
+          src = ms - D + r;
         }
-        const int32_t src = ms - D + r;
         DQ_CHK(!copy || (src >= 0 && src < x), CHK_K2_SRC);
         const bool done = !copy || src < sbk;
         fr[e] = copy ? src : x;
