@@ -1800,11 +1800,15 @@ DQ_AI uint32_t read_lengths_wave(LdsW& L, uint32_t P, int nlen, int ndist, uint3
   const int lane = tid_fresh() & 63;
   const int total = nlen + ndist;
   int have = 0, prev = -1, entry = 0;  // uniform
-  for (uint32_t W0 = P;; W0 += 64) {
-    if (W0 > endbits) {
-      set_err(L, ST_OVERREAD);
-      return W0;
-    }
+  // the symbol at bit W0 + lane and the window's successor table (successor^(2^b), 64 = past the
+  // window; an invalid code is a self-loop): independent of the path, so the next window's is
+  // computed while this window's path is taken (software-pipelined: its five dependent shuffles
+  // overlap the path's)
+  struct Win {
+    int J[6];
+    int rep, adv, sy;
+  };
+  auto window = [&](uint32_t W0, Win& w) {
     const uint32_t p = W0 + (uint32_t)lane;
     const uint32_t wi = min((p >> 5) - hbase, (uint32_t)HB_WORDS - 2);
     const uint32_t v = (uint32_t)((((uint64_t)hb[wi + 1] << 32) | hb[wi]) >> (p & 31));
@@ -1812,16 +1816,28 @@ DQ_AI uint32_t read_lengths_wave(LdsW& L, uint32_t P, int nlen, int ndist, uint3
     const uint32_t cl = ent & 7, sy = ent >> 3;
     const uint32_t ex = sy == 16 ? 2u : sy == 17 ? 3u : sy == 18 ? 7u : 0u;
     const int xv = (int)((v >> cl) & ((1u << ex) - 1));
-    const int rep = sy < 16 ? 1 : sy == 16 ? 3 + xv : sy == 17 ? 3 + xv : 11 + xv;
-    const int adv = cl ? (int)(cl + ex) : 0;  // 0: no code (a path reaching it stops)
-    // successor^(2^b), 64 = past the window; an invalid code is a self-loop
-    int J[6];
-    J[0] = adv ? min(lane + adv, 64) : lane;
+    w.sy = (int)sy;
+    w.rep = sy < 16 ? 1 : sy == 16 ? 3 + xv : sy == 17 ? 3 + xv : 11 + xv;
+    w.adv = cl ? (int)(cl + ex) : 0;  // 0: no code (a path reaching it stops)
+    w.J[0] = w.adv ? min(lane + w.adv, 64) : lane;
 #pragma unroll
     for (int k = 1; k < 6; k++) {
-      const int y = __shfl(J[k - 1], J[k - 1] & 63, 64);
-      J[k] = J[k - 1] >= 64 ? 64 : y;
+      const int y = __shfl(w.J[k - 1], w.J[k - 1] & 63, 64);
+      w.J[k] = w.J[k - 1] >= 64 ? 64 : y;
     }
+  };
+  Win cur;
+  window(P, cur);
+  for (uint32_t W0 = P;; W0 += 64) {
+    if (W0 > endbits) {
+      set_err(L, ST_OVERREAD);
+      return W0;
+    }
+    Win nxt;
+    window(W0 + 64, nxt);  // (past the staged words: clamped reads, unused)
+    const int rep = cur.rep, adv = cur.adv;
+    const uint32_t sy = (uint32_t)cur.sy;
+    const int* const J = cur.J;
     // lane k: offset of the k-th path symbol from `entry` (64: none)
     int pk = entry;
 #pragma unroll
@@ -1869,6 +1885,7 @@ DQ_AI uint32_t read_lengths_wave(LdsW& L, uint32_t P, int nlen, int ndist, uint3
     const int kl = __shfl(key, 63, 64);
     prev = kl > 0 ? (kl & 31) : prev;
     entry = __shfl(pk + s_adv, lastr, 64) - 64;
+    cur = nxt;
   }
 }
 

@@ -859,13 +859,21 @@ __device__ inline uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t sh) {  // (
 // (8-byte little-endian words, zero padded; DESIGN.md section "hash") from LDS.  Runs of records
 // longer than the staging buffer (long reads) are read straight from U.
 constexpr int REC_WAVE = 64;      // threads per workgroup (one wave)
-constexpr int REC_GROUP = 32;     // records per group: two lanes per record split its hash words
-constexpr int REC_STAGE = 12288;  // 32 short-read records (~10.5 KB): 13 waves per CU
+// lanes per record (they split its hash words); records per group = 64 / lanes; the staging holds
+// one group of short-read records (~330 B each): 2 lanes -> 32 records, 12 KB, 13 waves per CU;
+// 4 lanes -> 16 records, 6 KB, 26 waves per CU
+#ifndef DQ_REC_LANES
+#define DQ_REC_LANES 2
+#endif
+constexpr int REC_LANES = DQ_REC_LANES;
+static_assert(REC_LANES == 2 || REC_LANES == 4, "2 or 4 lanes per record");
+constexpr int REC_GROUP = REC_WAVE / REC_LANES;
+constexpr int REC_STAGE = REC_GROUP * 384;
 
 // Lane work of decode_group: record i (start p, n = 4 + block_size bytes) read through W, a
-// dword view in which the record starts at byte `off` (LDS staging or U itself).  Lane half 0
-// decodes the fixed fields; both halves hash the record's 8-byte words of their parity (the word
-// sum is order-free) and return the partial sum.
+// dword view in which the record starts at byte `off` (LDS staging or U itself).  Lane part 0
+// decodes the fixed fields; the REC_LANES parts hash the record's 8-byte words k = part mod
+// REC_LANES (the word sum is order-free) and return the partial sum.
 struct BlockOf {  // the htsjdk block of a record start: loaded before the staging wait
   int64_t j, u0, u1, bp;
 };
@@ -906,10 +914,10 @@ __device__ __attribute__((always_inline)) inline uint64_t decode_one(
     }
     soa.voffset[i] = ((uint64_t)bo.bp << 16) | (uint64_t)(p - bo.u0);
   }
-  // hash words k = half, half + 2, ... (a long record's words are hashed by long_hash_kernel)
+  // hash words k = half, half + REC_LANES, ... (a long record's words: long_hash_kernel)
   uint64_t part = 0;
   const int64_t nw = hash ? (n + 7) / 8 : 0;
-  for (int64_t k = half; k < nw; k += 2) {
+  for (int64_t k = half; k < nw; k += REC_LANES) {
     const int64_t wi = wi0 + 2 * k;
     const uint32_t w0 = W[wi], w1 = W[wi + 1], w2 = W[wi + 2];
     const uint32_t lo = funnel(w0, w1, sh), hi = funnel(w1, w2, sh);
@@ -992,11 +1000,14 @@ __device__ void decode_group(const uint8_t* __restrict__ U, int64_t ulen,
       for (int64_t j = 0; j < np && e0 + j < ll.cap; j++) ll.ent[e0 + j] = (uint64_t)i << 16 | (uint64_t)j;
     }
   }
-  // both halves' word sums (all lanes take part in the shuffles)
-  const uint32_t plo = (uint32_t)part, phi = (uint32_t)(part >> 32);
-  const uint64_t other = ((uint64_t)(uint32_t)__shfl_xor((int)phi, REC_GROUP, 64) << 32) |
-                         (uint32_t)__shfl_xor((int)plo, REC_GROUP, 64);
-  if (act && half == 0) soa.hash[i] = lng ? 0ull : dq_mix64((uint64_t)n * DQ_K_LEN + part + other);
+  // the parts' word sums (all lanes take part in the shuffles)
+#pragma unroll
+  for (int o = REC_GROUP; o < REC_WAVE; o <<= 1) {
+    const uint32_t plo = (uint32_t)part, phi = (uint32_t)(part >> 32);
+    part += ((uint64_t)(uint32_t)__shfl_xor((int)phi, o, 64) << 32) |
+            (uint32_t)__shfl_xor((int)plo, o, 64);
+  }
+  if (act && half == 0) soa.hash[i] = lng ? 0ull : dq_mix64((uint64_t)n * DQ_K_LEN + part);
 }
 
 // One workgroup per piece of a long record (grid-stride over the list): thread t sums the words

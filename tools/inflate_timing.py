@@ -11,4 +11,5 @@ for ver in sys.argv[2:] or ["3"]:
         c.open_bytes(r.bam)
         st = c.run_resident()
         st = c.run_resident()
-        print(ver, "inflate ms", st.ms_inflate, "total", st.ms_total, "ulen", st.decompressed_bytes, flush=True)
+        print(ver, "inflate ms", st.ms_inflate, "total", st.ms_total, "records", st.ms_records,
+              "ulen", st.decompressed_bytes, flush=True)
