@@ -610,10 +610,15 @@ DQ_AI void emit_seg(const S& W, LT& L, uint32_t start, uint32_t target,
   // three ds_write_b8 (a merged unaligned b16 store stalls): volatile keeps them apart, the LDS
   // address space keeps them DS stores (a generic volatile pointer became flat stores)
   uint32_t* const dummy32 = emit_dummy(L) + (tid_fresh() & 63);
-  lds8* const dummy = (lds8*)dummy32;
+  lds8* const dummy1 = (lds8*)dummy32 - 1;  // dummy1[1], dummy2[2]: the lane's dummy word
+  lds8* const dummy2 = (lds8*)dummy32 - 2;
   BitR r;
   br_init(r, W, start);
   const uint32_t te = min(target, endbits);
+  // the image position of output byte p is obase + p: the base in a VGPR (laundered), since the
+  // kernel's SGPRs are all taken and a uniform base was spilled -- a v_readlane per step
+  int32_t obase = sh - ibase;
+  asm("" : "+v"(obase));
   bool bad = false;
   for (;;) {
     const uint32_t q = br_pos(r);
@@ -629,10 +634,12 @@ DQ_AI void emit_seg(const S& W, LT& L, uint32_t start, uint32_t target,
     DQ_CHK(p >= ibase && sh + p - ibase + 2 < (int)sizeof(L.out) &&
                ((p - ibase) >> 5) < (int)(sizeof(L.bm) / 4), CHK_K2_IMAGE);
     const uint32_t desc = (dist - 1) | ((len - 3) << 15);
-    lds8* const o = (lds8*)(L.out + sh + (p - ibase));
+    lds8* const o = (lds8*)(L.out + (obase + p));
     o[0] = (uint8_t)(m ? desc : len);
-    *(m || two ? o + 1 : dummy) = (uint8_t)(m ? desc >> 8 : lit2);
-    *(m ? o + 2 : dummy) = (uint8_t)(desc >> 16);
+    // the stores a symbol does not need go to the dummy word: the base is selected and the +1 / +2
+    // stays in the DS offset field (the dummy's base is moved back by the same amount)
+    (m || two ? o : dummy1)[1] = (uint8_t)(m ? desc >> 8 : lit2);
+    (m ? o : dummy2)[2] = (uint8_t)(desc >> 16);
     atomicOr(m ? &L.bm[(p - ibase) >> 5] : dummy32, 1u << ((p - ibase) & 31));
     p += m ? (int32_t)len : (two ? 2 : 1);
   }
@@ -1800,15 +1807,11 @@ DQ_AI uint32_t read_lengths_wave(LdsW& L, uint32_t P, int nlen, int ndist, uint3
   const int lane = tid_fresh() & 63;
   const int total = nlen + ndist;
   int have = 0, prev = -1, entry = 0;  // uniform
-  // the symbol at bit W0 + lane and the window's successor table (successor^(2^b), 64 = past the
-  // window; an invalid code is a self-loop): independent of the path, so the next window's is
-  // computed while this window's path is taken (software-pipelined: its five dependent shuffles
-  // overlap the path's)
-  struct Win {
-    int J[6];
-    int rep, adv, sy;
-  };
-  auto window = [&](uint32_t W0, Win& w) {
+  for (uint32_t W0 = P;; W0 += 64) {
+    if (W0 > endbits) {
+      set_err(L, ST_OVERREAD);
+      return W0;
+    }
     const uint32_t p = W0 + (uint32_t)lane;
     const uint32_t wi = min((p >> 5) - hbase, (uint32_t)HB_WORDS - 2);
     const uint32_t v = (uint32_t)((((uint64_t)hb[wi + 1] << 32) | hb[wi]) >> (p & 31));
@@ -1816,28 +1819,18 @@ DQ_AI uint32_t read_lengths_wave(LdsW& L, uint32_t P, int nlen, int ndist, uint3
     const uint32_t cl = ent & 7, sy = ent >> 3;
     const uint32_t ex = sy == 16 ? 2u : sy == 17 ? 3u : sy == 18 ? 7u : 0u;
     const int xv = (int)((v >> cl) & ((1u << ex) - 1));
-    w.sy = (int)sy;
-    w.rep = sy < 16 ? 1 : sy == 16 ? 3 + xv : sy == 17 ? 3 + xv : 11 + xv;
-    w.adv = cl ? (int)(cl + ex) : 0;  // 0: no code (a path reaching it stops)
-    w.J[0] = w.adv ? min(lane + w.adv, 64) : lane;
+    const int rep = sy < 16 ? 1 : sy == 16 ? 3 + xv : sy == 17 ? 3 + xv : 11 + xv;
+    const int adv = cl ? (int)(cl + ex) : 0;  // 0: no code (a path reaching it stops)
+    // successor^(2^b), 64 = past the window; an invalid code is a self-loop.  (Computing the next
+    // window's table while this window's path is taken measured no faster, profiles/r6g_*: the
+    // shuffles' results return in order, so the path waits for the prefetched ones too.)
+    int J[6];
+    J[0] = adv ? min(lane + adv, 64) : lane;
 #pragma unroll
     for (int k = 1; k < 6; k++) {
-      const int y = __shfl(w.J[k - 1], w.J[k - 1] & 63, 64);
-      w.J[k] = w.J[k - 1] >= 64 ? 64 : y;
+      const int y = __shfl(J[k - 1], J[k - 1] & 63, 64);
+      J[k] = J[k - 1] >= 64 ? 64 : y;
     }
-  };
-  Win cur;
-  window(P, cur);
-  for (uint32_t W0 = P;; W0 += 64) {
-    if (W0 > endbits) {
-      set_err(L, ST_OVERREAD);
-      return W0;
-    }
-    Win nxt;
-    window(W0 + 64, nxt);  // (past the staged words: clamped reads, unused)
-    const int rep = cur.rep, adv = cur.adv;
-    const uint32_t sy = (uint32_t)cur.sy;
-    const int* const J = cur.J;
     // lane k: offset of the k-th path symbol from `entry` (64: none)
     int pk = entry;
 #pragma unroll
@@ -1885,7 +1878,6 @@ DQ_AI uint32_t read_lengths_wave(LdsW& L, uint32_t P, int nlen, int ndist, uint3
     const int kl = __shfl(key, 63, 64);
     prev = kl > 0 ? (kl & 31) : prev;
     entry = __shfl(pk + s_adv, lastr, 64) - 64;
-    cur = nxt;
   }
 }
 

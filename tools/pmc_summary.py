@@ -8,7 +8,11 @@ the run's dispatches (ratios are dispatch-count free):
                          SIMD-32 two cycles (MI355X_MICROARCH.md, 'Wave scheduling'); cycles =
                          GRBM_GUI_ACTIVE / 8 (rocprofv3 sums the 8 XCDs)
   valu_busy_quad_frac    SQ_ACTIVE_INST_VALU x 4 / (SIMDs x cycles): the same against the issue
-                         cycles waves report (quad-cycles), which count co-issued waves twice
+                         cycles waves report (quad-cycles).  For these kernels SQ_ACTIVE_INST_VALU
+                         equals SQ_INSTS_VALU: every VALU instruction holds a quad-cycle of its
+                         SIMD's issue, so this, not valu_issue_frac, is the issue utilisation
+                         (more waves per CU made K2 slower, fewer
+                         VALU instructions made it faster)
   lds_busy_frac          SQ_LDS_IDX_ACTIVE / (CUs x cycles)
   lds_bank_conflict_frac SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
   lds_unaligned_frac     SQ_LDS_UNALIGNED_STALL / SQ_LDS_IDX_ACTIVE
