@@ -914,17 +914,28 @@ __device__ __attribute__((always_inline)) inline uint64_t decode_one(
     }
     soa.voffset[i] = ((uint64_t)bo.bp << 16) | (uint64_t)(p - bo.u0);
   }
-  // hash words k = half, half + REC_LANES, ... (a long record's words: long_hash_kernel)
+  // hash words k = half, half + REC_LANES, ... (a long record's words: long_hash_kernel): the
+  // whole words first, with no mask and 32-bit counters, then the partial last word by the lane
+  // whose word it is (round 5 computed the partial-word mask and 64-bit counters for every word:
+  // 36 VALU per word, 7 of them the mask)
   uint64_t part = 0;
-  const int64_t nw = hash ? (n + 7) / 8 : 0;
-  for (int64_t k = half; k < nw; k += REC_LANES) {
-    const int64_t wi = wi0 + 2 * k;
-    const uint32_t w0 = W[wi], w1 = W[wi + 1], w2 = W[wi + 2];
-    const uint32_t lo = funnel(w0, w1, sh), hi = funnel(w1, w2, sh);
-    uint64_t w = ((uint64_t)hi << 32) | lo;
-    const int64_t rem = n - 8 * k;
-    if (rem < 8) w &= (1ull << (8 * rem)) - 1;
-    part += dq_mix64(w ^ ((uint64_t)(k + 1) * DQ_K_WORD));
+  if (hash) {
+    const int nfull = (int)(n >> 3), nw = (int)((n + 7) >> 3);
+    uint64_t kk = (uint64_t)(half + 1) * DQ_K_WORD;  // (k + 1) K_WORD
+    for (int k = half; k < nfull; k += REC_LANES) {
+      const int64_t wi = wi0 + 2 * k;
+      const uint32_t w0 = W[wi], w1 = W[wi + 1], w2 = W[wi + 2];
+      const uint64_t w = ((uint64_t)funnel(w1, w2, sh) << 32) | funnel(w0, w1, sh);
+      part += dq_mix64(w ^ kk);
+      kk += (uint64_t)REC_LANES * DQ_K_WORD;
+    }
+    if (nfull < nw && (nfull - half) % REC_LANES == 0) {
+      const int64_t wi = wi0 + 2 * nfull;
+      const uint32_t w0 = W[wi], w1 = W[wi + 1], w2 = W[wi + 2];
+      uint64_t w = ((uint64_t)funnel(w1, w2, sh) << 32) | funnel(w0, w1, sh);
+      w &= (1ull << (8 * (n - 8 * (int64_t)nfull))) - 1;
+      part += dq_mix64(w ^ ((uint64_t)(nfull + 1) * DQ_K_WORD));
+    }
   }
   return part;
 }
@@ -1030,18 +1041,25 @@ __global__ __launch_bounds__(LH_THREADS) void long_hash_kernel(
     const int64_t n = 4 + (int64_t)bs, nw = (n + 7) / 8;
     const int64_t k0 = j * (LONG_PIECE / 8), k1 = min(nw, k0 + LONG_PIECE / 8);
     uint64_t part = 0;
+    // whole word pairs without masks, then (one thread) the piece's odd or partial last words
+    const int64_t kf = min(k1, n >> 3);  // words with 8 valid bytes end here
+    const int64_t kp = k0 + ((kf - k0) & ~(int64_t)1);  // whole pairs [k0, kp)
 #pragma unroll 4
-    for (int64_t k = k0 + 2 * t; k < k1; k += 2 * LH_THREADS) {
+    for (int64_t k = k0 + 2 * t; k < kp; k += 2 * LH_THREADS) {
       const int64_t wi = (p >> 2) + 2 * k;
       const uint32_t w0 = U32[wi], w1 = U32[wi + 1], w2 = U32[wi + 2], w3 = U32[wi + 3], w4 = U32[wi + 4];
-      uint64_t a = ((uint64_t)funnel(w1, w2, sh) << 32) | funnel(w0, w1, sh);
-      uint64_t b = ((uint64_t)funnel(w3, w4, sh) << 32) | funnel(w2, w3, sh);
-      const int64_t ra = n - 8 * k, rb = ra - 8;
-      if (ra < 8) a &= (1ull << (8 * ra)) - 1;
-      if (rb < 8 && rb > 0) b &= (1ull << (8 * rb)) - 1;
-      part += dq_mix64(a ^ ((uint64_t)(k + 1) * DQ_K_WORD));
-      if (k + 1 < k1) part += dq_mix64(b ^ ((uint64_t)(k + 2) * DQ_K_WORD));
+      const uint64_t a = ((uint64_t)funnel(w1, w2, sh) << 32) | funnel(w0, w1, sh);
+      const uint64_t b = ((uint64_t)funnel(w3, w4, sh) << 32) | funnel(w2, w3, sh);
+      part += dq_mix64(a ^ ((uint64_t)(k + 1) * DQ_K_WORD)) + dq_mix64(b ^ ((uint64_t)(k + 2) * DQ_K_WORD));
     }
+    if (t == 0)
+      for (int64_t k = kp; k < k1; k++) {  // at most one whole word and one partial one
+        const int64_t wi = (p >> 2) + 2 * k;
+        uint64_t a = ((uint64_t)funnel(U32[wi + 1], U32[wi + 2], sh) << 32) | funnel(U32[wi], U32[wi + 1], sh);
+        const int64_t ra = n - 8 * k;
+        if (ra < 8) a &= (1ull << (8 * ra)) - 1;
+        part += dq_mix64(a ^ ((uint64_t)(k + 1) * DQ_K_WORD));
+      }
     for (int o = 32; o >= 1; o >>= 1) {
       const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)part, o, 64);
       const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(part >> 32), o, 64);

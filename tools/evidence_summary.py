@@ -45,7 +45,10 @@ with open(os.path.join(P, f"{tag}_rocprof_summary.txt"), "w") as f:
 v = {}
 for line in open(os.path.join(ev, "sq.log")):
     p = line.split()
-    if len(p) >= 2 and p[0].isupper():
+    # "block NAME value ..." (tools/pmc_inflate.sh: per kernel); the derived lines use the block kernel
+    if len(p) >= 3 and p[0] == "block" and p[1].isupper():
+        v[p[1]] = float(p[2])
+    elif len(p) >= 2 and p[0].isupper():
         v[p[0]] = float(p[1])
 with open(os.path.join(P, f"{tag}_inflate_pmc.txt"), "w") as f:
     f.write(f"# inflate_block_kernel PMC counters, {desc}\n")
