@@ -424,7 +424,7 @@ def main():
             "roofline": {
                 "bound": "hbm",
                 "limiter": "VALU issue (each VALU instruction holds its SIMD for a quad-cycle: "
-                           "busy ~0.8 of them, utilisation.valu_busy_quad_frac) + LDS/barrier "
+                           "busy 0.73 of them, utilisation.valu_busy_quad_frac) + LDS/barrier "
                            "latency of the serial Huffman decode (DESIGN.md section 3, Round 6), "
                            "far below the HBM roof",
                 "kernel": "inflate_block_kernel + inflate_tail_kernel (one K2 launch)",
