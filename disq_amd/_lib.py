@@ -628,7 +628,8 @@ CHECK_UNITS = ("K1/K3 kernels", "K2 inflate", "text", "deflate")
 CHECK_SITES = ("K1 candidate slot", "K2 bit reader word", "K2 image store", "K2 second-level table",
                "K2 per-lane arrays", "K2 match bitmap", "K2 resolve next pointer",
                "K2 resolve source", "K3 record staging", "K2 last_start",
-               "deflate bucket-list slot", "deflate staged symbol", "deflate image word")
+               "deflate bucket-list slot", "deflate staged symbol", "deflate image word",
+               "K3 segment speculation")
 
 
 def checked_report():

@@ -41,6 +41,7 @@ enum : int {
   CHK_Z_BL = 10,     // deflate: a bucket-list slot outside the chunk's position list
   CHK_Z_STAGE = 11,  // deflate: a staged symbol word outside its lane's staging
   CHK_Z_IMAGE = 12,  // deflate: an emitted word outside the LDS deflate image
+  CHK_K3_SPEC = 13,  // K3: the LDS-filtered segment speculation differs from seg_spec_kernel<64>
 };
 #ifdef DQ_CHECKED
 namespace {

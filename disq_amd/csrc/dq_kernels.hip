@@ -22,6 +22,30 @@ __device__ inline int32_t ld32(const uint8_t* p, int64_t i) {
   return (int32_t)(p[i] | (p[i + 1] << 8) | (p[i + 2] << 16) | ((uint32_t)p[i + 3] << 24));
 }
 
+#ifdef DQ_REC_TIMING  // dev builds: s_memtime cycles per phase summed over waves (tools/records_timing.py)
+__device__ unsigned long long g_rec_tim[8];
+#define REC_T(k)                                             \
+  do {                                                       \
+    const uint64_t now_ = __builtin_amdgcn_s_memtime();      \
+    rt_[k] += now_ - rt_last_;                               \
+    rt_last_ = now_;                                         \
+  } while (0)
+#define REC_T_DECL uint64_t rt_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, rt_last_ = __builtin_amdgcn_s_memtime()
+#define REC_T_FLUSH                                                                  \
+  do {                                                                               \
+    if (threadIdx.x == 0)                                                            \
+      for (int k_ = 0; k_ < 8; k_++) atomicAdd(&g_rec_tim[k_], (unsigned long long)rt_[k_]); \
+  } while (0)
+#define REC_T_PARAM , uint64_t (&rt_)[8], uint64_t &rt_last_
+#define REC_T_ARG , rt_, rt_last_
+#else
+#define REC_T_PARAM
+#define REC_T_ARG
+#define REC_T(k) do {} while (0)
+#define REC_T_DECL do {} while (0)
+#define REC_T_FLUSH do {} while (0)
+#endif
+
 // ------------------------------------------------------------------ Kernel 1: BGZF scan
 constexpr uint32_t BGZF_MAGIC = 0x04088b1fu;
 
@@ -655,6 +679,237 @@ __global__ __launch_bounds__(NT) void seg_spec_kernel(const uint8_t* __restrict_
   }
 }
 
+// seg_spec for short records with an LDS pre-filter: the wave stages 1 KiB windows of the segment
+// (coalesced 16-byte LDS-DMA pieces) and tests each candidate's fixed header against the
+// conditions checkInternal applies before it reads past the header (BamRecordGuesser.java:79-194:
+// ref ids and positions, name length, CIGAR/sequence presence, the name's NUL, block_size >= the
+// fixed parts).  Only candidates passing all of them run check_record_start<3> on U, so the
+// speculated start is the one seg_spec_kernel<64> finds (the pre-filter rejects only positions
+// whose first checkInternal returns 0, 3 or 4); seg_spec_kernel<64> ran the whole divergent check
+// for 64 candidates per step (round 6: 47 k cycles per segment, 57 % waiting,
+// profiles/r6h_records_pmc.txt).
+#ifndef DQ_SPEC_LDS  // 0: seg_spec_kernel<64>, 1: seg_spec_lds_kernel, 2: seg_spec_split_kernel<DQ_SPEC_SL>
+#define DQ_SPEC_LDS 2
+#endif
+#ifndef DQ_SPEC_SL
+#define DQ_SPEC_SL 16
+#endif
+constexpr int SPEC_WIN = 1024;                   // candidates per staged window
+constexpr int SPEC_PIECES = (SPEC_WIN + 64) / 16;  // + one header's bytes past the last candidate
+__device__ __forceinline__ bool spec_prefilter(const __attribute__((address_space(3))) uint32_t* W,
+                                               int o, int avail, int64_t v, int64_t ulen,
+                                               const int32_t* __restrict__ ref_len, int32_t n_ref) {
+  if (o + 36 > avail) return true;  // not staged: the full check decides
+  if (v + 36 > ulen) return false;  // rd_ok(v, 36) fails: 3 or 4
+  const uint32_t sh = (uint32_t)(o & 3);
+  const int wi = o >> 2;
+  uint32_t w[9], f[8];
+#pragma unroll
+  for (int k = 0; k < 9; k++) w[k] = W[wi + k];
+#pragma unroll
+  for (int k = 0; k < 8; k++) f[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+  const int32_t remaining = (int32_t)f[0], id = (int32_t)f[1], pos = (int32_t)f[2];
+  if (id < -1 || id >= n_ref || pos < -1) return false;
+  if (id >= 0 && pos > ref_len[id]) return false;
+  const int32_t nid = (int32_t)f[6], npos = (int32_t)f[7];
+  if (nid < -1 || nid >= n_ref || npos < -1) return false;
+  if (nid >= 0 && npos > ref_len[nid]) return false;
+  const int32_t name_len = (int32_t)(f[3] & 0xff);
+  if (name_len < 2) return false;
+  const int32_t flags = (int32_t)(f[4] >> 16), n_cig = (int32_t)(f[4] & 0xffff);
+  const int32_t cig_len = (int32_t)((uint32_t)n_cig * 4u);
+  const int32_t l_seq = (int32_t)f[5];
+  const int32_t seq_len = (int32_t)((uint32_t)l_seq + (uint32_t)((int32_t)((uint32_t)l_seq + 1u) / 2));
+  if ((flags & 4) == 0 && (seq_len == 0 || n_cig == 0)) return false;
+  if (v + 36 + name_len > ulen) return false;  // rd_ok(v + 36, name_len) fails: 3 or 4
+  const int t = o + 36 + name_len - 1;         // the name's NUL
+  if (t < avail) {
+    const uint32_t b = (W[t >> 2] >> (8 * (t & 3))) & 0xff;
+    if (b != 0) return false;
+  }
+  const int32_t zero_min =
+      (int32_t)((uint32_t)32 + (uint32_t)name_len + (uint32_t)cig_len + (uint32_t)seq_len);
+  return remaining >= zero_min;  // checked last by checkInternal; a start must pass it
+}
+
+__global__ __launch_bounds__(64) void seg_spec_lds_kernel(const uint8_t* __restrict__ U, int64_t ulen,
+                                                          int32_t u_is_eof,
+                                                          const int32_t* __restrict__ ref_len,
+                                                          int32_t n_ref, Seg* __restrict__ segs,
+                                                          int64_t nseg, int64_t seg_bytes,
+                                                          int64_t start_lin, int64_t chain_end) {
+  __shared__ uint4 win[SPEC_PIECES + 1];
+  const auto W = (const __attribute__((address_space(3))) uint32_t*)win;
+  const int lane = threadIdx.x;
+  for (int64_t s = blockIdx.x; s < nseg; s += gridDim.x) {
+    const int64_t sb = start_lin + s * seg_bytes;
+    const int64_t se = min(chain_end, sb + seg_bytes);
+    int64_t best = INT64_MAX;
+    if (s == 0) best = start_lin;
+    for (int64_t v0 = sb; s != 0 && v0 < se && best == INT64_MAX;) {
+      const int64_t wb = v0 & ~(int64_t)15;
+      const int64_t vend = min(se, wb + SPEC_WIN);
+      // pieces wholly inside [0, ulen) (U's padding is not assumed here)
+      const int np = (int)max((int64_t)0, min((int64_t)SPEC_PIECES, (ulen - wb) / 16));
+      const uint4* src = reinterpret_cast<const uint4*>(U + wb);
+      for (int c0 = 0; c0 < np; c0 += 64)
+        if (c0 + lane < np)
+          __builtin_amdgcn_global_load_lds(static_cast<const void*>(src + c0 + lane),
+                                           (__attribute__((address_space(3))) void*)(win + c0), 16, 0, 0);
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+      for (int64_t b = v0; b < vend; b += 64) {
+        const int64_t v = b + lane;
+        bool hit = v < vend && spec_prefilter(W, (int)(v - wb), 16 * np, v, ulen, ref_len, n_ref);
+        if (hit) hit = check_record_start<3>(U, ulen, u_is_eof, ref_len, n_ref, v) == 1;
+        const uint64_t m = __ballot(hit);
+        if (m) {
+          best = b + __builtin_ctzll(m);
+          break;
+        }
+      }
+      v0 = vend;
+      __syncthreads();  // every lane is done with the window before it is restaged
+    }
+    if (lane == 0) {
+      Seg g;
+      g.exact = s == 0;
+      g.status = 0;
+      g.start = best == INT64_MAX ? -1 : best;
+      g.exit = -1;
+      g.count = 0;
+      segs[s] = g;
+    }
+  }
+}
+
+// The same search with SL lanes per segment, 64 / SL segments per wave at once: a segment's cost is
+// the full check of its true start (three chained records, a dozen dependent round trips), so
+// several segments' checks in one wave overlap those latencies; the windows are 512 bytes.  Piece
+// k of sub-window u lands at LDS byte 1024 (k / SL) + 16 SL u + 16 (k % SL) (an LDS-DMA
+// instruction writes 16 bytes per lane at consecutive lane slots).
+template <int SL>
+__global__ __launch_bounds__(64) void seg_spec_split_kernel(const uint8_t* __restrict__ U, int64_t ulen,
+                                                            int32_t u_is_eof,
+                                                            const int32_t* __restrict__ ref_len,
+                                                            int32_t n_ref, Seg* __restrict__ segs,
+                                                            int64_t nseg, int64_t seg_bytes,
+                                                            int64_t start_lin, int64_t chain_end) {
+  constexpr int NSUB = 64 / SL, WINB = 512, NPC = (WINB + 64) / 16;  // pieces per sub-window
+  constexpr int NI = (NPC + SL - 1) / SL;                              // DMA instructions per window
+  __shared__ uint4 win[NI * 64 + 1];
+  const auto W = (const __attribute__((address_space(3))) uint8_t*)win;
+  const int lane = threadIdx.x, u = lane / SL, ll = lane % SL;
+  const uint64_t umask = (SL == 64 ? ~0ull : ((1ull << SL) - 1)) << (u * SL);
+  REC_T_DECL;
+  for (int64_t s0 = (int64_t)blockIdx.x * NSUB; s0 < nseg; s0 += (int64_t)gridDim.x * NSUB) {
+    const int64_t s = s0 + u;
+    const int64_t sb = start_lin + s * seg_bytes;
+    const int64_t se = s < nseg ? min(chain_end, sb + seg_bytes) : sb;
+    int64_t best = INT64_MAX;
+    if (s == 0) best = start_lin;
+    int64_t v0 = sb;
+    bool searching = s != 0 && s < nseg && v0 < se;
+    while (__any(searching)) {
+      const int64_t wb = v0 & ~(int64_t)15;
+      const int64_t vend = min(se, wb + WINB);
+      const int np = searching ? (int)max((int64_t)0, min((int64_t)NPC, (ulen - wb) / 16)) : 0;
+      const uint4* src = reinterpret_cast<const uint4*>(U + wb);
+#pragma unroll
+      for (int c = 0; c < NI; c++)
+        if (c * SL + ll < np)
+          __builtin_amdgcn_global_load_lds(static_cast<const void*>(src + c * SL + ll),
+                                           (__attribute__((address_space(3))) void*)(win + c * 64), 16, 0, 0);
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+      REC_T(0);
+      // sub-window byte o -> LDS byte (SB bytes of each sub-window per DMA instruction)
+      constexpr int SB = SL * 16;
+      const int ub = u * SB;
+      auto ldw = [&](int o) -> uint32_t {  // the dword at sub-window byte o (o % 4 == 0)
+        return *(const __attribute__((address_space(3))) uint32_t*)(W + (o / SB) * 1024 + ub + (o % SB));
+      };
+      bool scan = searching;
+      for (int64_t b = v0; __any(scan); b += SL) {
+        const int64_t v = b + ll;
+        bool hit = false;
+        if (scan && v < vend) {
+          const int o = (int)(v - wb), avail = 16 * np;
+          bool pass = true;
+          if (o + 36 <= avail) {
+            if (v + 36 > ulen) {
+              pass = false;
+            } else {
+              const uint32_t sh = (uint32_t)(o & 3);
+              const int o4 = o & ~3;
+              uint32_t w[9], f[8];
+#pragma unroll
+              for (int k = 0; k < 9; k++) w[k] = ldw(o4 + 4 * k);
+#pragma unroll
+              for (int k = 0; k < 8; k++) f[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+              const int32_t remaining = (int32_t)f[0], id = (int32_t)f[1], pos = (int32_t)f[2];
+              const int32_t nid = (int32_t)f[6], npos = (int32_t)f[7];
+              const int32_t name_len = (int32_t)(f[3] & 0xff);
+              const int32_t flags = (int32_t)(f[4] >> 16), n_cig = (int32_t)(f[4] & 0xffff);
+              const int32_t cig_len = (int32_t)((uint32_t)n_cig * 4u);
+              const int32_t l_seq = (int32_t)f[5];
+              const int32_t seq_len =
+                  (int32_t)((uint32_t)l_seq + (uint32_t)((int32_t)((uint32_t)l_seq + 1u) / 2));
+              const int32_t zero_min =
+                  (int32_t)((uint32_t)32 + (uint32_t)name_len + (uint32_t)cig_len + (uint32_t)seq_len);
+              pass = !(id < -1 || id >= n_ref || pos < -1) && !(nid < -1 || nid >= n_ref || npos < -1) &&
+                     name_len >= 2 && !((flags & 4) == 0 && (seq_len == 0 || n_cig == 0)) &&
+                     v + 36 + name_len <= ulen && remaining >= zero_min;
+              if (pass) {
+                const int t = o + 36 + name_len - 1;  // the name's NUL
+                if (t < avail && ((ldw(t & ~3) >> (8 * (t & 3))) & 0xff) != 0) pass = false;
+              }
+              if (pass && id >= 0 && pos > ref_len[id]) pass = false;
+              if (pass && nid >= 0 && npos > ref_len[nid]) pass = false;
+            }
+          }
+          REC_T(1);
+#ifdef DQ_REC_TIMING
+          rt_[3] += __any(pass) ? 1 : 0;
+          rt_[7] += __popcll(__ballot(pass));
+#endif
+          if (pass) hit = check_record_start<3>(U, ulen, u_is_eof, ref_len, n_ref, v) == 1;
+          REC_T(2);
+        }
+        const uint64_t m = __ballot(hit) & umask;
+        if (scan && m) {
+          best = b + (__builtin_ctzll(m) - u * SL);
+          scan = false;
+          searching = false;
+        }
+        if (b + SL >= vend) scan = false;  // this window is done
+      }
+      if (searching) {
+        v0 = vend;
+        searching = v0 < se;
+      }
+      __syncthreads();  // every lane is done with the windows before they are restaged
+    }
+    if (ll == 0 && s < nseg) {
+      Seg g;
+      g.exact = s == 0;
+      g.status = 0;
+      g.start = best == INT64_MAX ? -1 : best;
+      g.exit = -1;
+      g.count = 0;
+      segs[s] = g;
+    }
+  }
+  REC_T_FLUSH;
+}
+
+#ifdef DQ_CHECKED
+__global__ void spec_cmp_kernel(const Seg* __restrict__ a, const Seg* __restrict__ b, int64_t n) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < n) DQ_CHK(a[s].start == b[s].start, CHK_K3_SPEC);
+}
+#endif
+
 // The walks of all segments, one lane each (a walk is a chain of dependent loads: many walks per
 // wave keep many in flight).  With `offs` (64 KiB segments), the walk also records its record
 // starts as 16-bit offsets from the segment start, four per 8-byte store, so that seg_emit copies
@@ -919,6 +1174,9 @@ __device__ __attribute__((always_inline)) inline uint64_t decode_one(
   // whose word it is (round 5 computed the partial-word mask and 64-bit counters for every word:
   // 36 VALU per word, 7 of them the mask)
   uint64_t part = 0;
+#ifdef DQ_REC_NOHASH  // dev experiment: the decode without the hash (wrong hashes)
+  hash = false;
+#endif
   if (hash) {
     const int nfull = (int)(n >> 3), nw = (int)((n + 7) >> 3);
     uint64_t kk = (uint64_t)(half + 1) * DQ_K_WORD;  // (k + 1) K_WORD
@@ -957,7 +1215,7 @@ __device__ void decode_group(const uint8_t* __restrict__ U, int64_t ulen,
                              const int64_t* __restrict__ rec_lin, int64_t nrec,
                              const int64_t* __restrict__ blk_pos, const int64_t* __restrict__ uoff,
                              int64_t nblk, const int32_t* __restrict__ pt, const RecSoA& soa,
-                             int32_t* d_status, int64_t i0, uint4* stage4, LongList ll) {
+                             int32_t* d_status, int64_t i0, uint4* stage4, LongList ll REC_T_PARAM) {
   const int lane = threadIdx.x, r = lane & (REC_GROUP - 1), half = lane / REC_GROUP;
   const int nact = (int)min((int64_t)REC_GROUP, nrec - i0);
   const int64_t i = i0 + r;
@@ -985,6 +1243,7 @@ __device__ void decode_group(const uint8_t* __restrict__ U, int64_t ulen,
   const int64_t len = lastp + 4 + (int64_t)lastbs - base;
   uint64_t part = 0;
   bool lng = false;
+  REC_T(4);
   if (len + 32 <= REC_STAGE) {  // the hash reads up to 12 bytes past the last record
     // LDS-DMA: every 16-byte piece in flight at once (a register-staged loop waits per piece)
     const uint4* src = reinterpret_cast<const uint4*>(U + base);
@@ -999,6 +1258,7 @@ __device__ void decode_group(const uint8_t* __restrict__ U, int64_t ulen,
             (__attribute__((address_space(3))) void*)(stage4 + c0), 16, 0, 0);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
+    REC_T(5);
     if (act)  // DS reads from the staging buffer (a pointer that may be either would be flat)
       part = decode_one((const __attribute__((address_space(3))) uint32_t*)stage4, p - base, p, bs,
                         n, i, half, blk_pos, uoff, nblk, bo, soa);
@@ -1019,7 +1279,99 @@ __device__ void decode_group(const uint8_t* __restrict__ U, int64_t ulen,
             (uint32_t)__shfl_xor((int)plo, o, 64);
   }
   if (act && half == 0) soa.hash[i] = lng ? 0ull : dq_mix64((uint64_t)n * DQ_K_LEN + part);
+  REC_T(6);
 }
+
+// decode_group without the block-size loads before the staging (DQ_REC_HINT): records ascend and do
+// not overlap, so a group's bytes end at or before the next group's first record start, which
+// rec_lin already holds; the staging copies [first, that start) and each lane then reads its
+// block_size from LDS.  The dependent round trip to U (the first touch of the records' header
+// lines, an HBM miss) that sized the staging is gone; a lane whose record does not end inside the
+// staged bytes (rec_lin not ascending, e.g. a record listed twice) sends the group down the
+// unstaged path, which reads the block sizes from U as decode_group does.
+__device__ void decode_group_hint(const uint8_t* __restrict__ U, int64_t ulen,
+                                  const int64_t* __restrict__ rec_lin, int64_t nrec,
+                                  const int64_t* __restrict__ blk_pos, const int64_t* __restrict__ uoff,
+                                  int64_t nblk, const int32_t* __restrict__ pt, const RecSoA& soa,
+                                  int32_t* d_status, int64_t i0, uint4* stage4, LongList ll REC_T_PARAM) {
+  const int lane = threadIdx.x, r = lane & (REC_GROUP - 1), half = lane / REC_GROUP;
+  const int nact = (int)min((int64_t)REC_GROUP, nrec - i0);
+  const int64_t i = i0 + r;
+  const bool act = r < nact;
+  const int64_t p = act ? rec_lin[i] : rec_lin[i0];
+  const int64_t first = rec_lin[i0];
+  const bool more = i0 + nact < nrec;
+  const uint32_t* U32 = reinterpret_cast<const uint32_t*>(U);
+  int64_t end;
+  if (more) {
+    end = rec_lin[i0 + nact];
+  } else {  // the file's last group: its last record's block size
+    const int64_t lastp = rec_lin[i0 + nact - 1];
+    end = lastp + 4 + (int64_t)(int32_t)funnel(U32[lastp >> 2], U32[(lastp >> 2) + 1], (uint32_t)(lastp & 3));
+  }
+  // the block lookups of the voffset, issued now so their latency overlaps the staging
+  BlockOf bo;
+  bo.j = pt[p >> 16];
+  bo.u0 = uoff[bo.j];
+  bo.u1 = bo.j + 1 < nblk ? uoff[bo.j + 1] : INT64_MAX;
+  bo.bp = blk_pos[bo.j];
+  const int64_t base = first & ~(int64_t)15;
+  const int64_t len = end - base;
+  bool staged = len >= 0 && len + 32 <= REC_STAGE && end <= ulen;
+  int32_t bs = 0;
+  REC_T(4);
+  const auto S = (const __attribute__((address_space(3))) uint32_t*)stage4;
+  if (staged) {
+    const uint4* src = reinterpret_cast<const uint4*>(U + base);
+    const int npiece = (int)((len + 31) / 16);
+    for (int c0 = 0; c0 < npiece; c0 += REC_WAVE)
+      if (c0 + lane < npiece)
+        __builtin_amdgcn_global_load_lds(
+            static_cast<const void*>(src + c0 + lane),
+            (__attribute__((address_space(3))) void*)(stage4 + c0), 16, 0, 0);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    const int64_t o = p - base;
+    const bool inb = o >= 0 && o + 8 <= 16 * (int64_t)npiece;
+    bs = inb ? (int32_t)funnel(S[o >> 2], S[(o >> 2) + 1], (uint32_t)(o & 3)) : 0;
+    const bool fit = !act || (inb && bs >= 0 && p + 4 + (int64_t)bs <= end);
+    if (__any(!fit)) staged = false;
+    DQ_CHK(!staged || !act || (o + 4 * 10 <= REC_STAGE && o + 8 * ((4 + (int64_t)bs + 7) / 8) + 4 <= REC_STAGE),
+           CHK_K3_STAGE);
+  }
+  REC_T(5);
+  if (!staged) bs = (int32_t)funnel(U32[p >> 2], U32[(p >> 2) + 1], (uint32_t)(p & 3));
+  const int64_t n = 4 + (int64_t)bs;
+  const bool bad = act && p + n > ulen;
+  if (__any(bad)) {
+    if (bad) *d_status = ST_SHORT;
+    return;
+  }
+  uint64_t part = 0;
+  bool lng = false;
+  if (staged) {
+    if (act) part = decode_one(S, p - base, p, bs, n, i, half, blk_pos, uoff, nblk, bo, soa);
+  } else if (act) {
+    lng = n > LONG_N;
+    part = decode_one(U32, p, p, bs, n, i, half, blk_pos, uoff, nblk, bo, soa, !lng);
+    if (lng && half == 0) {  // its pieces go to long_hash_kernel
+      const int64_t np = (n + LONG_PIECE - 1) / LONG_PIECE;
+      const int64_t e0 = (int64_t)atomicAdd(ll.cnt, (unsigned long long)np);
+      for (int64_t j = 0; j < np && e0 + j < ll.cap; j++) ll.ent[e0 + j] = (uint64_t)i << 16 | (uint64_t)j;
+    }
+  }
+#pragma unroll
+  for (int o = REC_GROUP; o < REC_WAVE; o <<= 1) {
+    const uint32_t plo = (uint32_t)part, phi = (uint32_t)(part >> 32);
+    part += ((uint64_t)(uint32_t)__shfl_xor((int)phi, o, 64) << 32) |
+            (uint32_t)__shfl_xor((int)plo, o, 64);
+  }
+  if (act && half == 0) soa.hash[i] = lng ? 0ull : dq_mix64((uint64_t)n * DQ_K_LEN + part);
+  REC_T(6);
+}
+#ifndef DQ_REC_HINT
+#define DQ_REC_HINT 1
+#endif
 
 // One workgroup per piece of a long record (grid-stride over the list): thread t sums the words
 // of pairs t, t + 256, ... of the piece (five dword loads per pair, consecutive lanes on
@@ -1135,11 +1487,17 @@ __global__ __launch_bounds__(64) void decode_records_kernel(
     const int64_t* __restrict__ blk_pos, const int64_t* __restrict__ uoff, int64_t nblk,
     const int32_t* __restrict__ pt, RecSoA soa, int32_t* d_status, LongList ll) {
   __shared__ uint4 stage4[REC_STAGE / 16 + 1];
+  REC_T_DECL;
   for (int64_t g = blockIdx.x; g * REC_GROUP < nrec; g += gridDim.x) {
-    decode_group(U, ulen, rec_lin, nrec, blk_pos, uoff, nblk, pt, soa, d_status, g * REC_GROUP,
-                 stage4, ll);
+    if (DQ_REC_HINT)
+      decode_group_hint(U, ulen, rec_lin, nrec, blk_pos, uoff, nblk, pt, soa, d_status, g * REC_GROUP,
+                        stage4, ll REC_T_ARG);
+    else
+      decode_group(U, ulen, rec_lin, nrec, blk_pos, uoff, nblk, pt, soa, d_status, g * REC_GROUP,
+                   stage4, ll REC_T_ARG);
     __syncthreads();  // this group is done with the staging buffer
   }
+  REC_T_FLUSH;
 }
 
 // ------------------------------------------------------------------ partitions
@@ -1655,9 +2013,39 @@ void launch_seg_spec(const uint8_t* U, int64_t ulen, int32_t u_is_eof, int64_t c
   if (seg_bytes > 64 * 1024)  // long records (segments sized from the guesser's record span)
     hipLaunchKernelGGL(seg_spec_kernel<256>, dim3((unsigned)std::min<int64_t>(nseg, 16384)), dim3(256), 0, s, U,
                        ulen, u_is_eof, ref_len, n_ref, segs, nseg, seg_bytes, start_lin, chain_end);
+  else if (DQ_SPEC_LDS == 2)
+    hipLaunchKernelGGL(seg_spec_split_kernel<DQ_SPEC_SL>, dim3((unsigned)std::min<int64_t>((nseg + 64 / DQ_SPEC_SL - 1) / (64 / DQ_SPEC_SL), 16384)),
+                       dim3(64), 0, s, U, ulen, u_is_eof, ref_len, n_ref, segs, nseg, seg_bytes, start_lin, chain_end);
+  else if (DQ_SPEC_LDS == 1)
+    hipLaunchKernelGGL(seg_spec_lds_kernel, dim3((unsigned)std::min<int64_t>(nseg, 16384)), dim3(64), 0, s, U,
+                       ulen, u_is_eof, ref_len, n_ref, segs, nseg, seg_bytes, start_lin, chain_end);
   else
     hipLaunchKernelGGL(seg_spec_kernel<64>, dim3((unsigned)std::min<int64_t>(nseg, 16384)), dim3(64), 0, s, U,
                        ulen, u_is_eof, ref_len, n_ref, segs, nseg, seg_bytes, start_lin, chain_end);
+#ifdef DQ_CHECKED
+  if (seg_bytes <= 64 * 1024 && DQ_SPEC_LDS) {  // the filtered search finds seg_spec_kernel<64>'s starts
+    Seg* ref = nullptr;
+    if (hipMalloc(&ref, sizeof(Seg) * (size_t)nseg) == hipSuccess) {
+      hipLaunchKernelGGL(seg_spec_kernel<64>, dim3((unsigned)std::min<int64_t>(nseg, 16384)), dim3(64), 0, s, U,
+                         ulen, u_is_eof, ref_len, n_ref, ref, nseg, seg_bytes, start_lin, chain_end);
+      hipLaunchKernelGGL(spec_cmp_kernel, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, segs, ref, nseg);
+      (void)hipStreamSynchronize(s);
+      (void)hipFree(ref);
+    }
+  }
+#endif
+#ifdef DQ_REC_TIMING
+  {
+    unsigned long long h[8] = {0};
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_rec_tim), sizeof(h));
+    fprintf(stderr, "[dq] seg_spec cycles summed over waves: staging=%.3g prefilter=%.3g full_checks=%.3g; "
+            "steps with a full check %.3g, candidates passing the prefilter %.3g, segments %lld\n",
+            (double)h[0], (double)h[1], (double)h[2], (double)h[3], (double)h[7], (long long)nseg);
+    const unsigned long long z[8] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_rec_tim), z, sizeof(z));
+  }
+#endif
   hipLaunchKernelGGL(seg_walk_kernel, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, U, ulen,
                      u_is_eof, segs, nseg, seg_bytes, start_lin, chain_end,
                      seg_bytes <= 65536 ? offs : nullptr);
@@ -1714,10 +2102,21 @@ void launch_decode_records(const uint8_t* U, int64_t ulen, const int64_t* rec_li
                      uoff, nblk, pt, npages);
   (void)hipMemsetAsync(long_cnt, 0, sizeof(unsigned long long), s);
   const LongList ll{long_ent, long_cap, long_cnt};
-  hipLaunchKernelGGL(decode_records_kernel,
-                     dim3((unsigned)std::min<int64_t>((nrec + REC_GROUP - 1) / REC_GROUP, 16384)),
+  const int64_t ngroup = (nrec + REC_GROUP - 1) / REC_GROUP;
+  hipLaunchKernelGGL(decode_records_kernel, dim3((unsigned)std::min<int64_t>(ngroup, 16384)),
                      dim3(REC_WAVE), 0, s, U, ulen, rec_lin, nrec, blk_pos, uoff, nblk, pt, soa,
                      d_status, ll);
+#ifdef DQ_REC_TIMING
+  {
+    unsigned long long h[8] = {0};
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_rec_tim), sizeof(h));
+    fprintf(stderr, "[dq] decode_records cycles summed over waves: index=%.3g staging=%.3g decode=%.3g\n",
+            (double)h[4], (double)h[5], (double)h[6]);
+    const unsigned long long z[8] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_rec_tim), z, sizeof(z));
+  }
+#endif
   // the long records' pieces (an empty list costs two tiny launches that read the count)
   hipLaunchKernelGGL(long_hash_kernel, dim3(2048), dim3(LH_THREADS), 0, s, U, rec_lin, long_ent,
                      long_cnt, long_cap, soa.hash);

@@ -1,8 +1,8 @@
 #!/bin/bash
 # PMC passes (one rocprofv3 run each) over the kernels matching a regex, on the 2M-record file
-# (tools/inflate_timing.py runs the whole pipeline).  usage: tools/pmc_kernel.sh OUTDIR REGEX
+# (tools/records_timing.py runs the whole pipeline).  usage: tools/pmc_kernel.sh OUTDIR REGEX [NRECORDS]
 set -e
-out=$1; rx=$2
+out=$1; rx=$2; n=${3:-2000000}
 export TMPDIR=/tmp
 mkdir -p "$out"
 i=0
@@ -10,7 +10,7 @@ for pass in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD 
             "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_INST_LEVEL_VMEM SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" \
             "FETCH_SIZE GRBM_GUI_ACTIVE GRBM_COUNT" "WRITE_SIZE"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $pass --kernel-include-regex "$rx" --output-format csv -d $out/p$i -o run -- python3 -u tools/inflate_timing.py 2000000 1 > $out/p$i.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc $pass --kernel-include-regex "$rx" --output-format csv -d $out/p$i -o run -- python3 -u tools/records_timing.py $n 1 > $out/p$i.log 2>&1
 done
 python3 - "$out" <<'PY'
 import csv, glob, sys, collections
