@@ -1129,6 +1129,16 @@ constexpr int REC_STAGE = REC_GROUP * 384;
 // dword view in which the record starts at byte `off` (LDS staging or U itself).  Lane part 0
 // decodes the fixed fields; the REC_LANES parts hash the record's 8-byte words k = part mod
 // REC_LANES (the word sum is order-free) and return the partial sum.
+// SoA stores: non-temporal (the rows are not read again by this pass; 2 % faster records stage,
+// profiles/r6o_records_window_nt.txt); DQ_REC_NT=0: plain stores
+#ifndef DQ_REC_NT
+#define DQ_REC_NT 1
+#endif
+#if DQ_REC_NT
+#define REC_ST(dst, v) __builtin_nontemporal_store((v), &(dst))
+#else
+#define REC_ST(dst, v) ((dst) = (v))
+#endif
 struct BlockOf {  // the htsjdk block of a record start: loaded before the staging wait
   int64_t j, u0, u1, bp;
 };
@@ -1149,25 +1159,25 @@ __device__ __attribute__((always_inline)) inline uint64_t decode_one(
 #pragma unroll
       for (int k = 0; k < 9; k++) f[k] = funnel(w[k], w[k + 1], sh);
     }
-    soa.block_size[i] = bs;
-    soa.ref_id[i] = (int32_t)f[1];
-    soa.pos[i] = (int32_t)f[2];
-    soa.l_read_name[i] = (uint8_t)(f[3] & 0xff);
-    soa.mapq[i] = (uint8_t)((f[3] >> 8) & 0xff);
-    soa.bin[i] = (uint16_t)(f[3] >> 16);
-    soa.n_cigar[i] = (uint16_t)(f[4] & 0xffff);
-    soa.flag[i] = (uint16_t)(f[4] >> 16);
-    soa.l_seq[i] = (int32_t)f[5];
-    soa.next_ref_id[i] = (int32_t)f[6];
-    soa.next_pos[i] = (int32_t)f[7];
-    soa.tlen[i] = (int32_t)f[8];
+    REC_ST(soa.block_size[i], bs);
+    REC_ST(soa.ref_id[i], (int32_t)f[1]);
+    REC_ST(soa.pos[i], (int32_t)f[2]);
+    REC_ST(soa.l_read_name[i], (uint8_t)(f[3] & 0xff));
+    REC_ST(soa.mapq[i], (uint8_t)((f[3] >> 8) & 0xff));
+    REC_ST(soa.bin[i], (uint16_t)(f[3] >> 16));
+    REC_ST(soa.n_cigar[i], (uint16_t)(f[4] & 0xffff));
+    REC_ST(soa.flag[i], (uint16_t)(f[4] >> 16));
+    REC_ST(soa.l_seq[i], (int32_t)f[5]);
+    REC_ST(soa.next_ref_id[i], (int32_t)f[6]);
+    REC_ST(soa.next_pos[i], (int32_t)f[7]);
+    REC_ST(soa.tlen[i], (int32_t)f[8]);
     while (bo.j + 1 < nblk && bo.u1 <= p) {  // rare: the page's first block ends before p
       bo.j++;
       bo.u0 = bo.u1;
       bo.u1 = bo.j + 1 < nblk ? uoff[bo.j + 1] : INT64_MAX;
       bo.bp = blk_pos[bo.j];
     }
-    soa.voffset[i] = ((uint64_t)bo.bp << 16) | (uint64_t)(p - bo.u0);
+    REC_ST(soa.voffset[i], ((uint64_t)bo.bp << 16) | (uint64_t)(p - bo.u0));
   }
   // hash words k = half, half + REC_LANES, ... (a long record's words: long_hash_kernel): the
   // whole words first, with no mask and 32-bit counters, then the partial last word by the lane
@@ -1278,7 +1288,7 @@ __device__ void decode_group(const uint8_t* __restrict__ U, int64_t ulen,
     part += ((uint64_t)(uint32_t)__shfl_xor((int)phi, o, 64) << 32) |
             (uint32_t)__shfl_xor((int)plo, o, 64);
   }
-  if (act && half == 0) soa.hash[i] = lng ? 0ull : dq_mix64((uint64_t)n * DQ_K_LEN + part);
+  if (act && half == 0) REC_ST(soa.hash[i], lng ? 0ull : dq_mix64((uint64_t)n * DQ_K_LEN + part));
   REC_T(6);
 }
 
@@ -1366,7 +1376,7 @@ __device__ void decode_group_hint(const uint8_t* __restrict__ U, int64_t ulen,
     part += ((uint64_t)(uint32_t)__shfl_xor((int)phi, o, 64) << 32) |
             (uint32_t)__shfl_xor((int)plo, o, 64);
   }
-  if (act && half == 0) soa.hash[i] = lng ? 0ull : dq_mix64((uint64_t)n * DQ_K_LEN + part);
+  if (act && half == 0) REC_ST(soa.hash[i], lng ? 0ull : dq_mix64((uint64_t)n * DQ_K_LEN + part));
   REC_T(6);
 }
 #ifndef DQ_REC_HINT
