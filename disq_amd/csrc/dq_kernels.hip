@@ -1299,24 +1299,20 @@ __device__ void decode_group(const uint8_t* __restrict__ U, int64_t ulen,
 // lines, an HBM miss) that sized the staging is gone; a lane whose record does not end inside the
 // staged bytes (rec_lin not ascending, e.g. a record listed twice) sends the group down the
 // unstaged path, which reads the block sizes from U as decode_group does.
-__device__ void decode_group_hint(const uint8_t* __restrict__ U, int64_t ulen,
-                                  const int64_t* __restrict__ rec_lin, int64_t nrec,
+// The group's lane work given its record starts: lane r's start p (the group's first for inactive
+// lanes), `nact` records, the first start and an end bound (`end` < 0: the last record's block size
+// is loaded to find it).
+__device__ void decode_group_core(const uint8_t* __restrict__ U, int64_t ulen, int64_t p, int nact,
+                                  int64_t first, int64_t end,
                                   const int64_t* __restrict__ blk_pos, const int64_t* __restrict__ uoff,
                                   int64_t nblk, const int32_t* __restrict__ pt, const RecSoA& soa,
                                   int32_t* d_status, int64_t i0, uint4* stage4, LongList ll REC_T_PARAM) {
   const int lane = threadIdx.x, r = lane & (REC_GROUP - 1), half = lane / REC_GROUP;
-  const int nact = (int)min((int64_t)REC_GROUP, nrec - i0);
   const int64_t i = i0 + r;
   const bool act = r < nact;
-  const int64_t p = act ? rec_lin[i] : rec_lin[i0];
-  const int64_t first = rec_lin[i0];
-  const bool more = i0 + nact < nrec;
   const uint32_t* U32 = reinterpret_cast<const uint32_t*>(U);
-  int64_t end;
-  if (more) {
-    end = rec_lin[i0 + nact];
-  } else {  // the file's last group: its last record's block size
-    const int64_t lastp = rec_lin[i0 + nact - 1];
+  if (end < 0) {  // the chain's last group: its last record's block size
+    const int64_t lastp = __shfl(p, nact - 1, 64);
     end = lastp + 4 + (int64_t)(int32_t)funnel(U32[lastp >> 2], U32[(lastp >> 2) + 1], (uint32_t)(lastp & 3));
   }
   // the block lookups of the voffset, issued now so their latency overlaps the staging
@@ -1378,6 +1374,18 @@ __device__ void decode_group_hint(const uint8_t* __restrict__ U, int64_t ulen,
   }
   if (act && half == 0) REC_ST(soa.hash[i], lng ? 0ull : dq_mix64((uint64_t)n * DQ_K_LEN + part));
   REC_T(6);
+}
+__device__ void decode_group_hint(const uint8_t* __restrict__ U, int64_t ulen,
+                                  const int64_t* __restrict__ rec_lin, int64_t nrec,
+                                  const int64_t* __restrict__ blk_pos, const int64_t* __restrict__ uoff,
+                                  int64_t nblk, const int32_t* __restrict__ pt, const RecSoA& soa,
+                                  int32_t* d_status, int64_t i0, uint4* stage4, LongList ll REC_T_PARAM) {
+  const int r = threadIdx.x & (REC_GROUP - 1);
+  const int nact = (int)min((int64_t)REC_GROUP, nrec - i0);
+  const int64_t p = r < nact ? rec_lin[i0 + r] : rec_lin[i0];
+  const int64_t end = i0 + nact < nrec ? rec_lin[i0 + nact] : -1;
+  decode_group_core(U, ulen, p, nact, rec_lin[i0], end, blk_pos, uoff, nblk, pt, soa, d_status, i0, stage4,
+                    ll REC_T_ARG);
 }
 #ifndef DQ_REC_HINT
 #define DQ_REC_HINT 1
