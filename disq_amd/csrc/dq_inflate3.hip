@@ -133,6 +133,9 @@ enum : int32_t { F_EXIT = 0, F_EOB = 1, F_ERR = 2, F_END = 3 };
 constexpr int TOUT = 4096;            // tail output bytes one wave holds
 constexpr int TAIL_MAX_BITS = 32768;  // tail deflate bits (64 speculative lanes of <= 512 bits)
 constexpr int TW = 4;                 // tails (waves) per tail-kernel workgroup
+#ifndef DQ_TAIL_HDR1  // the tail's header loads in one round trip (0: block header first)
+#define DQ_TAIL_HDR1 1
+#endif
 constexpr int T_NCK = 4;              // checkpoints per speculative lane in the tail kernel
 #ifndef DQ_TAIL_SEG
 #define DQ_TAIL_SEG 96
@@ -2073,6 +2076,16 @@ __global__ __launch_bounds__(64 * TW, 4) void inflate_tail_kernel(
     // ---- header (as the block kernel: every lane reads it, the branches are uniform)
     const uint32_t clpos = pos + 17;
     const uint32_t hbase = clpos >> 5;
+#if DQ_TAIL_HDR1
+    // every load of the header in one round trip: the block header, a dynamic header's staged
+    // words and its code-length code lengths (HCLEN is not known yet: all 19 are loaded; a stored
+    // or fixed block's over-read stays inside the 4096 zero bytes that follow C)
+    constexpr int HWN = (HB_WORDS + 63) / 64;
+    uint32_t hw[HWN];
+#pragma unroll
+    for (int j = 0; j < HWN; j++) hw[j] = lane + 64 * j < HB_WORDS ? W[hbase + lane + 64 * j] : 0u;
+    const uint32_t clv = lane < 19 ? peek_bits(W, clpos + 3 * (uint32_t)lane, 3) : 0u;
+#endif
     const uint32_t h = peek_bits(W, pos, 17);
     const int32_t bfinal = (int32_t)(h & 1), btype = (int32_t)((h >> 1) & 3);
     const int32_t herr = pos + 3 > endbits ? ST_OVERREAD : btype == 3 ? ST_BAD_BLOCKTYPE : 0;
@@ -2114,9 +2127,16 @@ __global__ __launch_bounds__(64 * TW, 4) void inflate_tail_kernel(
     } else {
       const int ncode = (int)((h >> 13) & 15) + 4;
       for (int i = lane; i < 320; i += 64) L.u.d.x.h.lens[i] = 0;
+#if DQ_TAIL_HDR1
+#pragma unroll
+      for (int j = 0; j < HWN; j++)
+        if (lane + 64 * j < HB_WORDS) reinterpret_cast<uint32_t*>(L.u.d.T)[lane + 64 * j] = hw[j];
+      if (lane < 19) L.u.d.x.h.clen[c_clorder3[lane]] = lane < ncode ? (uint8_t)clv : 0;
+#else
       for (int i = lane; i < HB_WORDS; i += 64) reinterpret_cast<uint32_t*>(L.u.d.T)[i] = W[hbase + i];
       if (lane < 19)
         L.u.d.x.h.clen[c_clorder3[lane]] = lane < ncode ? (uint8_t)peek_bits(W, clpos + 3 * lane, 3) : 0;
+#endif
       __builtin_amdgcn_wave_barrier();
       bool ok = true;
       L.u.d.x.h.clt[lane] = clt_entry(L.u.d.x.h.clen, lane, &ok);
