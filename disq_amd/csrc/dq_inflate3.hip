@@ -133,6 +133,9 @@ enum : int32_t { F_EXIT = 0, F_EOB = 1, F_ERR = 2, F_END = 3 };
 constexpr int TOUT = 4096;            // tail output bytes one wave holds
 constexpr int TAIL_MAX_BITS = 32768;  // tail deflate bits (64 speculative lanes of <= 512 bits)
 constexpr int TW = 4;                 // tails (waves) per tail-kernel workgroup
+#ifndef DQ_ROOT_REG  // the tail's root-table fill with the length range ends in registers
+#define DQ_ROOT_REG 1
+#endif
 #ifndef DQ_TAIL_HDR1  // the tail's header loads in one round trip (0: block header first)
 #define DQ_TAIL_HDR1 1
 #endif
@@ -749,6 +752,29 @@ DQ_AI uint16_t root_entry(const LT& L, const HuffCanon& h, const uint16_t* end,
   int l = 1;
 #pragma unroll
   for (int k = 1; k <= R; k++) l += (uint32_t)end[k] <= r ? 1 : 0;
+  if (l > R) return 0;
+  const int q = (int)h.offs[l] + (int)(r >> (R - l)) - (int)h.first[l];
+  return ent[q];
+}
+// The range ends of the lengths 1..R in registers, for a loop of root_entry_r over many indices
+// (root_entry re-reads them from LDS per index: the table stores in the loop may alias them).
+template <int R>
+struct RootEnds {
+  uint32_t e[R + 1];
+};
+template <int R>
+DQ_AI RootEnds<R> root_ends(const uint16_t* end) {
+  RootEnds<R> x;
+  x.e[0] = 0;
+#pragma unroll
+  for (int k = 1; k <= R; k++) x.e[k] = end[k];
+  return x;
+}
+template <int R>
+DQ_AI uint16_t root_entry_r(const HuffCanon& h, const RootEnds<R>& E, const uint16_t* ent, uint32_t r) {
+  int l = 1;
+#pragma unroll
+  for (int k = 1; k <= R; k++) l += E.e[k] <= r ? 1 : 0;
   if (l > R) return 0;
   const int q = (int)h.offs[l] + (int)(r >> (R - l)) - (int)h.first[l];
   return ent[q];
@@ -1987,12 +2013,24 @@ DQ_AI void build_tables_wave(LdsW& L, int nlen, int ndist) {
                          L.u.d.hd.count[13] + L.u.d.hd.count[14] + L.u.d.hd.count[15] > 0;
   // (an index with no code in an incomplete code -- zlib allows one code of length 1 -- gets an
   // invalid-code entry of length 1: decoding it stops the run, as zlib's "invalid code")
+#if DQ_ROOT_REG
+  const RootEnds<LR> le = root_ends<LR>(L.u.d.lend);
+  const RootEnds<DR> de = root_ends<DR>(L.u.d.dend);
+#endif
   for (int i = lane; i < (1 << LR); i += 64) {
+#if DQ_ROOT_REG
+    const uint16_t v = root_entry_r<LR>(L.u.d.hl, le, L.u.d.lent, bitrev((uint32_t)i, LR));
+#else
     const uint16_t v = root_entry<LR>(L, L.u.d.hl, L.u.d.lend, L.u.d.lent, bitrev((uint32_t)i, LR));
+#endif
     L.u.d.T[i] = v ? v : lslow ? E_SLOW : (uint16_t)(LL_BAD | 1u);
   }
   for (int i = lane; i < (1 << DR); i += 64) {
+#if DQ_ROOT_REG
+    const uint16_t v = root_entry_r<DR>(L.u.d.hd, de, L.u.d.dent, bitrev((uint32_t)i, DR));
+#else
     const uint16_t v = root_entry<DR>(L, L.u.d.hd, L.u.d.dend, L.u.d.dent, bitrev((uint32_t)i, DR));
+#endif
     L.u.d.T[LdsW::kDROOT + i] = v ? v : dslow ? E_SLOW : (uint16_t)0x4001u;
   }
   __builtin_amdgcn_wave_barrier();
