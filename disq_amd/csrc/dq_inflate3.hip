@@ -69,6 +69,9 @@ static_assert(WG % 128 == 0 && WG >= 512 && WG <= 1024, "whole waves on every SI
 constexpr int NWV = WG / 64;      // waves per workgroup
 constexpr int NDEC = WG;          // speculative decode lanes (<= WG)
 constexpr uint32_t OV_DEFAULT = 96;  // speculative warm-up bits before each segment
+#ifndef DQ_TAIL_OV
+#define DQ_TAIL_OV OV_DEFAULT  // the tail kernel's (dev builds sweep it)
+#endif
 constexpr int OUTCAP = 65536 + 24;  // + alignment shift (<= 15) + descriptor overhang; bm 8-aligned
 // resolve shape (tuning builds): NB chunks of G * WG bytes per batch; DQ_CSTEP = 1: one ordered
 // step per chunk instead of per 512 bytes (longer in-step chains, fewer barriers; always so when
@@ -2630,12 +2633,12 @@ void launch_inflate3(const uint8_t* C, const int64_t* blk_pos, const int32_t* bl
   // words after them (16 per tail; dq_api allocates TIM_W + 16 per block)
   if (td && tim)
     hipLaunchKernelGGL((inflate_tail_kernel<true>), dim3((unsigned)((ngrid + TW - 1) / TW)), dim3(64 * TW), 0, s,
-                       C, blk_pos, blk_csize, blk_usize, uoff, ngrid, U, status, verify_crc, crc_init, ov,
-                       sflags, sel, td, tim + TIM_W * ngrid);  // 16 words per tail
+                       C, blk_pos, blk_csize, blk_usize, uoff, ngrid, U, status, verify_crc, crc_init,
+                       ov == OV_DEFAULT ? (uint32_t)DQ_TAIL_OV : ov, sflags, sel, td, tim + TIM_W * ngrid);  // 16 words per tail
   else if (td)
     hipLaunchKernelGGL((inflate_tail_kernel<false>), dim3((unsigned)((ngrid + TW - 1) / TW)), dim3(64 * TW), 0, s,
-                       C, blk_pos, blk_csize, blk_usize, uoff, ngrid, U, status, verify_crc, crc_init, ov,
-                       sflags, sel, td, nullptr);
+                       C, blk_pos, blk_csize, blk_usize, uoff, ngrid, U, status, verify_crc, crc_init,
+                       ov == OV_DEFAULT ? (uint32_t)DQ_TAIL_OV : ov, sflags, sel, td, nullptr);
 }
 
 }  // namespace dq
