@@ -718,6 +718,9 @@ def cpu_baseline(data, ctx, rs, shard, file_len, header, args, ncores):
     return cpu, parity
 
 
+FAST_DEFLATE = "16,16,32,4,1"  # chain, lazy, nice, good, fmerge (default 32,16,32,8,1)
+
+
 def write_path_bench(args):
     """Row f3: the decompressed stream of a synthetic WGS BAM, resident in
     HBM, compressed into htsjdk's 65280-byte BGZF blocks by the GPU (dq_bgzf_compress_resident,
@@ -736,12 +739,32 @@ def write_path_bench(args):
         z = c.bgzf_fetch(n).tobytes()
         n2 = c.bgzf_compress_resident()[0]  # once more: the same bytes (htsjdk's writer is deterministic)
         same = n2 == n and c.bgzf_fetch(n2).tobytes() == z
+        # the speed end of the search-effort curve (DQ_DEFLATE, read at every launch): not the
+        # default, whose level-5 search settings keep every golden stream within 0.5 % of zlib
+        # level 5; this one is 0.65-1.35 % larger there (profiles/r6x_deflate_settings.txt)
+        old_env = os.environ.get("DQ_DEFLATE")
+        os.environ["DQ_DEFLATE"] = FAST_DEFLATE
+        try:
+            fruns = [c.bgzf_compress_resident() for _ in range(4)]
+        finally:
+            if old_env is None:
+                os.environ.pop("DQ_DEFLATE", None)
+            else:
+                os.environ["DQ_DEFLATE"] = old_env
+        fn = fruns[-1][0]
+        fz = c.bgzf_fetch(fn).tobytes()
+    fms = sorted(x[1] for x in fruns[1:])[1]
     ms = sorted(x[1] for x in runs[1:])[1]
     with _lib.Context(verify_crc=True) as c:
         c.text_open_bytes(z + eof)
         c.text_run(False)
         back = c.inflated()
     ok = hashlib.sha256(u.tobytes()).digest() == hashlib.sha256(back.tobytes()).digest()
+    with _lib.Context(verify_crc=True) as c:
+        c.text_open_bytes(fz + eof)
+        c.text_run(False)
+        fback = c.inflated()
+    fok = hashlib.sha256(u.tobytes()).digest() == hashlib.sha256(fback.tobytes()).digest()
     out = {"workload": f"decompressed stream of {args.write_records} synthetic WGS records",
            "input_gb": round(len(u) / 1e9, 4), "compressed_gb": round(n / 1e9, 4),
            "ratio": round(len(u) / n, 3), "device_ms_median": round(ms, 3),
@@ -760,6 +783,11 @@ def write_path_bench(args):
                                        "0.162 GB: 3.98x the 0.218 GB algorithmic bytes)",
                         "limiter": "LZ77 parse latency of bgzf_parse_kernel (~88 % of device time; "
                                    "one 160 KB, 1024-thread workgroup per CU: 16 waves)"},
+           "speed_setting": {"dq_deflate": FAST_DEFLATE, "ratio": round(len(u) / fn, 3),
+                             "device_ms_median": round(fms, 3), "input_gbs": round(len(u) / fms / 1e6, 2),
+                             "roundtrip_gpu_inflate": "match" if fok else "MISMATCH",
+                             "golden_streams": "0.65-1.35 % larger than zlib level 5 (default: -1.9 to "
+                                               "+0.42 %), profiles/r6x_deflate_settings.txt"},
            "evidence": "profiles/r5n_deflate_parse_1024.txt, r5zc_deflate_fmerge.txt, "
                        "r5zi_deflate_parallel_header.txt, r5zk_deflate_atomic_scatter.txt (A/Bs, "
                        "per-phase cycles), profiles/r5zl_deflate_pmc.txt (SQ counters and traffic)"}
