@@ -40,10 +40,10 @@ sys.path.insert(0, ROOT)
 
 METRIC = "decompressed BAM GB/s + reads/sec (whole node) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.29 TB/s measured copy)
-TRAFFIC_PROFILE = "r6fin_inflate_traffic_pmc.json"
+TRAFFIC_PROFILE = "r6z_inflate_traffic_pmc.json"
 # utilisation of K2 from PMC counters of the benched build (tools/pmc_summary.py over a
 # tools/pmc_inflate.sh run): VALU issue, LDS busy / bank-conflict / unaligned fractions
-UTIL_PROFILE = "r6fin_inflate_util.json"
+UTIL_PROFILE = "r6z_inflate_util.json"
 
 
 def log(*a):
@@ -424,7 +424,7 @@ def main():
             "roofline": {
                 "bound": "hbm",
                 "limiter": "VALU issue (each VALU instruction holds its SIMD for a quad-cycle: "
-                           "busy 0.73 of them, utilisation.valu_busy_quad_frac) + LDS/barrier "
+                           "busy 0.72 of them, utilisation.valu_busy_quad_frac) + LDS/barrier "
                            "latency of the serial Huffman decode (DESIGN.md section 3, Round 6), "
                            "far below the HBM roof",
                 "kernel": "inflate_block_kernel + inflate_tail_kernel (one K2 launch)",
@@ -434,8 +434,8 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
                 "traffic_src": traffic_src,
-                "pmc_src": "profiles/r6fin_inflate_pmc.txt (SQ counters of both K2 kernels, this build)",
-                "trace_src": "profiles/r6fin_rocprof_summary.txt (rocprofv3 kernel trace of this bench command: block kernel 164.96 ms + tail kernel 15.30 ms per launch)",
+                "pmc_src": "profiles/r6z_inflate_pmc.txt (SQ counters of both K2 kernels, this build)",
+                "trace_src": "profiles/r6z_rocprof_summary.txt (rocprofv3 kernel trace of this bench command: block kernel 165.31 ms + tail kernel 15.04 ms per launch)",
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_launch_ms": round(infl_avg, 3),
                 "utilisation": util,
