@@ -308,65 +308,25 @@ __device__ int check_internal(const uint8_t* U, int64_t ulen, int u_is_eof, cons
                               int32_t n_ref, int64_t v, int64_t* next) {
   int e;
   if ((e = rd_ok(v, 36, ulen, u_is_eof))) return e;
-  // the fixed header as nine aligned dwords and both reference lengths, all loads issued before
-  // the first test (the tests below keep checkInternal's order: only the loads moved up; every
-  // byte read lies inside [v & ~3, v + 32), and the reference indices are clamped into the table)
-  const uint32_t* U32 = reinterpret_cast<const uint32_t*>(U);
-  const int64_t wi = v >> 2;
-  const uint32_t sh = (uint32_t)(v & 3);
-  uint32_t hw[9];
-#pragma unroll
-  for (int k = 0; k < 9; k++) hw[k] = U32[wi + k];
-  uint32_t f[8];
-#pragma unroll
-  for (int k = 0; k < 8; k++) f[k] = __builtin_amdgcn_alignbyte(hw[k + 1], hw[k], sh);
-  const int32_t remaining = (int32_t)f[0];
-  const int32_t id = (int32_t)f[1], pos = (int32_t)f[2];
-  const int32_t nid = (int32_t)f[6], npos = (int32_t)f[7];
-  const int32_t rl_id = n_ref > 0 ? ref_len[min(max(id, 0), n_ref - 1)] : 0;
-  const int32_t rl_nid = n_ref > 0 ? ref_len[min(max(nid, 0), n_ref - 1)] : 0;
+  int32_t remaining = ld32(U, v);
+  int32_t id = ld32(U, v + 4), pos = ld32(U, v + 8);
   if (id < -1 || id >= n_ref || pos < -1) return 0;
-  if (id >= 0 && pos > rl_id) return 0;
+  if (id >= 0 && pos > ref_len[id]) return 0;
+  int32_t nid = ld32(U, v + 24), npos = ld32(U, v + 28);
   if (nid < -1 || nid >= n_ref || npos < -1) return 0;
-  if (nid >= 0 && npos > rl_nid) return 0;
-  const int32_t name_len = (int32_t)(f[3] & 0xff);
+  if (nid >= 0 && npos > ref_len[nid]) return 0;
+  int32_t name_len = ld32(U, v + 12) & 0xff;
   if (name_len < 2) return 0;
-  const uint32_t flag_nc = f[4];
-  const int32_t flags = (int32_t)(flag_nc >> 16);
-  const int32_t n_cig = (int32_t)(flag_nc & 0xffff);
-  const int32_t cig_len = (int32_t)((uint32_t)n_cig * 4u);
-  const int32_t l_seq = (int32_t)f[5];
+  uint32_t flag_nc = (uint32_t)ld32(U, v + 16);
+  int32_t flags = (int32_t)(flag_nc >> 16);
+  int32_t n_cig = (int32_t)(flag_nc & 0xffff);
+  int32_t cig_len = (int32_t)((uint32_t)n_cig * 4u);
+  int32_t l_seq = ld32(U, v + 20);
   int32_t seq_len = (int32_t)((uint32_t)l_seq + (uint32_t)((int32_t)((uint32_t)l_seq + 1u) / 2));
   if ((flags & 4) == 0 && (seq_len == 0 || n_cig == 0)) return 0;
   if ((e = rd_ok(v + 36, name_len, ulen, u_is_eof))) return e;
-  // the name's NUL, its first 32 bytes (nine aligned dwords: U is padded past ulen) and the first
-  // eight CIGAR ops in one round of loads; the tests then run in checkInternal's order
-  const int64_t cp0 = v + 36 + name_len;
-  const uint8_t nul = U[cp0 - 1];
-  uint32_t nw[9];
-  {
-    const int64_t nwi = (v + 36) >> 2;
-#pragma unroll
-    for (int k = 0; k < 9; k++) nw[k] = U32[nwi + k];
-  }
-  const bool cig8 = 8 <= n_cig && cp0 + 32 <= ulen;
-  uint32_t d0[9];
-#pragma unroll
-  for (int k = 0; k < 9; k++) d0[k] = cig8 ? U32[(cp0 >> 2) + k] : 0u;
-  if (nul != 0) return 0;
-  {
-    const uint32_t nsh = (uint32_t)((v + 36) & 3);
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const uint32_t wd = __builtin_amdgcn_alignbyte(nw[k + 1], nw[k], nsh);
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const int8_t b = (int8_t)(wd >> (8 * j));
-        if (4 * k + j < name_len - 1 && !((b >= '!' && b <= '?') || (b >= 'A' && b <= '~'))) return 0;
-      }
-    }
-  }
-  for (int i = 32; i < name_len - 1; i += 16) {  // longer names: 16 bytes per round of loads
+  if (U[v + 36 + name_len - 1] != 0) return 0;
+  for (int i = 0; i < name_len - 1; i += 16) {  // 16 name bytes per round of loads
     uint8_t b16[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) b16[k] = i + k < name_len - 1 ? U[v + 36 + i + k] : (uint8_t)'A';
@@ -376,16 +336,17 @@ __device__ int check_internal(const uint8_t* U, int64_t ulen, int u_is_eof, cons
       if (!((b >= '!' && b <= '?') || (b >= 'A' && b <= '~'))) return 0;
     }
   }
-  int64_t cp = cp0;
+  int64_t cp = v + 36 + name_len;
   int i = 0;
   // the ops 8 at a time from nine aligned dwords, all loads in flight (a long read's CIGAR has
   // thousands of ops: one dependent byte-load round trip per op made the guesser the planning's
   // critical path); the checks keep the op order
+  const uint32_t* U32 = reinterpret_cast<const uint32_t*>(U);
   for (; i + 8 <= n_cig && cp + 32 <= ulen; i += 8, cp += 32) {
     const uint32_t sh = (uint32_t)(cp & 3);
     uint32_t d[9];
 #pragma unroll
-    for (int k = 0; k < 9; k++) d[k] = i == 0 ? d0[k] : U32[(cp >> 2) + k];
+    for (int k = 0; k < 9; k++) d[k] = U32[(cp >> 2) + k];
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       const int32_t op = (int32_t)__builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
