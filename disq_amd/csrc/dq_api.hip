@@ -748,6 +748,10 @@ static int run_pipeline(dq_ctx* ctx) {
                 "rows=%.0f store_crc=%.0f\n", ta[3], 100.0 * ta[3] / nb, ta[0] / ta[3],
                 ta[4] / ta[3], ta[5] / ta[3], ta[6] / ta[3], ta[7] / ta[3], ta[8] / ta[3],
                 ta[1] / ta[3], ta[2] / ta[3]);
+      if (ta[3] > 0)
+        fprintf(stderr, "[dq] tail rows per tail %.1f, jump rounds per row %.2f, rows with in-row chains %.1f %%, "
+                "round cycles per tail %.0f\n", ta[9] / ta[3], ta[10] / std::max(1.0, ta[9]),
+                100.0 * ta[11] / std::max(1.0, ta[9]), ta[12] / ta[3]);
     }
   }
   dbg(s, "inflate", nblk, ulen);

@@ -2356,6 +2356,7 @@ __global__ __launch_bounds__(64 * TW, 4) void inflate_tail_kernel(
     }
   };
   const int32_t Yend = sh + n;  // image bytes of the tail: [sh, Yend)
+  uint64_t rst[4] = {0, 0, 0, 0};  // TIMING: rows, jump rounds, rows with pending bytes, round cycles
   const uint64_t t2 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
   {  // the rows in order; a row's sources before the tail are loaded from U three rows ahead
     constexpr uint32_t TERM = 0x8000u;  // next pointer of a byte whose value is in place
@@ -2409,7 +2410,13 @@ __global__ __launch_bounds__(64 * TW, 4) void inflate_tail_kernel(
       // (b) pointer jumping inside the row (lock-step: a round's reads precede its writes): a
       //     pending pointer into the row takes that byte's pointer; a terminal byte or a byte of
       //     an earlier row ends it
+      const uint64_t tj0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
+      if (TIMING) {
+        rst[0] += 1;
+        rst[2] += __any(pend != 0) ? 1 : 0;
+      }
       for (int rnd = 0; __any(pend != 0) && rnd < 10; rnd++) {
+        if (TIMING) rst[1] += 1;
         uint32_t q[4];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
@@ -2428,6 +2435,7 @@ __global__ __launch_bounds__(64 * TW, 4) void inflate_tail_kernel(
         }
         publish();
       }
+      if (TIMING) rst[3] += __builtin_amdgcn_s_memtime() - tj0;
       // (c) the copies: every pointer is now a byte in place (terminal) or of an earlier row
       uint32_t v = own;
 #pragma unroll
@@ -2504,6 +2512,7 @@ __global__ __launch_bounds__(64 * TW, 4) void inflate_tail_kernel(
     tim[gi * 16 + 2] = __builtin_amdgcn_s_memtime() - t3;  // store, CRC
     tim[gi * 16 + 3] = 1;
     for (int k = 0; k < 5; k++) tim[gi * 16 + 4 + k] = tph[k];
+    for (int k = 0; k < 4; k++) tim[gi * 16 + 9 + k] = rst[k];
   }
 }
 
