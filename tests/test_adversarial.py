@@ -236,3 +236,37 @@ def test_gpu_dense_records_recorded_and_rewalked_segments():
     for split in (0, 70000, 150001):
         b = assert_parity(bam, split)
     assert (b["block_size"] == 40).sum() == n_tiny
+
+
+def midsize_bam(n_mid=1500):
+    """1500 records of 0.5-6 KB (reads of 300-4000 bases, names of 2-60 characters) in a row inside
+    a synthetic WGS BAM: a 64 KiB chain segment's first record start often lies past the
+    speculation's first 512-byte window (seg_spec_split_kernel searches several windows), and a
+    group of 32 such records exceeds the decode's 12 KiB staging (the unstaged path, its block
+    sizes read from U)."""
+    import struct
+    rng = np.random.default_rng(17)
+    r = synth.generate(900, seed=33, nthreads=4)
+    u = B.inflate_all(r.bam)
+    off, _ = B.record_spans(u)[450]
+    ref_id, pos = struct.unpack_from("<ii", u, off + 4)
+    mids = []
+    for k in range(n_mid):
+        l_seq = int(rng.integers(300, 4001))
+        name = (b"m%d_" % k) + b"x" * int(rng.integers(0, 50))
+        mids.append(B.make_record(ref_id, pos, name, l_seq, qual=int(rng.integers(20, 41))))
+    return B.bgzf(u[:off] + b"".join(mids) + u[off:], level=5), n_mid
+
+
+def test_oracle_midsize_records():
+    bam, n_mid = midsize_bam()
+    assert len(O.OracleBam(bam).read_all()) == 900 + n_mid
+
+
+@pytest.mark.gpu
+def test_gpu_midsize_records():
+    from test_gpu_parity import assert_parity
+    bam, n_mid = midsize_bam()
+    for split in (0, 70000, 150001, 1 << 20):
+        b = assert_parity(bam, split)
+    assert len(b["block_size"]) == 900 + n_mid
